@@ -1,0 +1,177 @@
+"""Benchmark: image_warping 4096x4096 fp32 Gauss-Newton + PCG through the Opt C ABI.
+
+One step = one Opt_ProblemStep (one GN iteration: J^T F + Jacobi preconditioner,
+lIterations x {fused p-update + J^T J p apply + p.Ap, PCG vector update + r.z},
+X += delta, cost). Inputs are resident in HBM before the timed region starts.
+
+  value       PCG unknowns processed per second over the whole job:
+              n_unknowns * lIterations * steps * ranks / wall time of the timed steps
+  roofline    the dominant kernel (the J^T J p apply), HIP events on the plan's stream
+  cpu_baseline the oracle's (C restatement of the reference CPU-MT backend) J^T J p
+              apply on this host's cores, bounded sample, rank 0 at N=1 only
+
+Multi-GPU (--gpus N under torch.distributed.run): each rank solves its own full-size
+replica (the row-slab decomposition is not wired into bench yet), so the
+scaling is weak.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "PCG JᵀJ·p throughput (unknowns/s) + GN iters/s, image_warping 4096² fp32"
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# Compulsory bytes of one J^T J p apply, per pixel: p read 12 + Angle 4
+# + UrShape 8 + flag byte 1 + Ap write 12 (the fused in-loop form also reads r, pre,
+# p_old and writes p: +24, reported separately).
+APPLY_BYTES_PER_PX = 37
+FUSED_APPLY_BYTES_PER_PX = 12 + 12 + 12 + 4 + 8 + 1 + 12 + 12  # r, pre, p_old, A, U, flag, p, Ap
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--liter", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(w, n_unknowns):
+    """Oracle J^T J p apply on host cores (bounded: one full-image apply)."""
+    from oracle import oracle
+
+    cores = min(16, os.cpu_count() or 1)
+    rng = np.random.default_rng(0)
+    p = rng.normal(size=n_unknowns).astype(np.float32)
+    oracle.iw_apply_jtj({**w, "H": 64, "Offset": w["Offset"][: 2 * w["W"] * 64],
+                         "Angle": w["Angle"][: w["W"] * 64], "UrShape": w["UrShape"][: 2 * w["W"] * 64],
+                         "Constraints": w["Constraints"][: 2 * w["W"] * 64], "Mask": w["Mask"][: w["W"] * 64]},
+                        p[: 3 * w["W"] * 64], nthreads=cores)  # warm
+    t0 = time.perf_counter()
+    oracle.iw_apply_jtj(w, p, nthreads=cores)
+    dt = time.perf_counter() - t0
+    return {
+        "value": n_unknowns / dt,
+        "unit": "unknowns/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"one J^T J p apply over the full {w['W']}x{w['H']} image "
+                  f"({n_unknowns} unknowns), oracle/image_warping.c, {cores} pthreads, {dt:.2f} s",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist_mod
+
+        dist = dist_mod
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from opt_amd import OptSolver, workloads
+
+    W = H = args.size
+    w = workloads.image_warping(W, H, seed=1234)
+    prm = [
+        torch.from_numpy(w["Offset"]).cuda(),
+        torch.from_numpy(w["Angle"]).cuda(),
+        torch.from_numpy(w["UrShape"]).cuda(),
+        torch.from_numpy(w["Constraints"]).cuda(),
+        torch.from_numpy(w["Mask"]).cuda(),
+        w["w_fitSqrt"],
+        w["w_regSqrt"],
+    ]
+    s = OptSolver([W, H], os.path.join(ROOT, "energies", "image_warping.t"), "gaussNewtonGPU")
+    n_unknowns = s.unknown_count()
+    total_steps = args.warmup + args.steps
+    s.set_solver_params({"nIterations": total_steps + 1, "lIterations": args.liter})
+    s.init(prm)
+    for _ in range(args.warmup):
+        s.step()
+    torch.cuda.synchronize()
+    s.set_kernel_timing(2)  # hipEvent pairs around the apply kernel only
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        s.step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    kname = s.apply_kernel_name()
+    n_apply, apply_ms = s.kernel_stat(kname)
+    s.set_kernel_timing(0)
+    avg_apply_s = (apply_ms / 1e3) / max(1, n_apply)
+    npx = W * H
+    fused_bytes = FUSED_APPLY_BYTES_PER_PX * npx
+    achieved = fused_bytes / avg_apply_s / 1e9
+    # the pure apply (reads p) timed separately for the kernel-only unknowns/s
+    p = torch.randn(n_unknowns, device="cuda")
+    Ap = torch.empty_like(p)
+    pure_us = s.time_apply(prm, p, Ap, 20)
+    result = {
+        "metric": METRIC,
+        "value": n_unknowns * args.liter * args.steps * world / dt,
+        "unit": "unknowns/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1000.0 * dt / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded image_warping inputs, SURVEY.md §8d)",
+        "config": {
+            "workload": f"image_warping {W}x{H} fp32 GN+PCG, lIterations={args.liter}",
+            "unknowns": n_unknowns,
+            "parallelism": "replicas" if world > 1 else "single",
+        },
+        "gn_iters_per_s": args.steps * world / dt,
+        "apply_unknowns_per_s": n_unknowns / avg_apply_s,
+        "pure_apply_us": pure_us,
+        "pure_apply_unknowns_per_s": n_unknowns / (pure_us * 1e-6),
+        "roofline": {
+            "kernel": kname,
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": PEAK_HBM_GBS,
+            "unit": "GB/s",
+            "frac": achieved / PEAK_HBM_GBS,
+            "traffic": None,
+            "avg_us": avg_apply_s * 1e6,
+            "launches": n_apply,
+            "bytes_per_px": FUSED_APPLY_BYTES_PER_PX,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(w, n_unknowns)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

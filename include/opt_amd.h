@@ -1,0 +1,79 @@
+/*
+ * opt_amd.h — extension entry points of libopt_amd.so beyond the reference ABI.
+ *
+ * The reference exposes its solver only through Opt.h; its kernels are reachable
+ * only from inside the generated step() (solverGPUGaussNewton.t:1913-2349). These
+ * entry points expose the same kernels one at a time so the parity tests and the
+ * benchmark can drive and time them without a full solve. Each cites the reference
+ * kernel whose per-unknown result it returns. All pointers are device pointers into
+ * the plan's unknown-vector layout: one contiguous block per unknown image in
+ * declaration order, channels interleaved inside an image (reference UnknownType,
+ * API/src/o.t:998-1100; e.g. image_warping = [Offset.xy * N | Angle * N]).
+ * Element type is float, or double when the state was created with doublePrecision.
+ * All calls are synchronous (they return after the device work completed).
+ * Return value 0 = success, nonzero = invalid arguments (message on stderr).
+ */
+#pragma once
+#include "Opt.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Total number of scalar unknowns of the plan (e.g. 3*W*H for image_warping). */
+long long OptAMD_PlanUnknownCount(Opt_Plan* plan);
+
+/* Energy family the problem was lowered to ("image_warping", "poisson_image_editing",
+ * ...); writes a NUL-terminated name into buf. Returns the name length. */
+int OptAMD_PlanFamily(Opt_Plan* plan, char* buf, int buflen);
+
+/* r = -J^T F and the CERES-guarded Jacobi preconditioner pre = 1/(1+sqrt(diag J^TJ))^2
+ * (or the reference's forced value when UsePreconditioner(false)) at the current
+ * unknowns; *r_dot_pre_r = sum r.(pre*r) (reference kernels.PCGInit1,
+ * solverGPUGaussNewton.t:521-563, with fmap.evalJTF o.t:2870-2913). Excluded
+ * elements get r = 0, pre = 0. */
+int OptAMD_EvalJTF(Opt_State* state, Opt_Plan* plan, void** problemparams,
+                   void* r, void* pre, double* r_dot_pre_r);
+
+/* Ap = J^T J p at the current unknowns (+ CtC*p for LM plans, with the CtC of the
+ * last LM step) and *p_dot_Ap = p.Ap (reference kernels.PCGStep1,
+ * solverGPUGaussNewton.t:607-632, with fmap.applyJTJ o.t:2770-2830). Excluded
+ * elements get Ap = 0. */
+int OptAMD_ApplyJTJ(Opt_State* state, Opt_Plan* plan, void** problemparams,
+                    const void* p, void* Ap, double* p_dot_Ap);
+
+/* Energy 1/2 sum r^2 at the current unknowns (reference kernels.computeCost,
+ * solverGPUGaussNewton.t:971-997, fmap.cost o.t:3119-3129). */
+double OptAMD_EvalCost(Opt_State* state, Opt_Plan* plan, void** problemparams);
+
+/* Launch the apply `reps` times back to back on the plan's stream, bracketed by
+ * hipEvents; returns the mean device time per launch in microseconds. */
+double OptAMD_TimeApplyJTJ(Opt_State* state, Opt_Plan* plan, void** problemparams,
+                           const void* p, void* Ap, int reps);
+
+/* Per-kernel device-time accounting (hipEvent pairs on the plan's stream).
+ * mode 0: off; 1: every kernel (the reference's collectPerKernelTimingInfo);
+ * 2: only the PCG J^T J p apply kernel. Resets the accumulated statistics. */
+void OptAMD_SetKernelTiming(Opt_Plan* plan, int mode);
+
+/* Accumulated statistics for kernel `name` since the last reset: number of launches
+ * and total device milliseconds. Returns 0 if the kernel was seen, 1 otherwise. */
+int OptAMD_KernelStat(Opt_Plan* plan, const char* name, long long* launches, double* total_ms);
+
+/* Name of the plan's dominant (PCG apply) kernel as it appears in KernelStat and in
+ * rocprofv3 kernel traces. */
+int OptAMD_ApplyKernelName(Opt_Plan* plan, char* buf, int buflen);
+
+/* Human-readable table of every timed kernel (reference timer report,
+ * backend_cuda.t:231-297). Returns the length written. */
+int OptAMD_KernelReport(Opt_Plan* plan, char* buf, int buflen);
+
+/* The HIP stream (hipStream_t) all of the plan's device work is issued on. */
+void* OptAMD_PlanStream(Opt_Plan* plan);
+
+/* Outer iterations completed since the last Init. */
+int OptAMD_PlanIterations(Opt_Plan* plan);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,264 @@
+"""ctypes binding of libopt_amd.so and a Python mirror of the reference's OptSolver.
+
+Mirrors examples/shared/OptSolver.h:46-106 (state/problem/plan lifetime, solve) and
+examples/shared/OptUtils.h:47-64 (profiled Init/Step loop) and 108-112 (solver
+parameters by name). Problem parameters are passed exactly as the reference's
+NamedParameters::data() packs them (examples/shared/NamedParameters.h:35-49): one
+``void*`` per declared index — a device (or, for the CPU backends, host) array
+pointer for Array/Unknown, a pointer to the value for Param.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, List, Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libopt_amd.so")
+
+
+class OptError(RuntimeError):
+    pass
+
+
+class InitParams(ctypes.Structure):
+    """Opt_InitializationParameters (include/Opt.h; reference Opt.h:10-35)."""
+
+    _fields_ = [
+        ("doublePrecision", ctypes.c_int),
+        ("verbosityLevel", ctypes.c_int),
+        ("collectPerKernelTimingInfo", ctypes.c_int),
+        ("backend", ctypes.c_char * 20),
+        ("numthreads", ctypes.c_int),
+        ("useMaterializedJTJ", ctypes.c_int),
+        ("useFusedJTJ", ctypes.c_int),
+    ]
+
+
+assert ctypes.sizeof(InitParams) == 44
+
+_lib = None
+
+# (name, restype, argtypes) for every symbol of include/Opt.h and include/opt_amd.h
+_VP = ctypes.c_void_p
+_SIGNATURES = [
+    ("Opt_NewState", _VP, [InitParams]),
+    ("Opt_ProblemDefine", _VP, [_VP, ctypes.c_char_p, ctypes.c_char_p]),
+    ("Opt_ProblemDelete", None, [_VP, _VP]),
+    ("Opt_ProblemPlan", _VP, [_VP, _VP, ctypes.POINTER(ctypes.c_uint)]),
+    ("Opt_PlanFree", None, [_VP, _VP]),
+    ("Opt_SetSolverParameter", None, [_VP, _VP, ctypes.c_char_p, _VP]),
+    ("Opt_ProblemSolve", None, [_VP, _VP, ctypes.POINTER(_VP)]),
+    ("Opt_ProblemInit", None, [_VP, _VP, ctypes.POINTER(_VP)]),
+    ("Opt_ProblemStep", ctypes.c_int, [_VP, _VP, ctypes.POINTER(_VP)]),
+    ("Opt_ProblemCurrentCost", ctypes.c_double, [_VP, _VP]),
+    ("OptAMD_PlanUnknownCount", ctypes.c_longlong, [_VP]),
+    ("OptAMD_PlanFamily", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int]),
+    ("OptAMD_EvalJTF", ctypes.c_int, [_VP, _VP, ctypes.POINTER(_VP), _VP, _VP, ctypes.POINTER(ctypes.c_double)]),
+    ("OptAMD_ApplyJTJ", ctypes.c_int, [_VP, _VP, ctypes.POINTER(_VP), _VP, _VP, ctypes.POINTER(ctypes.c_double)]),
+    ("OptAMD_EvalCost", ctypes.c_double, [_VP, _VP, ctypes.POINTER(_VP)]),
+    ("OptAMD_TimeApplyJTJ", ctypes.c_double, [_VP, _VP, ctypes.POINTER(_VP), _VP, _VP, ctypes.c_int]),
+    ("OptAMD_SetKernelTiming", None, [_VP, ctypes.c_int]),
+    ("OptAMD_KernelStat", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_double)]),
+    ("OptAMD_ApplyKernelName", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int]),
+    ("OptAMD_KernelReport", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int]),
+    ("OptAMD_PlanStream", _VP, [_VP]),
+    ("OptAMD_PlanIterations", ctypes.c_int, [_VP]),
+]
+EXPORTED_SYMBOLS = [s[0] for s in _SIGNATURES]
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libopt_amd.so; raise if it is missing (no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OptError(
+            f"{path} not found: build the HIP runtime first "
+            "(python -c 'import __graft_entry__ as g; g.build()' or `make`)"
+        )
+    lib = ctypes.CDLL(path)
+    for name, res, args in _SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _ptr(obj) -> int:
+    """Address of a problem parameter: torch tensor, numpy array, ctypes object or int."""
+    if obj is None:
+        return 0
+    if isinstance(obj, int):
+        return obj
+    if hasattr(obj, "data_ptr"):  # torch.Tensor
+        return obj.data_ptr()
+    if hasattr(obj, "ctypes"):  # numpy.ndarray
+        return obj.ctypes.data
+    return ctypes.addressof(obj)
+
+
+class ParamPack:
+    """The void** problemparams array; keeps scalar boxes alive."""
+
+    def __init__(self, values: Sequence):
+        self._keep = []
+        self.arr = (ctypes.c_void_p * max(1, len(values)))()
+        for i, v in enumerate(values):
+            if isinstance(v, float):
+                box = ctypes.c_float(v)
+                self._keep.append(box)
+                self.arr[i] = ctypes.addressof(box)
+            elif isinstance(v, tuple) and len(v) == 2 and v[0] in ("int", "float", "double"):
+                box = {"int": ctypes.c_int, "float": ctypes.c_float, "double": ctypes.c_double}[v[0]](v[1])
+                self._keep.append(box)
+                self.arr[i] = ctypes.addressof(box)
+            else:
+                self._keep.append(v)
+                self.arr[i] = _ptr(v)
+
+    @property
+    def ptr(self):
+        return ctypes.cast(self.arr, ctypes.POINTER(ctypes.c_void_p))
+
+
+class OptSolver:
+    """One Opt_State + Opt_Problem + Opt_Plan (reference OptSolver, OptSolver.h:46-84)."""
+
+    def __init__(
+        self,
+        dims: Sequence[int],
+        energy_file: str,
+        solver_kind: str = "gaussNewtonGPU",
+        double_precision: bool = False,
+        backend: str = "backend_cuda",
+        verbosity: int = 0,
+        kernel_timing: bool = False,
+        numthreads: int = 1,
+    ):
+        self.lib = load_library()
+        ip = InitParams()
+        ip.doublePrecision = int(double_precision)
+        ip.verbosityLevel = verbosity
+        ip.collectPerKernelTimingInfo = int(kernel_timing)
+        ip.backend = backend.encode()
+        ip.numthreads = numthreads
+        self.state = self.lib.Opt_NewState(ip)
+        if not self.state:
+            raise OptError("Opt_NewState failed")
+        self.problem = self.lib.Opt_ProblemDefine(self.state, energy_file.encode(), solver_kind.encode())
+        if not self.problem:
+            raise OptError(f"Opt_ProblemDefine failed for {energy_file}")
+        self._dims = (ctypes.c_uint * len(dims))(*dims)
+        self.plan = self.lib.Opt_ProblemPlan(self.state, self.problem, self._dims)
+        if not self.plan:
+            raise OptError("Opt_ProblemPlan failed")
+        self.double_precision = double_precision
+
+    # ---- reference API ---------------------------------------------------------
+    def set_solver_params(self, params: Dict[str, object]):
+        """setAllSolverParameters (OptUtils.h:108-112): ints for the iteration counts."""
+        keep = []
+        for name, v in params.items():
+            box = ctypes.c_int(v) if isinstance(v, int) else ctypes.c_float(v)
+            keep.append(box)
+            self.lib.Opt_SetSolverParameter(self.state, self.plan, name.encode(), ctypes.addressof(box))
+
+    def solve(self, problem_params: Sequence, solver_params: Optional[Dict[str, object]] = None) -> float:
+        if solver_params:
+            self.set_solver_params(solver_params)
+        pk = ParamPack(problem_params)
+        self.lib.Opt_ProblemSolve(self.state, self.plan, pk.ptr)
+        return self.cost()
+
+    def init(self, problem_params: Sequence):
+        self._pk = ParamPack(problem_params)
+        self.lib.Opt_ProblemInit(self.state, self.plan, self._pk.ptr)
+
+    def step(self, problem_params: Optional[Sequence] = None) -> int:
+        if problem_params is not None:
+            self._pk = ParamPack(problem_params)
+        return self.lib.Opt_ProblemStep(self.state, self.plan, self._pk.ptr)
+
+    def profiled_solve(self, problem_params: Sequence) -> List[float]:
+        """launchProfiledSolve (OptUtils.h:47-64): cost after Init and after each Step."""
+        self.init(problem_params)
+        costs = [self.cost()]
+        while self.step():
+            costs.append(self.cost())
+        return costs
+
+    def cost(self) -> float:
+        return self.lib.Opt_ProblemCurrentCost(self.state, self.plan)
+
+    # ---- extensions (include/opt_amd.h) ----------------------------------------
+    def unknown_count(self) -> int:
+        return self.lib.OptAMD_PlanUnknownCount(self.plan)
+
+    def family(self) -> str:
+        buf = ctypes.create_string_buffer(64)
+        self.lib.OptAMD_PlanFamily(self.plan, buf, 64)
+        return buf.value.decode()
+
+    def eval_jtf(self, problem_params, r, pre) -> float:
+        pk = ParamPack(problem_params)
+        out = ctypes.c_double()
+        if self.lib.OptAMD_EvalJTF(self.state, self.plan, pk.ptr, _ptr(r), _ptr(pre), ctypes.byref(out)):
+            raise OptError("OptAMD_EvalJTF failed")
+        return out.value
+
+    def apply_jtj(self, problem_params, p, Ap) -> float:
+        pk = ParamPack(problem_params)
+        out = ctypes.c_double()
+        if self.lib.OptAMD_ApplyJTJ(self.state, self.plan, pk.ptr, _ptr(p), _ptr(Ap), ctypes.byref(out)):
+            raise OptError("OptAMD_ApplyJTJ failed")
+        return out.value
+
+    def eval_cost(self, problem_params) -> float:
+        pk = ParamPack(problem_params)
+        return self.lib.OptAMD_EvalCost(self.state, self.plan, pk.ptr)
+
+    def time_apply(self, problem_params, p, Ap, reps: int) -> float:
+        pk = ParamPack(problem_params)
+        return self.lib.OptAMD_TimeApplyJTJ(self.state, self.plan, pk.ptr, _ptr(p), _ptr(Ap), reps)
+
+    def set_kernel_timing(self, mode: int):
+        self.lib.OptAMD_SetKernelTiming(self.plan, mode)
+
+    def kernel_stat(self, name: str):
+        n = ctypes.c_longlong()
+        ms = ctypes.c_double()
+        ok = self.lib.OptAMD_KernelStat(self.plan, name.encode(), ctypes.byref(n), ctypes.byref(ms)) == 0
+        return (n.value, ms.value) if ok else (0, 0.0)
+
+    def apply_kernel_name(self) -> str:
+        buf = ctypes.create_string_buffer(64)
+        self.lib.OptAMD_ApplyKernelName(self.plan, buf, 64)
+        return buf.value.decode()
+
+    def kernel_report(self) -> str:
+        buf = ctypes.create_string_buffer(1 << 16)
+        self.lib.OptAMD_KernelReport(self.plan, buf, 1 << 16)
+        return buf.value.decode()
+
+    def stream(self) -> int:
+        return self.lib.OptAMD_PlanStream(self.plan) or 0
+
+    def iterations(self) -> int:
+        return self.lib.OptAMD_PlanIterations(self.plan)
+
+    def close(self):
+        if getattr(self, "plan", None):
+            self.lib.Opt_PlanFree(self.state, self.plan)
+            self.plan = None
+        if getattr(self, "problem", None):
+            self.lib.Opt_ProblemDelete(self.state, self.problem)
+            self.problem = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,156 @@
+// common.h — shared HIP plumbing for libopt_amd: fail-stop error checks, the image
+// domain descriptor, DPP lane shifts and the deterministic device-wide reduction.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstdint>
+
+// Fail-stop on any HIP error, as the reference's `cd` macro does
+// (API/src/backend_cuda.t:26-40): print the call and exit.
+#define OPT_HIP_CHECK(call)                                                         \
+    do {                                                                            \
+        hipError_t e_ = (call);                                                     \
+        if (e_ != hipSuccess) {                                                     \
+            fprintf(stderr, "[opt_amd] HIP error %d (%s) in %s at %s:%d\n", (int)e_,\
+                    hipGetErrorString(e_), #call, __FILE__, __LINE__);              \
+            exit(1);                                                                \
+        }                                                                           \
+    } while (0)
+
+namespace optamd {
+
+constexpr int kWave = 64;           // CDNA wavefront
+constexpr int kBlock = 256;         // 4 waves per workgroup
+constexpr int kMaxReduce = 4;       // scalars one kernel may reduce at once
+
+// A 2-D image domain as one rank sees it. Global size W x H; this rank owns rows
+// [y_lo, y_hi) and holds rows [y_mem0, y_mem0 + mem_rows) in memory (owned rows plus
+// halo rows on multi-GPU slabs; identical to the owned rows on one GPU). Row-major,
+// x fastest, as the reference's IndexSpace:indextype (API/src/o.t:564-579).
+struct Domain {
+    int W, H;
+    int y_lo, y_hi;
+    int y_mem0, mem_rows;
+    __host__ __device__ long long npix_mem() const { return (long long)W * mem_rows; }
+    __host__ __device__ long long off(int x, int yg) const {
+        return (long long)(yg - y_mem0) * W + x;
+    }
+};
+
+// ---- DPP whole-wave lane shifts (gfx9 family: wave_shr:1 / wave_shl:1) ----------
+// from_left(v, e):  lane l gets v of lane l-1, lane 0 gets e.
+// from_right(v, e): lane l gets v of lane l+1, lane 63 gets e.
+__device__ __forceinline__ float from_left(float v, float e) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(e), __float_as_int(v),
+                                                      0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float from_right(float v, float e) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(e), __float_as_int(v),
+                                                      0x130, 0xf, 0xf, false));
+}
+__device__ __forceinline__ int from_left_i(int v, int e) {
+    return __builtin_amdgcn_update_dpp(e, v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int from_right_i(int v, int e) {
+    return __builtin_amdgcn_update_dpp(e, v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ double from_left(double v, double e) {
+    int2 vi = *reinterpret_cast<int2*>(&v), ei = *reinterpret_cast<int2*>(&e);
+    int2 r;
+    r.x = __builtin_amdgcn_update_dpp(ei.x, vi.x, 0x138, 0xf, 0xf, false);
+    r.y = __builtin_amdgcn_update_dpp(ei.y, vi.y, 0x138, 0xf, 0xf, false);
+    return *reinterpret_cast<double*>(&r);
+}
+__device__ __forceinline__ double from_right(double v, double e) {
+    int2 vi = *reinterpret_cast<int2*>(&v), ei = *reinterpret_cast<int2*>(&e);
+    int2 r;
+    r.x = __builtin_amdgcn_update_dpp(ei.x, vi.x, 0x130, 0xf, 0xf, false);
+    r.y = __builtin_amdgcn_update_dpp(ei.y, vi.y, 0x130, 0xf, 0xf, false);
+    return *reinterpret_cast<double*>(&r);
+}
+
+// ---- deterministic device-wide sums ---------------------------------------------
+// The reference sums every PCG scalar with one float atomic per 32-lane warp into a
+// single address (unknownWideReduction, solverGPUGaussNewton.t:466-472;
+// backend_cuda.t:366-375,447-495): order-dependent and contended. Here each block
+// reduces its values in a fixed tree (fp64), publishes ONE partial per scalar with an
+// agent-scope (sc1, write-through) store, drains it, and takes a ticket; the block
+// that draws the last ticket sums all partials in block-index order and writes the
+// scalars. Bitwise reproducible for any dispatch order or XCD placement
+// (MI355X_MICROARCH.md "Valid forms", row 1; cdna_hip_programming.md G16).
+struct ReduceSlot {
+    double* partials;     // [K][nblocks]
+    unsigned* ticket;     // one counter, zero between launches
+    double* out;          // K results
+    int nblocks;
+};
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, kWave);
+    return v;
+}
+
+// Called by every thread of a kBlock-thread block exactly once, after all the
+// block's stores of the kernel's outputs. v[k] is this thread's contribution.
+template <int K>
+__device__ __forceinline__ void block_reduce_publish(const double (&v)[K], const ReduceSlot& rs,
+                                                     int block_linear) {
+    __shared__ double red[kBlock / kWave][K];
+    __shared__ int last_flag;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wid = threadIdx.x / kWave;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double s = wave_sum(v[k]);
+        if (lane == 0) red[wid][k] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            double s = red[0][k];
+#pragma unroll
+            for (int w = 1; w < kBlock / kWave; ++w) s += red[w][k];
+            __hip_atomic_store(&rs.partials[(long long)k * rs.nblocks + block_linear], s,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned t = __hip_atomic_fetch_add(rs.ticket, 1u, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+        last_flag = (t == (unsigned)(rs.nblocks - 1));
+    }
+    __syncthreads();
+    if (!last_flag) return;
+    // Last arriver: fixed-order sum of all partials (sc1 loads bypass the stale L1).
+    __shared__ double acc[kBlock];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double s = 0.0;
+        for (int i = threadIdx.x; i < rs.nblocks; i += kBlock)
+            s += __hip_atomic_load(&rs.partials[(long long)k * rs.nblocks + i], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        acc[threadIdx.x] = s;
+        __syncthreads();
+        for (int stride = kBlock / 2; stride > 0; stride >>= 1) {
+            if (threadIdx.x < stride) acc[threadIdx.x] += acc[threadIdx.x + stride];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) rs.out[k] = acc[0];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *rs.ticket = 0u;
+}
+
+// XCD-aware bijective remap of a linear block id (cdna_hip_programming.md §5.5 T1):
+// blocks b and b+8 share an XCD, so consecutive remapped ids land on one XCD's L2
+// and neighbouring tiles share their halo lines there.
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+    const int q = nb / 8, r = nb % 8, xcd = b % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + b / 8;
+}
+
+template <typename T> struct Vec2 { T x, y; };
+
+}  // namespace optamd

@@ -1,0 +1,703 @@
+// image_warping.hip — MI355X kernels and GN driver for the image_warping energy
+// (reference examples/image_warping/image_warping.t):
+//
+//   unknowns  Offset O (float2 per pixel), Angle t (float)      -> 3 unknowns / px
+//   knowns    UrShape U (float2), Constraints C (float2), Mask M (float)
+//   params    w_fitSqrt wf, w_regSqrt wr
+//   Exclude(M != 0); UsePreconditioner(true)
+//   for s in {(1,0),(-1,0),(0,1),(0,-1)}:
+//       e_reg(k,s) = valid(k,s) ? wr * ((O_k - O_{k+s}) - R(t_k)(U_k - U_{k+s})) : 0
+//       valid(k,s) = InBounds(k+s) & M_{k+s}==0 & M_k==0
+//   e_fit(k) = wf * (C_k.x >= 0 & C_k.y >= 0 ? O_k - C_k : 0)
+//
+// Kernel map onto the reference's generated kernels (solverGPUGaussNewton.t):
+//   iw_jtf          PCGInit1 (:521-563) with evalJTF (o.t:2870-2913), CERES
+//                   guardedInvert (:478-507); also writes the per-pixel flag byte
+//   iw_apply<MODE>  PCGStep1 (:607-632) with applyJTJ (o.t:2770-2830); MODE 1/2 fuse
+//                   the previous iteration's PCGStep3 (:814-845): p = z + beta p
+//   pcg_step2       PCGStep2 (:665-731)                     (pcg_kernels.h)
+//   iw_update       PCGLinearUpdate (:854-859)
+//   iw_cost         computeCost (:971-997) with cost (o.t:3119-3129)
+//
+// Geometry (all stencil kernels): a wavefront owns a vertical strip of 64 columns,
+// x = 62*strip - 1 + lane, and writes lanes 1..62; it walks T rows top to bottom
+// keeping rows y-1, y, y+1 in registers (plus one row of prefetch). Vertical
+// neighbours therefore cost no reload, horizontal neighbours are one DPP
+// wave_shr/wave_shl move, and every residual instance is evaluated exactly once:
+// each lane computes its pixel's outgoing residuals (+x, -x, +y) and the residual
+// of the pixel below pointing up, and receives the rest from its lane neighbours
+// (DPP) or from the previous row (registers). The reference's generated gather
+// recomputes each residual (incl. sin/cos of the neighbour's angle) from both ends.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include "plan.h"
+#include "pcg_kernels.h"
+
+namespace optamd {
+namespace iw {
+
+constexpr int kStrip = 62;   // output columns per wavefront
+
+template <typename T>
+struct Args {
+    Domain dom;
+    const T* O;        // Offset (2 per px)
+    const T* A;        // Angle
+    const float* U;    // UrShape (float2)
+    const float* C;    // Constraints (float2)
+    const float* M;    // Mask
+    uint8_t* flags;    // bit0 active (inside, Mask==0), bit1 fit constraint valid
+    T wf, wr;
+    int use_pre;
+    int nstrips, nrowblocks, rows;   // rows per wavefront
+};
+
+// ---------------------------------------------------------------- helpers
+__device__ __forceinline__ void sc_of(float t, float* c, float* s) { sincosf(t, s, c); }
+__device__ __forceinline__ void sc_of(double t, double* c, double* s) { sincos(t, s, c); }
+
+struct WaveGeom {
+    int x, lane, y0, y1;
+    bool out_lane;
+};
+template <typename T>
+__device__ __forceinline__ WaveGeom geom(const Args<T>& a) {
+    WaveGeom g;
+    const int nb = a.nstrips * a.nrowblocks;
+    const int t = xcd_remap(blockIdx.x, nb);
+    const int strip = t % a.nstrips, rb = t / a.nstrips;
+    g.lane = threadIdx.x & (kWave - 1);
+    const int w = threadIdx.x / kWave;
+    g.x = strip * kStrip - 1 + g.lane;
+    g.y0 = a.dom.y_lo + (rb * (kBlock / kWave) + w) * a.rows;
+    g.y1 = min(g.y0 + a.rows, a.dom.y_hi);
+    g.out_lane = g.lane >= 1 && g.lane <= kStrip && g.x < a.dom.W;
+    return g;
+}
+
+// inside the image AND present in this rank's memory
+__device__ __forceinline__ bool present(const Domain& d, int x, int y) {
+    return x >= 0 && x < d.W && y >= 0 && y < d.H && y >= d.y_mem0 && y < d.y_mem0 + d.mem_rows;
+}
+
+// Linearised residual of the edge j -> t applied to p:
+//   a  = dR(t_j)/dt (U_j - U_t)
+//   Jp = valid ? wr (p_j - p_t - a p_tj) : 0
+template <typename T>
+__device__ __forceinline__ void jedge(T pjx, T pjy, T pjt, T cj, T sj, float ujx, float ujy,
+                                      T ptx, T pty, float utx, float uty, bool v, T wr,
+                                      T& Jx, T& Jy, T& ax, T& ay) {
+    const T dx = (T)(ujx - utx), dy = (T)(ujy - uty);
+    ax = -sj * dx - cj * dy;
+    ay = cj * dx - sj * dy;
+    Jx = v ? wr * (pjx - ptx - ax * pjt) : (T)0;
+    Jy = v ? wr * (pjy - pty - ay * pjt) : (T)0;
+}
+
+// Residual value of the edge j -> t at the current unknowns, plus its angle partial
+// direction a (d e / d t_j = -wr a).
+template <typename T>
+__device__ __forceinline__ void eedge(T ojx, T ojy, T cj, T sj, float ujx, float ujy, T otx,
+                                      T oty, float utx, float uty, bool v, T wr, T& ex, T& ey,
+                                      T& ax, T& ay) {
+    const T dx = (T)(ujx - utx), dy = (T)(ujy - uty);
+    const T rx = cj * dx - sj * dy, ry = sj * dx + cj * dy;
+    ax = -sj * dx - cj * dy;
+    ay = cj * dx - sj * dy;
+    ex = v ? wr * (ojx - otx - rx) : (T)0;
+    ey = v ? wr * (ojy - oty - ry) : (T)0;
+}
+
+// ------------------------------------------------------------ row records
+template <typename T>
+struct PRow {          // apply kernels
+    T px, py, pt;      // p (x, y, angle channel)
+    T c, s;            // cos / sin of the current angle
+    float ux, uy;
+    int act, fit;
+};
+
+template <typename T, int MODE>
+__device__ __forceinline__ PRow<T> load_prow(const Args<T>& a, int x, int y, const T* pin,
+                                             const T* r, const T* pre, T beta) {
+    PRow<T> q;
+    const bool in = present(a.dom, x, y);
+    const long long i = in ? a.dom.off(x, y) : 0;
+    const long long N = a.dom.npix_mem();
+    const int f = in ? a.flags[i] : 0;
+    q.act = f & 1;
+    q.fit = (f >> 1) & 1;
+    const float2 u = reinterpret_cast<const float2*>(a.U)[i];
+    q.ux = in ? u.x : 0.f;
+    q.uy = in ? u.y : 0.f;
+    T t = a.A[i];
+    q.c = in ? t : (T)0;   // angle; cos/sin filled by finish_row
+    if (MODE == 0) {
+        q.px = pin[2 * i]; q.py = pin[2 * i + 1]; q.pt = pin[2 * N + i];
+    } else {
+        const T rx = r[2 * i], ry = r[2 * i + 1], rt = r[2 * N + i];
+        const T wx = pre[2 * i], wy = pre[2 * i + 1], wt = pre[2 * N + i];
+        if (MODE == 1) {
+            q.px = wx * rx; q.py = wy * ry; q.pt = wt * rt;
+        } else {
+            T zx = rx, zy = ry, zt = rt;
+            if (a.use_pre) { zx = wx * rx; zy = wy * ry; zt = wt * rt; }
+            q.px = zx + beta * pin[2 * i];
+            q.py = zy + beta * pin[2 * i + 1];
+            q.pt = zt + beta * pin[2 * N + i];
+        }
+    }
+    if (!q.act) { q.px = 0; q.py = 0; q.pt = 0; }
+    return q;
+}
+template <typename T>
+__device__ __forceinline__ void finish_row(PRow<T>& q) {
+    T t = q.c;
+    sc_of(t, &q.c, &q.s);
+}
+
+// ------------------------------------------------------------- apply kernel
+// MODE 0: Ap = JtJ p for the given p.
+// MODE 1: p = pre*r (first PCG iteration; PCGInit1's p), Ap = JtJ p, writes p.
+// MODE 2: p = z + beta p_old with z = pre*r, beta = sc[ib_num]/sc[ib_den]
+//         (the previous iteration's PCGStep3), Ap = JtJ p, writes p.
+// Always: sc[rs.out] = sum p.Ap over active pixels (the alpha denominator).
+template <typename T, int MODE>
+__global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restrict__ pin,
+                                                   const T* __restrict__ r,
+                                                   const T* __restrict__ pre, T* __restrict__ pout,
+                                                   T* __restrict__ Ap, const double* __restrict__ sc,
+                                                   int ib_num, int ib_den, ReduceSlot rs) {
+    const WaveGeom g = geom(a);
+    const T beta = (MODE == 2) ? (T)(sc[ib_num] / sc[ib_den]) : (T)0;
+    const T wr = a.wr, wf2 = a.wf * a.wf;
+    const long long N = a.dom.npix_mem();
+    T dot = 0;
+    if (g.y0 < g.y1) {
+        PRow<T> up = load_prow<T, MODE>(a, g.x, g.y0 - 1, pin, r, pre, beta);
+        PRow<T> cur = load_prow<T, MODE>(a, g.x, g.y0, pin, r, pre, beta);
+        PRow<T> dn = load_prow<T, MODE>(a, g.x, g.y0 + 1, pin, r, pre, beta);
+        finish_row(up);
+        finish_row(cur);
+        finish_row(dn);
+        // carries from the row above: J(up->cur) and J(cur->up) with its angle term
+        T in_up_x, in_up_y, my_x, my_y, thm, ax, ay;
+        jedge(up.px, up.py, up.pt, up.c, up.s, up.ux, up.uy, cur.px, cur.py, cur.ux, cur.uy,
+              up.act && cur.act, wr, in_up_x, in_up_y, ax, ay);
+        jedge(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, up.px, up.py, up.ux, up.uy,
+              up.act && cur.act, wr, my_x, my_y, ax, ay);
+        thm = -wr * (ax * my_x + ay * my_y);
+        for (int y = g.y0; y < g.y1; ++y) {
+            PRow<T> nx = load_prow<T, MODE>(a, g.x, y + 2, pin, r, pre, beta);
+            // horizontal neighbours (lane 0 / 63 are halo lanes: never written)
+            const T lpx = from_left(cur.px, (T)0), lpy = from_left(cur.py, (T)0);
+            const T rpx = from_right(cur.px, (T)0), rpy = from_right(cur.py, (T)0);
+            const float lux = from_left(cur.ux, 0.f), luy = from_left(cur.uy, 0.f);
+            const float rux = from_right(cur.ux, 0.f), ruy = from_right(cur.uy, 0.f);
+            const int lact = from_left_i(cur.act, 0), ract = from_right_i(cur.act, 0);
+            T jpx_x, jpx_y, apx_x, apx_y, jmx_x, jmx_y, amx_x, amx_y;
+            T jpy_x, jpy_y, apy_x, apy_y, jdn_x, jdn_y, adn_x, adn_y;
+            jedge(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, rpx, rpy, rux, ruy,
+                  cur.act && ract, wr, jpx_x, jpx_y, apx_x, apx_y);
+            jedge(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, lpx, lpy, lux, luy,
+                  cur.act && lact, wr, jmx_x, jmx_y, amx_x, amx_y);
+            jedge(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, dn.px, dn.py, dn.ux, dn.uy,
+                  cur.act && dn.act, wr, jpy_x, jpy_y, apy_x, apy_y);
+            jedge(dn.px, dn.py, dn.pt, dn.c, dn.s, dn.ux, dn.uy, cur.px, cur.py, cur.ux, cur.uy,
+                  cur.act && dn.act, wr, jdn_x, jdn_y, adn_x, adn_y);
+            // residuals of the lane neighbours pointing at this pixel
+            const T inpx_x = from_right(jmx_x, (T)0), inpx_y = from_right(jmx_y, (T)0);
+            const T inmx_x = from_left(jpx_x, (T)0), inmx_y = from_left(jpx_y, (T)0);
+            T aox = wr * ((jpx_x + jmx_x + jpy_x + my_x) - (inpx_x + inmx_x + jdn_x + in_up_x));
+            T aoy = wr * ((jpx_y + jmx_y + jpy_y + my_y) - (inpx_y + inmx_y + jdn_y + in_up_y));
+            if (cur.fit) { aox += wf2 * cur.px; aoy += wf2 * cur.py; }
+            T aot = thm - wr * ((apx_x * jpx_x + apx_y * jpx_y) + (amx_x * jmx_x + amx_y * jmx_y) +
+                                (apy_x * jpy_x + apy_y * jpy_y));
+            if (!cur.act) { aox = 0; aoy = 0; aot = 0; }
+            if (g.out_lane) {
+                const long long i = a.dom.off(g.x, y);
+                Ap[2 * i] = aox; Ap[2 * i + 1] = aoy; Ap[2 * N + i] = aot;
+                if (MODE != 0) { pout[2 * i] = cur.px; pout[2 * i + 1] = cur.py; pout[2 * N + i] = cur.pt; }
+                dot += cur.px * aox + cur.py * aoy + cur.pt * aot;
+            }
+            // roll the window
+            in_up_x = jpy_x; in_up_y = jpy_y;
+            my_x = jdn_x; my_y = jdn_y;
+            thm = -wr * (adn_x * jdn_x + adn_y * jdn_y);
+            up = cur; cur = dn; dn = nx;
+            finish_row(dn);
+        }
+    }
+    double v[1] = {(double)dot};
+    block_reduce_publish<1>(v, rs, blockIdx.x);
+}
+
+// ------------------------------------------------------------- value rows
+template <typename T>
+struct VRow {
+    T ox, oy, t, c, s;
+    float ux, uy, cx, cy;
+    int act, fit;
+};
+template <typename T>
+__device__ __forceinline__ VRow<T> load_vrow(const Args<T>& a, int x, int y) {
+    VRow<T> q;
+    const bool in = present(a.dom, x, y);
+    const long long i = in ? a.dom.off(x, y) : 0;
+    q.ox = in ? a.O[2 * i] : (T)0;
+    q.oy = in ? a.O[2 * i + 1] : (T)0;
+    q.t = in ? a.A[i] : (T)0;
+    const float2 u = reinterpret_cast<const float2*>(a.U)[i];
+    const float2 c = reinterpret_cast<const float2*>(a.C)[i];
+    const float m = a.M[i];
+    q.ux = in ? u.x : 0.f; q.uy = in ? u.y : 0.f;
+    q.cx = in ? c.x : -1.f; q.cy = in ? c.y : -1.f;
+    q.act = in && (m == 0.f);
+    q.fit = (q.cx >= 0.f) && (q.cy >= 0.f);
+    return q;
+}
+template <typename T>
+__device__ __forceinline__ void finish_vrow(VRow<T>& q) { sc_of(q.t, &q.c, &q.s); }
+
+// ------------------------------------------------------------- J^T F kernel
+// r = -J^T F, pre = 1/(1+sqrt(diag J^T J))^2 (1/(1+1)^2 when UsePreconditioner(false)),
+// flags, and sc[rs.out] = sum r.(pre r) over active pixels (alpha numerator).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T* __restrict__ pre,
+                                                 ReduceSlot rs) {
+    const WaveGeom g = geom(a);
+    const T wr = a.wr, wf = a.wf, wr2 = a.wr * a.wr;
+    const long long N = a.dom.npix_mem();
+    T dot = 0;
+    if (g.y0 < g.y1) {
+        VRow<T> up = load_vrow(a, g.x, g.y0 - 1), cur = load_vrow(a, g.x, g.y0),
+                dn = load_vrow(a, g.x, g.y0 + 1);
+        finish_vrow(up); finish_vrow(cur); finish_vrow(dn);
+        T inup_x, inup_y, my_x, my_y, ax, ay;
+        const bool vup = up.act && cur.act;
+        eedge(up.ox, up.oy, up.c, up.s, up.ux, up.uy, cur.ox, cur.oy, cur.ux, cur.uy, vup, wr,
+              inup_x, inup_y, ax, ay);
+        eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, up.ox, up.oy, up.ux, up.uy, vup, wr,
+              my_x, my_y, ax, ay);
+        T thm = -wr * (ax * my_x + ay * my_y);
+        T dthm = vup ? wr2 * (ax * ax + ay * ay) : (T)0;
+        int vmy = vup;
+        for (int y = g.y0; y < g.y1; ++y) {
+            VRow<T> nx = load_vrow(a, g.x, y + 2);
+            const T lox = from_left(cur.ox, (T)0), loy = from_left(cur.oy, (T)0);
+            const T rox = from_right(cur.ox, (T)0), roy = from_right(cur.oy, (T)0);
+            const float lux = from_left(cur.ux, 0.f), luy = from_left(cur.uy, 0.f);
+            const float rux = from_right(cur.ux, 0.f), ruy = from_right(cur.uy, 0.f);
+            const int lact = from_left_i(cur.act, 0), ract = from_right_i(cur.act, 0);
+            const bool vpx = cur.act && ract, vmx = cur.act && lact, vpy = cur.act && dn.act;
+            T epx_x, epx_y, apx_x, apx_y, emx_x, emx_y, amx_x, amx_y;
+            T epy_x, epy_y, apy_x, apy_y, edn_x, edn_y, adn_x, adn_y;
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, rox, roy, rux, ruy, vpx, wr, epx_x,
+                  epx_y, apx_x, apx_y);
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, lox, loy, lux, luy, vmx, wr, emx_x,
+                  emx_y, amx_x, amx_y);
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, dn.ox, dn.oy, dn.ux, dn.uy, vpy, wr,
+                  epy_x, epy_y, apy_x, apy_y);
+            eedge(dn.ox, dn.oy, dn.c, dn.s, dn.ux, dn.uy, cur.ox, cur.oy, cur.ux, cur.uy, vpy, wr,
+                  edn_x, edn_y, adn_x, adn_y);
+            const T inpx_x = from_right(emx_x, (T)0), inpx_y = from_right(emx_y, (T)0);
+            const T inmx_x = from_left(epx_x, (T)0), inmx_y = from_left(epx_y, (T)0);
+            T fx = wr * ((epx_x + emx_x + epy_x + my_x) - (inpx_x + inmx_x + edn_x + inup_x));
+            T fy = wr * ((epx_y + emx_y + epy_y + my_y) - (inpx_y + inmx_y + edn_y + inup_y));
+            T ft = thm - wr * ((apx_x * epx_x + apx_y * epx_y) + (amx_x * emx_x + amx_y * emx_y) +
+                               (apy_x * epy_x + apy_y * epy_y));
+            const int nv = (int)vpx + (int)vmx + (int)vpy + vmy;
+            T dO = wr2 * (T)(2 * nv);
+            T dt = dthm + (vpx ? wr2 * (apx_x * apx_x + apx_y * apx_y) : (T)0) +
+                   (vmx ? wr2 * (amx_x * amx_x + amx_y * amx_y) : (T)0) +
+                   (vpy ? wr2 * (apy_x * apy_x + apy_y * apy_y) : (T)0);
+            if (cur.fit) {
+                fx += wf * wf * (cur.ox - (T)cur.cx);
+                fy += wf * wf * (cur.oy - (T)cur.cy);
+                dO += wf * wf;
+            }
+            if (g.out_lane) {
+                const long long i = a.dom.off(g.x, y);
+                a.flags[i] = (uint8_t)(cur.act | (cur.fit << 1));
+                T rx = 0, ry = 0, rt = 0, wx = 0, wy = 0, wt = 0;
+                if (cur.act) {
+                    rx = -fx; ry = -fy; rt = -ft;
+                    if (a.use_pre) {
+                        const T sO = (T)1 + sqrt(dO), st = (T)1 + sqrt(dt);
+                        wx = wy = (T)1 / (sO * sO);
+                        wt = (T)1 / (st * st);
+                    } else {
+                        wx = wy = wt = (T)0.25;   // guardedInvert(1), PCGInit1 :543-550
+                    }
+                    dot += rx * (wx * rx) + ry * (wy * ry) + rt * (wt * rt);
+                }
+                r[2 * i] = rx; r[2 * i + 1] = ry; r[2 * N + i] = rt;
+                pre[2 * i] = wx; pre[2 * i + 1] = wy; pre[2 * N + i] = wt;
+            }
+            inup_x = epy_x; inup_y = epy_y;
+            my_x = edn_x; my_y = edn_y;
+            thm = -wr * (adn_x * edn_x + adn_y * edn_y);
+            dthm = vpy ? wr2 * (adn_x * adn_x + adn_y * adn_y) : (T)0;
+            vmy = vpy;
+            up = cur; cur = dn; dn = nx;
+            finish_vrow(dn);
+        }
+    }
+    double v[1] = {(double)dot};
+    block_reduce_publish<1>(v, rs, blockIdx.x);
+}
+
+// ----------------------------------------------------------------- cost kernel
+// sc[rs.out] = sum over active pixels of 1/2 (sum_s |e_reg(k,s)|^2 + |e_fit(k)|^2).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void iw_cost(Args<T> a, ReduceSlot rs) {
+    const WaveGeom g = geom(a);
+    const T wr = a.wr, wf = a.wf;
+    T acc = 0;
+    if (g.y0 < g.y1) {
+        VRow<T> up = load_vrow(a, g.x, g.y0 - 1), cur = load_vrow(a, g.x, g.y0),
+                dn = load_vrow(a, g.x, g.y0 + 1);
+        finish_vrow(cur);
+        for (int y = g.y0; y < g.y1; ++y) {
+            VRow<T> nx = load_vrow(a, g.x, y + 2);
+            const T lox = from_left(cur.ox, (T)0), loy = from_left(cur.oy, (T)0);
+            const T rox = from_right(cur.ox, (T)0), roy = from_right(cur.oy, (T)0);
+            const float lux = from_left(cur.ux, 0.f), luy = from_left(cur.uy, 0.f);
+            const float rux = from_right(cur.ux, 0.f), ruy = from_right(cur.uy, 0.f);
+            const int lact = from_left_i(cur.act, 0), ract = from_right_i(cur.act, 0);
+            T ex, ey, ax, ay, sum = 0;
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, rox, roy, rux, ruy,
+                  cur.act && ract, wr, ex, ey, ax, ay);
+            sum += ex * ex + ey * ey;
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, lox, loy, lux, luy,
+                  cur.act && lact, wr, ex, ey, ax, ay);
+            sum += ex * ex + ey * ey;
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, dn.ox, dn.oy, dn.ux, dn.uy,
+                  cur.act && dn.act, wr, ex, ey, ax, ay);
+            sum += ex * ex + ey * ey;
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, up.ox, up.oy, up.ux, up.uy,
+                  cur.act && up.act, wr, ex, ey, ax, ay);
+            sum += ex * ex + ey * ey;
+            if (cur.fit) {
+                const T fx = wf * (cur.ox - (T)cur.cx), fy = wf * (cur.oy - (T)cur.cy);
+                sum += fx * fx + fy * fy;
+            }
+            if (g.out_lane && cur.act) acc += (T)0.5 * sum;
+            up = cur; cur = dn; dn = nx;
+            finish_vrow(cur);
+        }
+    }
+    double v[1] = {(double)acc};
+    block_reduce_publish<1>(v, rs, blockIdx.x);
+}
+
+// --------------------------------------------------------------- flag kernel
+// Only for the standalone apply entry point: flags without a J^T F evaluation.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void iw_flags(Args<T> a) {
+    const long long n = (long long)a.dom.W * a.dom.mem_rows;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        const float2 c = reinterpret_cast<const float2*>(a.C)[i];
+        const int act = a.M[i] == 0.f, fit = (c.x >= 0.f) && (c.y >= 0.f);
+        a.flags[i] = (uint8_t)(act | (fit << 1));
+    }
+}
+
+// --------------------------------------------------------------- update kernel
+// X += delta on active pixels of the owned rows (PCGLinearUpdate, :854-859).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O, T* __restrict__ A,
+                                                    const T* __restrict__ delta) {
+    const long long N = a.dom.npix_mem();
+    const long long b = a.dom.off(0, a.dom.y_lo), e = a.dom.off(0, a.dom.y_hi);
+    for (long long i = b + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < e;
+         i += (long long)gridDim.x * blockDim.x) {
+        if (a.flags[i] & 1) {
+            const Vec2<T> o = reinterpret_cast<const Vec2<T>*>(O)[i];
+            const Vec2<T> d = reinterpret_cast<const Vec2<T>*>(delta)[i];
+            reinterpret_cast<Vec2<T>*>(O)[i] = Vec2<T>{o.x + d.x, o.y + d.y};
+            A[i] = A[i] + delta[2 * N + i];
+        }
+    }
+}
+
+}  // namespace iw
+
+// ====================================================================== plan
+template <typename T>
+class ImageWarpingPlan final : public Plan {
+public:
+    ImageWarpingPlan(const ProblemSpec& spec, const StateOptions& opts, unsigned W, unsigned H)
+        : Plan(spec, opts) {
+        dom_ = Domain{(int)W, (int)H, 0, (int)H, 0, (int)H};
+        // roles by declared index order (image_warping.t:12-27)
+        idx_O_ = spec.unknown(0)->index;
+        idx_A_ = spec.unknown(1)->index;
+        idx_U_ = spec.array(0)->index;
+        idx_C_ = spec.array(1)->index;
+        idx_M_ = spec.array(2)->index;
+        std::vector<DeclParam> ps = spec.params;
+        std::sort(ps.begin(), ps.end(), [](auto& x, auto& y) { return x.index < y.index; });
+        idx_wf_ = ps[0].index;
+        idx_wr_ = ps[1].index;
+        for (auto& p : ps) {   // names win over order when they are the canonical ones
+            if (p.name == "w_fitSqrt") idx_wf_ = p.index;
+            if (p.name == "w_regSqrt") idx_wr_ = p.index;
+        }
+        const long long N = dom_.npix_mem();
+        nvec_ = 3 * N;
+        for (T** v : {&r_, &pre_, &p0_, &p1_, &Ap_, &delta_})
+            *v = (T*)dmalloc(sizeof(T) * nvec_);
+        for (T* v : {r_, pre_, p0_, p1_, Ap_, delta_})
+            OPT_HIP_CHECK(hipMemset(v, 0, sizeof(T) * nvec_));
+        flags_ = (uint8_t*)dmalloc(N);
+        OPT_HIP_CHECK(hipMemset(flags_, 0, N));
+        rows_ = 16;
+        nstrips_ = (dom_.W + iw::kStrip - 1) / iw::kStrip;
+        nrowblocks_ = (dom_.y_hi - dom_.y_lo + rows_ * 4 - 1) / (rows_ * 4);
+        timer_.apply_name = apply_kernel_name();
+        red_.ensure(std::max(stencil_blocks(), 2048), 1, 64);
+        if (opts.host_buffers) {
+            hO_bytes_ = sizeof(T) * 2 * N;
+            dO_ = (T*)dmalloc(hO_bytes_);
+            dA_ = (T*)dmalloc(sizeof(T) * N);
+            dU_ = (float*)dmalloc(sizeof(float) * 2 * N);
+            dC_ = (float*)dmalloc(sizeof(float) * 2 * N);
+            dM_ = (float*)dmalloc(sizeof(float) * N);
+        }
+    }
+    ~ImageWarpingPlan() override {
+        OPT_HIP_CHECK(hipStreamSynchronize(stream_));
+        for (T* v : {r_, pre_, p0_, p1_, Ap_, delta_}) dfree(v);
+        dfree(flags_);
+        dfree(dO_); dfree(dA_); dfree(dU_); dfree(dC_); dfree(dM_);
+    }
+
+    long long unknown_count() const override { return nvec_; }
+    std::string family() const override { return "image_warping"; }
+    std::string apply_kernel_name() const override { return "iw_apply"; }
+
+    void init(void** params) override {
+        begin_call();
+        bind(params, true);
+        tbegin("iw_cost"); launch_cost(kScCost); tend();
+        prev_cost_ = read_scalar(kScCost);
+        n_iter_ = 0;
+        initialised_ = true;
+        end_call();
+        if (opts_.verbosity > 0) fprintf(stderr, "[opt_amd] init cost %.9g\n", prev_cost_);
+    }
+
+    int step(void** params) override {
+        if (!initialised_) init(params);
+        if (n_iter_ >= sp_.nIterations) {
+            if (opts_.kernel_timing && opts_.verbosity > 0) fprintf(stderr, "%s", timer_.report().c_str());
+            return 0;
+        }
+        begin_call();
+        bind(params, false);
+        const int L = std::max(0, sp_.lIterations);
+        red_.ensure(std::max(stencil_blocks(), 2048), 1, kScBase + 2 * (L + 2));
+        // PCGInit1: r, pre, flags, rz[0]
+        tbegin("iw_jtf"); launch_jtf(r_, pre_, rz(0)); tend();
+        T* pcur = p0_;
+        T* pprev = p1_;
+        for (int i = 0; i < L; ++i) {
+            std::swap(pcur, pprev);   // pcur <- new p, pprev <- old p
+            tbegin("iw_apply");
+            if (i == 0) launch_apply<1>(nullptr, pcur, pap(i), 0, 0);
+            else launch_apply<2>(pprev, pcur, pap(i), rz(i), rz(i - 1));
+            tend();
+            tbegin("pcg_step2");
+            launch_step2(pcur, i == 0, rz(i), pap(i), rz(i + 1));
+            tend();
+        }
+        // PCGLinearUpdate + cost
+        const int ub = flat_grid(dom_.npix_mem(), 1);
+        tbegin("iw_update");
+        hipLaunchKernelGGL(iw::iw_update<T>, dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_, cur_A_,
+                           (const T*)delta_);
+        OPT_HIP_CHECK(hipGetLastError());
+        tend();
+        tbegin("iw_cost"); launch_cost(kScCost); tend();
+        const double c = read_scalar(kScCost);
+        unbind_after_step();
+        end_call();
+        prev_cost_ = c;
+        ++n_iter_;
+        if (opts_.verbosity > 0) fprintf(stderr, "[opt_amd] GN iter %d cost %.9g\n", n_iter_, c);
+        return 1;
+    }
+
+    int eval_jtf(void** params, void* r, void* pre, double* rzv) override {
+        begin_call();
+        bind(params, false);
+        launch_jtf((T*)r, (T*)pre, kScTmp);
+        *rzv = read_scalar(kScTmp);
+        end_call();
+        return 0;
+    }
+    int apply_jtj(void** params, const void* p, void* Ap, double* pAp) override {
+        begin_call();
+        bind(params, false);
+        launch_flags();
+        launch_apply<0>((const T*)p, nullptr, kScTmp, 0, 0, (T*)Ap);
+        *pAp = read_scalar(kScTmp);
+        end_call();
+        return 0;
+    }
+    double eval_cost(void** params) override {
+        begin_call();
+        bind(params, false);
+        launch_cost(kScTmp);
+        double c = read_scalar(kScTmp);
+        end_call();
+        return c;
+    }
+    double time_apply(void** params, const void* p, void* Ap, int reps) override {
+        begin_call();
+        bind(params, false);
+        launch_flags();
+        hipEvent_t e0, e1;
+        OPT_HIP_CHECK(hipEventCreate(&e0));
+        OPT_HIP_CHECK(hipEventCreate(&e1));
+        launch_apply<0>((const T*)p, nullptr, kScTmp, 0, 0, (T*)Ap);   // warm
+        OPT_HIP_CHECK(hipEventRecord(e0, stream_));
+        for (int i = 0; i < reps; ++i) launch_apply<0>((const T*)p, nullptr, kScTmp, 0, 0, (T*)Ap);
+        OPT_HIP_CHECK(hipEventRecord(e1, stream_));
+        OPT_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        OPT_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        end_call();
+        return 1000.0 * ms / std::max(1, reps);
+    }
+
+private:
+    // scalar slots in red_.scalars
+    static constexpr int kScCost = 0, kScTmp = 1, kScBase = 4;
+    int rz(int i) const { return kScBase + 2 * i; }
+    int pap(int i) const { return kScBase + 2 * i + 1; }
+
+    int stencil_blocks() const { return nstrips_ * nrowblocks_; }
+
+    iw::Args<T> args() const {
+        iw::Args<T> a;
+        a.dom = dom_;
+        a.O = cur_O_; a.A = cur_A_; a.U = cur_U_; a.C = cur_C_; a.M = cur_M_;
+        a.flags = flags_;
+        a.wf = (T)wf_; a.wr = (T)wr_;
+        a.use_pre = spec_.use_preconditioner ? 1 : 0;
+        a.nstrips = nstrips_; a.nrowblocks = nrowblocks_; a.rows = rows_;
+        return a;
+    }
+
+    // Re-read the problemparams pointers (setGPUptr on every step, :2001) and the
+    // scalar parameters; stage host arrays for the CPU-backend ABI modes.
+    void bind(void** params, bool /*is_init*/) {
+        wf_ = *(const float*)params[idx_wf_];
+        wr_ = *(const float*)params[idx_wr_];
+        user_O_ = (T*)params[idx_O_];
+        user_A_ = (T*)params[idx_A_];
+        if (!opts_.host_buffers) {
+            cur_O_ = user_O_; cur_A_ = user_A_;
+            cur_U_ = (const float*)params[idx_U_];
+            cur_C_ = (const float*)params[idx_C_];
+            cur_M_ = (const float*)params[idx_M_];
+        } else {
+            const long long N = dom_.npix_mem();
+            OPT_HIP_CHECK(hipMemcpyAsync(dO_, user_O_, sizeof(T) * 2 * N, hipMemcpyHostToDevice, stream_));
+            OPT_HIP_CHECK(hipMemcpyAsync(dA_, user_A_, sizeof(T) * N, hipMemcpyHostToDevice, stream_));
+            OPT_HIP_CHECK(hipMemcpyAsync(dU_, params[idx_U_], sizeof(float) * 2 * N, hipMemcpyHostToDevice, stream_));
+            OPT_HIP_CHECK(hipMemcpyAsync(dC_, params[idx_C_], sizeof(float) * 2 * N, hipMemcpyHostToDevice, stream_));
+            OPT_HIP_CHECK(hipMemcpyAsync(dM_, params[idx_M_], sizeof(float) * N, hipMemcpyHostToDevice, stream_));
+            cur_O_ = dO_; cur_A_ = dA_; cur_U_ = dU_; cur_C_ = dC_; cur_M_ = dM_;
+        }
+    }
+    void unbind_after_step() {
+        if (!opts_.host_buffers) return;
+        const long long N = dom_.npix_mem();
+        OPT_HIP_CHECK(hipMemcpyAsync(user_O_, dO_, sizeof(T) * 2 * N, hipMemcpyDeviceToHost, stream_));
+        OPT_HIP_CHECK(hipMemcpyAsync(user_A_, dA_, sizeof(T) * N, hipMemcpyDeviceToHost, stream_));
+    }
+
+    double read_scalar(int idx) {
+        double v;
+        OPT_HIP_CHECK(hipMemcpyAsync(&v, red_.scalars + idx, sizeof(double), hipMemcpyDeviceToHost, stream_));
+        OPT_HIP_CHECK(hipStreamSynchronize(stream_));
+        return v;
+    }
+
+    void launch_jtf(T* r, T* pre, int sc_out) {
+        const int nb = stencil_blocks();
+        hipLaunchKernelGGL(iw::iw_jtf<T>, dim3(nb), dim3(kBlock), 0, stream_, args(), r, pre,
+                           red_.slot(nb, sc_out));
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    template <int MODE>
+    void launch_apply(const T* pin, T* pout, int sc_out, int ib_num, int ib_den, T* Ap = nullptr) {
+        const int nb = stencil_blocks();
+        hipLaunchKernelGGL((iw::iw_apply<T, MODE>), dim3(nb), dim3(kBlock), 0, stream_, args(), pin,
+                           (const T*)r_, (const T*)pre_, pout, Ap ? Ap : Ap_, red_.scalars, ib_num,
+                           ib_den, red_.slot(nb, sc_out));
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    void launch_step2(const T* p, bool first, int i_num, int i_den, int sc_out) {
+        const int nb = flat_grid(nvec_);
+        if (first)
+            hipLaunchKernelGGL((pcg_step2_kernel<T, true>), dim3(nb), dim3(kBlock), 0, stream_, nvec_, p,
+                               (const T*)Ap_, (const T*)pre_, r_, delta_, red_.scalars, i_num, i_den,
+                               spec_.use_preconditioner ? 1 : 0, red_.slot(nb, sc_out));
+        else
+            hipLaunchKernelGGL((pcg_step2_kernel<T, false>), dim3(nb), dim3(kBlock), 0, stream_, nvec_, p,
+                               (const T*)Ap_, (const T*)pre_, r_, delta_, red_.scalars, i_num, i_den,
+                               spec_.use_preconditioner ? 1 : 0, red_.slot(nb, sc_out));
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    void launch_cost(int sc_out) {
+        const int nb = stencil_blocks();
+        hipLaunchKernelGGL(iw::iw_cost<T>, dim3(nb), dim3(kBlock), 0, stream_, args(), red_.slot(nb, sc_out));
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    void launch_flags() {
+        hipLaunchKernelGGL(iw::iw_flags<T>, dim3(flat_grid(dom_.npix_mem(), 1)), dim3(kBlock), 0, stream_,
+                           args());
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+
+    Domain dom_;
+    int idx_O_, idx_A_, idx_U_, idx_C_, idx_M_, idx_wf_, idx_wr_;
+    long long nvec_ = 0;
+    T *r_ = nullptr, *pre_ = nullptr, *p0_ = nullptr, *p1_ = nullptr, *Ap_ = nullptr, *delta_ = nullptr;
+    uint8_t* flags_ = nullptr;
+    int rows_ = 16, nstrips_ = 0, nrowblocks_ = 0;
+    float wf_ = 0, wr_ = 0;
+    T *user_O_ = nullptr, *user_A_ = nullptr;
+    T *cur_O_ = nullptr, *cur_A_ = nullptr;
+    const float *cur_U_ = nullptr, *cur_C_ = nullptr, *cur_M_ = nullptr;
+    // host-buffer staging (backend_cpu*)
+    size_t hO_bytes_ = 0;
+    T *dO_ = nullptr, *dA_ = nullptr;
+    float *dU_ = nullptr, *dC_ = nullptr, *dM_ = nullptr;
+};
+
+std::unique_ptr<Plan> make_image_warping_plan(const ProblemSpec& spec, const StateOptions& opts,
+                                              const unsigned* dims, std::string* err) {
+    // Dim("W",0), Dim("H",1)
+    unsigned W = 0, H = 0;
+    for (auto& d : spec.dims) {
+        if (d.name == spec.unknown(0)->dims[0]) W = dims[d.index];
+        if (d.name == spec.unknown(0)->dims[1]) H = dims[d.index];
+    }
+    if (W == 0 || H == 0) { *err = "image_warping: zero-sized domain"; return nullptr; }
+    if (opts.double_precision)
+        return std::unique_ptr<Plan>(new ImageWarpingPlan<double>(spec, opts, W, H));
+    return std::unique_ptr<Plan>(new ImageWarpingPlan<float>(spec, opts, W, H));
+}
+
+}  // namespace optamd

@@ -1,0 +1,216 @@
+// opt_api.cpp — the Opt.h C ABI (reference API/release/include/Opt.h, implemented in
+// the reference by the trampolines of API/src/createwrapper.t:291-305 into
+// API/src/o.t:3301-3352) plus the opt_amd.h extension entry points.
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+#include "../../include/Opt.h"
+#include "../../include/opt_amd.h"
+#include "plan.h"
+#include "problem.h"
+
+static_assert(sizeof(Opt_InitializationParameters) == 44,
+              "Opt_InitializationParameters must keep the reference layout (Opt.h:10-35)");
+
+struct Opt_State {
+    optamd::StateOptions opts;
+    int device = 0;
+};
+struct Opt_Problem {
+    optamd::ProblemSpec spec;
+};
+struct Opt_Plan {
+    std::unique_ptr<optamd::Plan> impl;
+};
+
+namespace {
+bool valid_state(Opt_State* s, const char* fn) {
+    if (!s) { fprintf(stderr, "[opt_amd] %s: null Opt_State\n", fn); return false; }
+    return true;
+}
+bool valid_plan(Opt_Plan* p, const char* fn) {
+    if (!p || !p->impl) { fprintf(stderr, "[opt_amd] %s: null Opt_Plan\n", fn); return false; }
+    return true;
+}
+}  // namespace
+
+extern "C" {
+
+Opt_State* Opt_NewState(Opt_InitializationParameters params) {
+    auto* s = new Opt_State();
+    char backend[21];
+    memcpy(backend, params.backend, 20);
+    backend[20] = 0;
+    std::string b = backend;
+    if (b.empty()) b = "backend_cuda";
+    if (b != "backend_cuda" && b != "backend_cpu" && b != "backend_cpu_mt") {
+        fprintf(stderr, "[opt_amd] unknown backend '%s' (backend_cuda | backend_cpu | backend_cpu_mt)\n",
+                b.c_str());
+        delete s;
+        return nullptr;
+    }
+    s->opts.backend = b;
+    s->opts.host_buffers = (b != "backend_cuda");
+    s->opts.double_precision = params.doublePrecision != 0;
+    s->opts.verbosity = params.verbosityLevel;
+    s->opts.kernel_timing = params.collectPerKernelTimingInfo != 0;
+    return s;
+}
+
+Opt_Problem* Opt_ProblemDefine(Opt_State* state, const char* filename, const char* solverkind) {
+    if (!valid_state(state, "Opt_ProblemDefine")) return nullptr;
+    std::string kind = solverkind ? solverkind : "";
+    if (kind != "gaussNewtonGPU" && kind != "LMGPU" && kind != "gaussNewtonCPU") {
+        fprintf(stderr, "[opt_amd] unknown solver kind '%s' (gaussNewtonGPU | LMGPU | gaussNewtonCPU)\n",
+                kind.c_str());
+        return nullptr;
+    }
+    std::ifstream in(filename ? filename : "");
+    if (!in.good()) {
+        fprintf(stderr, "[opt_amd] cannot read energy file '%s'\n", filename ? filename : "(null)");
+        return nullptr;
+    }
+    std::stringstream ss;
+    ss << in.rdbuf();
+    auto* p = new Opt_Problem();
+    p->spec.filename = filename;
+    p->spec.solverkind = kind;
+    std::string err;
+    if (!optamd::parse_energy(ss.str(), &p->spec, &err) || !optamd::classify(&p->spec, &err)) {
+        fprintf(stderr, "[opt_amd] %s\n", err.c_str());
+        delete p;
+        return nullptr;
+    }
+    return p;
+}
+
+void Opt_ProblemDelete(Opt_State*, Opt_Problem* problem) { delete problem; }
+
+Opt_Plan* Opt_ProblemPlan(Opt_State* state, Opt_Problem* problem, unsigned int* dimensions) {
+    if (!valid_state(state, "Opt_ProblemPlan")) return nullptr;
+    if (!problem || !dimensions) {
+        fprintf(stderr, "[opt_amd] Opt_ProblemPlan: null problem or dimensions\n");
+        return nullptr;
+    }
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        fprintf(stderr, "[opt_amd] Opt_ProblemPlan: no HIP device (this runtime has no CPU compute path)\n");
+        return nullptr;
+    }
+    OPT_HIP_CHECK(hipGetDevice(&state->device));
+    std::string err;
+    auto impl = optamd::make_plan(problem->spec, state->opts, dimensions, &err);
+    if (!impl) {
+        fprintf(stderr, "[opt_amd] plan failed: %s\n", err.c_str());
+        return nullptr;
+    }
+    auto* p = new Opt_Plan();
+    p->impl = std::move(impl);
+    return p;
+}
+
+void Opt_PlanFree(Opt_State*, Opt_Plan* plan) { delete plan; }
+
+void Opt_SetSolverParameter(Opt_State* state, Opt_Plan* plan, const char* name, void* value) {
+    if (!valid_state(state, "Opt_SetSolverParameter") || !valid_plan(plan, "Opt_SetSolverParameter"))
+        return;
+    if (!name || !value) return;
+    plan->impl->set_solver_param(name, value);
+}
+
+void Opt_ProblemInit(Opt_State* state, Opt_Plan* plan, void** problemparams) {
+    if (!valid_state(state, "Opt_ProblemInit") || !valid_plan(plan, "Opt_ProblemInit")) exit(1);
+    plan->impl->init(problemparams);
+}
+
+int Opt_ProblemStep(Opt_State* state, Opt_Plan* plan, void** problemparams) {
+    if (!valid_state(state, "Opt_ProblemStep") || !valid_plan(plan, "Opt_ProblemStep")) exit(1);
+    return plan->impl->step(problemparams);
+}
+
+void Opt_ProblemSolve(Opt_State* state, Opt_Plan* plan, void** problemparams) {
+    Opt_ProblemInit(state, plan, problemparams);
+    while (Opt_ProblemStep(state, plan, problemparams)) {
+    }
+}
+
+double Opt_ProblemCurrentCost(Opt_State* state, Opt_Plan* plan) {
+    if (!valid_state(state, "Opt_ProblemCurrentCost") || !valid_plan(plan, "Opt_ProblemCurrentCost"))
+        return 0.0;
+    return plan->impl->cost();
+}
+
+// ------------------------------------------------------------------ extensions
+long long OptAMD_PlanUnknownCount(Opt_Plan* plan) {
+    return valid_plan(plan, "OptAMD_PlanUnknownCount") ? plan->impl->unknown_count() : -1;
+}
+static int copy_name(const std::string& s, char* buf, int n) {
+    if (buf && n > 0) {
+        strncpy(buf, s.c_str(), n - 1);
+        buf[n - 1] = 0;
+    }
+    return (int)s.size();
+}
+int OptAMD_PlanFamily(Opt_Plan* plan, char* buf, int n) {
+    return valid_plan(plan, "OptAMD_PlanFamily") ? copy_name(plan->impl->family(), buf, n) : -1;
+}
+int OptAMD_EvalJTF(Opt_State* state, Opt_Plan* plan, void** params, void* r, void* pre, double* rz) {
+    if (!valid_state(state, "OptAMD_EvalJTF") || !valid_plan(plan, "OptAMD_EvalJTF") || !r || !pre)
+        return 1;
+    double t;
+    int e = plan->impl->eval_jtf(params, r, pre, &t);
+    if (rz) *rz = t;
+    return e;
+}
+int OptAMD_ApplyJTJ(Opt_State* state, Opt_Plan* plan, void** params, const void* p, void* Ap,
+                    double* pAp) {
+    if (!valid_state(state, "OptAMD_ApplyJTJ") || !valid_plan(plan, "OptAMD_ApplyJTJ") || !p || !Ap)
+        return 1;
+    double t;
+    int e = plan->impl->apply_jtj(params, p, Ap, &t);
+    if (pAp) *pAp = t;
+    return e;
+}
+double OptAMD_EvalCost(Opt_State* state, Opt_Plan* plan, void** params) {
+    if (!valid_state(state, "OptAMD_EvalCost") || !valid_plan(plan, "OptAMD_EvalCost")) return -1.0;
+    return plan->impl->eval_cost(params);
+}
+double OptAMD_TimeApplyJTJ(Opt_State* state, Opt_Plan* plan, void** params, const void* p, void* Ap,
+                           int reps) {
+    if (!valid_state(state, "OptAMD_TimeApplyJTJ") || !valid_plan(plan, "OptAMD_TimeApplyJTJ"))
+        return -1.0;
+    return plan->impl->time_apply(params, p, Ap, reps);
+}
+void OptAMD_SetKernelTiming(Opt_Plan* plan, int mode) {
+    if (!valid_plan(plan, "OptAMD_SetKernelTiming")) return;
+    plan->impl->timer().reset();
+    plan->impl->timer().mode = mode;
+}
+int OptAMD_KernelStat(Opt_Plan* plan, const char* name, long long* n, double* ms) {
+    if (!valid_plan(plan, "OptAMD_KernelStat") || !name) return 1;
+    long long nn;
+    double mm;
+    bool ok = plan->impl->timer().stat(name, &nn, &mm);
+    if (n) *n = nn;
+    if (ms) *ms = mm;
+    return ok ? 0 : 1;
+}
+int OptAMD_ApplyKernelName(Opt_Plan* plan, char* buf, int n) {
+    return valid_plan(plan, "OptAMD_ApplyKernelName") ? copy_name(plan->impl->apply_kernel_name(), buf, n)
+                                                      : -1;
+}
+int OptAMD_KernelReport(Opt_Plan* plan, char* buf, int n) {
+    return valid_plan(plan, "OptAMD_KernelReport") ? copy_name(plan->impl->timer().report(), buf, n) : -1;
+}
+void* OptAMD_PlanStream(Opt_Plan* plan) {
+    return valid_plan(plan, "OptAMD_PlanStream") ? (void*)plan->impl->stream() : nullptr;
+}
+int OptAMD_PlanIterations(Opt_Plan* plan) {
+    return valid_plan(plan, "OptAMD_PlanIterations") ? plan->impl->iterations() : -1;
+}
+
+}  // extern "C"

@@ -1,0 +1,154 @@
+// plan.cpp — Plan base class, solver parameters, kernel timer, reduction scratch.
+#include "plan.h"
+#include <cstring>
+#include <sstream>
+#include <iomanip>
+
+namespace optamd {
+
+void* dmalloc(size_t bytes) {
+    void* p = nullptr;
+    if (bytes == 0) bytes = 16;
+    OPT_HIP_CHECK(hipMalloc(&p, bytes));
+    return p;
+}
+void dfree(void* p) {
+    if (p) OPT_HIP_CHECK(hipFree(p));
+}
+
+bool SolverParams::set(const char* name, const void* v) {
+#define F(x) if (!strcmp(name, #x)) { x = *(const float*)v; return true; }
+#define I(x) if (!strcmp(name, #x)) { x = *(const int*)v; return true; }
+    F(min_relative_decrease) F(min_trust_region_radius) F(max_trust_region_radius)
+    F(q_tolerance) F(function_tolerance) F(trust_region_radius) F(radius_decrease_factor)
+    F(min_lm_diagonal) F(max_lm_diagonal)
+    I(residual_reset_period) I(nIterations) I(lIterations)
+#undef F
+#undef I
+    return false;
+}
+
+// ---------------------------------------------------------------- KernelTimer
+hipEvent_t KernelTimer::get_event() {
+    if (!pool_.empty()) { hipEvent_t e = pool_.back(); pool_.pop_back(); return e; }
+    hipEvent_t e;
+    OPT_HIP_CHECK(hipEventCreate(&e));
+    return e;
+}
+void KernelTimer::begin(hipStream_t s, const char* name) {
+    if (mode == 0) return;
+    if (mode == 2 && apply_name != name) return;
+    open_ = name;
+    open_ev_ = get_event();
+    OPT_HIP_CHECK(hipEventRecord(open_ev_, s));
+}
+void KernelTimer::end(hipStream_t s) {
+    if (!open_) return;
+    hipEvent_t b = get_event();
+    OPT_HIP_CHECK(hipEventRecord(b, s));
+    pending_.push_back({open_, open_ev_, b});
+    open_ = nullptr;
+    if (pending_.size() > 4096) flush();
+}
+void KernelTimer::flush() {
+    for (auto& p : pending_) {
+        OPT_HIP_CHECK(hipEventSynchronize(p.b));
+        float ms = 0.f;
+        OPT_HIP_CHECK(hipEventElapsedTime(&ms, p.a, p.b));
+        auto& a = acc_[p.name];
+        a.first += 1;
+        a.second += ms;
+        pool_.push_back(p.a);
+        pool_.push_back(p.b);
+    }
+    pending_.clear();
+}
+void KernelTimer::reset() { flush(); acc_.clear(); }
+bool KernelTimer::stat(const std::string& name, long long* n, double* ms) {
+    flush();
+    auto it = acc_.find(name);
+    if (it == acc_.end()) { *n = 0; *ms = 0; return false; }
+    *n = it->second.first;
+    *ms = it->second.second;
+    return true;
+}
+std::string KernelTimer::report() {
+    flush();
+    std::ostringstream o;
+    o << "--------------------------------------------------------------\n";
+    o << std::left << std::setw(34) << "Kernel" << std::right << std::setw(8) << "Count"
+      << std::setw(12) << "Total(ms)" << std::setw(12) << "Avg(us)" << "\n";
+    double total = 0;
+    for (auto& kv : acc_) {
+        o << std::left << std::setw(34) << kv.first << std::right << std::setw(8)
+          << kv.second.first << std::setw(12) << std::fixed << std::setprecision(3)
+          << kv.second.second << std::setw(12) << std::setprecision(2)
+          << 1000.0 * kv.second.second / std::max(1LL, kv.second.first) << "\n";
+        total += kv.second.second;
+    }
+    o << "TIMING total " << std::setprecision(3) << total << " ms\n";
+    return o.str();
+}
+KernelTimer::~KernelTimer() {
+    for (auto& p : pending_) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    for (auto e : pool_) (void)hipEventDestroy(e);
+}
+
+// ------------------------------------------------------------- ReduceScratch
+void ReduceScratch::ensure(int mb, int kmax, int ns) {
+    if (mb * kmax > max_blocks * kMaxReduce || !partials) {
+        dfree(partials);
+        max_blocks = std::max(mb, max_blocks);
+        partials = (double*)dmalloc(sizeof(double) * (size_t)max_blocks * kMaxReduce);
+    }
+    if (!ticket) {
+        ticket = (unsigned*)dmalloc(64);
+        OPT_HIP_CHECK(hipMemset(ticket, 0, 64));
+    }
+    if (ns > n_scalars) {
+        double* s = (double*)dmalloc(sizeof(double) * ns);
+        OPT_HIP_CHECK(hipMemset(s, 0, sizeof(double) * ns));
+        dfree(scalars);
+        scalars = s;
+        n_scalars = ns;
+    }
+}
+ReduceScratch::~ReduceScratch() {
+    dfree(partials);
+    dfree(ticket);
+    dfree(scalars);
+}
+
+// ----------------------------------------------------------------------- Plan
+Plan::Plan(const ProblemSpec& spec, const StateOptions& opts) : spec_(spec), opts_(opts) {
+    OPT_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    timer_.mode = opts.kernel_timing ? 1 : 0;
+}
+
+void Plan::set_solver_param(const char* name, const void* value) {
+    if (!sp_.set(name, value))
+        fprintf(stderr, "Warning: tried to set nonexistent solver parameter %s\n", name);
+}
+
+void Plan::begin_call() {
+    // Order this plan's stream after everything the caller queued on the default
+    // stream (the reference runs all device work on the default stream).
+    hipEvent_t e;
+    OPT_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    OPT_HIP_CHECK(hipEventRecord(e, 0));
+    OPT_HIP_CHECK(hipStreamWaitEvent(stream_, e, 0));
+    OPT_HIP_CHECK(hipEventDestroy(e));
+}
+void Plan::end_call() {
+    OPT_HIP_CHECK(hipStreamSynchronize(stream_));
+    OPT_HIP_CHECK(hipGetLastError());
+}
+
+std::unique_ptr<Plan> make_plan(const ProblemSpec& spec, const StateOptions& opts,
+                                const unsigned* dims, std::string* err) {
+    if (spec.family == "image_warping") return make_image_warping_plan(spec, opts, dims, err);
+    *err = "energy family '" + spec.family + "' has no kernels in this build";
+    return nullptr;
+}
+
+}  // namespace optamd

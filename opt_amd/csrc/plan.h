@@ -1,0 +1,128 @@
+// plan.h — the solver plan interface behind Opt_Plan, the GN/LM solver parameters,
+// per-kernel timing, and the device scratch every family shares.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+#include "common.h"
+#include "problem.h"
+
+namespace optamd {
+
+// Runtime solver parameters with the reference defaults
+// (API/src/solverGPUGaussNewton.t:41-55, struct SolverParameters :186-201).
+struct SolverParams {
+    float min_relative_decrease = 1e-3f;
+    float min_trust_region_radius = 1e-32f;
+    float max_trust_region_radius = 1e16f;
+    float q_tolerance = 0.0001f;
+    float function_tolerance = 0.000001f;
+    float trust_region_radius = 1e4f;
+    float radius_decrease_factor = 2.0f;
+    float min_lm_diagonal = 1e-6f;
+    float max_lm_diagonal = 1e32f;
+    int residual_reset_period = 10;
+    int nIterations = 10;
+    int lIterations = 10;
+    // strcmp dispatch as setSolverParameter (solverGPUGaussNewton.t:2382-2398).
+    bool set(const char* name, const void* value);
+};
+
+struct StateOptions {
+    bool double_precision = false;
+    int verbosity = 0;
+    bool kernel_timing = false;
+    bool host_buffers = false;   // backend_cpu / backend_cpu_mt: params are host pointers
+    std::string backend = "backend_cuda";
+};
+
+// hipEvent-pair accounting per kernel name (reference Timer, backend_cuda.t:152-297).
+class KernelTimer {
+public:
+    int mode = 0;  // 0 off, 1 all kernels, 2 apply kernel only
+    std::string apply_name;
+    void begin(hipStream_t s, const char* name);
+    void end(hipStream_t s);
+    void flush();  // resolve recorded pairs (synchronises)
+    void reset();
+    bool stat(const std::string& name, long long* n, double* ms);
+    std::string report();
+    ~KernelTimer();
+private:
+    struct Pending { std::string name; hipEvent_t a, b; };
+    std::vector<Pending> pending_;
+    std::vector<hipEvent_t> pool_;
+    const char* open_ = nullptr;
+    hipEvent_t open_ev_ = nullptr;
+    std::map<std::string, std::pair<long long, double>> acc_;
+    hipEvent_t get_event();
+};
+
+// Device scratch for the deterministic reductions (common.h ReduceSlot).
+struct ReduceScratch {
+    double* partials = nullptr;
+    unsigned* ticket = nullptr;
+    double* scalars = nullptr;
+    int max_blocks = 0;
+    int n_scalars = 0;
+    void ensure(int max_blocks, int k_max, int n_scalars);
+    ReduceSlot slot(int nblocks, int scalar_index) const {
+        return ReduceSlot{partials, ticket, scalars + scalar_index, nblocks};
+    }
+    ~ReduceScratch();
+};
+
+class Plan {
+public:
+    virtual ~Plan() {}
+    virtual void init(void** params) = 0;
+    virtual int step(void** params) = 0;
+    virtual double cost() const { return prev_cost_; }
+    virtual long long unknown_count() const = 0;
+    virtual std::string family() const = 0;
+    virtual int eval_jtf(void** params, void* r, void* pre, double* rz) = 0;
+    virtual int apply_jtj(void** params, const void* p, void* Ap, double* pAp) = 0;
+    virtual double eval_cost(void** params) = 0;
+    virtual double time_apply(void** params, const void* p, void* Ap, int reps) = 0;
+    virtual std::string apply_kernel_name() const = 0;
+
+    void set_solver_param(const char* name, const void* value);
+    int iterations() const { return n_iter_; }
+    hipStream_t stream() const { return stream_; }
+    KernelTimer& timer() { return timer_; }
+
+protected:
+    Plan(const ProblemSpec& spec, const StateOptions& opts);
+    void begin_call();              // order after the caller's default-stream work
+    void end_call();                // wait for this plan's device work
+    // Launch bookkeeping: wraps a kernel launch with the timer when enabled.
+    void tbegin(const char* name) { if (timer_.mode) timer_.begin(stream_, name); }
+    void tend() { if (timer_.mode) timer_.end(stream_); }
+
+    ProblemSpec spec_;
+    StateOptions opts_;
+    SolverParams sp_;
+    hipStream_t stream_ = nullptr;
+    KernelTimer timer_;
+    ReduceScratch red_;
+    double prev_cost_ = 0.0;
+    int n_iter_ = 0;
+    bool initialised_ = false;
+};
+
+// Factory: lower a parsed problem to a plan for the given dims (nullptr + message on
+// failure, as problemPlan returns nil on compile errors, o.t:1352,1526).
+std::unique_ptr<Plan> make_plan(const ProblemSpec& spec, const StateOptions& opts,
+                                const unsigned* dims, std::string* err);
+
+// Per-family factories.
+std::unique_ptr<Plan> make_image_warping_plan(const ProblemSpec&, const StateOptions&,
+                                              const unsigned* dims, std::string* err);
+
+// Device-memory helpers (fail-stop).
+void* dmalloc(size_t bytes);
+void dfree(void* p);
+
+}  // namespace optamd

@@ -1,0 +1,65 @@
+"""Seeded synthetic inputs for the benchmark configurations.
+
+No datasets can be fetched, so every configuration is generated with the shapes and
+value distributions the reference's example harnesses build from their input files.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+
+def image_warping(W: int, H: int, seed: int = 1234, n_handles: int = 9, hole: bool = True,
+                  max_move: float = 0.05):
+    """image_warping inputs (examples/image_warping/src/CombinedSolver.h:166-223, main.cpp:163-177).
+
+    UrShape(x,y) = (x,y); Offset = UrShape; Angle = 1e-5; Mask = 0 except a seeded
+    elliptical hole (~5 % of the pixels, value 255); Constraints = (-1,-1) except the
+    image border pinned to itself and `n_handles` seeded handles moved by up to
+    max_move*W. Weights w_fit = 100, w_reg = 0.01 passed as square roots
+    (CombinedSolver.h:130-134).
+
+    Returns a dict of flat float32 arrays in the Opt layout (row-major, x fastest,
+    channels interleaved) plus the two weights.
+    """
+    rng = np.random.default_rng(seed)
+    ys, xs = np.mgrid[0:H, 0:W].astype(np.float32)
+    U = np.stack([xs, ys], axis=-1)
+    M = np.zeros((H, W), np.float32)
+    if hole:
+        cx, cy = rng.uniform(0.35, 0.65) * W, rng.uniform(0.35, 0.65) * H
+        ax, ay = 0.13 * W, 0.12 * H
+        M[((xs - cx) / ax) ** 2 + ((ys - cy) / ay) ** 2 <= 1.0] = 255.0
+    C = np.full((H, W, 2), -1.0, np.float32)
+    border = np.zeros((H, W), bool)
+    border[0, :] = border[-1, :] = border[:, 0] = border[:, -1] = True
+    pin = border & (M == 0)
+    C[pin] = U[pin]
+    placed = 0
+    tries = 0
+    while placed < n_handles and tries < 100 * max(1, n_handles):
+        tries += 1
+        hx = int(rng.uniform(0.1, 0.9) * W)
+        hy = int(rng.uniform(0.1, 0.9) * H)
+        if M[hy, hx] != 0 or border[hy, hx]:
+            continue
+        tx = hx + rng.uniform(-max_move, max_move) * W
+        ty = hy + rng.uniform(-max_move, max_move) * H
+        C[hy, hx] = (max(tx, 0.0), max(ty, 0.0))
+        placed += 1
+    A = np.full((H, W), 1e-5, np.float32)
+    return {
+        "Offset": U.reshape(-1).copy(),
+        "Angle": A.reshape(-1),
+        "UrShape": U.reshape(-1).copy(),
+        "Constraints": C.reshape(-1),
+        "Mask": M.reshape(-1),
+        "w_fitSqrt": float(math.sqrt(100.0)),
+        "w_regSqrt": float(math.sqrt(0.01)),
+        "W": W,
+        "H": H,
+    }
+
+
+IMAGE_WARPING_ORDER = ["Offset", "Angle", "UrShape", "Constraints", "Mask", "w_fitSqrt", "w_regSqrt"]

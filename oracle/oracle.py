@@ -1,0 +1,89 @@
+"""ctypes binding of oracle/build/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+(the checker and the timed CPU baseline). Parity status: unpinned (oracle/README.md).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+_F = ctypes.POINTER(ctypes.c_float)
+_D = ctypes.POINTER(ctypes.c_double)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-C", _HERE], check=True, capture_output=True)
+    lib = ctypes.CDLL(LIB)
+    i, f, d = ctypes.c_int, ctypes.c_float, ctypes.c_double
+    lib.oracle_iw_cost.restype = d
+    lib.oracle_iw_cost.argtypes = [i, i, _F, _F, _F, _F, _F, f, f, i]
+    lib.oracle_iw_eval_jtf.restype = d
+    lib.oracle_iw_eval_jtf.argtypes = [i, i, _F, _F, _F, _F, _F, f, f, _F, _F, i]
+    lib.oracle_iw_apply_jtj.restype = d
+    lib.oracle_iw_apply_jtj.argtypes = [i, i, _F, _F, _F, _F, _F, f, f, _F, _F, i]
+    lib.oracle_iw_solve.restype = None
+    lib.oracle_iw_solve.argtypes = [i, i, _F, _F, _F, _F, _F, f, f, i, i, i, _D, _D]
+    lib.oracle_iw_residuals.restype = None
+    lib.oracle_iw_residuals.argtypes = [i, i, _F, _F, _F, _F, _F, f, f, _F]
+    _lib = lib
+    return lib
+
+
+def _f(a):
+    assert a.dtype == np.float32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_F)
+
+
+def _args(w):
+    return (w["W"], w["H"], _f(w["Offset"]), _f(w["Angle"]), _f(w["UrShape"]), _f(w["Constraints"]),
+            _f(w["Mask"]), w["w_fitSqrt"], w["w_regSqrt"])
+
+
+def iw_cost(w, nthreads=1):
+    return load().oracle_iw_cost(*_args(w), nthreads)
+
+
+def iw_eval_jtf(w, nthreads=1):
+    n = 3 * w["W"] * w["H"]
+    r = np.zeros(n, np.float32)
+    pre = np.zeros(n, np.float32)
+    rz = load().oracle_iw_eval_jtf(*_args(w), _f(r), _f(pre), nthreads)
+    return r, pre, rz
+
+
+def iw_apply_jtj(w, p, nthreads=1):
+    p = np.ascontiguousarray(p, np.float32)
+    Ap = np.zeros_like(p)
+    pAp = load().oracle_iw_apply_jtj(*_args(w), _f(p), _f(Ap), nthreads)
+    return Ap, pAp
+
+
+def iw_residuals(w):
+    """All residuals, 10 per pixel: for s in (+x,-x,+y,-y): (c=0,c=1), then fit (c=0,c=1)."""
+    res = np.zeros(10 * w["W"] * w["H"], np.float32)
+    load().oracle_iw_residuals(*_args(w), _f(res))
+    return res
+
+
+def iw_solve(w, n_iter, l_iter, nthreads=1, want_scalars=False):
+    """Full GN solve; returns (Offset, Angle, costs[n_iter+1], scalars|None)."""
+    O = w["Offset"].copy()
+    A = w["Angle"].copy()
+    costs = np.zeros(n_iter + 1, np.float64)
+    sc = np.zeros(max(1, 3 * n_iter * l_iter), np.float64) if want_scalars else None
+    load().oracle_iw_solve(w["W"], w["H"], _f(O), _f(A), _f(w["UrShape"]), _f(w["Constraints"]),
+                           _f(w["Mask"]), w["w_fitSqrt"], w["w_regSqrt"], n_iter, l_iter, nthreads,
+                           costs.ctypes.data_as(_D), sc.ctypes.data_as(_D) if sc is not None else None)
+    return O, A, costs, (sc.reshape(n_iter, l_iter, 3) if sc is not None else None)

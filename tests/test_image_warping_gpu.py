@@ -1,0 +1,166 @@
+"""GPU parity of the image_warping hot path (through the C ABI) against the C oracle.
+
+Tolerances (float32 path; the reference computes in opt_float = float, config.t:3-5):
+per-unknown kernel outputs (J^T F, pre, J^T J p) within 2e-5 of the largest
+magnitude (different but equally valid summation orders, sincosf vs cosf/sinf ULPs);
+scalar reductions within 1e-5 relative; GN energies within 1e-5 relative (the
+north_star bar). Integer/flag work is exact by construction.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from tests.iw_helpers import device_params, host_params, perturbed, rel_err, solver
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [(37, 29), (62, 5), (63, 64), (130, 70), (250, 131), (5, 3), (1, 9), (200, 1)]
+
+
+def to_np(t):
+    return t.detach().cpu().numpy()
+
+
+@pytest.mark.parametrize("W,H", SIZES)
+def test_cost_jtf_apply_match_oracle(W, H):
+    import torch
+
+    w = perturbed(W, H, seed=W * 7 + H)
+    s = solver(W, H)
+    prm = device_params(w)
+    n = 3 * W * H
+    assert s.unknown_count() == n
+    assert s.family() == "image_warping"
+    # cost
+    c_gpu = s.eval_cost(prm)
+    c_ref = oracle.iw_cost(w)
+    assert c_gpu == pytest.approx(c_ref, rel=1e-5, abs=1e-12)
+    # J^T F and preconditioner
+    r = torch.zeros(n, device="cuda")
+    pre = torch.zeros(n, device="cuda")
+    rz = s.eval_jtf(prm, r, pre)
+    r_ref, pre_ref, rz_ref = oracle.iw_eval_jtf(w)
+    assert rel_err(to_np(r), r_ref) < 2e-5
+    assert rel_err(to_np(pre), pre_ref) < 2e-5
+    assert rz == pytest.approx(rz_ref, rel=1e-5, abs=1e-20)
+    # J^T J p
+    rng = np.random.default_rng(1)
+    p = rng.normal(size=n).astype(np.float32)
+    Ap = torch.zeros(n, device="cuda")
+    pAp = s.apply_jtj(prm, torch.from_numpy(p).cuda(), Ap)
+    Ap_ref, pAp_ref = oracle.iw_apply_jtj(w, p)
+    assert rel_err(to_np(Ap), Ap_ref) < 2e-5
+    assert pAp == pytest.approx(pAp_ref, rel=1e-5, abs=1e-20)
+
+
+@pytest.mark.parametrize("W,H,nit,lit", [(37, 29, 4, 10), (130, 70, 3, 10), (250, 131, 2, 20), (64, 64, 6, 5)])
+def test_gn_solve_matches_oracle(W, H, nit, lit):
+    w = perturbed(W, H, seed=17 + W)
+    s = solver(W, H)
+    prm = device_params(w)
+    s.set_solver_params({"nIterations": nit, "lIterations": lit})
+    costs = s.profiled_solve(prm)
+    O_ref, A_ref, c_ref, _ = oracle.iw_solve(w, nit, lit)
+    assert len(costs) == nit + 1
+    np.testing.assert_allclose(costs, c_ref, rtol=1e-5)
+    assert costs[-1] < costs[0]
+    assert rel_err(to_np(prm[0]), O_ref) < 1e-5
+    assert np.abs(to_np(prm[1]) - A_ref).max() < 1e-4 * max(1.0, np.abs(A_ref).max())
+    assert s.iterations() == nit
+
+
+def test_solve_is_bitwise_deterministic():
+    W, H = 300, 200
+    w = perturbed(W, H, seed=99)
+    outs = []
+    for _ in range(2):
+        s = solver(W, H)
+        prm = device_params(w)
+        s.set_solver_params({"nIterations": 3, "lIterations": 10})
+        c = s.solve(prm)
+        outs.append((c, to_np(prm[0]).copy(), to_np(prm[1]).copy()))
+    assert outs[0][0] == outs[1][0]
+    assert np.array_equal(outs[0][1], outs[1][1]) and np.array_equal(outs[0][2], outs[1][2])
+
+
+@pytest.mark.parametrize("backend", ["backend_cpu", "backend_cpu_mt"])
+def test_host_buffer_backends_equal_device_path(backend):
+    W, H = 97, 61
+    w = perturbed(W, H, seed=4)
+    sd = solver(W, H)
+    pd = device_params(w)
+    sd.set_solver_params({"nIterations": 2, "lIterations": 8})
+    cd = sd.solve(pd)
+    sh = solver(W, H, backend=backend)
+    ph = host_params(w)
+    sh.set_solver_params({"nIterations": 2, "lIterations": 8})
+    ch = sh.solve(ph)
+    assert ch == cd
+    assert np.array_equal(ph[0], to_np(pd[0])) and np.array_equal(ph[1], to_np(pd[1]))
+
+
+def test_double_precision_path():
+    import torch
+
+    W, H = 90, 70
+    w = perturbed(W, H, seed=8)
+    s = solver(W, H, double=True)
+    prm = device_params(w, double=True)
+    n = 3 * W * H
+    r = torch.zeros(n, device="cuda", dtype=torch.float64)
+    pre = torch.zeros(n, device="cuda", dtype=torch.float64)
+    s.eval_jtf(prm, r, pre)
+    r_ref, pre_ref, _ = oracle.iw_eval_jtf(w)
+    assert rel_err(to_np(r), r_ref) < 1e-4   # oracle is float32: its own error dominates
+    p = torch.randn(n, device="cuda", dtype=torch.float64)
+    Ap = torch.zeros_like(p)
+    s.apply_jtj(prm, p, Ap)
+    Ap_ref, _ = oracle.iw_apply_jtj(w, to_np(p).astype(np.float32))
+    assert rel_err(to_np(Ap), Ap_ref) < 1e-4
+    s.set_solver_params({"nIterations": 3, "lIterations": 10})
+    costs = s.profiled_solve(prm)
+    _, _, c_ref, _ = oracle.iw_solve(w, 3, 10)
+    np.testing.assert_allclose(costs, c_ref, rtol=1e-4)
+
+
+def test_fully_masked_image_is_a_no_op():
+    W, H = 70, 40
+    w = perturbed(W, H, seed=2)
+    w["Mask"][:] = 255.0
+    s = solver(W, H)
+    prm = device_params(w)
+    O0, A0 = to_np(prm[0]).copy(), to_np(prm[1]).copy()
+    s.set_solver_params({"nIterations": 2, "lIterations": 3})
+    assert s.solve(prm) == 0.0
+    assert np.array_equal(to_np(prm[0]), O0) and np.array_equal(to_np(prm[1]), A0)
+
+
+@pytest.mark.parametrize("W,H", [(2048, 2048), (4096, 4096)])
+def test_full_size_properties(W, H):
+    """Size-independent properties at the BASELINE sizes: J^T J symmetric, PSD,
+    linear; cost equals the oracle's; one GN step lowers the energy."""
+    import torch
+
+    w = perturbed(W, H, seed=1, angle_sigma=0.01, offset_sigma=0.1)
+    s = solver(W, H)
+    prm = device_params(w)
+    n = 3 * W * H
+    g = torch.Generator(device="cuda").manual_seed(0)
+    p = torch.randn(n, device="cuda", generator=g)
+    q = torch.randn(n, device="cuda", generator=g)
+    Ap, Aq, Apq = (torch.zeros(n, device="cuda") for _ in range(3))
+    pAp = s.apply_jtj(prm, p, Ap)
+    s.apply_jtj(prm, q, Aq)
+    s.apply_jtj(prm, p + q, Apq)
+    act = torch.from_numpy(np.concatenate([np.repeat(w["Mask"] == 0, 2), w["Mask"] == 0])).cuda()
+    pm, qm = p * act, q * act
+    assert pAp > 0
+    qAp = float(torch.dot(qm.double(), Ap.double()))
+    pAq = float(torch.dot(pm.double(), Aq.double()))
+    assert qAp == pytest.approx(pAq, rel=1e-5)
+    lin = float((Apq - Ap - Aq).abs().max()) / float(Apq.abs().max())
+    assert lin < 1e-5
+    assert s.eval_cost(prm) == pytest.approx(oracle.iw_cost(w, nthreads=8), rel=1e-5)
+    s.set_solver_params({"nIterations": 1, "lIterations": 10})
+    costs = s.profiled_solve(prm)
+    assert costs[1] < costs[0]

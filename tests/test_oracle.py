@@ -1,0 +1,133 @@
+"""CPU: pin the C oracle to the energy definition (parity unpinned otherwise).
+
+The reference has no executable path and no golden vectors for this energy
+(oracle/README.md), so the oracle is checked against an independent float64 numpy
+restatement of examples/image_warping/image_warping.t and a finite-difference
+Jacobian of it: cost = 1/2|r|^2, r_oracle = -J^T F, pre = 1/(1+sqrt(diag J^T J))^2,
+Ap = J^T J p, plus symmetry / positive semi-definiteness and GN descent.
+"""
+import numpy as np
+import pytest
+
+from opt_amd import workloads
+from oracle import oracle
+
+DIRS = [(1, 0), (-1, 0), (0, 1), (0, -1)]
+
+
+def residuals64(w, O, A):
+    """image_warping.t, restated independently in float64 (10 residuals per pixel)."""
+    W, H = w["W"], w["H"]
+    U = w["UrShape"].reshape(H, W, 2).astype(np.float64)
+    C = w["Constraints"].reshape(H, W, 2).astype(np.float64)
+    M = w["Mask"].reshape(H, W)
+    O = O.reshape(H, W, 2)
+    A = A.reshape(H, W)
+    act = M == 0
+    res = np.zeros((H, W, 10))
+    wf, wr = float(np.float32(w["w_fitSqrt"])), float(np.float32(w["w_regSqrt"]))
+    for y in range(H):
+        for x in range(W):
+            if not act[y, x]:
+                continue
+            c, s = np.cos(A[y, x]), np.sin(A[y, x])
+            for k, (sx, sy) in enumerate(DIRS):
+                tx, ty = x + sx, y + sy
+                if not (0 <= tx < W and 0 <= ty < H) or not act[ty, tx]:
+                    continue
+                d = U[y, x] - U[ty, tx]
+                rot = np.array([c * d[0] - s * d[1], s * d[0] + c * d[1]])
+                res[y, x, 2 * k:2 * k + 2] = wr * ((O[y, x] - O[ty, tx]) - rot)
+            if C[y, x, 0] >= 0 and C[y, x, 1] >= 0:
+                res[y, x, 8:10] = wf * (O[y, x] - C[y, x])
+    return res.reshape(-1)
+
+
+def small_problem(W=7, H=6, seed=3):
+    rng = np.random.default_rng(seed)
+    w = workloads.image_warping(W, H, seed=seed, n_handles=2, hole=False)
+    M = w["Mask"].reshape(H, W)
+    M[2, 3] = 255.0  # a hole
+    M[4, 1] = 255.0
+    w["Offset"] = (w["Offset"] + rng.normal(0, 0.3, w["Offset"].shape)).astype(np.float32)
+    w["Angle"] = rng.normal(0, 0.4, w["Angle"].shape).astype(np.float32)
+    w["UrShape"] = (w["UrShape"] + rng.normal(0, 0.1, w["UrShape"].shape)).astype(np.float32)
+    C = w["Constraints"].reshape(H, W, 2)
+    C[3, 3] = (3.5, 2.2)  # an interior handle
+    return w
+
+
+def unknown_vec(w):
+    N = w["W"] * w["H"]
+    return np.concatenate([w["Offset"].astype(np.float64), w["Angle"].astype(np.float64)]), N
+
+
+def jacobian64(w):
+    x0, N = unknown_vec(w)
+    n = x0.size
+    r0 = residuals64(w, x0[:2 * N], x0[2 * N:])
+    J = np.zeros((r0.size, n))
+    h = 1e-6
+    for j in range(n):
+        xp, xm = x0.copy(), x0.copy()
+        xp[j] += h
+        xm[j] -= h
+        J[:, j] = (residuals64(w, xp[:2 * N], xp[2 * N:]) - residuals64(w, xm[:2 * N], xm[2 * N:])) / (2 * h)
+    return J, r0
+
+
+def active_unknowns(w):
+    N = w["W"] * w["H"]
+    act = w["Mask"] == 0
+    return np.concatenate([np.repeat(act, 2), act])
+
+
+def test_residuals_and_cost():
+    w = small_problem()
+    x0, N = unknown_vec(w)
+    r64 = residuals64(w, x0[:2 * N], x0[2 * N:])
+    r32 = oracle.iw_residuals(w)
+    np.testing.assert_allclose(r32, r64, rtol=1e-5, atol=2e-5)
+    c = oracle.iw_cost(w)
+    assert c == pytest.approx(0.5 * np.sum(r64 ** 2), rel=1e-5)
+
+
+def test_jtf_and_preconditioner_match_fd_jacobian():
+    w = small_problem()
+    J, r0 = jacobian64(w)
+    act = active_unknowns(w)
+    g = J.T @ r0
+    diag = np.sum(J * J, axis=0)
+    r, pre, rz = oracle.iw_eval_jtf(w)
+    scale = np.abs(g).max()
+    np.testing.assert_allclose(r[act], -g[act], atol=2e-5 * scale)
+    assert np.all(r[~act] == 0) and np.all(pre[~act] == 0)
+    np.testing.assert_allclose(pre[act], 1.0 / (1.0 + np.sqrt(diag[act])) ** 2, rtol=2e-4)
+    assert rz == pytest.approx(float(np.sum(r * pre * r)), rel=1e-5)
+
+
+def test_apply_matches_fd_jacobian_and_is_spd():
+    w = small_problem()
+    J, _ = jacobian64(w)
+    act = active_unknowns(w)
+    rng = np.random.default_rng(7)
+    p = rng.normal(size=J.shape[1]).astype(np.float32)
+    q = rng.normal(size=J.shape[1]).astype(np.float32)
+    p[~act] = 0
+    q[~act] = 0
+    Ap, pAp = oracle.iw_apply_jtj(w, p)
+    Aq, _ = oracle.iw_apply_jtj(w, q)
+    ref = J.T @ (J @ p.astype(np.float64))
+    np.testing.assert_allclose(Ap[act], ref[act], atol=2e-4 * np.abs(ref).max())
+    assert np.all(Ap[~act] == 0)
+    assert pAp == pytest.approx(float(p.astype(np.float64) @ ref), rel=1e-4)
+    assert pAp > 0
+    assert float(q @ Ap) == pytest.approx(float(p @ Aq), rel=1e-4)
+
+
+def test_gn_solve_decreases_cost_and_threads_agree():
+    w = workloads.image_warping(40, 30, seed=11, n_handles=5)
+    _, _, c1, _ = oracle.iw_solve(w, 3, 10, nthreads=1)
+    O4, A4, c4, _ = oracle.iw_solve(w, 3, 10, nthreads=4)
+    assert c1[0] > c1[1] > c1[2] > c1[3]
+    np.testing.assert_allclose(c4, c1, rtol=1e-6)
