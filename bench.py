@@ -28,11 +28,17 @@ import torch  # noqa: E402
 
 METRIC = "PCG JᵀJ·p throughput (unknowns/s) + GN iters/s, image_warping 4096² fp32"
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# Compulsory bytes of one J^T J p apply, per pixel: p read 12 + Angle 4
-# + UrShape 8 + flag byte 1 + Ap write 12 (the fused in-loop form also reads r, pre,
-# p_old and writes p: +24, reported separately).
-APPLY_BYTES_PER_PX = 37
-FUSED_APPLY_BYTES_PER_PX = 12 + 12 + 12 + 4 + 8 + 1 + 12 + 12  # r, pre, p_old, A, U, flag, p, Ap
+# Compulsory HBM bytes per pixel of the in-loop apply kernel iw_apply:
+# always Angle 4 + UrShape 8 + flag 1 + r 12 + pre 12 read, p 12 + Ap 12 written;
+# from PCG iteration 1 on also p_old 12 read and delta 12 written; from iteration 2 on
+# also delta 12 read.
+def apply_bytes_per_px(i: int) -> int:
+    b = 4 + 8 + 1 + 12 + 12 + 12 + 12
+    if i >= 1:
+        b += 12 + 12
+    if i >= 2:
+        b += 12
+    return b
 
 
 def parse():
@@ -124,8 +130,8 @@ def main():
     s.set_kernel_timing(0)
     avg_apply_s = (apply_ms / 1e3) / max(1, n_apply)
     npx = W * H
-    fused_bytes = FUSED_APPLY_BYTES_PER_PX * npx
-    achieved = fused_bytes / avg_apply_s / 1e9
+    bpp = sum(apply_bytes_per_px(i) for i in range(args.liter)) / args.liter
+    achieved = bpp * npx / avg_apply_s / 1e9
     # the pure apply (reads p) timed separately for the kernel-only unknowns/s
     p = torch.randn(n_unknowns, device="cuda")
     Ap = torch.empty_like(p)
@@ -162,7 +168,7 @@ def main():
             "traffic": None,
             "avg_us": avg_apply_s * 1e6,
             "launches": n_apply,
-            "bytes_per_px": FUSED_APPLY_BYTES_PER_PX,
+            "bytes_per_px": bpp,
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -81,10 +81,13 @@ __device__ __forceinline__ double from_right(double v, double e) {
 // (MI355X_MICROARCH.md "Valid forms", row 1; cdna_hip_programming.md G16).
 struct ReduceSlot {
     double* partials;     // [K][nblocks]
-    unsigned* ticket;     // one counter, zero between launches
+    unsigned* ticket;     // kTicketShards shard counters + 1 top counter, 64 B apart, zero between launches
     double* out;          // K results
     int nblocks;
 };
+constexpr int kTicketShards = 8;      // one arrival counter per XCD group (b % 8)
+constexpr int kTicketStride = 16;     // unsigned words between counters (64 B)
+constexpr int kTicketWords = (kTicketShards + 1) * kTicketStride;
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -94,6 +97,10 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 // Called by every thread of a kBlock-thread block exactly once, after all the
 // block's stores of the kernel's outputs. v[k] is this thread's contribution.
+// Arrivals are counted per XCD group (shard = block % 8, ~nblocks/8 adds per counter
+// instead of nblocks on one word: a single hot counter costs ~12 ns per add,
+// MI355X_MICROARCH.md row "fanin"); the last arriver of each shard then adds to a
+// top counter, and the last of those sums every partial in block order.
 template <int K>
 __device__ __forceinline__ void block_reduce_publish(const double (&v)[K], const ReduceSlot& rs,
                                                      int block_linear) {
@@ -117,9 +124,22 @@ __device__ __forceinline__ void block_reduce_publish(const double (&v)[K], const
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        unsigned t = __hip_atomic_fetch_add(rs.ticket, 1u, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-        last_flag = (t == (unsigned)(rs.nblocks - 1));
+        const int shard = block_linear % kTicketShards;
+        const int shards = rs.nblocks < kTicketShards ? rs.nblocks : kTicketShards;
+        const unsigned in_shard = (unsigned)((rs.nblocks - shard + kTicketShards - 1) / kTicketShards);
+        unsigned* sc = rs.ticket + shard * kTicketStride;
+        const unsigned t = __hip_atomic_fetch_add(sc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int last = 0;
+        if (t == in_shard - 1) {
+            __hip_atomic_store(sc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unsigned* top = rs.ticket + kTicketShards * kTicketStride;
+            const unsigned t2 = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (t2 == (unsigned)(shards - 1)) {
+                __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                last = 1;
+            }
+        }
+        last_flag = last;
     }
     __syncthreads();
     if (!last_flag) return;
@@ -137,10 +157,10 @@ __device__ __forceinline__ void block_reduce_publish(const double (&v)[K], const
             if (threadIdx.x < stride) acc[threadIdx.x] += acc[threadIdx.x + stride];
             __syncthreads();
         }
-        if (threadIdx.x == 0) rs.out[k] = acc[0];
+        if (threadIdx.x == 0)
+            __hip_atomic_store(&rs.out[k], acc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
     }
-    if (threadIdx.x == 0) *rs.ticket = 0u;
 }
 
 // XCD-aware bijective remap of a linear block id (cdna_hip_programming.md §5.5 T1):

@@ -39,7 +39,7 @@
 namespace optamd {
 namespace iw {
 
-constexpr int kStrip = 62;   // output columns per wavefront
+constexpr int kStrip = 64;   // columns per wavefront strip (aligned: x = 64*strip + lane)
 
 template <typename T>
 struct Args {
@@ -60,8 +60,8 @@ __device__ __forceinline__ void sc_of(float t, float* c, float* s) { sincosf(t, 
 __device__ __forceinline__ void sc_of(double t, double* c, double* s) { sincos(t, s, c); }
 
 struct WaveGeom {
-    int x, lane, y0, y1;
-    bool out_lane;
+    int x, ex, lane, y0, y1;
+    bool out_lane, edge_lane;
 };
 template <typename T>
 __device__ __forceinline__ WaveGeom geom(const Args<T>& a) {
@@ -71,10 +71,13 @@ __device__ __forceinline__ WaveGeom geom(const Args<T>& a) {
     const int strip = t % a.nstrips, rb = t / a.nstrips;
     g.lane = threadIdx.x & (kWave - 1);
     const int w = threadIdx.x / kWave;
-    g.x = strip * kStrip - 1 + g.lane;
+    g.x = strip * kStrip + g.lane;
+    // lane 0 fetches the column left of the strip, lane 63 the column right of it
+    g.edge_lane = (g.lane == 0) || (g.lane == kWave - 1);
+    g.ex = g.lane == 0 ? g.x - 1 : g.x + 1;
     g.y0 = a.dom.y_lo + (rb * (kBlock / kWave) + w) * a.rows;
     g.y1 = min(g.y0 + a.rows, a.dom.y_hi);
-    g.out_lane = g.lane >= 1 && g.lane <= kStrip && g.x < a.dom.W;
+    g.out_lane = g.x < a.dom.W;
     return g;
 }
 
@@ -112,77 +115,147 @@ __device__ __forceinline__ void eedge(T ojx, T ojy, T cj, T sj, float ujx, float
 }
 
 // ------------------------------------------------------------ row records
+// Every stencil kernel keeps rows y-1, y, y+1 finished in registers and has row y+2
+// (DEPTH 2: also y+3) in flight: a raw row is issued as pure loads (no arithmetic on
+// the loaded values, so no s_waitcnt there) and finished — combined, masked,
+// sin/cos — only after the current row has been computed, so each load has at least
+// a full row of compute to land. The strip's two outside neighbours (x0-1 for lane
+// 0, x0+64 for lane 63) travel with the row as a second, 2-lane "edge" record that
+// becomes the boundary operand of the DPP lane shifts.
 template <typename T>
-struct PRow {          // apply kernels
+struct PRaw {          // apply kernels: raw loads of one row (+ its edge pixel)
+    T v0, v1, v2;      // MODE 0: p | MODE 1,2: r
+    T w0, w1, w2;      // MODE 1,2: pre
+    T q0, q1, q2;      // MODE 2: p_old
+    T d0, d1, d2;      // MODE 2 with delta: delta
+    T ang;
+    float2 u;
+    int f, in;
+    // edge pixel
+    T ev0, ev1, ev2, ew0, ew1, ew2, eq0, eq1, eq2, eang;
+    float2 eu;
+    int ef, ein;
+};
+template <typename T>
+struct PRow {          // finished row
     T px, py, pt;      // p (x, y, angle channel)
     T c, s;            // cos / sin of the current angle
     float ux, uy;
     int act, fit;
+    T dx, dy, dt;      // delta after this iteration's update (MODE 2 with delta)
+    // edge pixel seen by this lane (lane 0: left of the strip, lane 63: right of it)
+    T epx, epy;        // its p (x, y)
+    float eux, euy;
+    int eact;
+    T ejx, ejy;        // its residual pointing at this lane: J(edge -> this pixel)
 };
 
 template <typename T, int MODE>
-__device__ __forceinline__ PRow<T> load_prow(const Args<T>& a, int x, int y, const T* pin,
-                                             const T* r, const T* pre, T beta) {
-    PRow<T> q;
-    const bool in = present(a.dom, x, y);
-    const long long i = in ? a.dom.off(x, y) : 0;
-    const long long N = a.dom.npix_mem();
-    const int f = in ? a.flags[i] : 0;
-    q.act = f & 1;
-    q.fit = (f >> 1) & 1;
-    const float2 u = reinterpret_cast<const float2*>(a.U)[i];
-    q.ux = in ? u.x : 0.f;
-    q.uy = in ? u.y : 0.f;
-    T t = a.A[i];
-    q.c = in ? t : (T)0;   // angle; cos/sin filled by finish_row
+__device__ __forceinline__ void raw_p(const T* pin, const T* r, const T* pre, long long i, long long N,
+                                      T& v0, T& v1, T& v2, T& w0, T& w1, T& w2, T& q0, T& q1, T& q2) {
     if (MODE == 0) {
-        q.px = pin[2 * i]; q.py = pin[2 * i + 1]; q.pt = pin[2 * N + i];
+        v0 = pin[2 * i]; v1 = pin[2 * i + 1]; v2 = pin[2 * N + i];
     } else {
-        const T rx = r[2 * i], ry = r[2 * i + 1], rt = r[2 * N + i];
-        const T wx = pre[2 * i], wy = pre[2 * i + 1], wt = pre[2 * N + i];
-        if (MODE == 1) {
-            q.px = wx * rx; q.py = wy * ry; q.pt = wt * rt;
-        } else {
-            T zx = rx, zy = ry, zt = rt;
-            if (a.use_pre) { zx = wx * rx; zy = wy * ry; zt = wt * rt; }
-            q.px = zx + beta * pin[2 * i];
-            q.py = zy + beta * pin[2 * i + 1];
-            q.pt = zt + beta * pin[2 * N + i];
-        }
+        v0 = r[2 * i]; v1 = r[2 * i + 1]; v2 = r[2 * N + i];
+        w0 = pre[2 * i]; w1 = pre[2 * i + 1]; w2 = pre[2 * N + i];
+        if (MODE == 2) { q0 = pin[2 * i]; q1 = pin[2 * i + 1]; q2 = pin[2 * N + i]; }
     }
-    if (!q.act) { q.px = 0; q.py = 0; q.pt = 0; }
+}
+
+template <typename T, int MODE, int DM>
+__device__ __forceinline__ PRaw<T> raw_prow(const Args<T>& a, const WaveGeom& g, int y, const T* pin,
+                                            const T* r, const T* pre, const T* delta) {
+    PRaw<T> q;
+    const long long N = a.dom.npix_mem();
+    q.in = present(a.dom, g.x, y);
+    const long long i = q.in ? a.dom.off(g.x, y) : 0;
+    q.f = a.flags[i];
+    q.u = reinterpret_cast<const float2*>(a.U)[i];
+    q.ang = a.A[i];
+    raw_p<T, MODE>(pin, r, pre, i, N, q.v0, q.v1, q.v2, q.w0, q.w1, q.w2, q.q0, q.q1, q.q2);
+    if (MODE == 2 && DM == 2) { q.d0 = delta[2 * i]; q.d1 = delta[2 * i + 1]; q.d2 = delta[2 * N + i]; }
+    q.ein = 0;
+    if (g.edge_lane) {
+        q.ein = present(a.dom, g.ex, y);
+        const long long e = q.ein ? a.dom.off(g.ex, y) : 0;
+        q.ef = a.flags[e];
+        q.eu = reinterpret_cast<const float2*>(a.U)[e];
+        q.eang = a.A[e];
+        raw_p<T, MODE>(pin, r, pre, e, N, q.ev0, q.ev1, q.ev2, q.ew0, q.ew1, q.ew2, q.eq0, q.eq1, q.eq2);
+    }
     return q;
 }
-template <typename T>
-__device__ __forceinline__ void finish_row(PRow<T>& q) {
-    T t = q.c;
-    sc_of(t, &q.c, &q.s);
+
+template <typename T, int MODE>
+__device__ __forceinline__ void make_p(const Args<T>& a, T beta, T v0, T v1, T v2, T w0, T w1, T w2,
+                                       T q0, T q1, T q2, T& px, T& py, T& pt) {
+    if (MODE == 0) {
+        px = v0; py = v1; pt = v2;
+    } else if (MODE == 1) {
+        px = w0 * v0; py = w1 * v1; pt = w2 * v2;
+    } else {
+        T zx = v0, zy = v1, zt = v2;
+        if (a.use_pre) { zx = w0 * v0; zy = w1 * v1; zt = w2 * v2; }
+        px = zx + beta * q0;
+        py = zy + beta * q1;
+        pt = zt + beta * q2;
+    }
+}
+
+template <typename T, int MODE, int DM>
+__device__ __forceinline__ PRow<T> finish_prow(const Args<T>& a, const PRaw<T>& q, T beta, T alpha) {
+    PRow<T> o;
+    const int f = q.in ? q.f : 0;
+    o.act = f & 1;
+    o.fit = (f >> 1) & 1;
+    o.ux = q.in ? q.u.x : 0.f;
+    o.uy = q.in ? q.u.y : 0.f;
+    sc_of(q.in ? q.ang : (T)0, &o.c, &o.s);
+    make_p<T, MODE>(a, beta, q.v0, q.v1, q.v2, q.w0, q.w1, q.w2, q.q0, q.q1, q.q2, o.px, o.py, o.pt);
+    if (MODE == 2 && DM == 1) { o.dx = alpha * q.q0; o.dy = alpha * q.q1; o.dt = alpha * q.q2; }
+    if (MODE == 2 && DM == 2) {
+        o.dx = q.d0 + alpha * q.q0; o.dy = q.d1 + alpha * q.q1; o.dt = q.d2 + alpha * q.q2;
+    }
+    if (!o.act) { o.px = 0; o.py = 0; o.pt = 0; }
+    // edge pixel: its p, and the residual it sends to this lane's pixel
+    const int ef = q.ein ? q.ef : 0;
+    o.eact = ef & 1;
+    o.eux = q.ein ? q.eu.x : 0.f;
+    o.euy = q.ein ? q.eu.y : 0.f;
+    T ec, es, ept, ax, ay;
+    sc_of(q.ein ? q.eang : (T)0, &ec, &es);
+    make_p<T, MODE>(a, beta, q.ev0, q.ev1, q.ev2, q.ew0, q.ew1, q.ew2, q.eq0, q.eq1, q.eq2, o.epx, o.epy, ept);
+    if (!o.eact) { o.epx = 0; o.epy = 0; ept = 0; }
+    jedge(o.epx, o.epy, ept, ec, es, o.eux, o.euy, o.px, o.py, o.ux, o.uy, o.eact && o.act, a.wr,
+          o.ejx, o.ejy, ax, ay);
+    return o;
 }
 
 // ------------------------------------------------------------- apply kernel
 // MODE 0: Ap = JtJ p for the given p.
 // MODE 1: p = pre*r (first PCG iteration; PCGInit1's p), Ap = JtJ p, writes p.
-// MODE 2: p = z + beta p_old with z = pre*r, beta = sc[ib_num]/sc[ib_den]
-//         (the previous iteration's PCGStep3), Ap = JtJ p, writes p.
+// MODE 2: p = z + beta p_old with z = pre*r, beta = sc[ib_num]/sc[ib_den] (the previous
+//         iteration's PCGStep3, :814-845), Ap = JtJ p, writes p; and the previous
+//         iteration's delta update (PCGStep2's delta += alpha p, :680), alpha =
+//         sc[ia_num]/sc[ia_den]: DM 1 delta = alpha p_old, DM 2 delta += alpha p_old.
 // Always: sc[rs.out] = sum p.Ap over active pixels (the alpha denominator).
-template <typename T, int MODE>
+template <typename T, int MODE, int DM, int DEPTH>
 __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restrict__ pin,
                                                    const T* __restrict__ r,
                                                    const T* __restrict__ pre, T* __restrict__ pout,
-                                                   T* __restrict__ Ap, const double* __restrict__ sc,
-                                                   int ib_num, int ib_den, ReduceSlot rs) {
+                                                   T* __restrict__ Ap, T* __restrict__ delta,
+                                                   const double* __restrict__ sc, int ib_num,
+                                                   int ib_den, int ia_num, int ia_den, ReduceSlot rs) {
     const WaveGeom g = geom(a);
     const T beta = (MODE == 2) ? (T)(sc[ib_num] / sc[ib_den]) : (T)0;
+    const T alpha = (MODE == 2 && DM != 0) ? (T)(sc[ia_num] / sc[ia_den]) : (T)0;
     const T wr = a.wr, wf2 = a.wf * a.wf;
     const long long N = a.dom.npix_mem();
     T dot = 0;
     if (g.y0 < g.y1) {
-        PRow<T> up = load_prow<T, MODE>(a, g.x, g.y0 - 1, pin, r, pre, beta);
-        PRow<T> cur = load_prow<T, MODE>(a, g.x, g.y0, pin, r, pre, beta);
-        PRow<T> dn = load_prow<T, MODE>(a, g.x, g.y0 + 1, pin, r, pre, beta);
-        finish_row(up);
-        finish_row(cur);
-        finish_row(dn);
+        PRow<T> up = finish_prow<T, MODE, DM>(a, raw_prow<T, MODE, DM>(a, g, g.y0 - 1, pin, r, pre, delta), beta, alpha);
+        PRow<T> cur = finish_prow<T, MODE, DM>(a, raw_prow<T, MODE, DM>(a, g, g.y0, pin, r, pre, delta), beta, alpha);
+        PRow<T> dn = finish_prow<T, MODE, DM>(a, raw_prow<T, MODE, DM>(a, g, g.y0 + 1, pin, r, pre, delta), beta, alpha);
         // carries from the row above: J(up->cur) and J(cur->up) with its angle term
         T in_up_x, in_up_y, my_x, my_y, thm, ax, ay;
         jedge(up.px, up.py, up.pt, up.c, up.s, up.ux, up.uy, cur.px, cur.py, cur.ux, cur.uy,
@@ -190,14 +263,19 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
         jedge(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, up.px, up.py, up.ux, up.uy,
               up.act && cur.act, wr, my_x, my_y, ax, ay);
         thm = -wr * (ax * my_x + ay * my_y);
+        PRaw<T> nx;
+        if (DEPTH == 2) nx = raw_prow<T, MODE, DM>(a, g, g.y0 + 2, pin, r, pre, delta);
         for (int y = g.y0; y < g.y1; ++y) {
-            PRow<T> nx = load_prow<T, MODE>(a, g.x, y + 2, pin, r, pre, beta);
-            // horizontal neighbours (lane 0 / 63 are halo lanes: never written)
-            const T lpx = from_left(cur.px, (T)0), lpy = from_left(cur.py, (T)0);
-            const T rpx = from_right(cur.px, (T)0), rpy = from_right(cur.py, (T)0);
-            const float lux = from_left(cur.ux, 0.f), luy = from_left(cur.uy, 0.f);
-            const float rux = from_right(cur.ux, 0.f), ruy = from_right(cur.uy, 0.f);
-            const int lact = from_left_i(cur.act, 0), ract = from_right_i(cur.act, 0);
+            // DEPTH 1: row y+2 in flight during row y; DEPTH 2: rows y+2 and y+3
+            PRaw<T> nn;
+            if (DEPTH == 1) nx = raw_prow<T, MODE, DM>(a, g, y + 2, pin, r, pre, delta);
+            else nn = raw_prow<T, MODE, DM>(a, g, y + 3, pin, r, pre, delta);
+            // horizontal neighbours; the strip's outside columns enter at lanes 0 / 63
+            const T lpx = from_left(cur.px, cur.epx), lpy = from_left(cur.py, cur.epy);
+            const T rpx = from_right(cur.px, cur.epx), rpy = from_right(cur.py, cur.epy);
+            const float lux = from_left(cur.ux, cur.eux), luy = from_left(cur.uy, cur.euy);
+            const float rux = from_right(cur.ux, cur.eux), ruy = from_right(cur.uy, cur.euy);
+            const int lact = from_left_i(cur.act, cur.eact), ract = from_right_i(cur.act, cur.eact);
             T jpx_x, jpx_y, apx_x, apx_y, jmx_x, jmx_y, amx_x, amx_y;
             T jpy_x, jpy_y, apy_x, apy_y, jdn_x, jdn_y, adn_x, adn_y;
             jedge(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, rpx, rpy, rux, ruy,
@@ -209,8 +287,8 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
             jedge(dn.px, dn.py, dn.pt, dn.c, dn.s, dn.ux, dn.uy, cur.px, cur.py, cur.ux, cur.uy,
                   cur.act && dn.act, wr, jdn_x, jdn_y, adn_x, adn_y);
             // residuals of the lane neighbours pointing at this pixel
-            const T inpx_x = from_right(jmx_x, (T)0), inpx_y = from_right(jmx_y, (T)0);
-            const T inmx_x = from_left(jpx_x, (T)0), inmx_y = from_left(jpx_y, (T)0);
+            const T inpx_x = from_right(jmx_x, cur.ejx), inpx_y = from_right(jmx_y, cur.ejy);
+            const T inmx_x = from_left(jpx_x, cur.ejx), inmx_y = from_left(jpx_y, cur.ejy);
             T aox = wr * ((jpx_x + jmx_x + jpy_x + my_x) - (inpx_x + inmx_x + jdn_x + in_up_x));
             T aoy = wr * ((jpx_y + jmx_y + jpy_y + my_y) - (inpx_y + inmx_y + jdn_y + in_up_y));
             if (cur.fit) { aox += wf2 * cur.px; aoy += wf2 * cur.py; }
@@ -221,14 +299,19 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
                 const long long i = a.dom.off(g.x, y);
                 Ap[2 * i] = aox; Ap[2 * i + 1] = aoy; Ap[2 * N + i] = aot;
                 if (MODE != 0) { pout[2 * i] = cur.px; pout[2 * i + 1] = cur.py; pout[2 * N + i] = cur.pt; }
+                if (MODE == 2 && DM != 0) {
+                    if (cur.act) { delta[2 * i] = cur.dx; delta[2 * i + 1] = cur.dy; delta[2 * N + i] = cur.dt; }
+                    else { delta[2 * i] = 0; delta[2 * i + 1] = 0; delta[2 * N + i] = 0; }
+                }
                 dot += cur.px * aox + cur.py * aoy + cur.pt * aot;
             }
-            // roll the window
+            // roll the window; the raw row is finished only now
             in_up_x = jpy_x; in_up_y = jpy_y;
             my_x = jdn_x; my_y = jdn_y;
             thm = -wr * (adn_x * jdn_x + adn_y * jdn_y);
-            up = cur; cur = dn; dn = nx;
-            finish_row(dn);
+            up = cur; cur = dn;
+            dn = finish_prow<T, MODE, DM>(a, nx, beta, alpha);
+            if (DEPTH == 2) nx = nn;
         }
     }
     double v[1] = {(double)dot};
@@ -237,30 +320,67 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
 
 // ------------------------------------------------------------- value rows
 template <typename T>
+struct VRaw {
+    Vec2<T> o;
+    T t;
+    float2 u, c;
+    float m;
+    int in;
+    Vec2<T> eo;        // edge pixel
+    T et;
+    float2 eu;
+    float em;
+    int ein;
+};
+template <typename T>
 struct VRow {
     T ox, oy, t, c, s;
     float ux, uy, cx, cy;
     int act, fit;
+    T eox, eoy;        // edge pixel seen by this lane
+    float eux, euy;
+    int eact;
+    T ec, es;          // its cos / sin (only the J^T F kernel needs them)
 };
-template <typename T>
-__device__ __forceinline__ VRow<T> load_vrow(const Args<T>& a, int x, int y) {
-    VRow<T> q;
-    const bool in = present(a.dom, x, y);
-    const long long i = in ? a.dom.off(x, y) : 0;
-    q.ox = in ? a.O[2 * i] : (T)0;
-    q.oy = in ? a.O[2 * i + 1] : (T)0;
-    q.t = in ? a.A[i] : (T)0;
-    const float2 u = reinterpret_cast<const float2*>(a.U)[i];
-    const float2 c = reinterpret_cast<const float2*>(a.C)[i];
-    const float m = a.M[i];
-    q.ux = in ? u.x : 0.f; q.uy = in ? u.y : 0.f;
-    q.cx = in ? c.x : -1.f; q.cy = in ? c.y : -1.f;
-    q.act = in && (m == 0.f);
-    q.fit = (q.cx >= 0.f) && (q.cy >= 0.f);
+template <typename T, bool EDGE_ANGLE>
+__device__ __forceinline__ VRaw<T> raw_vrow(const Args<T>& a, const WaveGeom& g, int y) {
+    VRaw<T> q;
+    q.in = present(a.dom, g.x, y);
+    const long long i = q.in ? a.dom.off(g.x, y) : 0;
+    q.o = reinterpret_cast<const Vec2<T>*>(a.O)[i];
+    q.t = a.A[i];
+    q.u = reinterpret_cast<const float2*>(a.U)[i];
+    q.c = reinterpret_cast<const float2*>(a.C)[i];
+    q.m = a.M[i];
+    q.ein = 0;
+    if (g.edge_lane) {
+        q.ein = present(a.dom, g.ex, y);
+        const long long e = q.ein ? a.dom.off(g.ex, y) : 0;
+        q.eo = reinterpret_cast<const Vec2<T>*>(a.O)[e];
+        if (EDGE_ANGLE) q.et = a.A[e];
+        q.eu = reinterpret_cast<const float2*>(a.U)[e];
+        q.em = a.M[e];
+    }
     return q;
 }
-template <typename T>
-__device__ __forceinline__ void finish_vrow(VRow<T>& q) { sc_of(q.t, &q.c, &q.s); }
+template <typename T, bool EDGE_ANGLE>
+__device__ __forceinline__ VRow<T> finish_vrow(const VRaw<T>& r) {
+    VRow<T> q;
+    q.ox = r.in ? r.o.x : (T)0;
+    q.oy = r.in ? r.o.y : (T)0;
+    q.t = r.in ? r.t : (T)0;
+    q.ux = r.in ? r.u.x : 0.f; q.uy = r.in ? r.u.y : 0.f;
+    q.cx = r.in ? r.c.x : -1.f; q.cy = r.in ? r.c.y : -1.f;
+    q.act = r.in && (r.m == 0.f);
+    q.fit = (q.cx >= 0.f) && (q.cy >= 0.f);
+    sc_of(q.t, &q.c, &q.s);
+    q.eox = r.ein ? r.eo.x : (T)0;
+    q.eoy = r.ein ? r.eo.y : (T)0;
+    q.eux = r.ein ? r.eu.x : 0.f; q.euy = r.ein ? r.eu.y : 0.f;
+    q.eact = r.ein && (r.em == 0.f);
+    if (EDGE_ANGLE) sc_of(r.ein ? r.et : (T)0, &q.ec, &q.es);
+    return q;
+}
 
 // ------------------------------------------------------------- J^T F kernel
 // r = -J^T F, pre = 1/(1+sqrt(diag J^T J))^2 (1/(1+1)^2 when UsePreconditioner(false)),
@@ -273,9 +393,9 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
     const long long N = a.dom.npix_mem();
     T dot = 0;
     if (g.y0 < g.y1) {
-        VRow<T> up = load_vrow(a, g.x, g.y0 - 1), cur = load_vrow(a, g.x, g.y0),
-                dn = load_vrow(a, g.x, g.y0 + 1);
-        finish_vrow(up); finish_vrow(cur); finish_vrow(dn);
+        VRow<T> up = finish_vrow<T, true>(raw_vrow<T, true>(a, g, g.y0 - 1)),
+                cur = finish_vrow<T, true>(raw_vrow<T, true>(a, g, g.y0)),
+                dn = finish_vrow<T, true>(raw_vrow<T, true>(a, g, g.y0 + 1));
         T inup_x, inup_y, my_x, my_y, ax, ay;
         const bool vup = up.act && cur.act;
         eedge(up.ox, up.oy, up.c, up.s, up.ux, up.uy, cur.ox, cur.oy, cur.ux, cur.uy, vup, wr,
@@ -286,15 +406,15 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
         T dthm = vup ? wr2 * (ax * ax + ay * ay) : (T)0;
         int vmy = vup;
         for (int y = g.y0; y < g.y1; ++y) {
-            VRow<T> nx = load_vrow(a, g.x, y + 2);
-            const T lox = from_left(cur.ox, (T)0), loy = from_left(cur.oy, (T)0);
-            const T rox = from_right(cur.ox, (T)0), roy = from_right(cur.oy, (T)0);
-            const float lux = from_left(cur.ux, 0.f), luy = from_left(cur.uy, 0.f);
-            const float rux = from_right(cur.ux, 0.f), ruy = from_right(cur.uy, 0.f);
-            const int lact = from_left_i(cur.act, 0), ract = from_right_i(cur.act, 0);
+            const VRaw<T> nx = raw_vrow<T, true>(a, g, y + 2);
+            const T lox = from_left(cur.ox, cur.eox), loy = from_left(cur.oy, cur.eoy);
+            const T rox = from_right(cur.ox, cur.eox), roy = from_right(cur.oy, cur.eoy);
+            const float lux = from_left(cur.ux, cur.eux), luy = from_left(cur.uy, cur.euy);
+            const float rux = from_right(cur.ux, cur.eux), ruy = from_right(cur.uy, cur.euy);
+            const int lact = from_left_i(cur.act, cur.eact), ract = from_right_i(cur.act, cur.eact);
             const bool vpx = cur.act && ract, vmx = cur.act && lact, vpy = cur.act && dn.act;
             T epx_x, epx_y, apx_x, apx_y, emx_x, emx_y, amx_x, amx_y;
-            T epy_x, epy_y, apy_x, apy_y, edn_x, edn_y, adn_x, adn_y;
+            T epy_x, epy_y, apy_x, apy_y, edn_x, edn_y, adn_x, adn_y, ee_x, ee_y;
             eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, rox, roy, rux, ruy, vpx, wr, epx_x,
                   epx_y, apx_x, apx_y);
             eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, lox, loy, lux, luy, vmx, wr, emx_x,
@@ -303,8 +423,11 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
                   epy_x, epy_y, apy_x, apy_y);
             eedge(dn.ox, dn.oy, dn.c, dn.s, dn.ux, dn.uy, cur.ox, cur.oy, cur.ux, cur.uy, vpy, wr,
                   edn_x, edn_y, adn_x, adn_y);
-            const T inpx_x = from_right(emx_x, (T)0), inpx_y = from_right(emx_y, (T)0);
-            const T inmx_x = from_left(epx_x, (T)0), inmx_y = from_left(epx_y, (T)0);
+            // the strip's outside neighbour's residual pointing at lane 0 / 63
+            eedge(cur.eox, cur.eoy, cur.ec, cur.es, cur.eux, cur.euy, cur.ox, cur.oy, cur.ux, cur.uy,
+                  cur.eact && cur.act, wr, ee_x, ee_y, ax, ay);
+            const T inpx_x = from_right(emx_x, ee_x), inpx_y = from_right(emx_y, ee_y);
+            const T inmx_x = from_left(epx_x, ee_x), inmx_y = from_left(epx_y, ee_y);
             T fx = wr * ((epx_x + emx_x + epy_x + my_x) - (inpx_x + inmx_x + edn_x + inup_x));
             T fy = wr * ((epx_y + emx_y + epy_y + my_y) - (inpx_y + inmx_y + edn_y + inup_y));
             T ft = thm - wr * ((apx_x * epx_x + apx_y * epx_y) + (amx_x * emx_x + amx_y * emx_y) +
@@ -342,8 +465,8 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
             thm = -wr * (adn_x * edn_x + adn_y * edn_y);
             dthm = vpy ? wr2 * (adn_x * adn_x + adn_y * adn_y) : (T)0;
             vmy = vpy;
-            up = cur; cur = dn; dn = nx;
-            finish_vrow(dn);
+            up = cur; cur = dn;
+            dn = finish_vrow<T, true>(nx);
         }
     }
     double v[1] = {(double)dot};
@@ -358,16 +481,16 @@ __global__ __launch_bounds__(kBlock) void iw_cost(Args<T> a, ReduceSlot rs) {
     const T wr = a.wr, wf = a.wf;
     T acc = 0;
     if (g.y0 < g.y1) {
-        VRow<T> up = load_vrow(a, g.x, g.y0 - 1), cur = load_vrow(a, g.x, g.y0),
-                dn = load_vrow(a, g.x, g.y0 + 1);
-        finish_vrow(cur);
+        VRow<T> up = finish_vrow<T, false>(raw_vrow<T, false>(a, g, g.y0 - 1)),
+                cur = finish_vrow<T, false>(raw_vrow<T, false>(a, g, g.y0)),
+                dn = finish_vrow<T, false>(raw_vrow<T, false>(a, g, g.y0 + 1));
         for (int y = g.y0; y < g.y1; ++y) {
-            VRow<T> nx = load_vrow(a, g.x, y + 2);
-            const T lox = from_left(cur.ox, (T)0), loy = from_left(cur.oy, (T)0);
-            const T rox = from_right(cur.ox, (T)0), roy = from_right(cur.oy, (T)0);
-            const float lux = from_left(cur.ux, 0.f), luy = from_left(cur.uy, 0.f);
-            const float rux = from_right(cur.ux, 0.f), ruy = from_right(cur.uy, 0.f);
-            const int lact = from_left_i(cur.act, 0), ract = from_right_i(cur.act, 0);
+            const VRaw<T> nx = raw_vrow<T, false>(a, g, y + 2);
+            const T lox = from_left(cur.ox, cur.eox), loy = from_left(cur.oy, cur.eoy);
+            const T rox = from_right(cur.ox, cur.eox), roy = from_right(cur.oy, cur.eoy);
+            const float lux = from_left(cur.ux, cur.eux), luy = from_left(cur.uy, cur.euy);
+            const float rux = from_right(cur.ux, cur.eux), ruy = from_right(cur.uy, cur.euy);
+            const int lact = from_left_i(cur.act, cur.eact), ract = from_right_i(cur.act, cur.eact);
             T ex, ey, ax, ay, sum = 0;
             eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, rox, roy, rux, ruy,
                   cur.act && ract, wr, ex, ey, ax, ay);
@@ -386,8 +509,8 @@ __global__ __launch_bounds__(kBlock) void iw_cost(Args<T> a, ReduceSlot rs) {
                 sum += fx * fx + fy * fy;
             }
             if (g.out_lane && cur.act) acc += (T)0.5 * sum;
-            up = cur; cur = dn; dn = nx;
-            finish_vrow(cur);
+            up = cur; cur = dn;
+            dn = finish_vrow<T, false>(nx);
         }
     }
     double v[1] = {(double)acc};
@@ -408,19 +531,34 @@ __global__ __launch_bounds__(kBlock) void iw_flags(Args<T> a) {
 }
 
 // --------------------------------------------------------------- update kernel
-// X += delta on active pixels of the owned rows (PCGLinearUpdate, :854-859).
-template <typename T>
+// X += delta_L on active pixels of the owned rows (PCGLinearUpdate, :854-859), where
+// delta_L = delta_{L-1} + alpha_{L-1} p_{L-1} is the last PCG iteration's delta update
+// (HAS_DELTA = false when lIterations == 1: delta_0 = 0).
+template <typename T, bool HAS_DELTA>
 __global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O, T* __restrict__ A,
-                                                    const T* __restrict__ delta) {
+                                                    const T* __restrict__ delta, const T* __restrict__ p,
+                                                    const double* __restrict__ sc, int ia_num, int ia_den) {
     const long long N = a.dom.npix_mem();
+    const T alpha = (T)(sc[ia_num] / sc[ia_den]);
     const long long b = a.dom.off(0, a.dom.y_lo), e = a.dom.off(0, a.dom.y_hi);
     for (long long i = b + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < e;
          i += (long long)gridDim.x * blockDim.x) {
-        if (a.flags[i] & 1) {
-            const Vec2<T> o = reinterpret_cast<const Vec2<T>*>(O)[i];
-            const Vec2<T> d = reinterpret_cast<const Vec2<T>*>(delta)[i];
+        const int f = a.flags[i];
+        const Vec2<T> o = reinterpret_cast<const Vec2<T>*>(O)[i];
+        const Vec2<T> pp = reinterpret_cast<const Vec2<T>*>(p)[i];
+        const T t = A[i], pt = p[2 * N + i];
+        Vec2<T> d;
+        T dt;
+        if (HAS_DELTA) {
+            d = reinterpret_cast<const Vec2<T>*>(delta)[i];
+            dt = delta[2 * N + i];
+            d.x = d.x + alpha * pp.x; d.y = d.y + alpha * pp.y; dt = dt + alpha * pt;
+        } else {
+            d.x = alpha * pp.x; d.y = alpha * pp.y; dt = alpha * pt;
+        }
+        if (f & 1) {
             reinterpret_cast<Vec2<T>*>(O)[i] = Vec2<T>{o.x + d.x, o.y + d.y};
-            A[i] = A[i] + delta[2 * N + i];
+            A[i] = t + dt;
         }
     }
 }
@@ -428,6 +566,11 @@ __global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O
 }  // namespace iw
 
 // ====================================================================== plan
+static int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+
 template <typename T>
 class ImageWarpingPlan final : public Plan {
 public:
@@ -456,7 +599,8 @@ public:
             OPT_HIP_CHECK(hipMemset(v, 0, sizeof(T) * nvec_));
         flags_ = (uint8_t*)dmalloc(N);
         OPT_HIP_CHECK(hipMemset(flags_, 0, N));
-        rows_ = 16;
+        rows_ = env_int("OPT_AMD_ROWS", 32);
+        depth_ = env_int("OPT_AMD_DEPTH", 1);
         nstrips_ = (dom_.W + iw::kStrip - 1) / iw::kStrip;
         nrowblocks_ = (dom_.y_hi - dom_.y_lo + rows_ * 4 - 1) / (rows_ * 4);
         timer_.apply_name = apply_kernel_name();
@@ -509,20 +653,27 @@ public:
         for (int i = 0; i < L; ++i) {
             std::swap(pcur, pprev);   // pcur <- new p, pprev <- old p
             tbegin("iw_apply");
-            if (i == 0) launch_apply<1>(nullptr, pcur, pap(i), 0, 0);
-            else launch_apply<2>(pprev, pcur, pap(i), rz(i), rz(i - 1));
+            if (i == 0) launch_apply<1, 0>(nullptr, pcur, pap(i), 0, 0, 0, 0);
+            else if (i == 1) launch_apply<2, 1>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1));
+            else launch_apply<2, 2>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1));
             tend();
-            tbegin("pcg_step2");
-            launch_step2(pcur, i == 0, rz(i), pap(i), rz(i + 1));
+            tbegin("pcg_residual");
+            launch_residual(rz(i), pap(i), rz(i + 1));
             tend();
         }
-        // PCGLinearUpdate + cost
-        const int ub = flat_grid(dom_.npix_mem(), 1);
-        tbegin("iw_update");
-        hipLaunchKernelGGL(iw::iw_update<T>, dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_, cur_A_,
-                           (const T*)delta_);
-        OPT_HIP_CHECK(hipGetLastError());
-        tend();
+        // PCGLinearUpdate (with the last delta += alpha p) + cost
+        if (L > 0) {
+            const int ub = flat_grid(dom_.npix_mem(), 1);
+            tbegin("iw_update");
+            if (L >= 2)
+                hipLaunchKernelGGL((iw::iw_update<T, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
+                                   cur_A_, (const T*)delta_, (const T*)pcur, red_.scalars, rz(L - 1), pap(L - 1));
+            else
+                hipLaunchKernelGGL((iw::iw_update<T, false>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
+                                   cur_A_, (const T*)delta_, (const T*)pcur, red_.scalars, rz(L - 1), pap(L - 1));
+            OPT_HIP_CHECK(hipGetLastError());
+            tend();
+        }
         tbegin("iw_cost"); launch_cost(kScCost); tend();
         const double c = read_scalar(kScCost);
         unbind_after_step();
@@ -545,7 +696,7 @@ public:
         begin_call();
         bind(params, false);
         launch_flags();
-        launch_apply<0>((const T*)p, nullptr, kScTmp, 0, 0, (T*)Ap);
+        launch_apply<0, 0>((const T*)p, nullptr, kScTmp, 0, 0, 0, 0, (T*)Ap);
         *pAp = read_scalar(kScTmp);
         end_call();
         return 0;
@@ -565,9 +716,9 @@ public:
         hipEvent_t e0, e1;
         OPT_HIP_CHECK(hipEventCreate(&e0));
         OPT_HIP_CHECK(hipEventCreate(&e1));
-        launch_apply<0>((const T*)p, nullptr, kScTmp, 0, 0, (T*)Ap);   // warm
+        launch_apply<0, 0>((const T*)p, nullptr, kScTmp, 0, 0, 0, 0, (T*)Ap);   // warm
         OPT_HIP_CHECK(hipEventRecord(e0, stream_));
-        for (int i = 0; i < reps; ++i) launch_apply<0>((const T*)p, nullptr, kScTmp, 0, 0, (T*)Ap);
+        for (int i = 0; i < reps; ++i) launch_apply<0, 0>((const T*)p, nullptr, kScTmp, 0, 0, 0, 0, (T*)Ap);
         OPT_HIP_CHECK(hipEventRecord(e1, stream_));
         OPT_HIP_CHECK(hipEventSynchronize(e1));
         float ms = 0;
@@ -639,24 +790,25 @@ private:
                            red_.slot(nb, sc_out));
         OPT_HIP_CHECK(hipGetLastError());
     }
-    template <int MODE>
-    void launch_apply(const T* pin, T* pout, int sc_out, int ib_num, int ib_den, T* Ap = nullptr) {
+    template <int MODE, int DM>
+    void launch_apply(const T* pin, T* pout, int sc_out, int ib_num, int ib_den, int ia_num, int ia_den,
+                      T* Ap = nullptr) {
         const int nb = stencil_blocks();
-        hipLaunchKernelGGL((iw::iw_apply<T, MODE>), dim3(nb), dim3(kBlock), 0, stream_, args(), pin,
-                           (const T*)r_, (const T*)pre_, pout, Ap ? Ap : Ap_, red_.scalars, ib_num,
-                           ib_den, red_.slot(nb, sc_out));
+        if (depth_ == 2)
+            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 2>), dim3(nb), dim3(kBlock), 0, stream_, args(), pin,
+                               (const T*)r_, (const T*)pre_, pout, Ap ? Ap : Ap_, delta_, red_.scalars, ib_num,
+                               ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
+        else
+            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1>), dim3(nb), dim3(kBlock), 0, stream_, args(), pin,
+                               (const T*)r_, (const T*)pre_, pout, Ap ? Ap : Ap_, delta_, red_.scalars, ib_num,
+                               ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
         OPT_HIP_CHECK(hipGetLastError());
     }
-    void launch_step2(const T* p, bool first, int i_num, int i_den, int sc_out) {
+    void launch_residual(int i_num, int i_den, int sc_out) {
         const int nb = flat_grid(nvec_);
-        if (first)
-            hipLaunchKernelGGL((pcg_step2_kernel<T, true>), dim3(nb), dim3(kBlock), 0, stream_, nvec_, p,
-                               (const T*)Ap_, (const T*)pre_, r_, delta_, red_.scalars, i_num, i_den,
-                               spec_.use_preconditioner ? 1 : 0, red_.slot(nb, sc_out));
-        else
-            hipLaunchKernelGGL((pcg_step2_kernel<T, false>), dim3(nb), dim3(kBlock), 0, stream_, nvec_, p,
-                               (const T*)Ap_, (const T*)pre_, r_, delta_, red_.scalars, i_num, i_den,
-                               spec_.use_preconditioner ? 1 : 0, red_.slot(nb, sc_out));
+        hipLaunchKernelGGL((pcg_residual_kernel<T>), dim3(nb), dim3(kBlock), 0, stream_, nvec_, (const T*)Ap_,
+                           (const T*)pre_, r_, red_.scalars, i_num, i_den, spec_.use_preconditioner ? 1 : 0,
+                           red_.slot(nb, sc_out));
         OPT_HIP_CHECK(hipGetLastError());
     }
     void launch_cost(int sc_out) {
@@ -675,7 +827,7 @@ private:
     long long nvec_ = 0;
     T *r_ = nullptr, *pre_ = nullptr, *p0_ = nullptr, *p1_ = nullptr, *Ap_ = nullptr, *delta_ = nullptr;
     uint8_t* flags_ = nullptr;
-    int rows_ = 16, nstrips_ = 0, nrowblocks_ = 0;
+    int rows_ = 16, depth_ = 1, nstrips_ = 0, nrowblocks_ = 0;
     float wf_ = 0, wr_ = 0;
     T *user_O_ = nullptr, *user_A_ = nullptr;
     T *cur_O_ = nullptr, *cur_A_ = nullptr;

@@ -102,8 +102,8 @@ void ReduceScratch::ensure(int mb, int kmax, int ns) {
         partials = (double*)dmalloc(sizeof(double) * (size_t)max_blocks * kMaxReduce);
     }
     if (!ticket) {
-        ticket = (unsigned*)dmalloc(64);
-        OPT_HIP_CHECK(hipMemset(ticket, 0, 64));
+        ticket = (unsigned*)dmalloc(sizeof(unsigned) * kTicketWords);
+        OPT_HIP_CHECK(hipMemset(ticket, 0, sizeof(unsigned) * kTicketWords));
     }
     if (ns > n_scalars) {
         double* s = (double*)dmalloc(sizeof(double) * ns);
