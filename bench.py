@@ -29,11 +29,11 @@ import torch  # noqa: E402
 METRIC = "PCG JᵀJ·p throughput (unknowns/s) + GN iters/s, image_warping 4096² fp32"
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # Compulsory HBM bytes per pixel of the in-loop apply kernel iw_apply:
-# always Angle 4 + UrShape 8 + flag 1 + r 12 + pre 12 read, p 12 + Ap 12 written;
+# always Angle 4 + UrShape 8 + flag 1 + r 12 + angle-channel pre 4 read, p 12 + Ap 12 written;
 # from PCG iteration 1 on also p_old 12 read and delta 12 written; from iteration 2 on
 # also delta 12 read.
 def apply_bytes_per_px(i: int) -> int:
-    b = 4 + 8 + 1 + 12 + 12 + 12 + 12
+    b = 4 + 8 + 1 + 12 + 4 + 12 + 12
     if i >= 1:
         b += 12 + 12
     if i >= 2:

@@ -49,11 +49,22 @@ struct Args {
     const float* U;    // UrShape (float2)
     const float* C;    // Constraints (float2)
     const float* M;    // Mask
-    uint8_t* flags;    // bit0 active (inside, Mask==0), bit1 fit constraint valid
+    uint8_t* flags;    // bit0 active (inside, Mask==0), bit1 fit constraint valid,
+                       // bits 2-4 number of valid rigidity edges (0..4)
     T wf, wr;
     int use_pre;
     int nstrips, nrowblocks, rows;   // rows per wavefront
+    // Jacobi preconditioner of the two Offset channels: diag(J^T J) there is
+    // 2 wr^2 (#valid edges) + wf^2 [fit], so pre = 1/(1+sqrt(diag))^2 takes one of ten
+    // values (host-computed once per step; 0.25 everywhere for UsePreconditioner(false)).
+    // Only the angle channel's preconditioner is stored per pixel.
+    T preO[2][5];
 };
+
+template <typename T>
+__device__ __forceinline__ T pre_offset(const Args<T>& a, int f) {
+    return (f & 1) ? a.preO[(f >> 1) & 1][(f >> 2) & 7] : (T)0;
+}
 
 // ---------------------------------------------------------------- helpers
 __device__ __forceinline__ void sc_of(float t, float* c, float* s) { sincosf(t, s, c); }
@@ -125,7 +136,7 @@ __device__ __forceinline__ void eedge(T ojx, T ojy, T cj, T sj, float ujx, float
 template <typename T>
 struct PRaw {          // apply kernels: raw loads of one row (+ its edge pixel)
     T v0, v1, v2;      // MODE 0: p | MODE 1,2: r
-    T w0, w1, w2;      // MODE 1,2: pre
+    T w0, w1, w2;      // MODE 1,2: angle-channel pre (w2)
     T q0, q1, q2;      // MODE 2: p_old
     T d0, d1, d2;      // MODE 2 with delta: delta
     T ang;
@@ -157,7 +168,7 @@ __device__ __forceinline__ void raw_p(const T* pin, const T* r, const T* pre, lo
         v0 = pin[2 * i]; v1 = pin[2 * i + 1]; v2 = pin[2 * N + i];
     } else {
         v0 = r[2 * i]; v1 = r[2 * i + 1]; v2 = r[2 * N + i];
-        w0 = pre[2 * i]; w1 = pre[2 * i + 1]; w2 = pre[2 * N + i];
+        w2 = pre[i];   // angle-channel preconditioner; Offset channels come from the flags
         if (MODE == 2) { q0 = pin[2 * i]; q1 = pin[2 * i + 1]; q2 = pin[2 * N + i]; }
     }
 }
@@ -187,8 +198,9 @@ __device__ __forceinline__ PRaw<T> raw_prow(const Args<T>& a, const WaveGeom& g,
 }
 
 template <typename T, int MODE>
-__device__ __forceinline__ void make_p(const Args<T>& a, T beta, T v0, T v1, T v2, T w0, T w1, T w2,
+__device__ __forceinline__ void make_p(const Args<T>& a, int f, T beta, T v0, T v1, T v2, T w2,
                                        T q0, T q1, T q2, T& px, T& py, T& pt) {
+    const T w0 = pre_offset(a, f), w1 = w0;
     if (MODE == 0) {
         px = v0; py = v1; pt = v2;
     } else if (MODE == 1) {
@@ -211,7 +223,7 @@ __device__ __forceinline__ PRow<T> finish_prow(const Args<T>& a, const PRaw<T>& 
     o.ux = q.in ? q.u.x : 0.f;
     o.uy = q.in ? q.u.y : 0.f;
     sc_of(q.in ? q.ang : (T)0, &o.c, &o.s);
-    make_p<T, MODE>(a, beta, q.v0, q.v1, q.v2, q.w0, q.w1, q.w2, q.q0, q.q1, q.q2, o.px, o.py, o.pt);
+    make_p<T, MODE>(a, f, beta, q.v0, q.v1, q.v2, q.w2, q.q0, q.q1, q.q2, o.px, o.py, o.pt);
     if (MODE == 2 && DM == 1) { o.dx = alpha * q.q0; o.dy = alpha * q.q1; o.dt = alpha * q.q2; }
     if (MODE == 2 && DM == 2) {
         o.dx = q.d0 + alpha * q.q0; o.dy = q.d1 + alpha * q.q1; o.dt = q.d2 + alpha * q.q2;
@@ -224,7 +236,7 @@ __device__ __forceinline__ PRow<T> finish_prow(const Args<T>& a, const PRaw<T>& 
     o.euy = q.ein ? q.eu.y : 0.f;
     T ec, es, ept, ax, ay;
     sc_of(q.ein ? q.eang : (T)0, &ec, &es);
-    make_p<T, MODE>(a, beta, q.ev0, q.ev1, q.ev2, q.ew0, q.ew1, q.ew2, q.eq0, q.eq1, q.eq2, o.epx, o.epy, ept);
+    make_p<T, MODE>(a, ef, beta, q.ev0, q.ev1, q.ev2, q.ew2, q.eq0, q.eq1, q.eq2, o.epx, o.epy, ept);
     if (!o.eact) { o.epx = 0; o.epy = 0; ept = 0; }
     jedge(o.epx, o.epy, ept, ec, es, o.eux, o.euy, o.px, o.py, o.ux, o.uy, o.eact && o.act, a.wr,
           o.ejx, o.ejy, ax, ay);
@@ -385,7 +397,9 @@ __device__ __forceinline__ VRow<T> finish_vrow(const VRaw<T>& r) {
 // ------------------------------------------------------------- J^T F kernel
 // r = -J^T F, pre = 1/(1+sqrt(diag J^T J))^2 (1/(1+1)^2 when UsePreconditioner(false)),
 // flags, and sc[rs.out] = sum r.(pre r) over active pixels (alpha numerator).
-template <typename T>
+// FULL_PRE: write all three preconditioner channels (OptAMD_EvalJTF layout); otherwise
+// only the angle channel (the solver's compressed layout, Args::preO).
+template <typename T, bool FULL_PRE>
 __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T* __restrict__ pre,
                                                  ReduceSlot rs) {
     const WaveGeom g = geom(a);
@@ -433,32 +447,32 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
             T ft = thm - wr * ((apx_x * epx_x + apx_y * epx_y) + (amx_x * emx_x + amx_y * emx_y) +
                                (apy_x * epy_x + apy_y * epy_y));
             const int nv = (int)vpx + (int)vmx + (int)vpy + vmy;
-            T dO = wr2 * (T)(2 * nv);
             T dt = dthm + (vpx ? wr2 * (apx_x * apx_x + apx_y * apx_y) : (T)0) +
                    (vmx ? wr2 * (amx_x * amx_x + amx_y * amx_y) : (T)0) +
                    (vpy ? wr2 * (apy_x * apy_x + apy_y * apy_y) : (T)0);
             if (cur.fit) {
                 fx += wf * wf * (cur.ox - (T)cur.cx);
                 fy += wf * wf * (cur.oy - (T)cur.cy);
-                dO += wf * wf;
             }
             if (g.out_lane) {
                 const long long i = a.dom.off(g.x, y);
-                a.flags[i] = (uint8_t)(cur.act | (cur.fit << 1));
-                T rx = 0, ry = 0, rt = 0, wx = 0, wy = 0, wt = 0;
+                const int f = cur.act | (cur.fit << 1) | (nv << 2);
+                a.flags[i] = (uint8_t)f;
+                T rx = 0, ry = 0, rt = 0, wo = 0, wt = 0;
                 if (cur.act) {
                     rx = -fx; ry = -fy; rt = -ft;
+                    wo = pre_offset(a, f);   // 1/(1+sqrt(2 wr^2 nv + wf^2 [fit]))^2
                     if (a.use_pre) {
-                        const T sO = (T)1 + sqrt(dO), st = (T)1 + sqrt(dt);
-                        wx = wy = (T)1 / (sO * sO);
+                        const T st = (T)1 + sqrt(dt);
                         wt = (T)1 / (st * st);
                     } else {
-                        wx = wy = wt = (T)0.25;   // guardedInvert(1), PCGInit1 :543-550
+                        wt = (T)0.25;   // guardedInvert(1), PCGInit1 :543-550
                     }
-                    dot += rx * (wx * rx) + ry * (wy * ry) + rt * (wt * rt);
+                    dot += rx * (wo * rx) + ry * (wo * ry) + rt * (wt * rt);
                 }
                 r[2 * i] = rx; r[2 * i + 1] = ry; r[2 * N + i] = rt;
-                pre[2 * i] = wx; pre[2 * i + 1] = wy; pre[2 * N + i] = wt;
+                if (FULL_PRE) { pre[2 * i] = wo; pre[2 * i + 1] = wo; pre[2 * N + i] = wt; }
+                else pre[i] = wt;
             }
             inup_x = epy_x; inup_y = epy_y;
             my_x = edn_x; my_y = edn_y;
@@ -511,6 +525,61 @@ __global__ __launch_bounds__(kBlock) void iw_cost(Args<T> a, ReduceSlot rs) {
             if (g.out_lane && cur.act) acc += (T)0.5 * sum;
             up = cur; cur = dn;
             dn = finish_vrow<T, false>(nx);
+        }
+    }
+    double v[1] = {(double)acc};
+    block_reduce_publish<1>(v, rs, blockIdx.x);
+}
+
+// ------------------------------------------------------------ residual kernel
+// PCGStep2's residual half for this layout (pcg_kernels.h has the generic flat form):
+//   r -= alpha Ap;  rz[i+1] = sum r.(pre r)  (pre = r's preconditioner; 1 when
+//   UsePreconditioner(false), :705-708). Two pixels per lane: Offset parts as one
+//   16-B access, angle parts and the angle preconditioner as 8-B, flags as 2 bytes.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void iw_residual(Args<T> a, const T* __restrict__ Ap,
+                                                      const T* __restrict__ pre, T* __restrict__ r,
+                                                      const double* __restrict__ sc, int i_num, int i_den,
+                                                      ReduceSlot rs) {
+    const long long N = a.dom.npix_mem();
+    const T alpha = (T)(sc[i_num] / sc[i_den]);
+    const long long b = a.dom.off(0, a.dom.y_lo), e = a.dom.off(0, a.dom.y_hi);
+    const long long npairs = (e - b) / 2;
+    T acc = 0;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < npairs; q += stride) {
+        const long long i = b + 2 * q;
+        V4<T> ro = *reinterpret_cast<const V4<T>*>(r + 2 * i);
+        const V4<T> ao = *reinterpret_cast<const V4<T>*>(Ap + 2 * i);
+        Vec2<T> rt = *reinterpret_cast<const Vec2<T>*>(r + 2 * N + i);
+        const Vec2<T> at = *reinterpret_cast<const Vec2<T>*>(Ap + 2 * N + i);
+        const Vec2<T> wt = *reinterpret_cast<const Vec2<T>*>(pre + i);
+        const unsigned short ff = *reinterpret_cast<const unsigned short*>(a.flags + i);
+        const int f0 = ff & 0xff, f1 = ff >> 8;
+        ro.a -= alpha * ao.a; ro.b -= alpha * ao.b; ro.c -= alpha * ao.c; ro.d -= alpha * ao.d;
+        rt.x -= alpha * at.x; rt.y -= alpha * at.y;
+        *reinterpret_cast<V4<T>*>(r + 2 * i) = ro;
+        *reinterpret_cast<Vec2<T>*>(r + 2 * N + i) = rt;
+        if (a.use_pre) {
+            const T w0 = pre_offset(a, f0), w1 = pre_offset(a, f1);
+            acc += w0 * ro.a * ro.a + w0 * ro.b * ro.b + w1 * ro.c * ro.c + w1 * ro.d * ro.d +
+                   wt.x * rt.x * rt.x + wt.y * rt.y * rt.y;
+        } else {
+            acc += ro.a * ro.a + ro.b * ro.b + ro.c * ro.c + ro.d * ro.d + rt.x * rt.x + rt.y * rt.y;
+        }
+    }
+    // odd pixel count: block 0 takes the last pixel
+    if (((e - b) & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+        const long long i = e - 1;
+        const int f = a.flags[i];
+        T r0 = r[2 * i] - alpha * Ap[2 * i], r1 = r[2 * i + 1] - alpha * Ap[2 * i + 1];
+        T r2 = r[2 * N + i] - alpha * Ap[2 * N + i];
+        r[2 * i] = r0; r[2 * i + 1] = r1; r[2 * N + i] = r2;
+        if (a.use_pre) {
+            const T w0 = pre_offset(a, f);
+            acc += w0 * r0 * r0 + w0 * r1 * r1 + pre[i] * r2 * r2;
+        } else {
+            acc += r0 * r0 + r1 * r1 + r2 * r2;
         }
     }
     double v[1] = {(double)acc};
@@ -593,10 +662,12 @@ public:
         }
         const long long N = dom_.npix_mem();
         nvec_ = 3 * N;
-        for (T** v : {&r_, &pre_, &p0_, &p1_, &Ap_, &delta_})
+        for (T** v : {&r_, &p0_, &p1_, &Ap_, &delta_})
             *v = (T*)dmalloc(sizeof(T) * nvec_);
-        for (T* v : {r_, pre_, p0_, p1_, Ap_, delta_})
+        for (T* v : {r_, p0_, p1_, Ap_, delta_})
             OPT_HIP_CHECK(hipMemset(v, 0, sizeof(T) * nvec_));
+        pre_ = (T*)dmalloc(sizeof(T) * N);   // angle channel only (Args::preO)
+        OPT_HIP_CHECK(hipMemset(pre_, 0, sizeof(T) * N));
         flags_ = (uint8_t*)dmalloc(N);
         OPT_HIP_CHECK(hipMemset(flags_, 0, N));
         rows_ = env_int("OPT_AMD_ROWS", 32);
@@ -657,7 +728,7 @@ public:
             else if (i == 1) launch_apply<2, 1>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1));
             else launch_apply<2, 2>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1));
             tend();
-            tbegin("pcg_residual");
+            tbegin("iw_residual");
             launch_residual(rz(i), pap(i), rz(i + 1));
             tend();
         }
@@ -687,7 +758,7 @@ public:
     int eval_jtf(void** params, void* r, void* pre, double* rzv) override {
         begin_call();
         bind(params, false);
-        launch_jtf((T*)r, (T*)pre, kScTmp);
+        launch_jtf((T*)r, (T*)pre, kScTmp, true);
         *rzv = read_scalar(kScTmp);
         end_call();
         return 0;
@@ -745,6 +816,15 @@ private:
         a.wf = (T)wf_; a.wr = (T)wr_;
         a.use_pre = spec_.use_preconditioner ? 1 : 0;
         a.nstrips = nstrips_; a.nrowblocks = nrowblocks_; a.rows = rows_;
+        // same float expression the reference's evalJTF + guardedInvert evaluate
+        const T wr2 = (T)wr_ * (T)wr_, wf2 = (T)wf_ * (T)wf_;
+        for (int fit = 0; fit < 2; ++fit)
+            for (int nv = 0; nv < 5; ++nv) {
+                T d = wr2 * (T)(2 * nv);
+                if (fit) d += wf2;
+                const T s1 = (T)1 + std::sqrt(d);
+                a.preO[fit][nv] = spec_.use_preconditioner ? (T)1 / (s1 * s1) : (T)0.25;
+            }
         return a;
     }
 
@@ -784,10 +864,14 @@ private:
         return v;
     }
 
-    void launch_jtf(T* r, T* pre, int sc_out) {
+    void launch_jtf(T* r, T* pre, int sc_out, bool full_pre = false) {
         const int nb = stencil_blocks();
-        hipLaunchKernelGGL(iw::iw_jtf<T>, dim3(nb), dim3(kBlock), 0, stream_, args(), r, pre,
-                           red_.slot(nb, sc_out));
+        if (full_pre)
+            hipLaunchKernelGGL((iw::iw_jtf<T, true>), dim3(nb), dim3(kBlock), 0, stream_, args(), r, pre,
+                               red_.slot(nb, sc_out));
+        else
+            hipLaunchKernelGGL((iw::iw_jtf<T, false>), dim3(nb), dim3(kBlock), 0, stream_, args(), r, pre,
+                               red_.slot(nb, sc_out));
         OPT_HIP_CHECK(hipGetLastError());
     }
     template <int MODE, int DM>
@@ -805,10 +889,9 @@ private:
         OPT_HIP_CHECK(hipGetLastError());
     }
     void launch_residual(int i_num, int i_den, int sc_out) {
-        const int nb = flat_grid(nvec_);
-        hipLaunchKernelGGL((pcg_residual_kernel<T>), dim3(nb), dim3(kBlock), 0, stream_, nvec_, (const T*)Ap_,
-                           (const T*)pre_, r_, red_.scalars, i_num, i_den, spec_.use_preconditioner ? 1 : 0,
-                           red_.slot(nb, sc_out));
+        const int nb = flat_grid(dom_.npix_mem(), 2);
+        hipLaunchKernelGGL((iw::iw_residual<T>), dim3(nb), dim3(kBlock), 0, stream_, args(), (const T*)Ap_,
+                           (const T*)pre_, r_, red_.scalars, i_num, i_den, red_.slot(nb, sc_out));
         OPT_HIP_CHECK(hipGetLastError());
     }
     void launch_cost(int sc_out) {

@@ -17,7 +17,7 @@ def main():
     base = [torch.from_numpy(w[k]).cuda() for k in ("Offset", "Angle", "UrShape", "Constraints", "Mask")]
     rows_list = [int(x) for x in os.environ.get("SWEEP_ROWS", "8,16,32,64").split(",")]
     depths = [int(x) for x in os.environ.get("SWEEP_DEPTH", "1,2").split(",")]
-    names = ["iw_apply", "pcg_residual", "iw_jtf", "iw_update", "iw_cost"]
+    names = ["iw_apply", "iw_residual", "iw_jtf", "iw_update", "iw_cost"]
     print(f"{'rows':>5} {'depth':>5} {'pure_us':>9} {'step_ms':>8} " + " ".join(f"{n:>13}" for n in names))
     for rows in rows_list:
         for depth in depths:
