@@ -74,6 +74,34 @@ void* OptAMD_PlanStream(Opt_Plan* plan);
 /* Outer iterations completed since the last Init. */
 int OptAMD_PlanIterations(Opt_Plan* plan);
 
+/* ---- multi-GPU row-slab decomposition (no reference counterpart:
+ * the reference is single-device, §2.3) ------------------------------------------ */
+typedef struct OptAMD_Comm OptAMD_Comm;
+typedef struct OptAMD_LocalGroup OptAMD_LocalGroup;
+
+/* 128-byte RCCL unique id, created on one rank and shared with the others by the
+ * caller (e.g. torch.distributed broadcast). Returns 0 on success. */
+int OptAMD_RcclUniqueId(void* out128);
+/* RCCL communicator over `nranks` processes, one GPU each (the current HIP device). */
+OptAMD_Comm* OptAMD_CommCreateRccl(const void* id128, int rank, int nranks);
+void OptAMD_CommDestroy(OptAMD_Comm* comm);
+/* All ranks as threads of one process (shared device or peer devices): for testing
+ * the decomposition on one GPU. The rank handles belong to the group. */
+OptAMD_LocalGroup* OptAMD_LocalGroupCreate(int nranks);
+OptAMD_Comm* OptAMD_LocalGroupRank(OptAMD_LocalGroup* group, int rank);
+void OptAMD_LocalGroupDestroy(OptAMD_LocalGroup* group);
+
+/* Stencil radius of the plan's energy (rows of neighbour data a slab needs). */
+int OptAMD_PlanHalo(Opt_Plan* plan);
+/* Make this plan one rank of a row-slab decomposition of the dims given to
+ * Opt_ProblemPlan: it owns global rows [y_lo, y_hi). From then on every array in
+ * problemparams (and every vector passed to the OptAMD_ kernels) holds rows
+ * [y_lo - hl, y_hi + hh) with hl = min(halo, y_lo), hh = min(halo, H - y_hi); the
+ * caller fills the known arrays' halo rows, the plan refreshes the unknowns' halo rows
+ * itself. Energies, costs and dot products are global (summed over ranks).
+ * Returns 0 on success. */
+int OptAMD_PlanSetDecomposition(Opt_Plan* plan, OptAMD_Comm* comm, int y_lo, int y_hi);
+
 #ifdef __cplusplus
 }
 #endif

@@ -64,6 +64,14 @@ _SIGNATURES = [
     ("OptAMD_KernelReport", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int]),
     ("OptAMD_PlanStream", _VP, [_VP]),
     ("OptAMD_PlanIterations", ctypes.c_int, [_VP]),
+    ("OptAMD_RcclUniqueId", ctypes.c_int, [_VP]),
+    ("OptAMD_CommCreateRccl", _VP, [_VP, ctypes.c_int, ctypes.c_int]),
+    ("OptAMD_CommDestroy", None, [_VP]),
+    ("OptAMD_LocalGroupCreate", _VP, [ctypes.c_int]),
+    ("OptAMD_LocalGroupRank", _VP, [_VP, ctypes.c_int]),
+    ("OptAMD_LocalGroupDestroy", None, [_VP]),
+    ("OptAMD_PlanHalo", ctypes.c_int, [_VP]),
+    ("OptAMD_PlanSetDecomposition", ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int]),
 ]
 EXPORTED_SYMBOLS = [s[0] for s in _SIGNATURES]
 
@@ -78,6 +86,13 @@ def load_library(path: str = LIB_PATH):
             f"{path} not found: build the HIP runtime first "
             "(python -c 'import __graft_entry__ as g; g.build()' or `make`)"
         )
+    # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7, and whichever
+    # copy is loaded first serves both (same soname). Load torch's first when it is
+    # installed, so tensors allocated by torch and our kernels share one runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     for name, res, args in _SIGNATURES:
         fn = getattr(lib, name)
@@ -248,6 +263,14 @@ class OptSolver:
 
     def iterations(self) -> int:
         return self.lib.OptAMD_PlanIterations(self.plan)
+
+    def halo(self) -> int:
+        return self.lib.OptAMD_PlanHalo(self.plan)
+
+    def set_decomposition(self, comm, y_lo: int, y_hi: int):
+        """Own global rows [y_lo, y_hi) of a row-slab decomposition (include/opt_amd.h)."""
+        if self.lib.OptAMD_PlanSetDecomposition(self.plan, comm, y_lo, y_hi):
+            raise OptError("OptAMD_PlanSetDecomposition failed")
 
     def close(self):
         if getattr(self, "plan", None):

@@ -543,7 +543,8 @@ __global__ __launch_bounds__(kBlock) void iw_residual(Args<T> a, const T* __rest
                                                       ReduceSlot rs) {
     const long long N = a.dom.npix_mem();
     const T alpha = (T)(sc[i_num] / sc[i_den]);
-    const long long b = a.dom.off(0, a.dom.y_lo), e = a.dom.off(0, a.dom.y_hi);
+    const long long b0 = a.dom.off(0, a.dom.y_lo), e = a.dom.off(0, a.dom.y_hi);
+    const long long b = b0 + (b0 & 1);   // 16-B aligned pairs (slabs may start on an odd pixel)
     const long long npairs = (e - b) / 2;
     T acc = 0;
     const long long stride = (long long)gridDim.x * blockDim.x;
@@ -568,9 +569,10 @@ __global__ __launch_bounds__(kBlock) void iw_residual(Args<T> a, const T* __rest
             acc += ro.a * ro.a + ro.b * ro.b + ro.c * ro.c + ro.d * ro.d + rt.x * rt.x + rt.y * rt.y;
         }
     }
-    // odd pixel count: block 0 takes the last pixel
-    if (((e - b) & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-        const long long i = e - 1;
+    // unpaired pixels (odd start, odd count): block 0 threads 0 / 1
+    const long long single = (threadIdx.x == 0) ? ((b0 & 1) ? b0 : -1) : (((e - b) & 1) ? e - 1 : -1);
+    if (blockIdx.x == 0 && threadIdx.x < 2 && single >= 0) {
+        const long long i = single;
         const int f = a.flags[i];
         T r0 = r[2 * i] - alpha * Ap[2 * i], r1 = r[2 * i + 1] - alpha * Ap[2 * i + 1];
         T r2 = r[2 * N + i] - alpha * Ap[2 * N + i];
@@ -660,36 +662,31 @@ public:
             if (p.name == "w_fitSqrt") idx_wf_ = p.index;
             if (p.name == "w_regSqrt") idx_wr_ = p.index;
         }
-        const long long N = dom_.npix_mem();
-        nvec_ = 3 * N;
-        for (T** v : {&r_, &p0_, &p1_, &Ap_, &delta_})
-            *v = (T*)dmalloc(sizeof(T) * nvec_);
-        for (T* v : {r_, p0_, p1_, Ap_, delta_})
-            OPT_HIP_CHECK(hipMemset(v, 0, sizeof(T) * nvec_));
-        pre_ = (T*)dmalloc(sizeof(T) * N);   // angle channel only (Args::preO)
-        OPT_HIP_CHECK(hipMemset(pre_, 0, sizeof(T) * N));
-        flags_ = (uint8_t*)dmalloc(N);
-        OPT_HIP_CHECK(hipMemset(flags_, 0, N));
         rows_ = env_int("OPT_AMD_ROWS", 32);
         depth_ = env_int("OPT_AMD_DEPTH", 1);
-        nstrips_ = (dom_.W + iw::kStrip - 1) / iw::kStrip;
-        nrowblocks_ = (dom_.y_hi - dom_.y_lo + rows_ * 4 - 1) / (rows_ * 4);
         timer_.apply_name = apply_kernel_name();
-        red_.ensure(std::max(stencil_blocks(), 2048), 1, 64);
-        if (opts.host_buffers) {
-            hO_bytes_ = sizeof(T) * 2 * N;
-            dO_ = (T*)dmalloc(hO_bytes_);
-            dA_ = (T*)dmalloc(sizeof(T) * N);
-            dU_ = (float*)dmalloc(sizeof(float) * 2 * N);
-            dC_ = (float*)dmalloc(sizeof(float) * 2 * N);
-            dM_ = (float*)dmalloc(sizeof(float) * N);
-        }
+        allocate();
     }
     ~ImageWarpingPlan() override {
         OPT_HIP_CHECK(hipStreamSynchronize(stream_));
-        for (T* v : {r_, pre_, p0_, p1_, Ap_, delta_}) dfree(v);
-        dfree(flags_);
-        dfree(dO_); dfree(dA_); dfree(dU_); dfree(dC_); dfree(dM_);
+        release();
+    }
+
+    int halo() const override { return 1; }   // radius of the 4-neighbour stencil
+
+    std::string set_decomposition(Comm* comm, int y_lo, int y_hi) override {
+        if (opts_.host_buffers) return "row-slab decomposition needs backend_cuda (device arrays)";
+        if (y_lo < 0 || y_hi > dom_.H || y_hi - y_lo < halo()) return "invalid slab rows";
+        comm_ = comm;
+        OPT_HIP_CHECK(hipStreamSynchronize(stream_));
+        release();
+        dom_.y_lo = y_lo;
+        dom_.y_hi = y_hi;
+        dom_.y_mem0 = std::max(0, y_lo - halo());
+        dom_.mem_rows = std::min(dom_.H, y_hi + halo()) - dom_.y_mem0;
+        allocate();
+        initialised_ = false;
+        return "";
     }
 
     long long unknown_count() const override { return nvec_; }
@@ -699,7 +696,9 @@ public:
     void init(void** params) override {
         begin_call();
         bind(params, true);
+        exchange_unknowns();
         tbegin("iw_cost"); launch_cost(kScCost); tend();
+        allreduce(kScCost);
         prev_cost_ = read_scalar(kScCost);
         n_iter_ = 0;
         initialised_ = true;
@@ -715,10 +714,19 @@ public:
         }
         begin_call();
         bind(params, false);
+        exchange_unknowns();
         const int L = std::max(0, sp_.lIterations);
         red_.ensure(std::max(stencil_blocks(), 2048), 1, kScBase + 2 * (L + 2));
         // PCGInit1: r, pre, flags, rz[0]
         tbegin("iw_jtf"); launch_jtf(r_, pre_, rz(0)); tend();
+        allreduce(rz(0));
+        if (distributed()) {
+            std::vector<HaloPlane> pl;
+            add_vec_planes(pl, r_);
+            pl.push_back({(void*)pre_, sizeof(T) * dom_.W});
+            pl.push_back({(void*)flags_, (size_t)dom_.W});
+            exchange(pl);
+        }
         T* pcur = p0_;
         T* pprev = p1_;
         for (int i = 0; i < L; ++i) {
@@ -728,9 +736,17 @@ public:
             else if (i == 1) launch_apply<2, 1>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1));
             else launch_apply<2, 2>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1));
             tend();
+            allreduce(pap(i));
             tbegin("iw_residual");
             launch_residual(rz(i), pap(i), rz(i + 1));
             tend();
+            allreduce(rz(i + 1));
+            if (distributed() && i + 1 < L) {   // the next apply reads r and p_i in the halo rows
+                std::vector<HaloPlane> pl;
+                add_vec_planes(pl, r_);
+                add_vec_planes(pl, pcur);
+                exchange(pl);
+            }
         }
         // PCGLinearUpdate (with the last delta += alpha p) + cost
         if (L > 0) {
@@ -744,8 +760,10 @@ public:
                                    cur_A_, (const T*)delta_, (const T*)pcur, red_.scalars, rz(L - 1), pap(L - 1));
             OPT_HIP_CHECK(hipGetLastError());
             tend();
+            exchange_unknowns();
         }
         tbegin("iw_cost"); launch_cost(kScCost); tend();
+        allreduce(kScCost);
         const double c = read_scalar(kScCost);
         unbind_after_step();
         end_call();
@@ -758,7 +776,9 @@ public:
     int eval_jtf(void** params, void* r, void* pre, double* rzv) override {
         begin_call();
         bind(params, false);
+        exchange_unknowns();
         launch_jtf((T*)r, (T*)pre, kScTmp, true);
+        allreduce(kScTmp);
         *rzv = read_scalar(kScTmp);
         end_call();
         return 0;
@@ -766,8 +786,15 @@ public:
     int apply_jtj(void** params, const void* p, void* Ap, double* pAp) override {
         begin_call();
         bind(params, false);
+        exchange_unknowns();
+        if (distributed()) {
+            std::vector<HaloPlane> pl;
+            add_vec_planes(pl, (const T*)p);
+            exchange(pl);
+        }
         launch_flags();
         launch_apply<0, 0>((const T*)p, nullptr, kScTmp, 0, 0, 0, 0, (T*)Ap);
+        allreduce(kScTmp);
         *pAp = read_scalar(kScTmp);
         end_call();
         return 0;
@@ -775,7 +802,9 @@ public:
     double eval_cost(void** params) override {
         begin_call();
         bind(params, false);
+        exchange_unknowns();
         launch_cost(kScTmp);
+        allreduce(kScTmp);
         double c = read_scalar(kScTmp);
         end_call();
         return c;
@@ -801,6 +830,55 @@ public:
     }
 
 private:
+    void allocate() {
+        const long long N = dom_.npix_mem();
+        nvec_ = 3 * N;
+        for (T** v : {&r_, &p0_, &p1_, &Ap_, &delta_})
+            *v = (T*)dmalloc(sizeof(T) * nvec_);
+        for (T* v : {r_, p0_, p1_, Ap_, delta_})
+            OPT_HIP_CHECK(hipMemset(v, 0, sizeof(T) * nvec_));
+        pre_ = (T*)dmalloc(sizeof(T) * N);   // angle channel only (Args::preO)
+        OPT_HIP_CHECK(hipMemset(pre_, 0, sizeof(T) * N));
+        flags_ = (uint8_t*)dmalloc(N);
+        OPT_HIP_CHECK(hipMemset(flags_, 0, N));
+        nstrips_ = (dom_.W + iw::kStrip - 1) / iw::kStrip;
+        nrowblocks_ = (dom_.y_hi - dom_.y_lo + rows_ * 4 - 1) / (rows_ * 4);
+        red_.ensure(std::max(stencil_blocks(), 2048), 1, 64);
+        if (opts_.host_buffers) {
+            dO_ = (T*)dmalloc(sizeof(T) * 2 * N);
+            dA_ = (T*)dmalloc(sizeof(T) * N);
+            dU_ = (float*)dmalloc(sizeof(float) * 2 * N);
+            dC_ = (float*)dmalloc(sizeof(float) * 2 * N);
+            dM_ = (float*)dmalloc(sizeof(float) * N);
+        }
+    }
+    void release() {
+        for (T** v : {&r_, &pre_, &p0_, &p1_, &Ap_, &delta_, &dO_, &dA_}) { dfree(*v); *v = nullptr; }
+        for (float** v : {&dU_, &dC_, &dM_}) { dfree(*v); *v = nullptr; }
+        dfree(flags_);
+        flags_ = nullptr;
+    }
+
+    bool distributed() const { return comm_ && comm_->size() > 1; }
+    // sum a scalar slot over ranks (no-op on one rank)
+    void allreduce(int idx) {
+        if (distributed()) comm_->allreduce_sum(red_.scalars + idx, 1, stream_);
+    }
+    // halo planes of an unknown-layout vector [Offset.xy | Angle]
+    void add_vec_planes(std::vector<HaloPlane>& v, const T* x) const {
+        v.push_back({(void*)x, sizeof(T) * 2 * dom_.W});
+        v.push_back({(void*)(x + 2 * dom_.npix_mem()), sizeof(T) * dom_.W});
+    }
+    void exchange(const std::vector<HaloPlane>& planes) {
+        if (!distributed()) return;
+        tbegin("halo_exchange");
+        comm_->halo_exchange(planes, dom_, halo(), stream_);
+        tend();
+    }
+    void exchange_unknowns() {
+        exchange({{(void*)cur_O_, sizeof(T) * 2 * dom_.W}, {(void*)cur_A_, sizeof(T) * dom_.W}});
+    }
+
     // scalar slots in red_.scalars
     static constexpr int kScCost = 0, kScTmp = 1, kScBase = 4;
     int rz(int i) const { return kScBase + 2 * i; }
@@ -911,12 +989,12 @@ private:
     T *r_ = nullptr, *pre_ = nullptr, *p0_ = nullptr, *p1_ = nullptr, *Ap_ = nullptr, *delta_ = nullptr;
     uint8_t* flags_ = nullptr;
     int rows_ = 16, depth_ = 1, nstrips_ = 0, nrowblocks_ = 0;
+    Comm* comm_ = nullptr;
     float wf_ = 0, wr_ = 0;
     T *user_O_ = nullptr, *user_A_ = nullptr;
     T *cur_O_ = nullptr, *cur_A_ = nullptr;
     const float *cur_U_ = nullptr, *cur_C_ = nullptr, *cur_M_ = nullptr;
     // host-buffer staging (backend_cpu*)
-    size_t hO_bytes_ = 0;
     T *dO_ = nullptr, *dA_ = nullptr;
     float *dU_ = nullptr, *dC_ = nullptr, *dM_ = nullptr;
 };

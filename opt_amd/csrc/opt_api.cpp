@@ -213,4 +213,63 @@ int OptAMD_PlanIterations(Opt_Plan* plan) {
     return valid_plan(plan, "OptAMD_PlanIterations") ? plan->impl->iterations() : -1;
 }
 
+struct OptAMD_Comm {
+    optamd::Comm* impl;
+    bool owned;
+};
+struct OptAMD_LocalGroup {
+    optamd::LocalGroup* impl;
+    std::vector<OptAMD_Comm> ranks;
+};
+
+int OptAMD_RcclUniqueId(void* out128) {
+    std::string err;
+    if (!out128 || !optamd::rccl_unique_id(out128, &err)) {
+        fprintf(stderr, "[opt_amd] %s\n", err.c_str());
+        return 1;
+    }
+    return 0;
+}
+OptAMD_Comm* OptAMD_CommCreateRccl(const void* id128, int rank, int nranks) {
+    std::string err;
+    optamd::Comm* c = optamd::make_rccl_comm(id128, rank, nranks, &err);
+    if (!c) {
+        fprintf(stderr, "[opt_amd] %s\n", err.c_str());
+        return nullptr;
+    }
+    return new OptAMD_Comm{c, true};
+}
+void OptAMD_CommDestroy(OptAMD_Comm* comm) {
+    if (!comm) return;
+    if (comm->owned) { delete comm->impl; delete comm; }
+}
+OptAMD_LocalGroup* OptAMD_LocalGroupCreate(int nranks) {
+    if (nranks < 1) return nullptr;
+    auto* g = new OptAMD_LocalGroup();
+    g->impl = optamd::make_local_group(nranks);
+    for (int r = 0; r < nranks; ++r) g->ranks.push_back(OptAMD_Comm{optamd::local_group_rank(g->impl, r), false});
+    return g;
+}
+OptAMD_Comm* OptAMD_LocalGroupRank(OptAMD_LocalGroup* g, int rank) {
+    if (!g || rank < 0 || rank >= (int)g->ranks.size()) return nullptr;
+    return &g->ranks[rank];
+}
+void OptAMD_LocalGroupDestroy(OptAMD_LocalGroup* g) {
+    if (!g) return;
+    optamd::destroy_local_group(g->impl);
+    delete g;
+}
+int OptAMD_PlanHalo(Opt_Plan* plan) {
+    return valid_plan(plan, "OptAMD_PlanHalo") ? plan->impl->halo() : -1;
+}
+int OptAMD_PlanSetDecomposition(Opt_Plan* plan, OptAMD_Comm* comm, int y_lo, int y_hi) {
+    if (!valid_plan(plan, "OptAMD_PlanSetDecomposition") || !comm) return 1;
+    std::string err = plan->impl->set_decomposition(comm->impl, y_lo, y_hi);
+    if (!err.empty()) {
+        fprintf(stderr, "[opt_amd] OptAMD_PlanSetDecomposition: %s\n", err.c_str());
+        return 1;
+    }
+    return 0;
+}
+
 }  // extern "C"

@@ -6,6 +6,7 @@
 #include <memory>
 #include <string>
 #include <vector>
+#include "comm.h"
 #include "common.h"
 #include "problem.h"
 
@@ -87,6 +88,15 @@ public:
     virtual double eval_cost(void** params) = 0;
     virtual double time_apply(void** params, const void* p, void* Ap, int reps) = 0;
     virtual std::string apply_kernel_name() const = 0;
+    // Row-slab decomposition (image domains): this rank owns global rows [y_lo, y_hi)
+    // and the caller's arrays hold rows [y_lo - halo_lo, y_hi + halo_hi) with
+    // halo_lo = min(halo, y_lo), halo_hi = min(halo, H - y_hi). Returns an error text
+    // (empty on success).
+    virtual std::string set_decomposition(Comm* comm, int y_lo, int y_hi) {
+        (void)comm; (void)y_lo; (void)y_hi;
+        return "this energy family does not support row-slab decomposition";
+    }
+    virtual int halo() const { return 0; }
 
     void set_solver_param(const char* name, const void* value);
     int iterations() const { return n_iter_; }

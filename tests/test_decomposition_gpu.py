@@ -1,0 +1,103 @@
+"""GPU: the row-slab decomposed solver (halo exchange + global reductions) against
+the single-domain solve. Ranks are threads of this process sharing the one GPU
+(OptAMD_LocalGroup transport); the RCCL transport runs the same solver code."""
+import threading
+
+import numpy as np
+import pytest
+
+from opt_amd import api
+from opt_amd import distributed as dd
+from tests.iw_helpers import device_params, perturbed, solver
+
+pytestmark = pytest.mark.gpu
+
+
+def to_np(t):
+    return t.detach().cpu().numpy()
+
+
+def run_decomposed(w, world, nit, lit):
+    W, H = w["W"], w["H"]
+    lib = api.load_library()
+    group = lib.OptAMD_LocalGroupCreate(world)
+    results = [None] * world
+    errors = []
+    solvers, params, slabs = [], [], []
+    for r in range(world):
+        s = dd.slab(H, r, world, 1)
+        sv = solver(W, H)
+        assert sv.halo() == 1
+        sv.set_decomposition(lib.OptAMD_LocalGroupRank(group, r), s.y_lo, s.y_hi)
+        sv.set_solver_params({"nIterations": nit, "lIterations": lit})
+        solvers.append(sv)
+        params.append(device_params(dd.local_image_warping(w, s)))
+        slabs.append(s)
+
+    def body(r):
+        try:
+            results[r] = solvers[r].profiled_solve(params[r])
+        except Exception as e:  # pragma: no cover
+            errors.append(e)
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errors, errors
+    O = np.concatenate([dd.owned(to_np(params[r][0]), W, 2, slabs[r]) for r in range(world)])
+    A = np.concatenate([dd.owned(to_np(params[r][1]), W, 1, slabs[r]) for r in range(world)])
+    for sv in solvers:
+        sv.close()
+    lib.OptAMD_LocalGroupDestroy(group)
+    return results, O, A
+
+
+@pytest.mark.parametrize("world,W,H", [(1, 130, 90), (2, 130, 90), (3, 97, 61), (4, 256, 200)])
+def test_decomposed_solve_matches_single_domain(world, W, H):
+    w = perturbed(W, H, seed=21 + world)
+    s = solver(W, H)
+    prm = device_params(w)
+    s.set_solver_params({"nIterations": 3, "lIterations": 10})
+    ref = s.profiled_solve(prm)
+    costs, O, A = run_decomposed(w, world, 3, 10)
+    for r in range(world):
+        assert len(costs[r]) == 4
+        assert costs[r] == costs[0]          # every rank reports the global energy
+    if world == 1:
+        assert costs[0] == ref               # no exchange: bitwise the single-domain path
+        assert np.array_equal(O, to_np(prm[0])) and np.array_equal(A, to_np(prm[1]))
+    else:
+        np.testing.assert_allclose(costs[0], ref, rtol=1e-5)
+        ro = to_np(prm[0])
+        assert np.abs(O - ro).max() / np.abs(ro).max() < 1e-5
+        ra = to_np(prm[1])   # angles reach ~10 rad here: relative bound as in the oracle tests
+        assert np.abs(A - ra).max() < 1e-4 * max(1.0, np.abs(ra).max())
+
+
+def test_rccl_transport_single_rank_is_exact():
+    """The RCCL transport (dlopen'd librccl, communicator init, device all-reduce)
+    with one rank must reproduce the undecomposed solve bitwise."""
+    import ctypes
+
+    lib = api.load_library()
+    W, H = 128, 96
+    w = perturbed(W, H, seed=5)
+    s0 = solver(W, H)
+    p0 = device_params(w)
+    s0.set_solver_params({"nIterations": 2, "lIterations": 6})
+    ref = s0.profiled_solve(p0)
+    uid = (ctypes.c_uint8 * 128)()
+    assert lib.OptAMD_RcclUniqueId(uid) == 0
+    comm = lib.OptAMD_CommCreateRccl(uid, 0, 1)
+    assert comm
+    s1 = solver(W, H)
+    s1.set_decomposition(comm, 0, H)
+    p1 = device_params(w)
+    s1.set_solver_params({"nIterations": 2, "lIterations": 6})
+    got = s1.profiled_solve(p1)
+    s1.close()
+    lib.OptAMD_CommDestroy(comm)
+    assert got == ref
+    assert np.array_equal(to_np(p0[0]), to_np(p1[0])) and np.array_equal(to_np(p0[1]), to_np(p1[1]))
