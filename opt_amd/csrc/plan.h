@@ -131,6 +131,9 @@ std::unique_ptr<Plan> make_plan(const ProblemSpec& spec, const StateOptions& opt
 std::unique_ptr<Plan> make_image_warping_plan(const ProblemSpec&, const StateOptions&,
                                               const unsigned* dims, std::string* err);
 
+std::unique_ptr<Plan> make_poisson_plan(const ProblemSpec&, const StateOptions&,
+                                        const unsigned* dims, std::string* err);
+
 // Device-memory helpers (fail-stop).
 void* dmalloc(size_t bytes);
 void dfree(void* p);

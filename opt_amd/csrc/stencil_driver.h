@@ -1,0 +1,197 @@
+// stencil_driver.h — the GN / LM + PCG solver for image-domain energies whose kernels
+// are supplied by a family operator (`Op`). This is the reference's solver skeleton
+// (API/src/solverGPUGaussNewton.t: init :1766-1897, step :1913-2349) with its kernels
+// PCGInit1 / PCGFinalizeDiagonal / PCGStep2 / PCGStep3 / the residual-reset halves /
+// PCGLinearUpdate / savePreviousUnknowns / revertUpdate as flat HBM streams over the
+// unknown vector, and the family's stencil kernels (J^T F + diag, J^T J p, cost,
+// model cost) from Op. The LM q/zeta early exit is decided on the device: the PCG
+// iterations are all enqueued, and once zeta < q_tolerance every later kernel of the
+// step returns at entry (the reference blocks on a D2H copy of q each iteration,
+// :2211-2220).
+#pragma once
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+#include "pcg_kernels.h"
+#include "plan.h"
+
+namespace optamd {
+
+// Element -> pixel map of the unknown vector [img0 (ch0 x N) | img1 (ch1 x N) | ...]
+// (reference UnknownType contiguous allocation, o.t:1056-1100).
+struct VecLayout {
+    int nimg;
+    int ch[4];
+    long long off[5];
+    long long N;       // pixels in memory
+    __host__ __device__ long long pix(long long e) const {
+        int k = 0;
+        while (k + 1 < nimg && e >= off[k + 1]) ++k;
+        return (e - off[k]) / ch[k];
+    }
+};
+
+struct LMScalars {      // trust-region parameters the diagonal kernels need
+    float radius, min_diag, max_diag;
+};
+
+__device__ __forceinline__ bool stopped(const int* stop) { return stop && *stop; }
+
+template <typename T>
+__device__ __forceinline__ T guarded_invert(T d) {   // CERES form, :480-487
+    const T s = (T)1 + sqrt(d);
+    return (T)1 / (s * s);
+}
+
+// PCGInit1's preconditioner and direction (after the family's evalJTF):
+// pre = guardedInvert(diag) (guardedInvert(1) = 1/4 for UsePreconditioner(false)),
+// p = pre r, rz[0] = sum r.p. Excluded unknowns get pre = p = 0.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void gn_init_kernel(VecLayout L, const uint8_t* __restrict__ flags,
+                                                         const T* __restrict__ r, const T* __restrict__ diag,
+                                                         T* __restrict__ pre, T* __restrict__ p, int use_pre,
+                                                         ReduceSlot rs) {
+    const long long n = L.off[L.nimg];
+    T acc = 0;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (long long)gridDim.x * blockDim.x) {
+        const bool act = flags[L.pix(e)] & 1;
+        const T w = act ? guarded_invert(use_pre ? diag[e] : (T)1) : (T)0;
+        const T pp = w * r[e];
+        pre[e] = w;
+        p[e] = pp;
+        acc += r[e] * pp;
+    }
+    double v[1] = {(double)acc};
+    block_reduce_publish<1>(v, rs, blockIdx.x);
+}
+
+// LM: PCGSaveSSq (first step), PCGComputeCtC (diag / radius, o.t:2996-3030) and
+// PCGFinalizeDiagonal (:1061-1103): CtC = clamp(diag/radius, min_lm/(SSq radius),
+// max_lm/(SSq radius)); pre = 1/(CtC + radius diag/radius); b = r; p = pre r;
+// rz[0] = sum r.p (q = 0 since delta = 0).
+template <typename T, bool FIRST>
+__global__ __launch_bounds__(kBlock) void lm_init_kernel(VecLayout L, const uint8_t* __restrict__ flags,
+                                                         const T* __restrict__ r, const T* __restrict__ diag,
+                                                         T* __restrict__ SSq, T* __restrict__ CtC,
+                                                         T* __restrict__ pre, T* __restrict__ b, T* __restrict__ p,
+                                                         int use_pre, LMScalars lm, ReduceSlot rs) {
+    const long long n = L.off[L.nimg];
+    const T radius = (T)lm.radius;
+    const T inv_radius = (T)1 / radius;
+    T acc = 0;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (long long)gridDim.x * blockDim.x) {
+        const bool act = flags[L.pix(e)] & 1;
+        if (!act) {
+            if (FIRST) SSq[e] = 0;
+            CtC[e] = 0; pre[e] = 0; b[e] = 0; p[e] = 0;
+            continue;
+        }
+        T ssq;
+        if (FIRST) { ssq = guarded_invert(use_pre ? diag[e] : (T)1); SSq[e] = ssq; }
+        else ssq = SSq[e];
+        const T unclamped = diag[e] * inv_radius;
+        const T clampm = ((T)1 / ssq) / radius;
+        const T lo = (T)lm.min_diag * clampm, hi = (T)lm.max_diag * clampm;
+        const T c = std::min(std::max(unclamped, lo), hi);
+        const T w = (T)1 / (c + radius * unclamped);
+        const T re = r[e];
+        CtC[e] = c;
+        pre[e] = w;
+        b[e] = re;
+        p[e] = w * re;
+        acc += re * (w * re);
+    }
+    double v[1] = {(double)acc};
+    block_reduce_publish<1>(v, rs, blockIdx.x);
+}
+
+// PCGStep2 (:665-731): alpha = sc[i_num]/sc[i_den]; delta (+)= alpha p; r -= alpha Ap;
+// z = pre r (r when UsePreconditioner(false)); out[0] = sum z.r; LM: out[1] = q =
+// sum 1/2 delta.(r + b).
+template <typename T, bool FIRST, bool LM>
+__global__ __launch_bounds__(kBlock) void step2_kernel(long long n, const T* __restrict__ p,
+                                                       const T* __restrict__ Ap, const T* __restrict__ pre,
+                                                       const T* __restrict__ b, T* __restrict__ r,
+                                                       T* __restrict__ delta, const double* __restrict__ sc,
+                                                       int i_num, int i_den, int use_pre, const int* stop,
+                                                       ReduceSlot rs) {
+    if (stopped(stop)) return;
+    const T alpha = (T)(sc[i_num] / sc[i_den]);
+    T acc = 0, accq = 0;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (long long)gridDim.x * blockDim.x) {
+        const T d = FIRST ? alpha * p[e] : delta[e] + alpha * p[e];
+        const T rr = r[e] - alpha * Ap[e];
+        delta[e] = d;
+        r[e] = rr;
+        const T z = use_pre ? pre[e] * rr : rr;
+        acc += z * rr;
+        if (LM) accq += (T)0.5 * (d * (rr + b[e]));
+    }
+    double v[2] = {(double)acc, (double)accq};
+    if (LM) block_reduce_publish<2>(v, rs, blockIdx.x);
+    else { double v1[1] = {v[0]}; block_reduce_publish<1>(v1, rs, blockIdx.x); }
+}
+
+// PCGStep3 (:814-845): beta = sc[i_num]/sc[i_den]; p = z + beta p.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void step3_kernel(long long n, const T* __restrict__ pre,
+                                                       const T* __restrict__ r, T* __restrict__ p,
+                                                       const double* __restrict__ sc, int i_num, int i_den,
+                                                       int use_pre, const int* stop) {
+    if (stopped(stop)) return;
+    const T beta = (T)(sc[i_num] / sc[i_den]);
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (long long)gridDim.x * blockDim.x) {
+        const T z = use_pre ? pre[e] * r[e] : r[e];
+        p[e] = z + beta * p[e];
+    }
+}
+
+// Residual reset, LM only (:738-801): first half delta += alpha p ...
+template <typename T>
+__global__ __launch_bounds__(kBlock) void half1_kernel(long long n, const T* __restrict__ p,
+                                                       T* __restrict__ delta, const double* __restrict__ sc,
+                                                       int i_num, int i_den, const int* stop) {
+    if (stopped(stop)) return;
+    const T alpha = (T)(sc[i_num] / sc[i_den]);
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (long long)gridDim.x * blockDim.x)
+        delta[e] = delta[e] + alpha * p[e];
+}
+// ... second half, after Adelta = (J^T J + CtC) delta: r = b - Adelta, rz, q.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void half2_kernel(long long n, const T* __restrict__ Adelta,
+                                                       const T* __restrict__ b, const T* __restrict__ pre,
+                                                       const T* __restrict__ delta, T* __restrict__ r,
+                                                       int use_pre, const int* stop, ReduceSlot rs) {
+    if (stopped(stop)) return;
+    T acc = 0, accq = 0;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (long long)gridDim.x * blockDim.x) {
+        const T rr = b[e] - Adelta[e];
+        r[e] = rr;
+        const T z = use_pre ? pre[e] * rr : rr;
+        acc += z * rr;
+        accq += (T)0.5 * (delta[e] * (rr + b[e]));
+    }
+    double v[2] = {(double)acc, (double)accq};
+    block_reduce_publish<2>(v, rs, blockIdx.x);
+}
+
+// LM inner-loop exit test (:2211-2220), in opt_float arithmetic:
+// zeta = (lIter+1) (Q1 - Q0) / Q1; stop if zeta < q_tolerance, else Q0 = Q1.
+template <typename T>
+__global__ void zeta_kernel(const double* __restrict__ sc, int i_q1, double* __restrict__ q0, int liter,
+                            float q_tol, int* stop) {
+    if (*stop) return;
+    const T Q1 = (T)sc[i_q1], Q0 = (T)*q0;
+    const T zeta = (T)(liter + 1) * (Q1 - Q0) / Q1;
+    if (zeta < (T)q_tol) *stop = 1;
+    else *q0 = (double)Q1;
+}
+
+}  // namespace optamd

@@ -1,0 +1,321 @@
+// stencil_plan.h — host side of the generic image-domain GN / LM solver
+// (stencil_driver.h kernels + a family operator). Control flow follows the
+// reference's init / step exactly (API/src/solverGPUGaussNewton.t:1766-2349),
+// including the LM trust-region update and its early exits.
+#pragma once
+#include "stencil_driver.h"
+
+namespace optamd {
+
+// X += delta on the active pixels (PCGLinearUpdate, :854-859); LM also keeps the
+// previous unknowns (savePreviousUnknowns :882-887) for revertUpdate (:864-869).
+template <typename T, bool SAVE>
+__global__ __launch_bounds__(kBlock) void update_images_kernel(VecLayout L, const uint8_t* __restrict__ flags,
+                                                               T* x0, T* x1, const T* __restrict__ delta,
+                                                               T* __restrict__ prev, long long pix_lo,
+                                                               long long pix_hi) {
+    const long long n = L.off[L.nimg];
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (long long)gridDim.x * blockDim.x) {
+        const int k = (L.nimg > 1 && e >= L.off[1]) ? 1 : 0;
+        const long long local = e - L.off[k];
+        const long long px = local / L.ch[k];
+        if (px < pix_lo || px >= pix_hi || !(flags[px] & 1)) continue;
+        T* x = k ? x1 : x0;
+        const T v = x[local];
+        if (SAVE) prev[e] = v;
+        x[local] = v + delta[e];
+    }
+}
+template <typename T>
+__global__ __launch_bounds__(kBlock) void revert_images_kernel(VecLayout L, const uint8_t* __restrict__ flags,
+                                                               T* x0, T* x1, const T* __restrict__ prev,
+                                                               long long pix_lo, long long pix_hi) {
+    const long long n = L.off[L.nimg];
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (long long)gridDim.x * blockDim.x) {
+        const int k = (L.nimg > 1 && e >= L.off[1]) ? 1 : 0;
+        const long long local = e - L.off[k];
+        const long long px = local / L.ch[k];
+        if (px < pix_lo || px >= pix_hi || !(flags[px] & 1)) continue;
+        (k ? x1 : x0)[local] = prev[e];
+    }
+}
+
+// Op contract (see poisson.hip):
+//   using T; static constexpr const char* kName, kApplyName;
+//   Op(const ProblemSpec&, const StateOptions&, Domain)   — roles from declarations
+//   VecLayout layout() const; int halo() const;
+//   void bind(void** params, hipStream_t)                 — pointers + scalar params
+//   T* unknown(int k)                                     — device unknown image k
+//   void jtf(T* r, T* diag, uint8_t* flags, hipStream_t)  — r = -J^T F, diag(J^T J), flags
+//   void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot, hipStream_t)
+//                     — Ap = J^T J p (+ dadd p), sum p.Ap; returns early if *stop
+//   void cost(ReduceSlot, hipStream_t); void model_cost(const T* delta, ReduceSlot, hipStream_t)
+//   void unbind(hipStream_t)                               — copy unknowns back (host mode)
+template <class Op>
+class StencilPlan final : public Plan {
+public:
+    using T = typename Op::T;
+    StencilPlan(const ProblemSpec& spec, const StateOptions& opts, Domain dom)
+        : Plan(spec, opts), dom_(dom), op_(spec, opts, dom) {
+        lm_ = spec.lm();
+        L_ = op_.layout();
+        n_ = L_.off[L_.nimg];
+        for (T** v : {&r_, &diag_, &pre_, &p_, &Ap_, &delta_})
+            *v = (T*)dmalloc(sizeof(T) * n_);
+        if (lm_)
+            for (T** v : {&b_, &CtC_, &SSq_, &prev_, &Adelta_})
+                *v = (T*)dmalloc(sizeof(T) * n_);
+        for (T* v : {r_, diag_, pre_, p_, Ap_, delta_, b_, CtC_, SSq_, prev_, Adelta_})
+            if (v) OPT_HIP_CHECK(hipMemset(v, 0, sizeof(T) * n_));
+        flags_ = (uint8_t*)dmalloc(dom_.npix_mem());
+        OPT_HIP_CHECK(hipMemset(flags_, 0, dom_.npix_mem()));
+        stop_ = (int*)dmalloc(64);
+        OPT_HIP_CHECK(hipMemset(stop_, 0, 64));
+        timer_.apply_name = Op::kApplyName;
+        red_.ensure(std::max(op_.stencil_blocks(), 4096), 2, 64);
+    }
+    ~StencilPlan() override {
+        OPT_HIP_CHECK(hipStreamSynchronize(stream_));
+        for (T* v : {r_, diag_, pre_, p_, Ap_, delta_, b_, CtC_, SSq_, prev_, Adelta_}) dfree(v);
+        dfree(flags_);
+        dfree(stop_);
+    }
+
+    long long unknown_count() const override { return n_; }
+    std::string family() const override { return Op::kName; }
+    std::string apply_kernel_name() const override { return Op::kApplyName; }
+
+    void init(void** params) override {
+        begin_call();
+        op_.bind(params, stream_);
+        // reference init: LM parameters copied into the plan (:1863-1872), precompute,
+        // prevCost = cost; PCGInit1 is redone by every step
+        radius_ = sp_.trust_region_radius;
+        decrease_ = sp_.radius_decrease_factor;
+        tbegin("cost"); op_.cost(red_.slot(nb(), kScCost), stream_); tend();
+        prev_cost_ = read(kScCost);
+        n_iter_ = 0;
+        initialised_ = true;
+        end_call();
+    }
+
+    int step(void** params) override {
+        if (!initialised_) init(params);
+        if (n_iter_ >= sp_.nIterations) return 0;
+        begin_call();
+        op_.bind(params, stream_);
+        const int Lit = std::max(0, sp_.lIterations);
+        red_.ensure(std::max(op_.stencil_blocks(), 4096), 2, kScBase + 3 * (Lit + 2));
+        OPT_HIP_CHECK(hipMemsetAsync(stop_, 0, 64, stream_));
+        OPT_HIP_CHECK(hipMemsetAsync(delta_, 0, sizeof(T) * n_, stream_));   // PCGInit1: delta = 0
+        const int use_pre = spec_.use_preconditioner ? 1 : 0;
+        // PCGInit1 (+ LM diagonal)
+        tbegin("jtf"); op_.jtf(r_, diag_, flags_, stream_); tend();
+        if (!lm_) {
+            tbegin("gn_init");
+            hipLaunchKernelGGL((gn_init_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, L_, (const uint8_t*)flags_,
+                               (const T*)r_, (const T*)diag_, pre_, p_, use_pre, red_.slot(fg(), rz(0)));
+            tend();
+        } else {
+            LMScalars lm{radius_, sp_.min_lm_diagonal, sp_.max_lm_diagonal};
+            tbegin("lm_init");
+            if (n_iter_ == 0)
+                hipLaunchKernelGGL((lm_init_kernel<T, true>), dim3(fg()), dim3(kBlock), 0, stream_, L_,
+                                   (const uint8_t*)flags_, (const T*)r_, (const T*)diag_, SSq_, CtC_, pre_, b_, p_,
+                                   use_pre, lm, red_.slot(fg(), rz(0)));
+            else
+                hipLaunchKernelGGL((lm_init_kernel<T, false>), dim3(fg()), dim3(kBlock), 0, stream_, L_,
+                                   (const uint8_t*)flags_, (const T*)r_, (const T*)diag_, SSq_, CtC_, pre_, b_, p_,
+                                   use_pre, lm, red_.slot(fg(), rz(0)));
+            tend();
+            OPT_HIP_CHECK(hipMemsetAsync(red_.scalars + kScQ0, 0, sizeof(double), stream_));
+        }
+        OPT_HIP_CHECK(hipGetLastError());
+        const int* stop = lm_ ? stop_ : nullptr;
+        for (int i = 0; i < Lit; ++i) {
+            tbegin(Op::kApplyName);
+            op_.apply(p_, Ap_, lm_ ? CtC_ : nullptr, stop, red_.slot(nb(), pap(i)), stream_);
+            tend();
+            const bool reset = lm_ && ((i + 1) % std::max(1, sp_.residual_reset_period)) == 0;
+            if (reset) {
+                hipLaunchKernelGGL((half1_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)p_, delta_,
+                                   red_.scalars, rz(i), pap(i), stop);
+                op_.apply(delta_, Adelta_, CtC_, stop, red_.slot(nb(), kScTmp), stream_);
+                hipLaunchKernelGGL((half2_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)Adelta_,
+                                   (const T*)b_, (const T*)pre_, (const T*)delta_, r_, use_pre, stop,
+                                   red_.slot(fg(), rz(i + 1)));
+            } else {
+                tbegin("step2");
+                launch_step2(i == 0, rz(i), pap(i), rz(i + 1), stop);
+                tend();
+            }
+            tbegin("step3");
+            hipLaunchKernelGGL((step3_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)pre_,
+                               (const T*)r_, p_, red_.scalars, rz(i + 1), rz(i), use_pre, stop);
+            tend();
+            if (lm_)
+                hipLaunchKernelGGL((zeta_kernel<T>), dim3(1), dim3(1), 0, stream_, red_.scalars, q(i + 1),
+                                   red_.scalars + kScQ0, i, sp_.q_tolerance, stop_);
+            OPT_HIP_CHECK(hipGetLastError());
+        }
+        if (!lm_) {
+            if (Lit > 0) update(false);
+            tbegin("cost"); op_.cost(red_.slot(nb(), kScCost), stream_); tend();
+            const double c = read(kScCost);
+            op_.unbind(stream_);
+            end_call();
+            prev_cost_ = c;
+            ++n_iter_;
+            return 1;
+        }
+        // ---- LM: model cost, speculative update, accept / reject (:2229-2292)
+        tbegin("model_cost"); op_.model_cost(delta_, red_.slot(nb(), kScModel), stream_); tend();
+        if (Lit > 0) update(true);
+        tbegin("cost"); op_.cost(red_.slot(nb(), kScCost), stream_); tend();
+        double h[2];
+        OPT_HIP_CHECK(hipMemcpyAsync(h, red_.scalars + kScModel, sizeof(h), hipMemcpyDeviceToHost, stream_));
+        OPT_HIP_CHECK(hipStreamSynchronize(stream_));
+        const T model_cost = (T)h[0], new_cost = (T)h[1];
+        const T prev = (T)prev_cost_;
+        const T model_change = prev - model_cost;
+        const T cost_change = prev - new_cost;
+        const T rel = cost_change / model_change;
+        int ret = 1;
+        if (cost_change >= (T)0 && rel > (T)sp_.min_relative_decrease) {
+            const T abs_tol = prev * (T)sp_.function_tolerance;
+            if (cost_change <= abs_tol) {
+                ret = 0;   // function tolerance reached (prevCost is left as it was, :2254-2258)
+            } else {
+                const T q = rel;
+                const T min_factor = (T)(1.0 / 3.0);
+                const T tmp = (T)1 - (T)std::pow((double)((T)2 * q - (T)1), 3.0);
+                float rad = (float)((T)radius_ / std::max(min_factor, tmp));
+                radius_ = std::min(rad, sp_.max_trust_region_radius);
+                decrease_ = 2.0f;
+                prev_cost_ = (double)new_cost;
+            }
+        } else {
+            if (Lit > 0) revert();
+            radius_ = radius_ / decrease_;
+            decrease_ = 2.0f * decrease_;
+            if (radius_ <= sp_.min_trust_region_radius) ret = 0;
+        }
+        op_.unbind(stream_);
+        end_call();
+        if (ret) ++n_iter_;
+        return ret;
+    }
+
+    int eval_jtf(void** params, void* r, void* pre, double* rzv) override {
+        begin_call();
+        op_.bind(params, stream_);
+        op_.jtf((T*)r, diag_, flags_, stream_);
+        hipLaunchKernelGGL((gn_init_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, L_, (const uint8_t*)flags_,
+                           (const T*)r, (const T*)diag_, (T*)pre, p_, spec_.use_preconditioner ? 1 : 0,
+                           red_.slot(fg(), kScTmp));
+        *rzv = read(kScTmp);
+        end_call();
+        return 0;
+    }
+    int apply_jtj(void** params, const void* p, void* Ap, double* pAp) override {
+        begin_call();
+        op_.bind(params, stream_);
+        op_.jtf(r_, diag_, flags_, stream_);   // flags for the exclusion mask
+        op_.apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
+        *pAp = read(kScTmp);
+        end_call();
+        return 0;
+    }
+    double eval_cost(void** params) override {
+        begin_call();
+        op_.bind(params, stream_);
+        op_.cost(red_.slot(nb(), kScTmp), stream_);
+        const double c = read(kScTmp);
+        end_call();
+        return c;
+    }
+    double time_apply(void** params, const void* p, void* Ap, int reps) override {
+        begin_call();
+        op_.bind(params, stream_);
+        op_.jtf(r_, diag_, flags_, stream_);
+        hipEvent_t e0, e1;
+        OPT_HIP_CHECK(hipEventCreate(&e0));
+        OPT_HIP_CHECK(hipEventCreate(&e1));
+        op_.apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
+        OPT_HIP_CHECK(hipEventRecord(e0, stream_));
+        for (int i = 0; i < reps; ++i)
+            op_.apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
+        OPT_HIP_CHECK(hipEventRecord(e1, stream_));
+        OPT_HIP_CHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        OPT_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        end_call();
+        return 1000.0 * ms / std::max(1, reps);
+    }
+
+private:
+    static constexpr int kScCost = 1, kScModel = 0, kScTmp = 2, kScQ0 = 3, kScBase = 8;
+    // cost sits right after model cost so one 16-byte copy fetches both
+    // per PCG iteration: rz[i], q[i] (written together by step2 as a pair), pAp[i]
+    int rz(int i) const { return kScBase + 3 * i; }
+    int q(int i) const { return kScBase + 3 * i + 1; }
+    int pap(int i) const { return kScBase + 3 * i + 2; }
+    int nb() const { return op_.stencil_blocks(); }
+    int fg() const { return flat_grid(n_, 1); }
+
+    void launch_step2(bool first, int i_num, int i_den, int out, const int* stop) {
+        const int g = fg();
+        const int use_pre = spec_.use_preconditioner ? 1 : 0;
+        auto slot = red_.slot(g, out);
+#define S2(F, LMV)                                                                                     \
+    hipLaunchKernelGGL((step2_kernel<T, F, LMV>), dim3(g), dim3(kBlock), 0, stream_, n_, (const T*)p_,   \
+                       (const T*)Ap_, (const T*)pre_, (const T*)b_, r_, delta_, red_.scalars, i_num,    \
+                       i_den, use_pre, stop, slot)
+        if (first && lm_) S2(true, true);
+        else if (first) S2(true, false);
+        else if (lm_) S2(false, true);
+        else S2(false, false);
+#undef S2
+    }
+    void update(bool save) {
+        const long long lo = dom_.off(0, dom_.y_lo), hi = dom_.off(0, dom_.y_hi);
+        tbegin("update");
+        if (save)
+            hipLaunchKernelGGL((update_images_kernel<T, true>), dim3(fg()), dim3(kBlock), 0, stream_, L_,
+                               (const uint8_t*)flags_, op_.unknown(0), op_.unknown(1), (const T*)delta_, prev_, lo, hi);
+        else
+            hipLaunchKernelGGL((update_images_kernel<T, false>), dim3(fg()), dim3(kBlock), 0, stream_, L_,
+                               (const uint8_t*)flags_, op_.unknown(0), op_.unknown(1), (const T*)delta_, prev_, lo, hi);
+        OPT_HIP_CHECK(hipGetLastError());
+        tend();
+    }
+    void revert() {
+        const long long lo = dom_.off(0, dom_.y_lo), hi = dom_.off(0, dom_.y_hi);
+        hipLaunchKernelGGL((revert_images_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, L_,
+                           (const uint8_t*)flags_, op_.unknown(0), op_.unknown(1), (const T*)prev_, lo, hi);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    double read(int idx) {
+        double v;
+        OPT_HIP_CHECK(hipMemcpyAsync(&v, red_.scalars + idx, sizeof(double), hipMemcpyDeviceToHost, stream_));
+        OPT_HIP_CHECK(hipStreamSynchronize(stream_));
+        return v;
+    }
+
+    Domain dom_;
+    Op op_;
+    bool lm_ = false;
+    VecLayout L_;
+    long long n_ = 0;
+    T *r_ = nullptr, *diag_ = nullptr, *pre_ = nullptr, *p_ = nullptr, *Ap_ = nullptr, *delta_ = nullptr;
+    T *b_ = nullptr, *CtC_ = nullptr, *SSq_ = nullptr, *prev_ = nullptr, *Adelta_ = nullptr;
+    uint8_t* flags_ = nullptr;
+    int* stop_ = nullptr;
+    float radius_ = 1e4f, decrease_ = 2.0f;
+};
+
+}  // namespace optamd

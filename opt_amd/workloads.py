@@ -63,3 +63,34 @@ def image_warping(W: int, H: int, seed: int = 1234, n_handles: int = 9, hole: bo
 
 
 IMAGE_WARPING_ORDER = ["Offset", "Angle", "UrShape", "Constraints", "Mask", "w_fitSqrt", "w_regSqrt"]
+
+
+def poisson_image_editing(W: int, H: int, seed: int = 7):
+    """poisson_image_editing inputs (examples/poisson_image_editing/src/CombinedSolver.h:66-90).
+
+    X = a smooth seeded RGBA base image (alpha 255), T = a second seeded image to be
+    blended in, M = 0 (solve) inside a disk covering ~30 % of the image and 255 (fixed)
+    outside; X starts as the base image everywhere.
+    """
+    rng = np.random.default_rng(seed)
+    ys, xs = np.mgrid[0:H, 0:W].astype(np.float32)
+
+    def smooth_image(k):
+        img = np.zeros((H, W, 4), np.float32)
+        for c in range(3):
+            acc = np.zeros((H, W), np.float32)
+            for _ in range(k):
+                fx, fy, ph = rng.uniform(0.5, 4.0), rng.uniform(0.5, 4.0), rng.uniform(0, 2 * np.pi)
+                acc += np.sin(2 * np.pi * (fx * xs / W + fy * ys / H) + ph).astype(np.float32)
+            img[..., c] = 127.5 + 60.0 * acc / k
+        img[..., 3] = 255.0
+        return img
+
+    X = smooth_image(4)
+    T = smooth_image(3)
+    cx, cy, rad = 0.5 * W, 0.5 * H, 0.31 * min(W, H)
+    M = np.where((xs - cx) ** 2 + (ys - cy) ** 2 <= rad * rad, 0.0, 255.0).astype(np.float32)
+    return {"X": X.reshape(-1).copy(), "T": T.reshape(-1).copy(), "M": M.reshape(-1).copy(), "W": W, "H": H}
+
+
+POISSON_ORDER = ["X", "T", "M"]

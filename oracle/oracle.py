@@ -87,3 +87,47 @@ def iw_solve(w, n_iter, l_iter, nthreads=1, want_scalars=False):
                            _f(w["Mask"]), w["w_fitSqrt"], w["w_regSqrt"], n_iter, l_iter, nthreads,
                            costs.ctypes.data_as(_D), sc.ctypes.data_as(_D) if sc is not None else None)
     return O, A, costs, (sc.reshape(n_iter, l_iter, 3) if sc is not None else None)
+
+
+# ------------------------------------------------------------ poisson_image_editing
+def _pie_lib():
+    lib = load()
+    if not getattr(lib, "_pie", False):
+        i, d = ctypes.c_int, ctypes.c_double
+        lib.oracle_pie_cost.restype = d
+        lib.oracle_pie_cost.argtypes = [i, i, _F, _F, _F]
+        lib.oracle_pie_jtf.restype = None
+        lib.oracle_pie_jtf.argtypes = [i, i, _F, _F, _F, _F, _F]
+        lib.oracle_pie_apply.restype = d
+        lib.oracle_pie_apply.argtypes = [i, i, _F, _F, _F, _F, _F]
+        lib.oracle_pie_solve.restype = i
+        lib.oracle_pie_solve.argtypes = [i, i, _F, _F, _F, i, i, i, _D]
+        lib._pie = True
+    return lib
+
+
+def pie_cost(w):
+    return _pie_lib().oracle_pie_cost(w["W"], w["H"], _f(w["X"]), _f(w["T"]), _f(w["M"]))
+
+
+def pie_jtf(w):
+    n = 4 * w["W"] * w["H"]
+    r = np.zeros(n, np.float32)
+    dg = np.zeros(n, np.float32)
+    _pie_lib().oracle_pie_jtf(w["W"], w["H"], _f(w["X"]), _f(w["T"]), _f(w["M"]), _f(r), _f(dg))
+    return r, dg
+
+
+def pie_apply(w, p):
+    p = np.ascontiguousarray(p, np.float32)
+    Ap = np.zeros_like(p)
+    pAp = _pie_lib().oracle_pie_apply(w["W"], w["H"], _f(w["X"]), _f(w["T"]), _f(w["M"]), _f(p), _f(Ap))
+    return Ap, pAp
+
+
+def pie_solve(w, n_iter, l_iter, lm=False):
+    X = w["X"].copy()
+    costs = np.zeros(n_iter + 1, np.float64)
+    k = _pie_lib().oracle_pie_solve(w["W"], w["H"], _f(X), _f(w["T"]), _f(w["M"]), int(lm), n_iter, l_iter,
+                                    costs.ctypes.data_as(_D))
+    return X, costs[: k + 1]
