@@ -35,6 +35,7 @@
 #include <string>
 #include "plan.h"
 #include "pcg_kernels.h"
+#include "stencil_plan.h"
 
 namespace optamd {
 namespace iw {
@@ -251,13 +252,19 @@ __device__ __forceinline__ PRow<T> finish_prow(const Args<T>& a, const PRaw<T>& 
 //         iteration's delta update (PCGStep2's delta += alpha p, :680), alpha =
 //         sc[ia_num]/sc[ia_den]: DM 1 delta = alpha p_old, DM 2 delta += alpha p_old.
 // Always: sc[rs.out] = sum p.Ap over active pixels (the alpha denominator).
-template <typename T, int MODE, int DM, int DEPTH>
+// LMX (MODE 0 only, the generic LM driver): Ap += dadd p (the CtC term of
+// PCGStep1's LM variant, :617-622) and the whole grid returns at entry once the
+// device-side zeta test has set *stop.
+template <typename T, int MODE, int DM, int DEPTH, bool LMX = false>
 __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restrict__ pin,
                                                    const T* __restrict__ r,
                                                    const T* __restrict__ pre, T* __restrict__ pout,
                                                    T* __restrict__ Ap, T* __restrict__ delta,
                                                    const double* __restrict__ sc, int ib_num,
-                                                   int ib_den, int ia_num, int ia_den, ReduceSlot rs) {
+                                                   int ib_den, int ia_num, int ia_den, ReduceSlot rs,
+                                                   const T* __restrict__ dadd = nullptr,
+                                                   const int* stop = nullptr) {
+    if (LMX && stop && *stop) return;
     const WaveGeom g = geom(a);
     const T beta = (MODE == 2) ? (T)(sc[ib_num] / sc[ib_den]) : (T)0;
     const T alpha = (MODE == 2 && DM != 0) ? (T)(sc[ia_num] / sc[ia_den]) : (T)0;
@@ -309,6 +316,9 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
             if (!cur.act) { aox = 0; aoy = 0; aot = 0; }
             if (g.out_lane) {
                 const long long i = a.dom.off(g.x, y);
+                if (LMX && dadd) {
+                    aox += dadd[2 * i] * cur.px; aoy += dadd[2 * i + 1] * cur.py; aot += dadd[2 * N + i] * cur.pt;
+                }
                 Ap[2 * i] = aox; Ap[2 * i + 1] = aoy; Ap[2 * N + i] = aot;
                 if (MODE != 0) { pout[2 * i] = cur.px; pout[2 * i + 1] = cur.py; pout[2 * N + i] = cur.pt; }
                 if (MODE == 2 && DM != 0) {
@@ -397,9 +407,11 @@ __device__ __forceinline__ VRow<T> finish_vrow(const VRaw<T>& r) {
 // ------------------------------------------------------------- J^T F kernel
 // r = -J^T F, pre = 1/(1+sqrt(diag J^T J))^2 (1/(1+1)^2 when UsePreconditioner(false)),
 // flags, and sc[rs.out] = sum r.(pre r) over active pixels (alpha numerator).
-// FULL_PRE: write all three preconditioner channels (OptAMD_EvalJTF layout); otherwise
-// only the angle channel (the solver's compressed layout, Args::preO).
-template <typename T, bool FULL_PRE>
+// OUT 0: only the angle channel of pre (the solver's compressed layout, Args::preO);
+// OUT 1: all three preconditioner channels (OptAMD_EvalJTF layout);
+// OUT 2: diag(J^T J) in all three channels instead of pre, no reduction (the generic
+//        GN/LM driver, which forms pre / the LM diagonal itself).
+template <typename T, int OUT>
 __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T* __restrict__ pre,
                                                  ReduceSlot rs) {
     const WaveGeom g = geom(a);
@@ -471,8 +483,18 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
                     dot += rx * (wo * rx) + ry * (wo * ry) + rt * (wt * rt);
                 }
                 r[2 * i] = rx; r[2 * i + 1] = ry; r[2 * N + i] = rt;
-                if (FULL_PRE) { pre[2 * i] = wo; pre[2 * i + 1] = wo; pre[2 * N + i] = wt; }
-                else pre[i] = wt;
+                if (OUT == 2) {
+                    // the reference sums (d e/d O)^2 = wr^2 once per valid residual, then wf^2
+                    T dox = 0;
+                    for (int j = 0; j < 2 * nv; ++j) dox += wr2;
+                    if (cur.fit) dox += wf * wf;
+                    if (!cur.act) { dox = 0; dt = 0; }
+                    pre[2 * i] = dox; pre[2 * i + 1] = dox; pre[2 * N + i] = dt;
+                } else if (OUT == 1) {
+                    pre[2 * i] = wo; pre[2 * i + 1] = wo; pre[2 * N + i] = wt;
+                } else {
+                    pre[i] = wt;
+                }
             }
             inup_x = epy_x; inup_y = epy_y;
             my_x = edn_x; my_y = edn_y;
@@ -483,6 +505,7 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
             dn = finish_vrow<T, true>(nx);
         }
     }
+    if (OUT == 2) return;
     double v[1] = {(double)dot};
     block_reduce_publish<1>(v, rs, blockIdx.x);
 }
@@ -526,6 +549,51 @@ __global__ __launch_bounds__(kBlock) void iw_cost(Args<T> a, ReduceSlot rs) {
             up = cur; cur = dn;
             dn = finish_vrow<T, false>(nx);
         }
+    }
+    double v[1] = {(double)acc};
+    block_reduce_publish<1>(v, rs, blockIdx.x);
+}
+
+// ----------------------------------------------------------- model cost kernel
+// LM only, once per step: sc[rs.out] = sum over active pixels of
+// 1/2 (sum_s |e_reg(k,s) + J_reg(k,s) delta|^2 + |e_fit(k) + wf delta_O(k)|^2)
+// (createmodelcost, o.t:2915-2943). Strip geometry (same grid, hence the same
+// reduction slot, as the other stencil kernels); neighbours are direct loads (L2 hits).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void iw_model_cost(Args<T> a, const T* __restrict__ delta, ReduceSlot rs) {
+    const WaveGeom g = geom(a);
+    const long long N = a.dom.npix_mem();
+    const int x = g.x;
+    T acc = 0;
+    for (int y = g.y0; y < g.y1 && g.out_lane; ++y) {
+        const long long k = a.dom.off(x, y);
+        if (a.M[k] != 0.f) continue;
+        const T ox = a.O[2 * k], oy = a.O[2 * k + 1];
+        T c, s;
+        sc_of(a.A[k], &c, &s);
+        const float ux = a.U[2 * k], uy = a.U[2 * k + 1];
+        const T dkx = delta[2 * k], dky = delta[2 * k + 1], dkt = delta[2 * N + k];
+        constexpr int DX[4] = {1, -1, 0, 0}, DY[4] = {0, 0, 1, -1};
+        T sum = 0;
+        for (int d = 0; d < 4; ++d) {
+            const int tx = x + DX[d], ty = y + DY[d];
+            if (!present(a.dom, tx, ty)) continue;
+            const long long t = a.dom.off(tx, ty);
+            if (a.M[t] != 0.f) continue;
+            T ex, ey, ax, ay, jx, jy;
+            eedge(ox, oy, c, s, ux, uy, a.O[2 * t], a.O[2 * t + 1], a.U[2 * t], a.U[2 * t + 1], true, a.wr,
+                  ex, ey, ax, ay);
+            jedge(dkx, dky, dkt, c, s, ux, uy, delta[2 * t], delta[2 * t + 1], a.U[2 * t], a.U[2 * t + 1], true,
+                  a.wr, jx, jy, ax, ay);
+            ex += jx; ey += jy;
+            sum += ex * ex + ey * ey;
+        }
+        const float cx = a.C[2 * k], cy = a.C[2 * k + 1];
+        if (cx >= 0.f && cy >= 0.f) {
+            const T fx = a.wf * (ox - (T)cx) + a.wf * dkx, fy = a.wf * (oy - (T)cy) + a.wf * dky;
+            sum += fx * fx + fy * fy;
+        }
+        acc += (T)0.5 * sum;
     }
     double v[1] = {(double)acc};
     block_reduce_publish<1>(v, rs, blockIdx.x);
@@ -945,10 +1013,10 @@ private:
     void launch_jtf(T* r, T* pre, int sc_out, bool full_pre = false) {
         const int nb = stencil_blocks();
         if (full_pre)
-            hipLaunchKernelGGL((iw::iw_jtf<T, true>), dim3(nb), dim3(kBlock), 0, stream_, args(), r, pre,
+            hipLaunchKernelGGL((iw::iw_jtf<T, 1>), dim3(nb), dim3(kBlock), 0, stream_, args(), r, pre,
                                red_.slot(nb, sc_out));
         else
-            hipLaunchKernelGGL((iw::iw_jtf<T, false>), dim3(nb), dim3(kBlock), 0, stream_, args(), r, pre,
+            hipLaunchKernelGGL((iw::iw_jtf<T, 0>), dim3(nb), dim3(kBlock), 0, stream_, args(), r, pre,
                                red_.slot(nb, sc_out));
         OPT_HIP_CHECK(hipGetLastError());
     }
@@ -999,6 +1067,122 @@ private:
     float *dU_ = nullptr, *dC_ = nullptr, *dM_ = nullptr;
 };
 
+// ====================================================== operator for LM
+// image_warping under the generic GN/LM driver (stencil_plan.h): used for LMGPU, where
+// the trust-region diagonal, the residual resets and the device-side zeta exit live in
+// the driver and the family supplies J^T F + diag, J^T J p (+ CtC p), cost and model
+// cost. Same strip kernels as the GN plan above.
+template <typename TT>
+class ImageWarpingOp {
+public:
+    using T = TT;
+    static constexpr const char* kName = "image_warping";
+    static constexpr const char* kApplyName = "iw_apply";
+    ImageWarpingOp(const ProblemSpec& spec, const StateOptions& opts, Domain dom) : dom_(dom), opts_(opts) {
+        idx_O_ = spec.unknown(0)->index;
+        idx_A_ = spec.unknown(1)->index;
+        idx_U_ = spec.array(0)->index;
+        idx_C_ = spec.array(1)->index;
+        idx_M_ = spec.array(2)->index;
+        std::vector<DeclParam> ps = spec.params;
+        std::sort(ps.begin(), ps.end(), [](auto& x, auto& y) { return x.index < y.index; });
+        idx_wf_ = ps[0].index;
+        idx_wr_ = ps[1].index;
+        for (auto& p : ps) {
+            if (p.name == "w_fitSqrt") idx_wf_ = p.index;
+            if (p.name == "w_regSqrt") idx_wr_ = p.index;
+        }
+        use_pre_ = spec.use_preconditioner;
+        rows_ = env_int("OPT_AMD_ROWS", 32);
+        nstrips_ = (dom_.W + iw::kStrip - 1) / iw::kStrip;
+        nrowblocks_ = (dom_.y_hi - dom_.y_lo + rows_ * 4 - 1) / (rows_ * 4);
+        const long long N = dom_.npix_mem();
+        if (opts.host_buffers) {
+            dO_ = (T*)dmalloc(sizeof(T) * 2 * N);
+            dA_ = (T*)dmalloc(sizeof(T) * N);
+            dU_ = (float*)dmalloc(sizeof(float) * 2 * N);
+            dC_ = (float*)dmalloc(sizeof(float) * 2 * N);
+            dM_ = (float*)dmalloc(sizeof(float) * N);
+        }
+    }
+    ~ImageWarpingOp() {
+        dfree(dO_); dfree(dA_);
+        for (float* v : {dU_, dC_, dM_}) dfree(v);
+    }
+    VecLayout layout() const {
+        VecLayout L{};
+        const long long N = dom_.npix_mem();
+        L.nimg = 2;
+        L.ch[0] = 2; L.ch[1] = 1;
+        L.off[0] = 0; L.off[1] = 2 * N; L.off[2] = 3 * N;
+        L.N = N;
+        return L;
+    }
+    int halo() const { return 1; }
+    int stencil_blocks() const { return nstrips_ * nrowblocks_; }
+    void bind(void** params, hipStream_t s) {
+        a_.wf = (T)*(const float*)params[idx_wf_];
+        a_.wr = (T)*(const float*)params[idx_wr_];
+        user_O_ = (T*)params[idx_O_];
+        user_A_ = (T*)params[idx_A_];
+        if (!opts_.host_buffers) {
+            a_.O = user_O_; a_.A = user_A_;
+            a_.U = (const float*)params[idx_U_];
+            a_.C = (const float*)params[idx_C_];
+            a_.M = (const float*)params[idx_M_];
+        } else {
+            const long long N = dom_.npix_mem();
+            OPT_HIP_CHECK(hipMemcpyAsync(dO_, user_O_, sizeof(T) * 2 * N, hipMemcpyHostToDevice, s));
+            OPT_HIP_CHECK(hipMemcpyAsync(dA_, user_A_, sizeof(T) * N, hipMemcpyHostToDevice, s));
+            OPT_HIP_CHECK(hipMemcpyAsync(dU_, params[idx_U_], sizeof(float) * 2 * N, hipMemcpyHostToDevice, s));
+            OPT_HIP_CHECK(hipMemcpyAsync(dC_, params[idx_C_], sizeof(float) * 2 * N, hipMemcpyHostToDevice, s));
+            OPT_HIP_CHECK(hipMemcpyAsync(dM_, params[idx_M_], sizeof(float) * N, hipMemcpyHostToDevice, s));
+            a_.O = dO_; a_.A = dA_; a_.U = dU_; a_.C = dC_; a_.M = dM_;
+        }
+        a_.dom = dom_;
+        a_.use_pre = use_pre_ ? 1 : 0;
+        a_.nstrips = nstrips_; a_.nrowblocks = nrowblocks_; a_.rows = rows_;
+        for (int f = 0; f < 2; ++f)
+            for (int v = 0; v < 5; ++v) a_.preO[f][v] = 0;   // MODE 0 never reads them
+    }
+    void unbind(hipStream_t s) {
+        if (!opts_.host_buffers) return;
+        const long long N = dom_.npix_mem();
+        OPT_HIP_CHECK(hipMemcpyAsync(user_O_, dO_, sizeof(T) * 2 * N, hipMemcpyDeviceToHost, s));
+        OPT_HIP_CHECK(hipMemcpyAsync(user_A_, dA_, sizeof(T) * N, hipMemcpyDeviceToHost, s));
+    }
+    T* unknown(int k) { return k == 0 ? (T*)a_.O : (T*)a_.A; }
+    void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
+        a_.flags = flags;
+        hipLaunchKernelGGL((iw::iw_jtf<T, 2>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, r, diag, ReduceSlot{});
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
+        hipLaunchKernelGGL((iw::iw_apply<T, 0, 0, 1, true>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p,
+                           (const T*)nullptr, (const T*)nullptr, (T*)nullptr, Ap, (T*)nullptr,
+                           (const double*)nullptr, 0, 0, 0, 0, rs, dadd, stop);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    void cost(ReduceSlot rs, hipStream_t s) {
+        hipLaunchKernelGGL(iw::iw_cost<T>, dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, rs);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    void model_cost(const T* delta, ReduceSlot rs, hipStream_t s) {
+        hipLaunchKernelGGL(iw::iw_model_cost<T>, dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, delta, rs);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+
+private:
+    Domain dom_;
+    StateOptions opts_;
+    int idx_O_, idx_A_, idx_U_, idx_C_, idx_M_, idx_wf_, idx_wr_;
+    bool use_pre_ = true;
+    int rows_ = 32, nstrips_ = 0, nrowblocks_ = 0;
+    iw::Args<T> a_{};
+    T *user_O_ = nullptr, *user_A_ = nullptr, *dO_ = nullptr, *dA_ = nullptr;
+    float *dU_ = nullptr, *dC_ = nullptr, *dM_ = nullptr;
+};
+
 std::unique_ptr<Plan> make_image_warping_plan(const ProblemSpec& spec, const StateOptions& opts,
                                               const unsigned* dims, std::string* err) {
     // Dim("W",0), Dim("H",1)
@@ -1008,6 +1192,12 @@ std::unique_ptr<Plan> make_image_warping_plan(const ProblemSpec& spec, const Sta
         if (d.name == spec.unknown(0)->dims[1]) H = dims[d.index];
     }
     if (W == 0 || H == 0) { *err = "image_warping: zero-sized domain"; return nullptr; }
+    if (spec.lm()) {
+        Domain dom{(int)W, (int)H, 0, (int)H, 0, (int)H};
+        if (opts.double_precision)
+            return std::unique_ptr<Plan>(new StencilPlan<ImageWarpingOp<double>>(spec, opts, dom));
+        return std::unique_ptr<Plan>(new StencilPlan<ImageWarpingOp<float>>(spec, opts, dom));
+    }
     if (opts.double_precision)
         return std::unique_ptr<Plan>(new ImageWarpingPlan<double>(spec, opts, W, H));
     return std::unique_ptr<Plan>(new ImageWarpingPlan<float>(spec, opts, W, H));

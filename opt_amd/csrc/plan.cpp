@@ -146,7 +146,7 @@ void Plan::end_call() {
 
 std::unique_ptr<Plan> make_plan(const ProblemSpec& spec, const StateOptions& opts,
                                 const unsigned* dims, std::string* err) {
-    if (spec.family == "image_warping" && !spec.lm()) return make_image_warping_plan(spec, opts, dims, err);
+    if (spec.family == "image_warping") return make_image_warping_plan(spec, opts, dims, err);
     if (spec.family == "poisson_image_editing") return make_poisson_plan(spec, opts, dims, err);
     *err = "energy family '" + spec.family + "' has no kernels in this build";
     return nullptr;

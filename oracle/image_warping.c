@@ -349,3 +349,119 @@ void oracle_iw_residuals(int W, int H, const float* O, const float* A, const flo
                 for (int c = 0; c < 2; ++c) o[8 + c] = wf * (O[2 * k + c] - C[2 * k + c]);
         }
 }
+
+/* ------------------------------------------------ generic GN / LM (solver_impl.h) ---- */
+/* Vector layout [Offset.xy * N | Angle * N]; an element is active iff its pixel's Mask
+ * is 0. Model cost = 1/2 sum (F + J delta)^2 over the residuals of active pixels
+ * (createmodelcost, API/src/o.t:2915-2943). */
+#include "solver.h"
+typedef struct {
+    iw_problem P;
+    float *O, *A, *prevO, *prevA;
+    int nthreads;
+} iw_ctx;
+
+static double iwg_cost(void* v) {
+    iw_ctx* c = (iw_ctx*)v;
+    return run_slabs(&c->P, c->nthreads, w_cost, NULL, NULL, NULL);
+}
+static void iwg_jtf(void* v, float* r, float* diag) {
+    iw_ctx* c = (iw_ctx*)v;
+    const iw_problem* P = &c->P;
+    const int N = P->W * P->H;
+    for (int y = 0; y < P->H; ++y)
+        for (int x = 0; x < P->W; ++x) {
+            const int k = y * P->W + x;
+            float F[3] = {0.f, 0.f, 0.f}, D[3] = {0.f, 0.f, 0.f};
+            if (!excluded(P, x, y)) jtf_px(P, x, y, F, D);
+            r[2 * k] = -F[0]; r[2 * k + 1] = -F[1]; r[2 * N + k] = -F[2];
+            diag[2 * k] = D[0]; diag[2 * k + 1] = D[1]; diag[2 * N + k] = D[2];
+        }
+}
+static double iwg_apply(void* v, const float* p, float* Ap) {
+    iw_ctx* c = (iw_ctx*)v;
+    return run_slabs(&c->P, c->nthreads, w_apply, p, Ap, NULL);
+}
+static double iwg_model(void* v, const float* d) {
+    iw_ctx* c = (iw_ctx*)v;
+    const iw_problem* P = &c->P;
+    const int N = P->W * P->H;
+    double acc = 0.0;
+    for (int y = 0; y < P->H; ++y)
+        for (int x = 0; x < P->W; ++x) {
+            if (excluded(P, x, y)) continue;
+            const int k = y * P->W + x;
+            float sum = 0.f;
+            for (int s = 0; s < 4; ++s)
+                for (int ch = 0; ch < 2; ++ch) {
+                    reg_res r = reg_residual(P, x, y, s, ch);
+                    if (!r.valid) continue;
+                    const int t = (y + SY[s]) * P->W + (x + SX[s]);
+                    const float e = r.value + (r.dOc * d[2 * k + ch] + r.dOsc * d[2 * t + ch] + r.dA * d[2 * N + k]);
+                    sum += e * e;
+                }
+            if (fit_valid(P, k))
+                for (int ch = 0; ch < 2; ++ch) {
+                    const float e = P->wf * (P->O[2 * k + ch] - P->C[2 * k + ch]) + P->wf * d[2 * k + ch];
+                    sum += e * e;
+                }
+            acc += 0.5f * sum;
+        }
+    return acc;
+}
+static void iwg_update(void* v, const float* d) {
+    iw_ctx* c = (iw_ctx*)v;
+    const int N = c->P.W * c->P.H;
+    for (int k = 0; k < N; ++k) {
+        if (c->P.M[k] != 0.f) continue;
+        c->O[2 * k] += d[2 * k];
+        c->O[2 * k + 1] += d[2 * k + 1];
+        c->A[k] += d[2 * N + k];
+    }
+}
+static void iwg_save(void* v) {
+    iw_ctx* c = (iw_ctx*)v;
+    const int N = c->P.W * c->P.H;
+    memcpy(c->prevO, c->O, sizeof(float) * 2 * N);
+    memcpy(c->prevA, c->A, sizeof(float) * N);
+}
+static void iwg_revert(void* v) {
+    iw_ctx* c = (iw_ctx*)v;
+    const int N = c->P.W * c->P.H;
+    for (int k = 0; k < N; ++k) {
+        if (c->P.M[k] != 0.f) continue;
+        c->O[2 * k] = c->prevO[2 * k];
+        c->O[2 * k + 1] = c->prevO[2 * k + 1];
+        c->A[k] = c->prevA[k];
+    }
+}
+
+/* GN (lm = 0) or LM solve through the generic loop; returns completed steps. */
+int oracle_iw_solve_generic(int W, int H, float* O, float* A, const float* U, const float* C, const float* M,
+                            float wf, float wr, int lm, int nIter, int lIter, int nthreads, double* costs) {
+    const int N = W * H;
+    iw_ctx c = {{W, H, O, A, U, C, M, wf, wr}, O, A, NULL, NULL, nthreads};
+    c.prevO = (float*)malloc(sizeof(float) * 2 * N);
+    c.prevA = (float*)malloc(sizeof(float) * N);
+    unsigned char* act = (unsigned char*)malloc((size_t)3 * N);
+    for (int k = 0; k < N; ++k) act[2 * k] = act[2 * k + 1] = act[2 * N + k] = M[k] == 0.f;
+    oracle_problem_float P = {3LL * N, act, 1, &c, iwg_cost, iwg_jtf, iwg_apply, iwg_model,
+                              iwg_update, iwg_save, iwg_revert};
+    oracle_params sp = oracle_default_params();
+    sp.nIterations = nIter;
+    sp.lIterations = lIter;
+    const int k = oracle_solve_f32(&P, lm, &sp, costs);
+    free(act); free(c.prevO); free(c.prevA);
+    return k;
+}
+/* J^T F and the raw diagonal (generic layout), for the LM kernel tests */
+void oracle_iw_jtf_diag(int W, int H, const float* O, const float* A, const float* U, const float* C,
+                        const float* M, float wf, float wr, float* r, float* diag) {
+    iw_ctx c = {{W, H, O, A, U, C, M, wf, wr}, (float*)O, (float*)A, NULL, NULL, 1};
+    iwg_jtf(&c, r, diag);
+}
+double oracle_iw_model_cost(int W, int H, const float* O, const float* A, const float* U, const float* C,
+                            const float* M, float wf, float wr, const float* d) {
+    iw_ctx c = {{W, H, O, A, U, C, M, wf, wr}, (float*)O, (float*)A, NULL, NULL, 1};
+    return iwg_model(&c, d);
+}

@@ -89,6 +89,45 @@ def iw_solve(w, n_iter, l_iter, nthreads=1, want_scalars=False):
     return O, A, costs, (sc.reshape(n_iter, l_iter, 3) if sc is not None else None)
 
 
+def _iwg_lib():
+    lib = load()
+    if not getattr(lib, "_iwg", False):
+        i, f, d = ctypes.c_int, ctypes.c_float, ctypes.c_double
+        lib.oracle_iw_solve_generic.restype = i
+        lib.oracle_iw_solve_generic.argtypes = [i, i, _F, _F, _F, _F, _F, f, f, i, i, i, i, _D]
+        lib.oracle_iw_jtf_diag.restype = None
+        lib.oracle_iw_jtf_diag.argtypes = [i, i, _F, _F, _F, _F, _F, f, f, _F, _F]
+        lib.oracle_iw_model_cost.restype = d
+        lib.oracle_iw_model_cost.argtypes = [i, i, _F, _F, _F, _F, _F, f, f, _F]
+        lib._iwg = True
+    return lib
+
+
+def iw_jtf_diag(w):
+    """r = -J^T F and the raw diagonal of J^T J (generic driver layout)."""
+    n = 3 * w["W"] * w["H"]
+    r = np.zeros(n, np.float32)
+    dg = np.zeros(n, np.float32)
+    _iwg_lib().oracle_iw_jtf_diag(*_args(w), _f(r), _f(dg))
+    return r, dg
+
+
+def iw_model_cost(w, delta):
+    delta = np.ascontiguousarray(delta, np.float32)
+    return _iwg_lib().oracle_iw_model_cost(*_args(w), _f(delta))
+
+
+def iw_solve_generic(w, n_iter, l_iter, lm=False, nthreads=1):
+    """GN or LM solve through the generic loop (solver_impl.h); returns (O, A, costs)."""
+    O = w["Offset"].copy()
+    A = w["Angle"].copy()
+    costs = np.zeros(n_iter + 1, np.float64)
+    k = _iwg_lib().oracle_iw_solve_generic(w["W"], w["H"], _f(O), _f(A), _f(w["UrShape"]), _f(w["Constraints"]),
+                                           _f(w["Mask"]), w["w_fitSqrt"], w["w_regSqrt"], int(lm), n_iter, l_iter,
+                                           nthreads, costs.ctypes.data_as(_D))
+    return O, A, costs[: k + 1]
+
+
 # ------------------------------------------------------------ poisson_image_editing
 def _pie_lib():
     lib = load()

@@ -131,3 +131,37 @@ def test_gn_solve_decreases_cost_and_threads_agree():
     O4, A4, c4, _ = oracle.iw_solve(w, 3, 10, nthreads=4)
     assert c1[0] > c1[1] > c1[2] > c1[3]
     np.testing.assert_allclose(c4, c1, rtol=1e-6)
+
+
+def test_generic_gn_loop_equals_image_warping_loop():
+    """The generic GN/LM loop (solver_impl.h) run as GN reproduces the image_warping
+    specific PCG loop bit for bit (same float operations, same order)."""
+    w = workloads.image_warping(40, 30, seed=5, n_handles=5)
+    O1, A1, c1, _ = oracle.iw_solve(w, 3, 10)
+    O2, A2, c2 = oracle.iw_solve_generic(w, 3, 10, lm=False)
+    np.testing.assert_array_equal(c1, c2)
+    np.testing.assert_array_equal(O1, O2)
+    np.testing.assert_array_equal(A1, A2)
+
+
+def test_model_cost_is_the_gauss_newton_quadratic():
+    """m(d) = 1/2|F + J d|^2 = cost - r.d + 1/2 d.J^T J d (r = -J^T F), m(0) = cost."""
+    w = small_problem()
+    act = active_unknowns(w)
+    rng = np.random.default_rng(5)
+    d = (0.05 * rng.normal(size=act.size)).astype(np.float32)
+    d[~act] = 0
+    c = oracle.iw_cost(w)
+    assert oracle.iw_model_cost(w, np.zeros_like(d)) == pytest.approx(c, rel=1e-6)
+    r, dg = oracle.iw_jtf_diag(w)
+    Ad, _ = oracle.iw_apply_jtj(w, d)
+    quad = c - float(r.astype(np.float64) @ d) + 0.5 * float(d.astype(np.float64) @ Ad)
+    assert oracle.iw_model_cost(w, d) == pytest.approx(quad, rel=1e-4)
+    J, _ = jacobian64(w)
+    np.testing.assert_allclose(dg[act], np.sum(J * J, axis=0)[act], rtol=2e-4)
+
+
+def test_lm_solve_decreases_cost():
+    w = workloads.image_warping(40, 30, seed=11, n_handles=5)
+    _, _, c = oracle.iw_solve_generic(w, 5, 10, lm=True)
+    assert len(c) >= 2 and np.all(np.diff(c) <= 0) and c[-1] < c[0]
