@@ -134,6 +134,9 @@ std::unique_ptr<Plan> make_image_warping_plan(const ProblemSpec&, const StateOpt
 std::unique_ptr<Plan> make_poisson_plan(const ProblemSpec&, const StateOptions&,
                                         const unsigned* dims, std::string* err);
 
+std::unique_ptr<Plan> make_optical_flow_plan(const ProblemSpec&, const StateOptions&,
+                                             const unsigned* dims, std::string* err);
+
 // Device-memory helpers (fail-stop).
 void* dmalloc(size_t bytes);
 void dfree(void* p);

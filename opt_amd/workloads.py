@@ -94,3 +94,54 @@ def poisson_image_editing(W: int, H: int, seed: int = 7):
 
 
 POISSON_ORDER = ["X", "T", "M"]
+
+
+def _sobel_like(img: np.ndarray, axis: int) -> np.ndarray:
+    """examples/optical_flow/src/CombinedSolver.h computeDU / computeDV (float32, the
+    same operation order; one-pixel border left at 0)."""
+    d = np.zeros_like(img)
+    c = img
+    if axis == 0:   # DU: right column minus left column over the 3 rows
+        v = (-c[:-2, :-2] - c[1:-1, :-2] - c[2:, :-2]) + c[:-2, 2:] + c[1:-1, 2:] + c[2:, 2:]
+    else:           # DV: bottom row minus top row over the 3 columns
+        v = (-c[:-2, :-2] - c[:-2, 1:-1] - c[:-2, 2:]) + c[2:, :-2] + c[2:, 1:-1] + c[2:, 2:]
+    d[1:-1, 1:-1] = (v / np.float32(8.0)).astype(np.float32)
+    return d
+
+
+def optical_flow(W: int, H: int, seed: int = 5, sigma: float = 5.0, max_flow: float = 4.0):
+    """optical_flow inputs (examples/optical_flow/src/CombinedSolver.h).
+
+    I = Gaussian-filtered (sigma, the harness's coarse level) seeded noise scaled to
+    [0, 255]; I_hat = I warped by a smooth seeded flow u with |u| <= max_flow px
+    (I_hat(q) = I(q - u(q)), bilinear), so I(p) ~ I_hat(p + u); I_hat_dx / I_hat_dy by
+    the harness's 3x3 difference formula; w_fit = 10, w_reg = 0.1 passed as square
+    roots; X = 0.
+    """
+    from scipy import ndimage
+
+    rng = np.random.default_rng(seed)
+    noise = rng.normal(size=(H, W)).astype(np.float32)
+    I = ndimage.gaussian_filter(noise, sigma, mode="nearest")
+    I = (255.0 * (I - I.min()) / max(float(I.max() - I.min()), 1e-12)).astype(np.float32)
+    ys, xs = np.mgrid[0:H, 0:W].astype(np.float32)
+    ph = rng.uniform(0, 2 * np.pi, 4)
+    fx = rng.uniform(0.5, 2.0, 4)
+    ux = 0.5 * max_flow * (np.sin(2 * np.pi * fx[0] * xs / W + ph[0]) + np.cos(2 * np.pi * fx[1] * ys / H + ph[1]))
+    uy = 0.5 * max_flow * (np.cos(2 * np.pi * fx[2] * xs / W + ph[2]) + np.sin(2 * np.pi * fx[3] * ys / H + ph[3]))
+    I_hat = ndimage.map_coordinates(I, [ys - uy, xs - ux], order=1, mode="nearest").astype(np.float32)
+    return {
+        "X": np.zeros(2 * W * H, np.float32),
+        "I": I.reshape(-1).copy(),
+        "I_hat": I_hat.reshape(-1).copy(),
+        "I_hat_dx": _sobel_like(I_hat, 0).reshape(-1).copy(),
+        "I_hat_dy": _sobel_like(I_hat, 1).reshape(-1).copy(),
+        "w_fitSqrt": float(np.sqrt(np.float32(10.0))),
+        "w_regSqrt": float(np.sqrt(np.float32(0.1))),
+        "W": W,
+        "H": H,
+    }
+
+
+# Param("w_fit",0), Param("w_reg",1), Unknown X 2, Arrays I 3, I_hat 4, I_hat_dx 5, I_hat_dy 6
+OPTICAL_FLOW_ORDER = ["w_fitSqrt", "w_regSqrt", "X", "I", "I_hat", "I_hat_dx", "I_hat_dy"]

@@ -170,3 +170,73 @@ def pie_solve(w, n_iter, l_iter, lm=False):
     k = _pie_lib().oracle_pie_solve(w["W"], w["H"], _f(X), _f(w["T"]), _f(w["M"]), int(lm), n_iter, l_iter,
                                     costs.ctypes.data_as(_D))
     return X, costs[: k + 1]
+
+
+# ------------------------------------------------------------ optical_flow
+def _of_lib():
+    lib = load()
+    if not getattr(lib, "_of", False):
+        i, f, d = ctypes.c_int, ctypes.c_float, ctypes.c_double
+        for R, P in (("float", _F), ("double", _D)):
+            g = getattr(lib, "oracle_of_cost_" + R)
+            g.restype, g.argtypes = d, [i, i, P, _F, _F, _F, _F, f, f]
+            g = getattr(lib, "oracle_of_jtf_" + R)
+            g.restype, g.argtypes = None, [i, i, P, _F, _F, _F, _F, f, f, P, P]
+            g = getattr(lib, "oracle_of_apply_" + R)
+            g.restype, g.argtypes = d, [i, i, P, _F, _F, _F, _F, f, f, P, P]
+            g = getattr(lib, "oracle_of_model_cost_" + R)
+            g.restype, g.argtypes = d, [i, i, P, _F, _F, _F, _F, f, f, P]
+            g = getattr(lib, "oracle_of_solve_" + R)
+            g.restype, g.argtypes = i, [i, i, P, _F, _F, _F, _F, f, f, i, i, i, _D]
+        lib._of = True
+    return lib
+
+
+def _of_real(double):
+    return (np.float64, _D, "double") if double else (np.float32, _F, "float")
+
+
+def _of_args(w, X, double):
+    dt, P, _ = _of_real(double)
+    X = np.ascontiguousarray(X, dt)
+    return X, (w["W"], w["H"], X.ctypes.data_as(P), _f(w["I"]), _f(w["I_hat"]), _f(w["I_hat_dx"]),
+               _f(w["I_hat_dy"]), w["w_fitSqrt"], w["w_regSqrt"])
+
+
+def of_cost(w, X=None, double=False):
+    X, a = _of_args(w, w["X"] if X is None else X, double)
+    return getattr(_of_lib(), "oracle_of_cost_" + _of_real(double)[2])(*a)
+
+
+def of_jtf(w, X=None, double=False):
+    dt, P, R = _of_real(double)
+    X, a = _of_args(w, w["X"] if X is None else X, double)
+    n = 2 * w["W"] * w["H"]
+    r, dg = np.zeros(n, dt), np.zeros(n, dt)
+    getattr(_of_lib(), "oracle_of_jtf_" + R)(*a, r.ctypes.data_as(P), dg.ctypes.data_as(P))
+    return r, dg
+
+
+def of_apply(w, p, X=None, double=False):
+    dt, P, R = _of_real(double)
+    X, a = _of_args(w, w["X"] if X is None else X, double)
+    p = np.ascontiguousarray(p, dt)
+    Ap = np.zeros_like(p)
+    v = getattr(_of_lib(), "oracle_of_apply_" + R)(*a, p.ctypes.data_as(P), Ap.ctypes.data_as(P))
+    return Ap, v
+
+
+def of_model_cost(w, d, X=None, double=False):
+    dt, P, R = _of_real(double)
+    X, a = _of_args(w, w["X"] if X is None else X, double)
+    d = np.ascontiguousarray(d, dt)
+    return getattr(_of_lib(), "oracle_of_model_cost_" + R)(*a, d.ctypes.data_as(P))
+
+
+def of_solve(w, n_iter, l_iter, lm=False, double=False, X=None):
+    """GN / LM solve; returns (X, costs)."""
+    X, a = _of_args(w, (w["X"] if X is None else X).copy(), double)
+    costs = np.zeros(n_iter + 1, np.float64)
+    k = getattr(_of_lib(), "oracle_of_solve_" + _of_real(double)[2])(*a, int(lm), n_iter, l_iter,
+                                                                     costs.ctypes.data_as(_D))
+    return X, costs[: k + 1]

@@ -1,6 +1,7 @@
 /* oracle/solver.c — TEST INFRASTRUCTURE ONLY: instantiates the generic GN/LM loop
  * (solver_impl.h) for float and double. */
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include "solver.h"
 

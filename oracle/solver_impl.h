@@ -121,6 +121,7 @@ static int CAT(oracle_solve_, REAL)(CAT(oracle_problem_, REAL)* P, int lm, const
         const REAL prevc = (REAL)prev_cost;
         const REAL model_change = prevc - model_cost, cost_change = prevc - new_cost;
         const REAL rel = cost_change / model_change;
+        if (getenv("ORACLE_DEBUG")) fprintf(stderr, "it %d prev %g model %g new %g rel %g radius %g\n", it, (double)prevc, (double)model_cost, (double)new_cost, (double)rel, radius);
         if (cost_change >= 0 && rel > (REAL)sp->min_relative_decrease) {
             if (cost_change <= prevc * (REAL)sp->function_tolerance) { done = 1; break; }
             const REAL qq = rel;

@@ -49,8 +49,9 @@ def _define(path, kind="gaussNewtonGPU"):
     return lib, st, lib.Opt_ProblemDefine(st, path.encode(), kind.encode())
 
 
-def test_define_accepts_our_energy_files(energy):
-    lib, st, pr = _define(energy("image_warping"))
+@pytest.mark.parametrize("name", ["image_warping", "poisson_image_editing", "optical_flow"])
+def test_define_accepts_our_energy_files(energy, name):
+    lib, st, pr = _define(energy(name))
     assert pr
     lib.Opt_ProblemDelete(st, pr)
 
