@@ -39,7 +39,7 @@ struct ProblemSpec {
     std::vector<DeclImage> images;
     std::vector<DeclParam> params;
     std::vector<DeclGraph> graphs;
-    bool use_preconditioner = true;   // default (o.t ProblemSpec usepreconditioner)
+    bool use_preconditioner = false;  // default: opt.ProblemSpec, API/src/o.t:258
     int n_exclude = 0;
     std::vector<std::string> computed_arrays;
     bool uses_sampled_image = false;

@@ -145,3 +145,66 @@ def optical_flow(W: int, H: int, seed: int = 5, sigma: float = 5.0, max_flow: fl
 
 # Param("w_fit",0), Param("w_reg",1), Unknown X 2, Arrays I 3, I_hat 4, I_hat_dx 5, I_hat_dy 6
 OPTICAL_FLOW_ORDER = ["w_fitSqrt", "w_regSqrt", "X", "I", "I_hat", "I_hat_dx", "I_hat_dy"]
+
+
+# lightingCoefficients of the reference's examples/data/shape_from_shading/default.SFSSolverParameters
+SFS_LIGHTING = [0.6908318, 0.04459886, 0.0181296, -0.17731632, -0.04067883, 0.1446765, 0.02393525,
+                -0.24658696, 0.005797]
+
+
+def sfs_shading(X, fx, fy, ux, uy, L):
+    """B(x,y) of shape_from_shading.t (normalAt / B, eq. 8-10) for a depth image X, float64."""
+    X = X.astype(np.float64)
+    H, W = X.shape
+    j, i = np.mgrid[0:H, 0:W].astype(np.float64)
+    d = X
+    a = np.zeros_like(X); a[:, 1:] = X[:, :-1]    # X(-1,0)
+    b = np.zeros_like(X); b[1:, :] = X[:-1, :]    # X(0,-1)
+    nx = b * (d - a) / fy
+    ny = a * (d - b) / fx
+    nz = nx * (ux - i) / fx + ny * (uy - j) / fy - a * b / (fx * fy)
+    sq = nx * nx + ny * ny + nz * nz
+    inv = np.where(sq > 0, 1.0 / np.sqrt(np.where(sq > 0, sq, 1.0)), 1.0)
+    Nx, Ny, Nz = inv * nx, inv * ny, inv * nz
+    return (L[0] + L[1] * Ny + L[2] * Nz + L[3] * Nx + L[4] * Nx * Ny + L[5] * Ny * Nz +
+            L[6] * (-Nx * Nx - Ny * Ny + 2 * Nz * Nz) + L[7] * Nz * Nx + L[8] * (Nx * Nx - Ny * Ny))
+
+
+def shape_from_shading(W: int, H: int, seed: int = 3, valid_frac: float = 0.6, noise: float = 0.002):
+    """shape_from_shading inputs (examples/shape_from_shading).
+
+    D_i = a smooth seeded depth surface in [0.38, 0.56] (the range of the reference's
+    default_targetDepth), invalid (-10000, as the harness clamps -inf) outside a seeded
+    blob covering ~valid_frac of the image; Im = the surface's spherical-harmonics
+    shading with the reference's lighting coefficients, plus seeded noise; camera
+    f = 574.0528 * W / 640 (the reference intrinsics scaled to the width), u = (W/2, H/2);
+    edge masks all 1; weights w_p = 100, w_s = 100, w_g = 1 (default.SFSSolverParameters);
+    X0 = D_i plus seeded noise (so the fit and smoothness terms are active).
+    """
+    from scipy import ndimage
+
+    rng = np.random.default_rng(seed)
+    ys, xs = np.mgrid[0:H, 0:W].astype(np.float64)
+    base = ndimage.gaussian_filter(rng.normal(size=(H, W)), max(W, H) / 24.0, mode="nearest")
+    base = (base - base.min()) / max(base.max() - base.min(), 1e-12)
+    depth = 0.38 + 0.18 * base
+    blob = ndimage.gaussian_filter(rng.normal(size=(H, W)), max(W, H) / 16.0, mode="nearest")
+    thr = np.quantile(blob, 1.0 - valid_frac)
+    valid = blob >= thr
+    fx = fy = 574.0528 * W / 640.0
+    ux, uy = W / 2.0, H / 2.0
+    Bimg = sfs_shading(depth, fx, fy, ux, uy, SFS_LIGHTING)
+    Im = np.clip(Bimg + noise * rng.normal(size=(H, W)), 0.0, 1.0).astype(np.float32)
+    D = np.where(valid, depth, -10000.0).astype(np.float32)
+    X0 = np.where(valid, depth + 0.002 * rng.normal(size=(H, W)), -10000.0).astype(np.float32)
+    params = [100.0, 100.0, 1.0, float(np.float32(fx)), float(np.float32(fy)), ux, uy] + list(SFS_LIGHTING)
+    return {
+        "params": np.array(params, np.float32),
+        "X": X0.reshape(-1).copy(),
+        "D_i": D.reshape(-1).copy(),
+        "Im": Im.reshape(-1).copy(),
+        "edgeMaskR": np.ones(W * H, np.uint8),
+        "edgeMaskC": np.ones(W * H, np.uint8),
+        "W": W,
+        "H": H,
+    }

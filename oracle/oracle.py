@@ -240,3 +240,73 @@ def of_solve(w, n_iter, l_iter, lm=False, double=False, X=None):
     k = getattr(_of_lib(), "oracle_of_solve_" + _of_real(double)[2])(*a, int(lm), n_iter, l_iter,
                                                                      costs.ctypes.data_as(_D))
     return X, costs[: k + 1]
+
+
+# ------------------------------------------------------------ shape_from_shading
+_U8 = ctypes.POINTER(ctypes.c_ubyte)
+
+
+def _sfs_lib():
+    lib = load()
+    if not getattr(lib, "_sfs", False):
+        i, d = ctypes.c_int, ctypes.c_double
+        base = [i, i, _F, _F, _F, _U8, _U8, _F]
+        lib.oracle_sfs_precompute.restype, lib.oracle_sfs_precompute.argtypes = None, base + [_F]
+        lib.oracle_sfs_cost.restype, lib.oracle_sfs_cost.argtypes = d, base
+        lib.oracle_sfs_jtf.restype, lib.oracle_sfs_jtf.argtypes = None, base + [_F, _F]
+        lib.oracle_sfs_apply.restype, lib.oracle_sfs_apply.argtypes = d, base + [_F, _F]
+        lib.oracle_sfs_model_cost.restype, lib.oracle_sfs_model_cost.argtypes = d, base + [_F]
+        lib.oracle_sfs_solve.restype, lib.oracle_sfs_solve.argtypes = i, base + [i, i, i, _D]
+        lib._sfs = True
+    return lib
+
+
+def _sfs_args(w, X):
+    X = np.ascontiguousarray(X, np.float32)
+    u8 = lambda a: np.ascontiguousarray(a, np.uint8).ctypes.data_as(_U8)
+    keep = [np.ascontiguousarray(w["edgeMaskR"], np.uint8), np.ascontiguousarray(w["edgeMaskC"], np.uint8),
+            np.ascontiguousarray(w["params"], np.float32)]
+    return X, keep, (w["W"], w["H"], _f(X), _f(w["D_i"]), _f(w["Im"]), keep[0].ctypes.data_as(_U8),
+                     keep[1].ctypes.data_as(_U8), _f(keep[2]))
+
+
+def sfs_precompute(w, X=None):
+    """[B_I, dB_I/dX(0,0), dB_I/dX(-1,0), dB_I/dX(0,-1), valid], each W*H."""
+    X, keep, a = _sfs_args(w, w["X"] if X is None else X)
+    out = np.zeros(5 * w["W"] * w["H"], np.float32)
+    _sfs_lib().oracle_sfs_precompute(*a, _f(out))
+    return out.reshape(5, -1)
+
+
+def sfs_cost(w, X=None):
+    X, keep, a = _sfs_args(w, w["X"] if X is None else X)
+    return _sfs_lib().oracle_sfs_cost(*a)
+
+
+def sfs_jtf(w, X=None):
+    X, keep, a = _sfs_args(w, w["X"] if X is None else X)
+    n = w["W"] * w["H"]
+    r, dg = np.zeros(n, np.float32), np.zeros(n, np.float32)
+    _sfs_lib().oracle_sfs_jtf(*a, _f(r), _f(dg))
+    return r, dg
+
+
+def sfs_apply(w, p, X=None):
+    X, keep, a = _sfs_args(w, w["X"] if X is None else X)
+    p = np.ascontiguousarray(p, np.float32)
+    Ap = np.zeros_like(p)
+    v = _sfs_lib().oracle_sfs_apply(*a, _f(p), _f(Ap))
+    return Ap, v
+
+
+def sfs_model_cost(w, d, X=None):
+    X, keep, a = _sfs_args(w, w["X"] if X is None else X)
+    d = np.ascontiguousarray(d, np.float32)
+    return _sfs_lib().oracle_sfs_model_cost(*a, _f(d))
+
+
+def sfs_solve(w, n_iter, l_iter, lm=True):
+    X, keep, a = _sfs_args(w, w["X"].copy())
+    costs = np.zeros(n_iter + 1, np.float64)
+    k = _sfs_lib().oracle_sfs_solve(*a, int(lm), n_iter, l_iter, costs.ctypes.data_as(_D))
+    return X, costs[: k + 1]

@@ -1,0 +1,159 @@
+"""CPU: pin the shape_from_shading oracle (parity unpinned otherwise: the reference
+holds inputs but no expected outputs for this energy) to an independent float64 numpy
+restatement of examples/shape_from_shading/shape_from_shading.t.
+
+The numpy side evaluates every residual of every centre directly from the depth image
+(B_I recomputed from X, no gradient images) and differentiates by central finite
+differences, so the oracle's analytic ComputedArray gradient images, its gathers and its
+exclusion / cost-domain rules are all checked against first principles. `valid` is held
+at its value at X (its gradient is zero: comparisons only)."""
+import os
+
+import numpy as np
+import pytest
+
+from opt_amd import workloads
+from oracle import oracle
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "sfs_default.npz")
+
+
+def small(W=11, H=9, seed=4):
+    w = workloads.shape_from_shading(W, H, seed=seed, valid_frac=0.8)
+    rng = np.random.default_rng(seed)
+    w["edgeMaskR"] = (rng.uniform(size=W * H) < 0.8).astype(np.uint8)
+    w["edgeMaskC"] = (rng.uniform(size=W * H) < 0.8).astype(np.uint8)
+    return w
+
+
+def residuals64(w, X, valid_fixed):
+    """All residual components of all centres: (values[N, 6], excluded-centre mask)."""
+    W, H = w["W"], w["H"]
+    p = w["params"].astype(np.float64)
+    wp, ws, wg = np.sqrt(p[0]), np.sqrt(p[1]), np.sqrt(p[2])
+    fx, fy, ux, uy = p[3:7]
+    L = p[7:16]
+    D = w["D_i"].reshape(H, W).astype(np.float64)
+    Im = w["Im"].reshape(H, W).astype(np.float64)
+    mR = w["edgeMaskR"].reshape(H, W).astype(np.float64)
+    mC = w["edgeMaskC"].reshape(H, W).astype(np.float64)
+    X = X.reshape(H, W).astype(np.float64)
+
+    def g(a, x, y):
+        return a[y, x] if 0 <= x < W and 0 <= y < H else 0.0
+
+    def dv(x, y):
+        return g(D, x, y) > 0
+
+    def inbe(x, y):
+        return 1 <= x < W - 1 and 1 <= y < H - 1
+
+    B = workloads.sfs_shading(X, fx, fy, ux, uy, L)
+
+    def BI(x, y):
+        if not (inbe(x, y) and dv(x - 1, y) and dv(x, y) and dv(x, y - 1)):
+            return 0.0
+        I = g(Im, x, y) * 0.5 + 0.25 * (g(Im, x - 1, y) + g(Im, x, y - 1))
+        return B[y, x] - I
+
+    out = np.zeros((H * W, 6))
+    for y in range(H):
+        for x in range(W):
+            k = y * W + x
+            if dv(x, y):
+                out[k, 0] = wp * (X[y, x] - D[y, x])
+            if inbe(x, y):
+                out[k, 1] = wg * (BI(x, y) - BI(x + 1, y)) * mR[y, x]
+                out[k, 2] = wg * (BI(x, y) - BI(x, y + 1)) * mC[y, x]
+            if valid_fixed[k] == 1:
+                def pv(ox, oy):
+                    d = g(X, x + ox, y + oy)
+                    return np.array([((x + ox) - ux) / fx * d, ((y + oy) - uy) / fy * d, d])
+                out[k, 3:6] = ws * (4 * pv(0, 0) - (pv(-1, 0) + pv(0, -1) + pv(1, 0) + pv(0, 1)))
+    return out, ~(D.reshape(-1) > 0)
+
+
+def jacobian(w, valid_fixed, h=1e-6):
+    X0 = w["X"].astype(np.float64)
+    F, excl = residuals64(w, X0, valid_fixed)
+    J = np.zeros((F.size, X0.size))
+    for j in range(X0.size):
+        if excl[j]:
+            continue   # excluded unknowns are constants
+        xp, xm = X0.copy(), X0.copy()
+        xp[j] += h
+        xm[j] -= h
+        J[:, j] = (residuals64(w, xp, valid_fixed)[0] - residuals64(w, xm, valid_fixed)[0]).reshape(-1) / (2 * h)
+    return F, excl, J
+
+
+def test_precomputed_gradient_images_match_finite_differences():
+    w = small()
+    W, H = w["W"], w["H"]
+    pc = oracle.sfs_precompute(w)
+    p = w["params"].astype(np.float64)
+    X0 = w["X"].reshape(H, W).astype(np.float64)
+    B0 = workloads.sfs_shading(X0, *p[3:7], p[7:16])
+    for (ox, oy), G in (((0, 0), pc[1]), ((-1, 0), pc[2]), ((0, -1), pc[3])):
+        Xp, Xm = X0.copy(), X0.copy()
+        h = 1e-6
+        fd = np.zeros((H, W))
+        for y in range(1, H - 1):
+            for x in range(1, W - 1):
+                Xp[:] = X0; Xm[:] = X0
+                Xp[y + oy, x + ox] += h
+                Xm[y + oy, x + ox] -= h
+                fd[y, x] = (workloads.sfs_shading(Xp, *p[3:7], p[7:16])[y, x] -
+                            workloads.sfs_shading(Xm, *p[3:7], p[7:16])[y, x]) / (2 * h)
+        m = G.reshape(H, W) != 0
+        assert m.sum() > 20
+        np.testing.assert_allclose(G.reshape(H, W)[m], fd[m], rtol=2e-3, atol=1e-3 * np.abs(fd).max())
+    assert np.all(np.isin(pc[4], [0.0, 1.0]))
+    del B0
+
+
+def test_cost_jtf_apply_model_match_numpy():
+    w = small()
+    valid = oracle.sfs_precompute(w)[4]
+    F, excl, J = jacobian(w, valid)
+    Fc = F.copy()
+    Fc[excl] = 0          # cost / model cost skip excluded centres
+    assert oracle.sfs_cost(w) == pytest.approx(0.5 * np.sum(Fc ** 2), rel=1e-4)
+    Jf = J.reshape(F.shape[0], 6, -1)
+    Jall = Jf.reshape(-1, J.shape[1])
+    g = Jall.T @ F.reshape(-1)   # gathers include residuals of excluded centres
+    r, dg = oracle.sfs_jtf(w)
+    act = ~excl
+    np.testing.assert_allclose(r[act], -g[act], atol=2e-3 * np.abs(g).max())
+    assert np.all(r[excl] == 0)
+    np.testing.assert_allclose(dg[act], np.sum(Jall ** 2, axis=0)[act], rtol=5e-3, atol=1e-3 * dg.max())
+    rng = np.random.default_rng(1)
+    pvec = rng.normal(size=J.shape[1]).astype(np.float32)
+    pvec[excl] = 0
+    Ap, pAp = oracle.sfs_apply(w, pvec)
+    ref = Jall.T @ (Jall @ pvec.astype(np.float64))
+    np.testing.assert_allclose(Ap[act], ref[act], atol=3e-3 * np.abs(ref).max())
+    assert pAp == pytest.approx(float(pvec @ ref), rel=3e-3)
+    d = (1e-3 * rng.normal(size=J.shape[1])).astype(np.float32)
+    d[excl] = 0
+    Jc = Jf.copy()
+    Jc[excl] = 0
+    m = Fc.reshape(-1) + Jc.reshape(-1, J.shape[1]) @ d
+    assert oracle.sfs_model_cost(w, d) == pytest.approx(0.5 * m @ m, rel=1e-4)
+
+
+def test_lm_and_gn_decrease_cost_on_reference_inputs():
+    """The reference's own example inputs (examples/data/shape_from_shading/default*,
+    640x480, tests/golden/sfs_default.npz): LM monotone and both solvers descend."""
+    z = np.load(GOLDEN)
+    H, W = z["D_i"].shape
+    crop = (slice(100, 196), slice(200, 328))   # 96 x 128 window keeps the CPU test short
+    w = {"params": z["params"], "W": 128, "H": 96}
+    for k in ("D_i", "Im", "edgeMaskR", "edgeMaskC"):
+        w[k] = np.ascontiguousarray(z[k][crop]).reshape(-1)
+    w["X"] = np.ascontiguousarray(z["X0"][crop]).reshape(-1)
+    assert (w["D_i"] > 0).mean() > 0.3
+    _, c = oracle.sfs_solve(w, 8, 10, lm=True)
+    assert np.all(np.diff(c) <= 0) and c[-1] < c[0]
+    _, c = oracle.sfs_solve(w, 2, 10, lm=False)
+    assert c[-1] < c[0]
