@@ -1152,6 +1152,7 @@ public:
         OPT_HIP_CHECK(hipMemcpyAsync(user_A_, dA_, sizeof(T) * N, hipMemcpyDeviceToHost, s));
     }
     T* unknown(int k) { return k == 0 ? (T*)a_.O : (T*)a_.A; }
+    void precompute(hipStream_t) {}   // no ComputedArrays in this energy
     void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
         a_.flags = flags;
         hipLaunchKernelGGL((iw::iw_jtf<T, 2>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, r, diag, ReduceSlot{});

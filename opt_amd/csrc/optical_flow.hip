@@ -276,6 +276,7 @@ public:
             OPT_HIP_CHECK(hipMemcpyAsync(userX_, dX_, sizeof(T) * 2 * dom_.npix_mem(), hipMemcpyDeviceToHost, s));
     }
     T* unknown(int k) { return k == 0 ? a_.X : nullptr; }
+    void precompute(hipStream_t) {}   // no ComputedArrays in this energy
     void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
         a_.flags = flags;
         hipLaunchKernelGGL((of::of_jtf<T>), grid(), dim3(kBlock), 0, s, a_, r, diag);

@@ -149,6 +149,7 @@ std::unique_ptr<Plan> make_plan(const ProblemSpec& spec, const StateOptions& opt
     if (spec.family == "image_warping") return make_image_warping_plan(spec, opts, dims, err);
     if (spec.family == "poisson_image_editing") return make_poisson_plan(spec, opts, dims, err);
     if (spec.family == "optical_flow") return make_optical_flow_plan(spec, opts, dims, err);
+    if (spec.family == "shape_from_shading") return make_sfs_plan(spec, opts, dims, err);
     *err = "energy family '" + spec.family + "' has no kernels in this build";
     return nullptr;
 }

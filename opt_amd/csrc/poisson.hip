@@ -211,6 +211,7 @@ public:
             OPT_HIP_CHECK(hipMemcpyAsync(userX_, dX_, sizeof(T) * 4 * dom_.npix_mem(), hipMemcpyDeviceToHost, s));
     }
     T* unknown(int k) { return k == 0 ? (T*)a_.X : nullptr; }
+    void precompute(hipStream_t) {}   // no ComputedArrays in this energy
     void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
         a_.flags = flags;
         hipLaunchKernelGGL((pie::pie_jtf<T>), grid(), dim3(kBlock), 0, s, a_, r, diag);

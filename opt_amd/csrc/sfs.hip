@@ -1,0 +1,476 @@
+// sfs.hip — kernels for the shape_from_shading energy
+// (reference examples/shape_from_shading/shape_from_shading.t):
+//
+//   unknown X (depth), knowns D_i, Im (float), edgeMaskR / edgeMaskC (uint8)
+//   params w_p, w_s, w_g (square-rooted by the energy), f_x, f_y, u_x, u_y, L_1..L_9
+//   Exclude(D_i <= 0); no UsePreconditioner (default false, o.t:258)
+//   ComputedArray B_I = Select(InBoundsExpanded(0,0,1) & DV(-1,0) DV(0,0) DV(0,-1), B - I, 0)
+//     with its gradient images w.r.t. X(0,0), X(-1,0), X(0,-1) (o.t:1686-1716), and
+//   ComputedArray valid (comparisons only, so no gradient images)
+//   E_p   = DV ? w_p (X - D_i) : 0
+//   E_g_h = InBoundsExpanded(0,0,1) ? w_g (B_I(0,0) - B_I(1,0)) edgeMaskR : 0
+//   E_g_v = InBoundsExpanded(0,0,1) ? w_g (B_I(0,0) - B_I(0,1)) edgeMaskC : 0
+//   E_s   = valid == 1 ? w_s (4 p(0,0) - p(-1,0) - p(0,-1) - p(1,0) - p(0,1)) : 0  (3-vector)
+//
+// sfs_precompute materialises B_I, its three gradient images and valid once per
+// precompute point (init, after an update, after a revert: solverGPUGaussNewton.t:1876,
+// 2242, 2284). The gathers (J^T F + diag, J^T J p) visit, for each unknown, every
+// residual instance containing it — centred anywhere, including excluded centres — as
+// the reference's residualsincludingX00 does (o.t:2723-2733); cost and model cost sum
+// only non-excluded centres (computeCost, :971-997). The E_s partial w.r.t. X(q) is
+// w_s c (px(q), py(q), 1) with px, py functions of q alone, so it is formed in registers.
+// One thread per unknown, 64 x 4 pixel blocks; the 5x5 neighbourhood reads are L1/L2 hits.
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include "plan.h"
+#include "stencil_plan.h"
+
+namespace optamd {
+namespace sfs {
+
+template <typename T>
+struct Args {
+    Domain dom;
+    T* X;
+    const float* D;
+    const float* Im;
+    const uint8_t* mR;
+    const uint8_t* mC;
+    // precomputed images (unknown precision)
+    T *BI, *G00, *Gm0, *G0m;
+    uint8_t* valid;
+    uint8_t* flags;     // bit0: unknown active (D_i > 0)
+    T wp, ws, wg, fx, fy, ux, uy;
+    T L[9];
+};
+
+struct PixGeom { int x, y; bool ok; long long i; };
+__device__ __forceinline__ PixGeom pix(const Domain& d) {
+    PixGeom g;
+    g.x = blockIdx.x * 64 + (threadIdx.x & 63);
+    g.y = d.y_lo + blockIdx.y * 4 + (threadIdx.x >> 6);
+    g.ok = g.x < d.W && g.y < d.y_hi;
+    g.i = g.ok ? d.off(g.x, g.y) : 0;
+    return g;
+}
+__device__ __forceinline__ bool inside(const Domain& d, int x, int y) {
+    return x >= 0 && x < d.W && y >= 0 && y < d.H;
+}
+__device__ __forceinline__ bool inbe(const Domain& d, int x, int y) {
+    return x >= 1 && x < d.W - 1 && y >= 1 && y < d.H - 1;
+}
+template <typename V>
+__device__ __forceinline__ V get(const V* a, const Domain& d, int x, int y) {
+    return inside(d, x, y) ? a[d.off(x, y)] : (V)0;
+}
+template <typename T>
+__device__ __forceinline__ bool DV(const Args<T>& a, int x, int y) { return get(a.D, a.dom, x, y) > 0.f; }
+
+// ---------------------------------------------------------------- precompute
+template <typename T>
+__global__ __launch_bounds__(kBlock) void sfs_precompute(Args<T> a) {
+    const PixGeom g = pix(a.dom);
+    if (!g.ok) return;
+    const int x = g.x, y = g.y;
+    T bi = 0, g0 = 0, g1 = 0, g2 = 0;
+    if (inbe(a.dom, x, y) && DV(a, x - 1, y) && DV(a, x, y) && DV(a, x, y - 1)) {
+        const T d = a.X[g.i], A = get(a.X, a.dom, x - 1, y), B = get(a.X, a.dom, x, y - 1);
+        const T fx = a.fx, fy = a.fy, ux = a.ux, uy = a.uy;
+        const T i = (T)x, j = (T)y;
+        const T nx = B * (d - A) / fy;
+        const T ny = A * (d - B) / fx;
+        const T nz = (nx * (ux - i) / fx) + (ny * (uy - j) / fy) - (A * B / (fx * fy));
+        const T sq = nx * nx + ny * ny + nz * nz;
+        const T inv = sq > (T)0 ? (T)1 / sqrt(sq) : (T)1;
+        const T Nx = inv * nx, Ny = inv * ny, Nz = inv * nz;
+        const T* L = a.L;
+        const T Bv = L[0] + L[1] * Ny + L[2] * Nz + L[3] * Nx + L[4] * Nx * Ny + L[5] * Ny * Nz +
+                     L[6] * (-Nx * Nx - Ny * Ny + (T)2 * Nz * Nz) + L[7] * Nz * Nx + L[8] * (Nx * Nx - Ny * Ny);
+        const T I = (T)a.Im[g.i] * (T)0.5 + (T)0.25 * ((T)get(a.Im, a.dom, x - 1, y) + (T)get(a.Im, a.dom, x, y - 1));
+        bi = Bv - I;
+        const T dBx = L[3] + L[4] * Ny + L[7] * Nz + (T)2 * Nx * (L[8] - L[6]);
+        const T dBy = L[1] + L[4] * Nx + L[5] * Nz - (T)2 * Ny * (L[6] + L[8]);
+        const T dBz = L[2] + L[5] * Ny + (T)4 * L[6] * Nz + L[7] * Nx;
+        const T dnx[3] = {B / fy, -B / fy, (d - A) / fy};
+        const T dny[3] = {A / fx, (d - B) / fx, -A / fx};
+        const T dab[3] = {(T)0, B, A};
+        T gv[3];
+#pragma unroll
+        for (int v = 0; v < 3; ++v) {
+            const T dnz = dnx[v] * (ux - i) / fx + dny[v] * (uy - j) / fy - dab[v] / (fx * fy);
+            const T dinv = sq > (T)0 ? -(inv * inv * inv) * (nx * dnx[v] + ny * dny[v] + nz * dnz) : (T)0;
+            const T dNx = dinv * nx + inv * dnx[v], dNy = dinv * ny + inv * dny[v], dNz = dinv * nz + inv * dnz;
+            gv[v] = dBx * dNx + dBy * dNy + dBz * dNz;
+        }
+        g0 = gv[0]; g1 = gv[1]; g2 = gv[2];
+    }
+    a.BI[g.i] = bi; a.G00[g.i] = g0; a.Gm0[g.i] = g1; a.G0m[g.i] = g2;
+    bool v = inbe(a.dom, x, y) && DV(a, x, y) && DV(a, x, y - 1) && DV(a, x, y + 1) && DV(a, x - 1, y) &&
+             DV(a, x + 1, y);
+    if (v) {
+        const T xc = a.X[g.i];
+        v = fabs(xc - get(a.X, a.dom, x, y - 1)) < (T)0.01 && fabs(xc - get(a.X, a.dom, x, y + 1)) < (T)0.01 &&
+            fabs(xc - get(a.X, a.dom, x - 1, y)) < (T)0.01 && fabs(xc - get(a.X, a.dom, x + 1, y)) < (T)0.01;
+    }
+    a.valid[g.i] = v;
+}
+
+// ------------------------------------------------------- residual instances
+// Shading residual of direction (sx, sy) = (1,0) [E_g_h] or (0,1) [E_g_v] centred at c:
+// value and the partial w.r.t. X(c + o) for the five support offsets, as in the oracle
+// (the two X(c) partials combined).
+template <typename T>
+__device__ __forceinline__ T shade_coef(const Args<T>& a, int cx, int cy, int sx, int ox, int oy, T m) {
+    const Domain& d = a.dom;
+    const long long c = d.off(cx, cy);
+    const long long n = d.off(cx + sx, cy + (1 - sx));
+    const T wg = a.wg;
+    if (ox == 0 && oy == 0)
+        return wg * m * a.G00[c] + (sx ? -wg * m * a.Gm0[n] : -wg * m * a.G0m[n]);
+    if (ox == -1 && oy == 0) return wg * m * a.Gm0[c];
+    if (ox == 0 && oy == -1) return wg * m * a.G0m[c];
+    if (sx) {   // (1,0), (1,-1)
+        if (oy == 0) return -wg * m * a.G00[n];
+        return -wg * m * a.G0m[n];
+    }
+    // (0,1), (-1,1)
+    if (ox == 0) return -wg * m * a.G00[n];
+    return -wg * m * a.Gm0[n];
+}
+template <typename T>
+__device__ __forceinline__ T pget(const T* p, const Domain& d, int x, int y) { return get(p, d, x, y); }
+
+// J p of the shading residual at centre c (entries in the oracle's order:
+// (0,0), (-1,0), (0,-1), (s), (s) - (1,0) or (s) - (0,1))
+template <typename T>
+__device__ __forceinline__ T shade_jp(const Args<T>& a, const T* p, int cx, int cy, int sx, T m) {
+    const Domain& d = a.dom;
+    const int tx = sx, ty = 1 - sx;
+    T jp = shade_coef(a, cx, cy, sx, 0, 0, m) * pget(p, d, cx, cy);
+    jp += shade_coef(a, cx, cy, sx, -1, 0, m) * pget(p, d, cx - 1, cy);
+    jp += shade_coef(a, cx, cy, sx, 0, -1, m) * pget(p, d, cx, cy - 1);
+    jp += shade_coef(a, cx, cy, sx, tx, ty, m) * pget(p, d, cx + tx, cy + ty);
+    if (sx) jp += shade_coef(a, cx, cy, sx, 1, -1, m) * pget(p, d, cx + 1, cy - 1);
+    else jp += shade_coef(a, cx, cy, sx, -1, 1, m) * pget(p, d, cx - 1, cy + 1);
+    return jp;
+}
+
+template <typename T>
+__device__ __forceinline__ void pvec(const Args<T>& a, int x, int y, T& px, T& py) {
+    px = ((T)x - a.ux) / a.fx;
+    py = ((T)y - a.uy) / a.fy;
+}
+// E_s: partial w.r.t. X(q) = ws co (px(q), py(q), 1); J p of the instance at c
+template <typename T>
+__device__ __forceinline__ void smooth_jp(const Args<T>& a, const T* p, int cx, int cy, T out[3]) {
+    constexpr int OX[5] = {0, -1, 0, 1, 0}, OY[5] = {0, 0, -1, 0, 1};
+    out[0] = out[1] = out[2] = 0;
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        T px, py;
+        pvec(a, cx + OX[s], cy + OY[s], px, py);
+        const T co = s == 0 ? (T)4 : (T)-1;
+        const T pv = pget(p, a.dom, cx + OX[s], cy + OY[s]);
+        out[0] += a.ws * co * px * pv;
+        out[1] += a.ws * co * py * pv;
+        out[2] += a.ws * co * pv;
+    }
+}
+// E_s value at c (oracle order: 4 p(0,0) - (sum of the four in order (-1,0),(0,-1),(1,0),(0,1)))
+template <typename T>
+__device__ __forceinline__ void smooth_val(const Args<T>& a, const T* X, int cx, int cy, T out[3]) {
+    constexpr int OX[5] = {0, -1, 0, 1, 0}, OY[5] = {0, 0, -1, 0, 1};
+    T sx = 0, sy = 0, sz = 0, x0 = 0, y0 = 0, z0 = 0;
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+        T px, py;
+        pvec(a, cx + OX[s], cy + OY[s], px, py);
+        const T xv = get(X, a.dom, cx + OX[s], cy + OY[s]);
+        if (s == 0) { x0 = px * xv; y0 = py * xv; z0 = xv; }
+        else { sx += px * xv; sy += py * xv; sz += xv; }
+    }
+    out[0] = a.ws * ((T)4 * x0 - sx);
+    out[1] = a.ws * ((T)4 * y0 - sy);
+    out[2] = a.ws * ((T)4 * z0 - sz);
+}
+
+// support offsets (where X_k sits relative to the centre) of E_g_h, E_g_v, E_s
+constexpr int HX[5] = {0, -1, 0, 1, 1}, HY[5] = {0, 0, -1, 0, -1};
+constexpr int VX[5] = {0, -1, 0, 0, -1}, VY[5] = {0, 0, -1, 1, 1};
+constexpr int SX5[5] = {0, -1, 0, 1, 0}, SY5[5] = {0, 0, -1, 0, 1};
+
+// ------------------------------------------------------------------- J^T F
+template <typename T>
+__global__ __launch_bounds__(kBlock) void sfs_jtf(Args<T> a, T* __restrict__ r, T* __restrict__ diag) {
+    const PixGeom g = pix(a.dom);
+    if (!g.ok) return;
+    const int x = g.x, y = g.y;
+    const bool act = a.D[g.i] > 0.f;
+    a.flags[g.i] = act;
+    T F = 0, Dg = 0;
+    if (act) {
+        // E_p (only offset (0,0))
+        const T ep = a.wp * (a.X[g.i] - (T)a.D[g.i]);
+        F += a.wp * ep;
+        Dg += a.wp * a.wp;
+        // E_g_h, E_g_v
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const int sx = t == 0 ? 1 : 0;
+            for (int s = 0; s < 5; ++s) {
+                const int ox = t == 0 ? HX[s] : VX[s], oy = t == 0 ? HY[s] : VY[s];
+                const int cx = x - ox, cy = y - oy;
+                if (!inbe(a.dom, cx, cy)) continue;
+                const long long c = a.dom.off(cx, cy);
+                const T m = (T)(t == 0 ? a.mR[c] : a.mC[c]);
+                const long long n = a.dom.off(cx + sx, cy + 1 - sx);
+                const T val = a.wg * (a.BI[c] - a.BI[n]) * m;
+                const T dk = shade_coef(a, cx, cy, sx, ox, oy, m);
+                F += dk * val;
+                Dg += dk * dk;
+            }
+        }
+        // E_s
+        T px, py;
+        pvec(a, x, y, px, py);
+        for (int s = 0; s < 5; ++s) {
+            const int cx = x - SX5[s], cy = y - SY5[s];
+            if (!inside(a.dom, cx, cy) || a.valid[a.dom.off(cx, cy)] != 1) continue;
+            T v[3];
+            smooth_val(a, a.X, cx, cy, v);
+            const T co = s == 0 ? (T)4 : (T)-1;
+            const T d0 = a.ws * co * px, d1 = a.ws * co * py, d2 = a.ws * co;
+            F += d0 * v[0]; Dg += d0 * d0;
+            F += d1 * v[1]; Dg += d1 * d1;
+            F += d2 * v[2]; Dg += d2 * d2;
+        }
+    }
+    r[g.i] = -F;
+    diag[g.i] = Dg;
+}
+
+// ------------------------------------------------------------------- J^T J p
+template <typename T>
+__global__ __launch_bounds__(kBlock) void sfs_apply(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
+                                                    const T* __restrict__ dadd, const int* stop, ReduceSlot rs) {
+    if (stop && *stop) return;
+    const PixGeom g = pix(a.dom);
+    T dot = 0;
+    if (g.ok) {
+        const int x = g.x, y = g.y;
+        T acc = 0;
+        if (a.flags[g.i] & 1) {
+            const T pk = p[g.i];
+            acc += a.wp * (a.wp * pk);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int sx = t == 0 ? 1 : 0;
+                for (int s = 0; s < 5; ++s) {
+                    const int ox = t == 0 ? HX[s] : VX[s], oy = t == 0 ? HY[s] : VY[s];
+                    const int cx = x - ox, cy = y - oy;
+                    if (!inbe(a.dom, cx, cy)) continue;
+                    const long long c = a.dom.off(cx, cy);
+                    const T m = (T)(t == 0 ? a.mR[c] : a.mC[c]);
+                    acc += shade_coef(a, cx, cy, sx, ox, oy, m) * shade_jp(a, p, cx, cy, sx, m);
+                }
+            }
+            T px, py;
+            pvec(a, x, y, px, py);
+            for (int s = 0; s < 5; ++s) {
+                const int cx = x - SX5[s], cy = y - SY5[s];
+                if (!inside(a.dom, cx, cy) || a.valid[a.dom.off(cx, cy)] != 1) continue;
+                T jp[3];
+                smooth_jp(a, p, cx, cy, jp);
+                const T co = s == 0 ? (T)4 : (T)-1;
+                acc += (a.ws * co * px) * jp[0];
+                acc += (a.ws * co * py) * jp[1];
+                acc += (a.ws * co) * jp[2];
+            }
+            if (dadd) acc += dadd[g.i] * pk;
+            dot = pk * acc;
+        }
+        Ap[g.i] = acc;
+    }
+    double v[1] = {(double)dot};
+    block_reduce_publish<1>(v, rs, blockIdx.y * gridDim.x + blockIdx.x);
+}
+
+// ------------------------------------------------------- cost / model cost
+template <typename T>
+__global__ __launch_bounds__(kBlock) void sfs_cost(Args<T> a, const T* __restrict__ delta, ReduceSlot rs) {
+    const PixGeom g = pix(a.dom);
+    T acc = 0;
+    if (g.ok && a.D[g.i] > 0.f) {
+        const int x = g.x, y = g.y;
+        T s2 = 0;
+        {   // E_p
+            T e = a.wp * (a.X[g.i] - (T)a.D[g.i]);
+            if (delta) e += a.wp * delta[g.i];
+            s2 += e * e;
+        }
+        if (inbe(a.dom, x, y)) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int sx = t == 0 ? 1 : 0;
+                const T m = (T)(t == 0 ? a.mR[g.i] : a.mC[g.i]);
+                const long long n = a.dom.off(x + sx, y + 1 - sx);
+                T e = a.wg * (a.BI[g.i] - a.BI[n]) * m;
+                if (delta) e += shade_jp(a, delta, x, y, sx, m);
+                s2 += e * e;
+            }
+        }
+        if (a.valid[g.i] == 1) {
+            T v[3];
+            smooth_val(a, a.X, x, y, v);
+            if (delta) {
+                T jd[3];
+                smooth_jp(a, delta, x, y, jd);
+                v[0] += jd[0]; v[1] += jd[1]; v[2] += jd[2];
+            }
+            s2 += v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+        }
+        acc = (T)0.5 * s2;
+    }
+    double v[1] = {(double)acc};
+    block_reduce_publish<1>(v, rs, blockIdx.y * gridDim.x + blockIdx.x);
+}
+
+}  // namespace sfs
+
+template <typename TT>
+class ShapeFromShadingOp {
+public:
+    using T = TT;
+    static constexpr const char* kName = "shape_from_shading";
+    static constexpr const char* kApplyName = "sfs_apply";
+    ShapeFromShadingOp(const ProblemSpec& spec, const StateOptions& opts, Domain dom) : dom_(dom), opts_(opts) {
+        idx_X_ = spec.unknown(0)->index;
+        idx_D_ = spec.array(0)->index;
+        idx_Im_ = spec.array(1)->index;
+        idx_mR_ = spec.array(2)->index;
+        idx_mC_ = spec.array(3)->index;
+        static const char* names[16] = {"w_p", "w_s", "w_g", "f_x", "f_y", "u_x", "u_y", "L_1", "L_2",
+                                        "L_3", "L_4", "L_5", "L_6", "L_7", "L_8", "L_9"};
+        std::vector<DeclParam> ps = spec.params;
+        std::sort(ps.begin(), ps.end(), [](auto& x, auto& y) { return x.index < y.index; });
+        for (int k = 0; k < 16; ++k) {
+            idx_p_[k] = k < (int)ps.size() ? ps[k].index : -1;
+            for (auto& p : ps)
+                if (p.name == names[k]) idx_p_[k] = p.index;
+        }
+        const long long N = dom_.npix_mem();
+        for (T** v : {&BI_, &G00_, &Gm0_, &G0m_}) {
+            *v = (T*)dmalloc(sizeof(T) * N);
+            OPT_HIP_CHECK(hipMemset(*v, 0, sizeof(T) * N));
+        }
+        valid_ = (uint8_t*)dmalloc(N);
+        OPT_HIP_CHECK(hipMemset(valid_, 0, N));
+        if (opts.host_buffers) {
+            dX_ = (T*)dmalloc(sizeof(T) * N);
+            dD_ = (float*)dmalloc(sizeof(float) * N);
+            dIm_ = (float*)dmalloc(sizeof(float) * N);
+            dmR_ = (uint8_t*)dmalloc(N);
+            dmC_ = (uint8_t*)dmalloc(N);
+        }
+    }
+    ~ShapeFromShadingOp() {
+        for (T* v : {BI_, G00_, Gm0_, G0m_, dX_}) dfree(v);
+        dfree(valid_); dfree(dD_); dfree(dIm_); dfree(dmR_); dfree(dmC_);
+    }
+    VecLayout layout() const {
+        VecLayout L{};
+        L.nimg = 1;
+        L.ch[0] = 1;
+        L.off[0] = 0;
+        L.off[1] = dom_.npix_mem();
+        L.N = dom_.npix_mem();
+        return L;
+    }
+    int halo() const { return 2; }
+    int stencil_blocks() const { return grid().x * grid().y; }
+    void bind(void** params, hipStream_t s) {
+        auto pf = [&](int k) { return (T)*(const float*)params[idx_p_[k]]; };
+        // w_p, w_s, w_g enter the energy as sqrt(Param) (shape_from_shading.t:4-6)
+        a_.wp = std::sqrt(pf(0));
+        a_.ws = std::sqrt(pf(1));
+        a_.wg = std::sqrt(pf(2));
+        a_.fx = pf(3); a_.fy = pf(4); a_.ux = pf(5); a_.uy = pf(6);
+        for (int k = 0; k < 9; ++k) a_.L[k] = pf(7 + k);
+        userX_ = (T*)params[idx_X_];
+        const long long N = dom_.npix_mem();
+        if (!opts_.host_buffers) {
+            a_.X = userX_;
+            a_.D = (const float*)params[idx_D_];
+            a_.Im = (const float*)params[idx_Im_];
+            a_.mR = (const uint8_t*)params[idx_mR_];
+            a_.mC = (const uint8_t*)params[idx_mC_];
+        } else {
+            OPT_HIP_CHECK(hipMemcpyAsync(dX_, userX_, sizeof(T) * N, hipMemcpyHostToDevice, s));
+            OPT_HIP_CHECK(hipMemcpyAsync(dD_, params[idx_D_], sizeof(float) * N, hipMemcpyHostToDevice, s));
+            OPT_HIP_CHECK(hipMemcpyAsync(dIm_, params[idx_Im_], sizeof(float) * N, hipMemcpyHostToDevice, s));
+            OPT_HIP_CHECK(hipMemcpyAsync(dmR_, params[idx_mR_], N, hipMemcpyHostToDevice, s));
+            OPT_HIP_CHECK(hipMemcpyAsync(dmC_, params[idx_mC_], N, hipMemcpyHostToDevice, s));
+            a_.X = dX_; a_.D = dD_; a_.Im = dIm_; a_.mR = dmR_; a_.mC = dmC_;
+        }
+        a_.BI = BI_; a_.G00 = G00_; a_.Gm0 = Gm0_; a_.G0m = G0m_; a_.valid = valid_;
+        a_.dom = dom_;
+    }
+    void unbind(hipStream_t s) {
+        if (opts_.host_buffers)
+            OPT_HIP_CHECK(hipMemcpyAsync(userX_, dX_, sizeof(T) * dom_.npix_mem(), hipMemcpyDeviceToHost, s));
+    }
+    T* unknown(int k) { return k == 0 ? a_.X : nullptr; }
+    void precompute(hipStream_t s) {
+        hipLaunchKernelGGL((sfs::sfs_precompute<T>), grid(), dim3(kBlock), 0, s, a_);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
+        a_.flags = flags;
+        hipLaunchKernelGGL((sfs::sfs_jtf<T>), grid(), dim3(kBlock), 0, s, a_, r, diag);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
+        hipLaunchKernelGGL((sfs::sfs_apply<T>), grid(), dim3(kBlock), 0, s, a_, p, Ap, dadd, stop, rs);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    void cost(ReduceSlot rs, hipStream_t s) {
+        hipLaunchKernelGGL((sfs::sfs_cost<T>), grid(), dim3(kBlock), 0, s, a_, (const T*)nullptr, rs);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    void model_cost(const T* delta, ReduceSlot rs, hipStream_t s) {
+        hipLaunchKernelGGL((sfs::sfs_cost<T>), grid(), dim3(kBlock), 0, s, a_, delta, rs);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+
+private:
+    dim3 grid() const { return dim3((dom_.W + 63) / 64, (dom_.y_hi - dom_.y_lo + 3) / 4); }
+    Domain dom_;
+    StateOptions opts_;
+    int idx_X_, idx_D_, idx_Im_, idx_mR_, idx_mC_, idx_p_[16];
+    sfs::Args<T> a_{};
+    T *BI_ = nullptr, *G00_ = nullptr, *Gm0_ = nullptr, *G0m_ = nullptr;
+    uint8_t* valid_ = nullptr;
+    T* userX_ = nullptr;
+    T* dX_ = nullptr;
+    float *dD_ = nullptr, *dIm_ = nullptr;
+    uint8_t *dmR_ = nullptr, *dmC_ = nullptr;
+};
+
+std::unique_ptr<Plan> make_sfs_plan(const ProblemSpec& spec, const StateOptions& opts, const unsigned* dims,
+                                    std::string* err) {
+    unsigned W = 0, H = 0;
+    for (auto& d : spec.dims) {
+        if (d.name == spec.unknown(0)->dims[0]) W = dims[d.index];
+        if (d.name == spec.unknown(0)->dims[1]) H = dims[d.index];
+    }
+    if (W == 0 || H == 0) { *err = "shape_from_shading: zero-sized domain"; return nullptr; }
+    if (spec.params.size() < 16) { *err = "shape_from_shading: expects 16 scalar parameters"; return nullptr; }
+    Domain dom{(int)W, (int)H, 0, (int)H, 0, (int)H};
+    if (opts.double_precision)
+        return std::unique_ptr<Plan>(new StencilPlan<ShapeFromShadingOp<double>>(spec, opts, dom));
+    return std::unique_ptr<Plan>(new StencilPlan<ShapeFromShadingOp<float>>(spec, opts, dom));
+}
+
+}  // namespace optamd

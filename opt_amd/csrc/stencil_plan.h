@@ -48,6 +48,8 @@ __global__ __launch_bounds__(kBlock) void revert_images_kernel(VecLayout L, cons
 //   VecLayout layout() const; int halo() const;
 //   void bind(void** params, hipStream_t)                 — pointers + scalar params
 //   T* unknown(int k)                                     — device unknown image k
+//   void precompute(hipStream_t)                           — materialise ComputedArrays
+//                     (init, after each update and after a revert: :1876, 2242, 2284)
 //   void jtf(T* r, T* diag, uint8_t* flags, hipStream_t)  — r = -J^T F, diag(J^T J), flags
 //   void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot, hipStream_t)
 //                     — Ap = J^T J p (+ dadd p), sum p.Ap; returns early if *stop
@@ -94,6 +96,7 @@ public:
         // prevCost = cost; PCGInit1 is redone by every step
         radius_ = sp_.trust_region_radius;
         decrease_ = sp_.radius_decrease_factor;
+        tbegin("precompute"); op_.precompute(stream_); tend();
         tbegin("cost"); op_.cost(red_.slot(nb(), kScCost), stream_); tend();
         prev_cost_ = read(kScCost);
         n_iter_ = 0;
@@ -162,6 +165,7 @@ public:
         }
         if (!lm_) {
             if (Lit > 0) update(false);
+            tbegin("precompute"); op_.precompute(stream_); tend();
             tbegin("cost"); op_.cost(red_.slot(nb(), kScCost), stream_); tend();
             const double c = read(kScCost);
             op_.unbind(stream_);
@@ -173,6 +177,7 @@ public:
         // ---- LM: model cost, speculative update, accept / reject (:2229-2292)
         tbegin("model_cost"); op_.model_cost(delta_, red_.slot(nb(), kScModel), stream_); tend();
         if (Lit > 0) update(true);
+        tbegin("precompute"); op_.precompute(stream_); tend();
         tbegin("cost"); op_.cost(red_.slot(nb(), kScCost), stream_); tend();
         double h[2];
         OPT_HIP_CHECK(hipMemcpyAsync(h, red_.scalars + kScModel, sizeof(h), hipMemcpyDeviceToHost, stream_));
@@ -198,6 +203,7 @@ public:
             }
         } else {
             if (Lit > 0) revert();
+            op_.precompute(stream_);
             radius_ = radius_ / decrease_;
             decrease_ = 2.0f * decrease_;
             if (radius_ <= sp_.min_trust_region_radius) ret = 0;
@@ -211,6 +217,7 @@ public:
     int eval_jtf(void** params, void* r, void* pre, double* rzv) override {
         begin_call();
         op_.bind(params, stream_);
+        op_.precompute(stream_);
         op_.jtf((T*)r, diag_, flags_, stream_);
         hipLaunchKernelGGL((gn_init_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, L_, (const uint8_t*)flags_,
                            (const T*)r, (const T*)diag_, (T*)pre, p_, spec_.use_preconditioner ? 1 : 0,
@@ -222,6 +229,7 @@ public:
     int apply_jtj(void** params, const void* p, void* Ap, double* pAp) override {
         begin_call();
         op_.bind(params, stream_);
+        op_.precompute(stream_);
         op_.jtf(r_, diag_, flags_, stream_);   // flags for the exclusion mask
         op_.apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
         *pAp = read(kScTmp);
@@ -231,6 +239,7 @@ public:
     double eval_cost(void** params) override {
         begin_call();
         op_.bind(params, stream_);
+        op_.precompute(stream_);
         op_.cost(red_.slot(nb(), kScTmp), stream_);
         const double c = read(kScTmp);
         end_call();
@@ -239,6 +248,7 @@ public:
     double time_apply(void** params, const void* p, void* Ap, int reps) override {
         begin_call();
         op_.bind(params, stream_);
+        op_.precompute(stream_);
         op_.jtf(r_, diag_, flags_, stream_);
         hipEvent_t e0, e1;
         OPT_HIP_CHECK(hipEventCreate(&e0));

@@ -1,0 +1,139 @@
+"""GPU parity of the shape_from_shading path (generic GN/LM driver + sfs_* kernels:
+ComputedArray precompute with gradient images, radius-2 gathers) against the C oracle,
+through the C ABI, on synthetic inputs and on the reference's own example inputs
+(tests/golden/sfs_default.npz, 640x480). BASELINE config 3 (4096^2, LM) at full size
+through size-independent properties (LM monotonicity, determinism)."""
+import os
+
+import numpy as np
+import pytest
+
+from opt_amd import OptSolver, workloads
+from oracle import oracle
+from tests.iw_helpers import ROOT, rel_err
+
+pytestmark = pytest.mark.gpu
+ENERGY = os.path.join(ROOT, "energies", "shape_from_shading.t")
+GOLDEN = os.path.join(ROOT, "tests", "golden", "sfs_default.npz")
+
+
+def params(w, host=False):
+    scal = [float(v) for v in w["params"]]
+    arrs = [w["X"].copy(), w["D_i"], w["Im"], w["edgeMaskR"], w["edgeMaskC"]]
+    if host:
+        return scal + arrs
+    import torch
+    return scal + [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
+
+
+def to_np(t):
+    return t.detach().cpu().numpy() if hasattr(t, "detach") else t
+
+
+def synthetic(W, H, seed):
+    w = workloads.shape_from_shading(W, H, seed=seed, valid_frac=0.7)
+    rng = np.random.default_rng(seed)
+    w["edgeMaskR"] = (rng.uniform(size=W * H) < 0.9).astype(np.uint8)
+    w["edgeMaskC"] = (rng.uniform(size=W * H) < 0.9).astype(np.uint8)
+    return w
+
+
+def reference_inputs(crop=None):
+    z = np.load(GOLDEN)
+    H, W = z["D_i"].shape
+    sl = crop or (slice(0, H), slice(0, W))
+    w = {"params": z["params"]}
+    for k in ("D_i", "Im", "edgeMaskR", "edgeMaskC"):
+        w[k] = np.ascontiguousarray(z[k][sl]).reshape(-1)
+    X = np.ascontiguousarray(z["X0"][sl])
+    w["H"], w["W"] = X.shape
+    w["X"] = X.reshape(-1)
+    return w
+
+
+@pytest.mark.parametrize("W,H", [(64, 48), (97, 61), (130, 9), (5, 40)])
+def test_kernels_match_oracle(W, H):
+    import torch
+
+    w = synthetic(W, H, seed=W + H)
+    s = OptSolver([W, H], ENERGY, "LMGPU")
+    assert s.family() == "shape_from_shading"
+    prm = params(w)
+    assert s.eval_cost(prm) == pytest.approx(oracle.sfs_cost(w), rel=2e-5)
+    n = W * H
+    r = torch.zeros(n, device="cuda")
+    pre = torch.zeros(n, device="cuda")
+    s.eval_jtf(prm, r, pre)
+    r_ref, _ = oracle.sfs_jtf(w)
+    assert rel_err(to_np(r), r_ref) < 5e-5
+    act = w["D_i"] > 0
+    assert np.all(to_np(pre)[act] == 0.25) and np.all(to_np(pre)[~act] == 0)
+    p = np.random.default_rng(3).normal(size=n).astype(np.float32)
+    p[~act] = 0
+    Ap = torch.zeros(n, device="cuda")
+    pAp = s.apply_jtj(prm, torch.from_numpy(p).cuda(), Ap)
+    Ap_ref, pAp_ref = oracle.sfs_apply(w, p)
+    assert rel_err(to_np(Ap), Ap_ref) < 5e-5
+    assert pAp == pytest.approx(pAp_ref, rel=5e-5)
+
+
+@pytest.mark.parametrize("kind,nit,lit", [("gaussNewtonGPU", 3, 10), ("LMGPU", 6, 10), ("LMGPU", 3, 25)])
+def test_solve_matches_oracle_synthetic(kind, nit, lit):
+    W, H = 96, 72
+    w = synthetic(W, H, seed=12)
+    s = OptSolver([W, H], ENERGY, kind)
+    prm = params(w)
+    s.set_solver_params({"nIterations": nit, "lIterations": lit})
+    costs = s.profiled_solve(prm)
+    X_ref, c_ref = oracle.sfs_solve(w, nit, lit, lm=(kind == "LMGPU"))
+    assert len(costs) == len(c_ref)
+    np.testing.assert_allclose(costs, c_ref, rtol=1e-4)
+    assert rel_err(to_np(prm[16]), X_ref) < 1e-4
+
+
+def test_solve_matches_oracle_reference_inputs():
+    """The reference's own example (examples/data/shape_from_shading/default*), 640x480,
+    LM, the harness's X0 = initialUnknown."""
+    w = reference_inputs()
+    s = OptSolver([w["W"], w["H"]], ENERGY, "LMGPU")
+    prm = params(w)
+    s.set_solver_params({"nIterations": 5, "lIterations": 10})
+    costs = s.profiled_solve(prm)
+    X_ref, c_ref = oracle.sfs_solve(w, 5, 10, lm=True)
+    assert len(costs) == len(c_ref)
+    np.testing.assert_allclose(costs, c_ref, rtol=1e-4)
+    act = w["D_i"] > 0
+    assert rel_err(to_np(prm[16])[act], X_ref[act]) < 1e-4
+    assert costs[-1] < costs[0]
+
+
+def test_host_buffers_equal_device_path():
+    w = reference_inputs((slice(120, 220), slice(250, 400)))
+    W, H = w["W"], w["H"]
+    sd = OptSolver([W, H], ENERGY, "LMGPU")
+    pd = params(w)
+    sd.set_solver_params({"nIterations": 4, "lIterations": 10})
+    cd = sd.profiled_solve(pd)
+    sh = OptSolver([W, H], ENERGY, "LMGPU", backend="backend_cpu")
+    ph = params(w, host=True)
+    sh.set_solver_params({"nIterations": 4, "lIterations": 10})
+    ch = sh.profiled_solve(ph)
+    np.testing.assert_array_equal(cd, ch)
+    np.testing.assert_array_equal(to_np(pd[16]), ph[16])
+
+
+def test_config3_full_size_properties():
+    """BASELINE config 3 (4096^2, LM): monotone LM energy, descent, bitwise determinism."""
+    W = H = 4096
+    w = workloads.shape_from_shading(W, H, seed=3)
+    runs = []
+    for _ in range(2):
+        s = OptSolver([W, H], ENERGY, "LMGPU")
+        prm = params(w)
+        s.set_solver_params({"nIterations": 4, "lIterations": 10})
+        runs.append((s.profiled_solve(prm), to_np(prm[16])))
+        s.close()
+    c, X = runs[0]
+    assert np.all(np.diff(c) <= 0) and c[-1] < c[0]
+    np.testing.assert_array_equal(runs[1][0], c)
+    np.testing.assert_array_equal(runs[1][1], X)
