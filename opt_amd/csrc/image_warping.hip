@@ -1078,6 +1078,7 @@ public:
     using T = TT;
     static constexpr const char* kName = "image_warping";
     static constexpr const char* kApplyName = "iw_apply";
+    static constexpr bool kSlabs = true;
     ImageWarpingOp(const ProblemSpec& spec, const StateOptions& opts, Domain dom) : dom_(dom), opts_(opts) {
         idx_O_ = spec.unknown(0)->index;
         idx_A_ = spec.unknown(1)->index;
@@ -1153,6 +1154,7 @@ public:
     }
     T* unknown(int k) { return k == 0 ? (T*)a_.O : (T*)a_.A; }
     void precompute(hipStream_t) {}   // no ComputedArrays in this energy
+    void computed_planes(std::vector<HaloPlane>&) const {}
     void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
         a_.flags = flags;
         hipLaunchKernelGGL((iw::iw_jtf<T, 2>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, r, diag, ReduceSlot{});

@@ -215,6 +215,7 @@ public:
     using T = TT;
     static constexpr const char* kName = "optical_flow";
     static constexpr const char* kApplyName = "of_apply";
+    static constexpr bool kSlabs = false;   // sampled reads land anywhere in the image
     OpticalFlowOp(const ProblemSpec& spec, const StateOptions& opts, Domain dom) : dom_(dom), opts_(opts) {
         idx_X_ = spec.unknown(0)->index;
         idx_I_ = spec.array(0)->index;
@@ -277,6 +278,7 @@ public:
     }
     T* unknown(int k) { return k == 0 ? a_.X : nullptr; }
     void precompute(hipStream_t) {}   // no ComputedArrays in this energy
+    void computed_planes(std::vector<HaloPlane>&) const {}
     void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
         a_.flags = flags;
         hipLaunchKernelGGL((of::of_jtf<T>), grid(), dim3(kBlock), 0, s, a_, r, diag);

@@ -168,6 +168,7 @@ public:
     using T = TT;
     static constexpr const char* kName = "poisson_image_editing";
     static constexpr const char* kApplyName = "pie_apply";
+    static constexpr bool kSlabs = true;
     PoissonOp(const ProblemSpec& spec, const StateOptions& opts, Domain dom) : dom_(dom), opts_(opts) {
         idx_X_ = spec.unknown(0)->index;
         idx_T_ = spec.array(0)->index;
@@ -212,6 +213,7 @@ public:
     }
     T* unknown(int k) { return k == 0 ? (T*)a_.X : nullptr; }
     void precompute(hipStream_t) {}   // no ComputedArrays in this energy
+    void computed_planes(std::vector<HaloPlane>&) const {}
     void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
         a_.flags = flags;
         hipLaunchKernelGGL((pie::pie_jtf<T>), grid(), dim3(kBlock), 0, s, a_, r, diag);

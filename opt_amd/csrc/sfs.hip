@@ -345,6 +345,7 @@ public:
     using T = TT;
     static constexpr const char* kName = "shape_from_shading";
     static constexpr const char* kApplyName = "sfs_apply";
+    static constexpr bool kSlabs = true;
     ShapeFromShadingOp(const ProblemSpec& spec, const StateOptions& opts, Domain dom) : dom_(dom), opts_(opts) {
         idx_X_ = spec.unknown(0)->index;
         idx_D_ = spec.array(0)->index;
@@ -425,6 +426,10 @@ public:
     void precompute(hipStream_t s) {
         hipLaunchKernelGGL((sfs::sfs_precompute<T>), grid(), dim3(kBlock), 0, s, a_);
         OPT_HIP_CHECK(hipGetLastError());
+    }
+    void computed_planes(std::vector<HaloPlane>& v) const {
+        for (T* im : {BI_, G00_, Gm0_, G0m_}) v.push_back({(void*)im, sizeof(T) * dom_.W});
+        v.push_back({(void*)valid_, (size_t)dom_.W});
     }
     void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
         a_.flags = flags;

@@ -46,22 +46,27 @@ __device__ __forceinline__ T guarded_invert(T d) {   // CERES form, :480-487
 
 // PCGInit1's preconditioner and direction (after the family's evalJTF):
 // pre = guardedInvert(diag) (guardedInvert(1) = 1/4 for UsePreconditioner(false)),
-// p = pre r, rz[0] = sum r.p. Excluded unknowns get pre = p = 0.
+// p = pre r, rz[0] = sum r.p. Excluded unknowns get pre = p = 0; so do the halo rows of
+// a decomposed slab (pixels outside [pix_lo, pix_hi)), whose r is zeroed too.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void gn_init_kernel(VecLayout L, const uint8_t* __restrict__ flags,
-                                                         const T* __restrict__ r, const T* __restrict__ diag,
+                                                         T* __restrict__ r, const T* __restrict__ diag,
                                                          T* __restrict__ pre, T* __restrict__ p, int use_pre,
-                                                         ReduceSlot rs) {
+                                                         long long pix_lo, long long pix_hi, ReduceSlot rs) {
     const long long n = L.off[L.nimg];
     T acc = 0;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
-        const bool act = flags[L.pix(e)] & 1;
+        const long long px = L.pix(e);
+        const bool own = px >= pix_lo && px < pix_hi;
+        const bool act = own && (flags[px] & 1);
         const T w = act ? guarded_invert(use_pre ? diag[e] : (T)1) : (T)0;
-        const T pp = w * r[e];
+        const T re = own ? r[e] : (T)0;
+        const T pp = w * re;
+        if (!own) r[e] = 0;
         pre[e] = w;
         p[e] = pp;
-        acc += r[e] * pp;
+        acc += re * pp;
     }
     double v[1] = {(double)acc};
     block_reduce_publish<1>(v, rs, blockIdx.x);
@@ -73,20 +78,23 @@ __global__ __launch_bounds__(kBlock) void gn_init_kernel(VecLayout L, const uint
 // rz[0] = sum r.p (q = 0 since delta = 0).
 template <typename T, bool FIRST>
 __global__ __launch_bounds__(kBlock) void lm_init_kernel(VecLayout L, const uint8_t* __restrict__ flags,
-                                                         const T* __restrict__ r, const T* __restrict__ diag,
+                                                         T* __restrict__ r, const T* __restrict__ diag,
                                                          T* __restrict__ SSq, T* __restrict__ CtC,
                                                          T* __restrict__ pre, T* __restrict__ b, T* __restrict__ p,
-                                                         int use_pre, LMScalars lm, ReduceSlot rs) {
+                                                         int use_pre, LMScalars lm, long long pix_lo,
+                                                         long long pix_hi, ReduceSlot rs) {
     const long long n = L.off[L.nimg];
     const T radius = (T)lm.radius;
     const T inv_radius = (T)1 / radius;
     T acc = 0;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
-        const bool act = flags[L.pix(e)] & 1;
-        if (!act) {
+        const long long px = L.pix(e);
+        const bool own = px >= pix_lo && px < pix_hi;
+        if (!own || !(flags[px] & 1)) {
             if (FIRST) SSq[e] = 0;
             CtC[e] = 0; pre[e] = 0; b[e] = 0; p[e] = 0;
+            if (!own) r[e] = 0;
             continue;
         }
         T ssq;

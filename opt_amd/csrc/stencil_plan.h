@@ -44,60 +44,79 @@ __global__ __launch_bounds__(kBlock) void revert_images_kernel(VecLayout L, cons
 
 // Op contract (see poisson.hip):
 //   using T; static constexpr const char* kName, kApplyName;
+//   static constexpr bool kSlabs                          — row-slab decomposition allowed
 //   Op(const ProblemSpec&, const StateOptions&, Domain)   — roles from declarations
 //   VecLayout layout() const; int halo() const;
 //   void bind(void** params, hipStream_t)                 — pointers + scalar params
 //   T* unknown(int k)                                     — device unknown image k
 //   void precompute(hipStream_t)                           — materialise ComputedArrays
 //                     (init, after each update and after a revert: :1876, 2242, 2284)
+//   void computed_planes(std::vector<HaloPlane>&)          — what precompute writes
 //   void jtf(T* r, T* diag, uint8_t* flags, hipStream_t)  — r = -J^T F, diag(J^T J), flags
 //   void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot, hipStream_t)
 //                     — Ap = J^T J p (+ dadd p), sum p.Ap; returns early if *stop
 //   void cost(ReduceSlot, hipStream_t); void model_cost(const T* delta, ReduceSlot, hipStream_t)
 //   void unbind(hipStream_t)                               — copy unknowns back (host mode)
+// All stencil kernels cover the owned rows [y_lo, y_hi) of the Domain and read up to
+// halo() rows beyond them.
+//
+// Row-slab decomposition: each rank owns rows [y_lo, y_hi) and holds
+// halo() rows of each neighbour. The flat PCG kernels run over the whole memory slab:
+// the init kernels zero pre / p / r / b / CtC outside the owned rows (and the stencil
+// kernels write Ap only there), so every flat reduction sums owned elements only. The
+// exchanges are: unknowns after bind / update / revert, computed arrays after each
+// precompute, flags after J^T F, p before each apply (delta before an apply of delta
+// and before the model cost); every scalar is all-reduced right after its kernel.
 template <class Op>
 class StencilPlan final : public Plan {
 public:
     using T = typename Op::T;
-    StencilPlan(const ProblemSpec& spec, const StateOptions& opts, Domain dom)
-        : Plan(spec, opts), dom_(dom), op_(spec, opts, dom) {
+    StencilPlan(const ProblemSpec& spec, const StateOptions& opts, Domain dom) : Plan(spec, opts), dom_(dom) {
         lm_ = spec.lm();
-        L_ = op_.layout();
-        n_ = L_.off[L_.nimg];
-        for (T** v : {&r_, &diag_, &pre_, &p_, &Ap_, &delta_})
-            *v = (T*)dmalloc(sizeof(T) * n_);
-        if (lm_)
-            for (T** v : {&b_, &CtC_, &SSq_, &prev_, &Adelta_})
-                *v = (T*)dmalloc(sizeof(T) * n_);
-        for (T* v : {r_, diag_, pre_, p_, Ap_, delta_, b_, CtC_, SSq_, prev_, Adelta_})
-            if (v) OPT_HIP_CHECK(hipMemset(v, 0, sizeof(T) * n_));
-        flags_ = (uint8_t*)dmalloc(dom_.npix_mem());
-        OPT_HIP_CHECK(hipMemset(flags_, 0, dom_.npix_mem()));
         stop_ = (int*)dmalloc(64);
         OPT_HIP_CHECK(hipMemset(stop_, 0, 64));
         timer_.apply_name = Op::kApplyName;
-        red_.ensure(std::max(op_.stencil_blocks(), 4096), 2, 64);
+        allocate();
     }
     ~StencilPlan() override {
         OPT_HIP_CHECK(hipStreamSynchronize(stream_));
-        for (T* v : {r_, diag_, pre_, p_, Ap_, delta_, b_, CtC_, SSq_, prev_, Adelta_}) dfree(v);
-        dfree(flags_);
+        release();
         dfree(stop_);
     }
 
     long long unknown_count() const override { return n_; }
     std::string family() const override { return Op::kName; }
     std::string apply_kernel_name() const override { return Op::kApplyName; }
+    int halo() const override { return op_->halo(); }
+
+    std::string set_decomposition(Comm* comm, int y_lo, int y_hi) override {
+        if (!Op::kSlabs) return std::string(Op::kName) + ": no row-slab decomposition (data-dependent reads)";
+        if (opts_.host_buffers) return "row-slab decomposition needs backend_cuda (device arrays)";
+        const int h = op_->halo();
+        if (y_lo < 0 || y_hi > dom_.H || y_hi - y_lo < h) return "invalid slab rows";
+        comm_ = comm;
+        OPT_HIP_CHECK(hipStreamSynchronize(stream_));
+        release();
+        dom_.y_lo = y_lo;
+        dom_.y_hi = y_hi;
+        dom_.y_mem0 = std::max(0, y_lo - h);
+        dom_.mem_rows = std::min(dom_.H, y_hi + h) - dom_.y_mem0;
+        allocate();
+        initialised_ = false;
+        return "";
+    }
 
     void init(void** params) override {
         begin_call();
-        op_.bind(params, stream_);
+        op_->bind(params, stream_);
+        exchange_unknowns();
         // reference init: LM parameters copied into the plan (:1863-1872), precompute,
         // prevCost = cost; PCGInit1 is redone by every step
         radius_ = sp_.trust_region_radius;
         decrease_ = sp_.radius_decrease_factor;
-        tbegin("precompute"); op_.precompute(stream_); tend();
-        tbegin("cost"); op_.cost(red_.slot(nb(), kScCost), stream_); tend();
+        precompute();
+        tbegin("cost"); op_->cost(red_.slot(nb(), kScCost), stream_); tend();
+        allreduce(kScCost, 1);
         prev_cost_ = read(kScCost);
         n_iter_ = 0;
         initialised_ = true;
@@ -108,44 +127,51 @@ public:
         if (!initialised_) init(params);
         if (n_iter_ >= sp_.nIterations) return 0;
         begin_call();
-        op_.bind(params, stream_);
+        op_->bind(params, stream_);
+        exchange_unknowns();
         const int Lit = std::max(0, sp_.lIterations);
-        red_.ensure(std::max(op_.stencil_blocks(), 4096), 2, kScBase + 3 * (Lit + 2));
+        red_.ensure(std::max(op_->stencil_blocks(), 4096), 2, kScBase + 3 * (Lit + 2));
         OPT_HIP_CHECK(hipMemsetAsync(stop_, 0, 64, stream_));
         OPT_HIP_CHECK(hipMemsetAsync(delta_, 0, sizeof(T) * n_, stream_));   // PCGInit1: delta = 0
         const int use_pre = spec_.use_preconditioner ? 1 : 0;
+        const long long lo = pix_lo(), hi = pix_hi();
         // PCGInit1 (+ LM diagonal)
-        tbegin("jtf"); op_.jtf(r_, diag_, flags_, stream_); tend();
+        tbegin("jtf"); op_->jtf(r_, diag_, flags_, stream_); tend();
+        exchange({{(void*)flags_, (size_t)dom_.W}});
         if (!lm_) {
             tbegin("gn_init");
             hipLaunchKernelGGL((gn_init_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, L_, (const uint8_t*)flags_,
-                               (const T*)r_, (const T*)diag_, pre_, p_, use_pre, red_.slot(fg(), rz(0)));
+                               r_, (const T*)diag_, pre_, p_, use_pre, lo, hi, red_.slot(fg(), rz(0)));
             tend();
         } else {
             LMScalars lm{radius_, sp_.min_lm_diagonal, sp_.max_lm_diagonal};
             tbegin("lm_init");
             if (n_iter_ == 0)
                 hipLaunchKernelGGL((lm_init_kernel<T, true>), dim3(fg()), dim3(kBlock), 0, stream_, L_,
-                                   (const uint8_t*)flags_, (const T*)r_, (const T*)diag_, SSq_, CtC_, pre_, b_, p_,
-                                   use_pre, lm, red_.slot(fg(), rz(0)));
+                                   (const uint8_t*)flags_, r_, (const T*)diag_, SSq_, CtC_, pre_, b_, p_,
+                                   use_pre, lm, lo, hi, red_.slot(fg(), rz(0)));
             else
                 hipLaunchKernelGGL((lm_init_kernel<T, false>), dim3(fg()), dim3(kBlock), 0, stream_, L_,
-                                   (const uint8_t*)flags_, (const T*)r_, (const T*)diag_, SSq_, CtC_, pre_, b_, p_,
-                                   use_pre, lm, red_.slot(fg(), rz(0)));
+                                   (const uint8_t*)flags_, r_, (const T*)diag_, SSq_, CtC_, pre_, b_, p_,
+                                   use_pre, lm, lo, hi, red_.slot(fg(), rz(0)));
             tend();
             OPT_HIP_CHECK(hipMemsetAsync(red_.scalars + kScQ0, 0, sizeof(double), stream_));
         }
         OPT_HIP_CHECK(hipGetLastError());
+        allreduce(rz(0), 1);
         const int* stop = lm_ ? stop_ : nullptr;
         for (int i = 0; i < Lit; ++i) {
+            exchange_vec(p_);
             tbegin(Op::kApplyName);
-            op_.apply(p_, Ap_, lm_ ? CtC_ : nullptr, stop, red_.slot(nb(), pap(i)), stream_);
+            op_->apply(p_, Ap_, lm_ ? CtC_ : nullptr, stop, red_.slot(nb(), pap(i)), stream_);
             tend();
+            allreduce(pap(i), 1);
             const bool reset = lm_ && ((i + 1) % std::max(1, sp_.residual_reset_period)) == 0;
             if (reset) {
                 hipLaunchKernelGGL((half1_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)p_, delta_,
                                    red_.scalars, rz(i), pap(i), stop);
-                op_.apply(delta_, Adelta_, CtC_, stop, red_.slot(nb(), kScTmp), stream_);
+                exchange_vec(delta_);
+                op_->apply(delta_, Adelta_, CtC_, stop, red_.slot(nb(), kScTmp), stream_);
                 hipLaunchKernelGGL((half2_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)Adelta_,
                                    (const T*)b_, (const T*)pre_, (const T*)delta_, r_, use_pre, stop,
                                    red_.slot(fg(), rz(i + 1)));
@@ -154,6 +180,7 @@ public:
                 launch_step2(i == 0, rz(i), pap(i), rz(i + 1), stop);
                 tend();
             }
+            allreduce(rz(i + 1), lm_ ? 2 : 1);   // rz and q sit side by side
             tbegin("step3");
             hipLaunchKernelGGL((step3_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)pre_,
                                (const T*)r_, p_, red_.scalars, rz(i + 1), rz(i), use_pre, stop);
@@ -165,20 +192,23 @@ public:
         }
         if (!lm_) {
             if (Lit > 0) update(false);
-            tbegin("precompute"); op_.precompute(stream_); tend();
-            tbegin("cost"); op_.cost(red_.slot(nb(), kScCost), stream_); tend();
+            precompute();
+            tbegin("cost"); op_->cost(red_.slot(nb(), kScCost), stream_); tend();
+            allreduce(kScCost, 1);
             const double c = read(kScCost);
-            op_.unbind(stream_);
+            op_->unbind(stream_);
             end_call();
             prev_cost_ = c;
             ++n_iter_;
             return 1;
         }
         // ---- LM: model cost, speculative update, accept / reject (:2229-2292)
-        tbegin("model_cost"); op_.model_cost(delta_, red_.slot(nb(), kScModel), stream_); tend();
+        exchange_vec(delta_);
+        tbegin("model_cost"); op_->model_cost(delta_, red_.slot(nb(), kScModel), stream_); tend();
         if (Lit > 0) update(true);
-        tbegin("precompute"); op_.precompute(stream_); tend();
-        tbegin("cost"); op_.cost(red_.slot(nb(), kScCost), stream_); tend();
+        precompute();
+        tbegin("cost"); op_->cost(red_.slot(nb(), kScCost), stream_); tend();
+        allreduce(kScModel, 2);   // model cost and cost
         double h[2];
         OPT_HIP_CHECK(hipMemcpyAsync(h, red_.scalars + kScModel, sizeof(h), hipMemcpyDeviceToHost, stream_));
         OPT_HIP_CHECK(hipStreamSynchronize(stream_));
@@ -193,9 +223,9 @@ public:
             if (cost_change <= abs_tol) {
                 ret = 0;   // function tolerance reached (prevCost is left as it was, :2254-2258)
             } else {
-                const T q = rel;
+                const T qv = rel;
                 const T min_factor = (T)(1.0 / 3.0);
-                const T tmp = (T)1 - (T)std::pow((double)((T)2 * q - (T)1), 3.0);
+                const T tmp = (T)1 - (T)std::pow((double)((T)2 * qv - (T)1), 3.0);
                 float rad = (float)((T)radius_ / std::max(min_factor, tmp));
                 radius_ = std::min(rad, sp_.max_trust_region_radius);
                 decrease_ = 2.0f;
@@ -203,12 +233,12 @@ public:
             }
         } else {
             if (Lit > 0) revert();
-            op_.precompute(stream_);
+            precompute();
             radius_ = radius_ / decrease_;
             decrease_ = 2.0f * decrease_;
             if (radius_ <= sp_.min_trust_region_radius) ret = 0;
         }
-        op_.unbind(stream_);
+        op_->unbind(stream_);
         end_call();
         if (ret) ++n_iter_;
         return ret;
@@ -216,47 +246,48 @@ public:
 
     int eval_jtf(void** params, void* r, void* pre, double* rzv) override {
         begin_call();
-        op_.bind(params, stream_);
-        op_.precompute(stream_);
-        op_.jtf((T*)r, diag_, flags_, stream_);
+        prepare(params);
+        op_->jtf((T*)r, diag_, flags_, stream_);
         hipLaunchKernelGGL((gn_init_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, L_, (const uint8_t*)flags_,
-                           (const T*)r, (const T*)diag_, (T*)pre, p_, spec_.use_preconditioner ? 1 : 0,
-                           red_.slot(fg(), kScTmp));
+                           (T*)r, (const T*)diag_, (T*)pre, p_, spec_.use_preconditioner ? 1 : 0, pix_lo(),
+                           pix_hi(), red_.slot(fg(), kScTmp));
+        allreduce(kScTmp, 1);
         *rzv = read(kScTmp);
         end_call();
         return 0;
     }
     int apply_jtj(void** params, const void* p, void* Ap, double* pAp) override {
         begin_call();
-        op_.bind(params, stream_);
-        op_.precompute(stream_);
-        op_.jtf(r_, diag_, flags_, stream_);   // flags for the exclusion mask
-        op_.apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
+        prepare(params);
+        op_->jtf(r_, diag_, flags_, stream_);   // flags for the exclusion mask
+        exchange({{(void*)flags_, (size_t)dom_.W}});
+        exchange_vec((T*)p);
+        op_->apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
+        allreduce(kScTmp, 1);
         *pAp = read(kScTmp);
         end_call();
         return 0;
     }
     double eval_cost(void** params) override {
         begin_call();
-        op_.bind(params, stream_);
-        op_.precompute(stream_);
-        op_.cost(red_.slot(nb(), kScTmp), stream_);
+        prepare(params);
+        op_->cost(red_.slot(nb(), kScTmp), stream_);
+        allreduce(kScTmp, 1);
         const double c = read(kScTmp);
         end_call();
         return c;
     }
     double time_apply(void** params, const void* p, void* Ap, int reps) override {
         begin_call();
-        op_.bind(params, stream_);
-        op_.precompute(stream_);
-        op_.jtf(r_, diag_, flags_, stream_);
+        prepare(params);
+        op_->jtf(r_, diag_, flags_, stream_);
         hipEvent_t e0, e1;
         OPT_HIP_CHECK(hipEventCreate(&e0));
         OPT_HIP_CHECK(hipEventCreate(&e1));
-        op_.apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
+        op_->apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
         OPT_HIP_CHECK(hipEventRecord(e0, stream_));
         for (int i = 0; i < reps; ++i)
-            op_.apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
+            op_->apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
         OPT_HIP_CHECK(hipEventRecord(e1, stream_));
         OPT_HIP_CHECK(hipEventSynchronize(e1));
         float ms = 0;
@@ -269,13 +300,81 @@ public:
 
 private:
     static constexpr int kScCost = 1, kScModel = 0, kScTmp = 2, kScQ0 = 3, kScBase = 8;
-    // cost sits right after model cost so one 16-byte copy fetches both
+    // cost sits right after model cost so one 16-byte copy (and one all-reduce) takes both
     // per PCG iteration: rz[i], q[i] (written together by step2 as a pair), pAp[i]
     int rz(int i) const { return kScBase + 3 * i; }
     int q(int i) const { return kScBase + 3 * i + 1; }
     int pap(int i) const { return kScBase + 3 * i + 2; }
-    int nb() const { return op_.stencil_blocks(); }
+    int nb() const { return op_->stencil_blocks(); }
     int fg() const { return flat_grid(n_, 1); }
+    long long pix_lo() const { return dom_.off(0, dom_.y_lo); }
+    long long pix_hi() const { return dom_.off(0, dom_.y_hi); }
+
+    void allocate() {
+        op_.reset(new Op(spec_, opts_, dom_));
+        L_ = op_->layout();
+        n_ = L_.off[L_.nimg];
+        for (T** v : {&r_, &diag_, &pre_, &p_, &Ap_, &delta_})
+            *v = (T*)dmalloc(sizeof(T) * n_);
+        if (lm_)
+            for (T** v : {&b_, &CtC_, &SSq_, &prev_, &Adelta_})
+                *v = (T*)dmalloc(sizeof(T) * n_);
+        for (T* v : {r_, diag_, pre_, p_, Ap_, delta_, b_, CtC_, SSq_, prev_, Adelta_})
+            if (v) OPT_HIP_CHECK(hipMemset(v, 0, sizeof(T) * n_));
+        flags_ = (uint8_t*)dmalloc(dom_.npix_mem());
+        OPT_HIP_CHECK(hipMemset(flags_, 0, dom_.npix_mem()));
+        red_.ensure(std::max(op_->stencil_blocks(), 4096), 2, 64);
+    }
+    void release() {
+        for (T** v : {&r_, &diag_, &pre_, &p_, &Ap_, &delta_, &b_, &CtC_, &SSq_, &prev_, &Adelta_}) {
+            dfree(*v);
+            *v = nullptr;
+        }
+        dfree(flags_);
+        flags_ = nullptr;
+        op_.reset();
+    }
+
+    // bind + unknown halo + ComputedArrays, for the standalone entry points
+    void prepare(void** params) {
+        op_->bind(params, stream_);
+        exchange_unknowns();
+        op_->precompute(stream_);
+        exchange_computed();
+    }
+    void precompute() {
+        tbegin("precompute"); op_->precompute(stream_); tend();
+        exchange_computed();
+    }
+
+    bool distributed() const { return comm_ && comm_->size() > 1; }
+    void allreduce(int idx, int n) {
+        if (distributed()) comm_->allreduce_sum(red_.scalars + idx, n, stream_);
+    }
+    void exchange(const std::vector<HaloPlane>& planes) {
+        if (!distributed() || planes.empty()) return;
+        tbegin("halo_exchange");
+        comm_->halo_exchange(planes, dom_, op_->halo(), stream_);
+        tend();
+    }
+    void exchange_vec(T* v) {
+        if (!distributed()) return;
+        std::vector<HaloPlane> pl;
+        for (int k = 0; k < L_.nimg; ++k) pl.push_back({(void*)(v + L_.off[k]), sizeof(T) * L_.ch[k] * dom_.W});
+        exchange(pl);
+    }
+    void exchange_unknowns() {
+        if (!distributed()) return;
+        std::vector<HaloPlane> pl;
+        for (int k = 0; k < L_.nimg; ++k) pl.push_back({(void*)op_->unknown(k), sizeof(T) * L_.ch[k] * dom_.W});
+        exchange(pl);
+    }
+    void exchange_computed() {
+        if (!distributed()) return;
+        std::vector<HaloPlane> pl;
+        op_->computed_planes(pl);
+        exchange(pl);
+    }
 
     void launch_step2(bool first, int i_num, int i_den, int out, const int* stop) {
         const int g = fg();
@@ -292,22 +391,25 @@ private:
 #undef S2
     }
     void update(bool save) {
-        const long long lo = dom_.off(0, dom_.y_lo), hi = dom_.off(0, dom_.y_hi);
         tbegin("update");
         if (save)
             hipLaunchKernelGGL((update_images_kernel<T, true>), dim3(fg()), dim3(kBlock), 0, stream_, L_,
-                               (const uint8_t*)flags_, op_.unknown(0), op_.unknown(1), (const T*)delta_, prev_, lo, hi);
+                               (const uint8_t*)flags_, op_->unknown(0), op_->unknown(1), (const T*)delta_, prev_,
+                               pix_lo(), pix_hi());
         else
             hipLaunchKernelGGL((update_images_kernel<T, false>), dim3(fg()), dim3(kBlock), 0, stream_, L_,
-                               (const uint8_t*)flags_, op_.unknown(0), op_.unknown(1), (const T*)delta_, prev_, lo, hi);
+                               (const uint8_t*)flags_, op_->unknown(0), op_->unknown(1), (const T*)delta_, prev_,
+                               pix_lo(), pix_hi());
         OPT_HIP_CHECK(hipGetLastError());
         tend();
+        exchange_unknowns();
     }
     void revert() {
-        const long long lo = dom_.off(0, dom_.y_lo), hi = dom_.off(0, dom_.y_hi);
         hipLaunchKernelGGL((revert_images_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, L_,
-                           (const uint8_t*)flags_, op_.unknown(0), op_.unknown(1), (const T*)prev_, lo, hi);
+                           (const uint8_t*)flags_, op_->unknown(0), op_->unknown(1), (const T*)prev_, pix_lo(),
+                           pix_hi());
         OPT_HIP_CHECK(hipGetLastError());
+        exchange_unknowns();
     }
     double read(int idx) {
         double v;
@@ -317,7 +419,8 @@ private:
     }
 
     Domain dom_;
-    Op op_;
+    std::unique_ptr<Op> op_;
+    Comm* comm_ = nullptr;
     bool lm_ = false;
     VecLayout L_;
     long long n_ = 0;
