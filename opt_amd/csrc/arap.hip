@@ -1,0 +1,457 @@
+// arap.hip — kernels for the arap_mesh_deformation energy (graph domain)
+// (reference examples/arap_mesh_deformation/arap_mesh_deformation.t):
+//
+//   unknowns Offset O, Angle A (3 per vertex); knowns UrShape U, Constraints C (float3)
+//   graph G: edges v0 -> v1 (int32); UsePreconditioner(true)
+//   e_fit(v) = C(v).x >= -999999.9 ? w_fit (O(v) - C(v)) : 0          (centred, per vertex)
+//   e_reg(e) = w_reg ((O(v0) - O(v1)) - R(A(v0)) (U(v0) - U(v1)))     (per edge, 3 comps)
+//
+// The reference scatters every graph term with float atomics (createjtjgraph /
+// createjtfgraph, o.t:2833-2867, 2969-2994; PCGStep1_Graph, solverGPUGaussNewton.t:
+// 1216-1233). Here the graph is turned into two CSR adjacency lists once per bind
+// (out-edges grouped by v0, in-edges grouped by v1; stable radix sorts, so the per-vertex
+// order is the edge order) and every kernel is a deterministic per-vertex gather:
+//   J_e p = w (p_O(v0) - p_O(v1) - K_v0 d_e),  K_v = sum_j p_A,j(v) dR/dA_j(v),  d_e = U(v0) - U(v1)
+//   (J^T J p)_O(v) = w sum_out J_e p - w sum_in J_e p (+ w_fit^2 p_O(v))
+//   (J^T J p)_A,j(v) = -w sum_out (dR_j(v) d_e) . J_e p
+// For an in-edge the neighbour's K_u is rebuilt from its angle and p_A (three sincos),
+// which costs less than storing 9 floats per vertex per apply.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <algorithm>
+#include <cmath>
+#include "plan.h"
+#include "stencil_plan.h"
+
+namespace optamd {
+namespace arap {
+
+template <typename T>
+struct Args {
+    int N;
+    T* O;
+    T* A;
+    const float* U;
+    const float* C;
+    const int* out_off;
+    const int* out_nbr;
+    const int* in_off;
+    const int* in_nbr;
+    uint8_t* flags;
+    T wf, wr;
+};
+
+template <typename T> struct V3 { T x, y, z; };
+template <typename T, typename S>
+__device__ __forceinline__ V3<T> ld3(const S* a, long long v) {
+    return V3<T>{(T)a[3 * v], (T)a[3 * v + 1], (T)a[3 * v + 2]};
+}
+template <typename T>
+__device__ __forceinline__ V3<T> mv(const T* M, const V3<T>& v) {
+    return {M[0] * v.x + M[1] * v.y + M[2] * v.z, M[3] * v.x + M[4] * v.y + M[5] * v.z,
+            M[6] * v.x + M[7] * v.y + M[8] * v.z};
+}
+__device__ __forceinline__ void sc(float t, float* s, float* c) { sincosf(t, s, c); }
+__device__ __forceinline__ void sc(double t, double* s, double* c) { sincos(t, s, c); }
+
+// Rotate3D (API/src/lib.t:84-98) and its partials w.r.t. the three angles
+template <typename T>
+__device__ __forceinline__ void rotation(const V3<T>& a, T* R, T dR[3][9]) {
+    T sa, ca, sb, cb, sg, cg;
+    sc(a.x, &sa, &ca); sc(a.y, &sb, &cb); sc(a.z, &sg, &cg);
+    R[0] = cg * cb;  R[1] = -sg * ca + cg * sb * sa; R[2] = sg * sa + cg * sb * ca;
+    R[3] = sg * cb;  R[4] = cg * ca + sg * sb * sa;  R[5] = -cg * sa + sg * sb * ca;
+    R[6] = -sb;      R[7] = cb * sa;                 R[8] = cb * ca;
+    if (!dR) return;
+    dR[0][0] = 0; dR[0][1] = sg * sa + cg * sb * ca; dR[0][2] = sg * ca - cg * sb * sa;
+    dR[0][3] = 0; dR[0][4] = -cg * sa + sg * sb * ca; dR[0][5] = -cg * ca - sg * sb * sa;
+    dR[0][6] = 0; dR[0][7] = cb * ca; dR[0][8] = -cb * sa;
+    dR[1][0] = -cg * sb; dR[1][1] = cg * cb * sa; dR[1][2] = cg * cb * ca;
+    dR[1][3] = -sg * sb; dR[1][4] = sg * cb * sa; dR[1][5] = sg * cb * ca;
+    dR[1][6] = -cb;      dR[1][7] = -sb * sa;     dR[1][8] = -sb * ca;
+    dR[2][0] = -sg * cb; dR[2][1] = -cg * ca - sg * sb * sa; dR[2][2] = cg * sa - sg * sb * ca;
+    dR[2][3] = cg * cb;  dR[2][4] = -sg * ca + cg * sb * sa; dR[2][5] = sg * sa + cg * sb * ca;
+    dR[2][6] = 0;        dR[2][7] = 0;                       dR[2][8] = 0;
+}
+// K = sum_j q_j dR_j
+template <typename T>
+__device__ __forceinline__ void directional(T dR[3][9], const V3<T>& q, T* K) {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) K[i] = q.x * dR[0][i] + q.y * dR[1][i] + q.z * dR[2][i];
+}
+template <typename T>
+__device__ __forceinline__ bool fit_valid(const Args<T>& a, int v) { return a.C[3 * v] >= -999999.9f; }
+
+// ------------------------------------------------------------------ J^T F
+template <typename T>
+__global__ __launch_bounds__(kBlock) void arap_jtf(Args<T> a, T* __restrict__ r, T* __restrict__ diag) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= a.N) return;
+    const long long N = a.N;
+    const T wr = a.wr, wf = a.wf;
+    const V3<T> Ov = ld3<T>(a.O, v), Av = ld3<T>(a.A, v);
+    const V3<float> Uv = ld3<float>(a.U, v);
+    T R[9], dR[3][9];
+    rotation(Av, R, dR);
+    V3<T> rO = {0, 0, 0}, dO = {0, 0, 0}, rA = {0, 0, 0}, dA = {0, 0, 0};
+    if (fit_valid(a, v)) {
+        const V3<float> Cv = ld3<float>(a.C, v);
+        rO = {-(wf * (wf * (Ov.x - (T)Cv.x))), -(wf * (wf * (Ov.y - (T)Cv.y))), -(wf * (wf * (Ov.z - (T)Cv.z)))};
+        dO = {wf * wf, wf * wf, wf * wf};
+    }
+    for (int i = a.out_off[v]; i < a.out_off[v + 1]; ++i) {   // residuals centred here
+        const int u = a.out_nbr[i];
+        const V3<T> Ou = ld3<T>(a.O, u);
+        const V3<float> Uu = ld3<float>(a.U, u);
+        const V3<T> d = {(T)(Uv.x - Uu.x), (T)(Uv.y - Uu.y), (T)(Uv.z - Uu.z)};
+        const V3<T> Rd = mv(R, d);
+        const V3<T> e = {wr * ((Ov.x - Ou.x) - Rd.x), wr * ((Ov.y - Ou.y) - Rd.y), wr * ((Ov.z - Ou.z) - Rd.z)};
+        rO.x -= wr * e.x; rO.y -= wr * e.y; rO.z -= wr * e.z;
+        dO.x += wr * wr; dO.y += wr * wr; dO.z += wr * wr;
+        T* rAj[3] = {&rA.x, &rA.y, &rA.z};
+        T* dAj[3] = {&dA.x, &dA.y, &dA.z};
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const V3<T> col = mv(dR[j], d);
+            const T px = -wr * col.x, py = -wr * col.y, pz = -wr * col.z;
+            *rAj[j] -= px * e.x + py * e.y + pz * e.z;
+            *dAj[j] += px * px + py * py + pz * pz;
+        }
+    }
+    for (int i = a.in_off[v]; i < a.in_off[v + 1]; ++i) {     // residuals whose tail is v
+        const int u = a.in_nbr[i];
+        const V3<T> Ou = ld3<T>(a.O, u), Au = ld3<T>(a.A, u);
+        const V3<float> Uu = ld3<float>(a.U, u);
+        T Ru[9];
+        rotation<T>(Au, Ru, nullptr);
+        const V3<T> d = {(T)(Uu.x - Uv.x), (T)(Uu.y - Uv.y), (T)(Uu.z - Uv.z)};
+        const V3<T> Rd = mv(Ru, d);
+        const V3<T> e = {wr * ((Ou.x - Ov.x) - Rd.x), wr * ((Ou.y - Ov.y) - Rd.y), wr * ((Ou.z - Ov.z) - Rd.z)};
+        rO.x += wr * e.x; rO.y += wr * e.y; rO.z += wr * e.z;
+        dO.x += wr * wr; dO.y += wr * wr; dO.z += wr * wr;
+    }
+    r[3 * v] = rO.x; r[3 * v + 1] = rO.y; r[3 * v + 2] = rO.z;
+    r[3 * N + 3 * v] = rA.x; r[3 * N + 3 * v + 1] = rA.y; r[3 * N + 3 * v + 2] = rA.z;
+    diag[3 * v] = dO.x; diag[3 * v + 1] = dO.y; diag[3 * v + 2] = dO.z;
+    diag[3 * N + 3 * v] = dA.x; diag[3 * N + 3 * v + 1] = dA.y; diag[3 * N + 3 * v + 2] = dA.z;
+    a.flags[v] = 1;
+}
+
+// ------------------------------------------------------------------ J^T J p
+template <typename T>
+__global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
+                                                     const T* __restrict__ dadd, const int* stop, ReduceSlot rs) {
+    if (stop && *stop) return;
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    T dot = 0;
+    if (v < a.N) {
+        const long long N = a.N;
+        const T wr = a.wr, wf = a.wf;
+        const V3<T> pO = ld3<T>(p, v), pA = ld3<T>(p + 3 * N, v);
+        const V3<T> Av = ld3<T>(a.A, v);
+        const V3<float> Uv = ld3<float>(a.U, v);
+        T R[9], dR[3][9], K[9];
+        rotation(Av, R, dR);
+        directional(dR, pA, K);
+        V3<T> aO = {0, 0, 0}, aA = {0, 0, 0};
+        if (fit_valid(a, v)) aO = {wf * (wf * pO.x), wf * (wf * pO.y), wf * (wf * pO.z)};
+        for (int i = a.out_off[v]; i < a.out_off[v + 1]; ++i) {
+            const int u = a.out_nbr[i];
+            const V3<T> pu = ld3<T>(p, u);
+            const V3<float> Uu = ld3<float>(a.U, u);
+            const V3<T> d = {(T)(Uv.x - Uu.x), (T)(Uv.y - Uu.y), (T)(Uv.z - Uu.z)};
+            const V3<T> Kd = mv(K, d);
+            const V3<T> jp = {wr * (pO.x - pu.x - Kd.x), wr * (pO.y - pu.y - Kd.y), wr * (pO.z - pu.z - Kd.z)};
+            aO.x += wr * jp.x; aO.y += wr * jp.y; aO.z += wr * jp.z;
+            const V3<T> c0 = mv(dR[0], d), c1 = mv(dR[1], d), c2 = mv(dR[2], d);
+            aA.x -= wr * (c0.x * jp.x + c0.y * jp.y + c0.z * jp.z);
+            aA.y -= wr * (c1.x * jp.x + c1.y * jp.y + c1.z * jp.z);
+            aA.z -= wr * (c2.x * jp.x + c2.y * jp.y + c2.z * jp.z);
+        }
+        for (int i = a.in_off[v]; i < a.in_off[v + 1]; ++i) {
+            const int u = a.in_nbr[i];
+            const V3<T> pu = ld3<T>(p, u), pAu = ld3<T>(p + 3 * N, u), Au = ld3<T>(a.A, u);
+            const V3<float> Uu = ld3<float>(a.U, u);
+            T Ru[9], dRu[3][9], Ku[9];
+            rotation(Au, Ru, dRu);
+            directional(dRu, pAu, Ku);
+            const V3<T> d = {(T)(Uu.x - Uv.x), (T)(Uu.y - Uv.y), (T)(Uu.z - Uv.z)};
+            const V3<T> Kd = mv(Ku, d);
+            const V3<T> jp = {wr * (pu.x - pO.x - Kd.x), wr * (pu.y - pO.y - Kd.y), wr * (pu.z - pO.z - Kd.z)};
+            aO.x -= wr * jp.x; aO.y -= wr * jp.y; aO.z -= wr * jp.z;
+        }
+        if (dadd) {
+            aO.x += dadd[3 * v] * pO.x; aO.y += dadd[3 * v + 1] * pO.y; aO.z += dadd[3 * v + 2] * pO.z;
+            aA.x += dadd[3 * N + 3 * v] * pA.x; aA.y += dadd[3 * N + 3 * v + 1] * pA.y;
+            aA.z += dadd[3 * N + 3 * v + 2] * pA.z;
+        }
+        Ap[3 * v] = aO.x; Ap[3 * v + 1] = aO.y; Ap[3 * v + 2] = aO.z;
+        Ap[3 * N + 3 * v] = aA.x; Ap[3 * N + 3 * v + 1] = aA.y; Ap[3 * N + 3 * v + 2] = aA.z;
+        dot = pO.x * aO.x + pO.y * aO.y + pO.z * aO.z + pA.x * aA.x + pA.y * aA.y + pA.z * aA.z;
+    }
+    double vv[1] = {(double)dot};
+    block_reduce_publish<1>(vv, rs, blockIdx.x);
+}
+
+// ------------------------------------------------------- cost / model cost
+// Each edge residual is summed by its head vertex (the edge's out-list owner).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void arap_cost(Args<T> a, const T* __restrict__ delta, ReduceSlot rs) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    T acc = 0;
+    if (v < a.N) {
+        const long long N = a.N;
+        const T wr = a.wr, wf = a.wf;
+        const V3<T> Ov = ld3<T>(a.O, v), Av = ld3<T>(a.A, v);
+        const V3<float> Uv = ld3<float>(a.U, v);
+        V3<T> dO = {0, 0, 0}, dAv = {0, 0, 0};
+        if (delta) { dO = ld3<T>(delta, v); dAv = ld3<T>(delta + 3 * N, v); }
+        T R[9], dR[3][9], K[9];
+        rotation(Av, R, delta ? dR : nullptr);
+        if (delta) directional(dR, dAv, K);
+        T fit = 0;
+        if (fit_valid(a, v)) {
+            const V3<float> Cv = ld3<float>(a.C, v);
+            T ex = wf * (Ov.x - (T)Cv.x), ey = wf * (Ov.y - (T)Cv.y), ez = wf * (Ov.z - (T)Cv.z);
+            if (delta) { ex += wf * dO.x; ey += wf * dO.y; ez += wf * dO.z; }
+            fit = (T)0.5 * (ex * ex + ey * ey + ez * ez);
+        }
+        T reg = 0;
+        for (int i = a.out_off[v]; i < a.out_off[v + 1]; ++i) {
+            const int u = a.out_nbr[i];
+            const V3<T> Ou = ld3<T>(a.O, u);
+            const V3<float> Uu = ld3<float>(a.U, u);
+            const V3<T> d = {(T)(Uv.x - Uu.x), (T)(Uv.y - Uu.y), (T)(Uv.z - Uu.z)};
+            const V3<T> Rd = mv(R, d);
+            V3<T> e = {wr * ((Ov.x - Ou.x) - Rd.x), wr * ((Ov.y - Ou.y) - Rd.y), wr * ((Ov.z - Ou.z) - Rd.z)};
+            if (delta) {
+                const V3<T> du = ld3<T>(delta, u);
+                const V3<T> Kd = mv(K, d);
+                e.x += wr * (dO.x - du.x - Kd.x);
+                e.y += wr * (dO.y - du.y - Kd.y);
+                e.z += wr * (dO.z - du.z - Kd.z);
+            }
+            reg += (T)0.5 * (e.x * e.x + e.y * e.y + e.z * e.z);
+        }
+        acc = fit + reg;
+    }
+    double vv[1] = {(double)acc};
+    block_reduce_publish<1>(vv, rs, blockIdx.x);
+}
+
+// vertex indices of the graph must lie in [0, N): checked once per CSR build
+__global__ void check_indices(const int* v0, const int* v1, int E, int N, int* bad) {
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x)
+        if (v0[e] < 0 || v0[e] >= N || v1[e] < 0 || v1[e] >= N) atomicOr(bad, 1);
+}
+__global__ void count_heads(const int* keys, int E, int* counts) {
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x)
+        atomicAdd(&counts[keys[e]], 1);
+}
+
+}  // namespace arap
+
+// Deterministic CSR of a directed edge list grouped by `keys` (stable: edge order kept).
+struct GraphCSR {
+    int* off = nullptr;   // N + 1
+    int* nbr = nullptr;   // E
+    void release() { dfree(off); dfree(nbr); off = nbr = nullptr; }
+};
+
+template <typename TT>
+class ArapOp {
+public:
+    using T = TT;
+    static constexpr const char* kName = "arap_mesh_deformation";
+    static constexpr const char* kApplyName = "arap_apply";
+    static constexpr bool kSlabs = false;   // graph domain: single GPU (replicas only)
+    ArapOp(const ProblemSpec& spec, const StateOptions& opts, Domain dom) : opts_(opts) {
+        N_ = dom.W;
+        E_ = dom.edges;
+        idx_O_ = spec.unknown(0)->index;
+        idx_A_ = spec.unknown(1)->index;
+        idx_U_ = spec.array(0)->index;
+        idx_C_ = spec.array(1)->index;
+        idx_v0_ = spec.graphs[0].vertices[0].second;
+        idx_v1_ = spec.graphs[0].vertices[1].second;
+        std::vector<DeclParam> ps = spec.params;
+        std::sort(ps.begin(), ps.end(), [](auto& x, auto& y) { return x.index < y.index; });
+        idx_wf_ = ps[0].index;
+        idx_wr_ = ps[1].index;
+        for (auto& p : ps) {
+            if (p.name == "w_fitSqrt") idx_wf_ = p.index;
+            if (p.name == "w_regSqrt") idx_wr_ = p.index;
+        }
+        if (opts.host_buffers) {
+            dO_ = (T*)dmalloc(sizeof(T) * 3 * N_);
+            dA_ = (T*)dmalloc(sizeof(T) * 3 * N_);
+            dU_ = (float*)dmalloc(sizeof(float) * 3 * N_);
+            dC_ = (float*)dmalloc(sizeof(float) * 3 * N_);
+            dv0_ = (int*)dmalloc(sizeof(int) * std::max(E_, 1));
+            dv1_ = (int*)dmalloc(sizeof(int) * std::max(E_, 1));
+        }
+    }
+    ~ArapOp() {
+        out_.release(); in_.release();
+        dfree(dO_); dfree(dA_); dfree(dU_); dfree(dC_); dfree(dv0_); dfree(dv1_);
+        dfree(scratch_); dfree(keys_tmp_);
+    }
+    VecLayout layout() const {
+        VecLayout L{};
+        L.nimg = 2;
+        L.ch[0] = 3; L.ch[1] = 3;
+        L.off[0] = 0; L.off[1] = 3LL * N_; L.off[2] = 6LL * N_;
+        L.N = N_;
+        return L;
+    }
+    int halo() const { return 0; }
+    int stencil_blocks() const { return (N_ + kBlock - 1) / kBlock; }
+    void bind(void** params, hipStream_t s) {
+        a_.wf = (T)*(const float*)params[idx_wf_];
+        a_.wr = (T)*(const float*)params[idx_wr_];
+        userO_ = (T*)params[idx_O_];
+        userA_ = (T*)params[idx_A_];
+        const int* v0;
+        const int* v1;
+        if (!opts_.host_buffers) {
+            a_.O = userO_; a_.A = userA_;
+            a_.U = (const float*)params[idx_U_];
+            a_.C = (const float*)params[idx_C_];
+            v0 = (const int*)params[idx_v0_];
+            v1 = (const int*)params[idx_v1_];
+        } else {
+            OPT_HIP_CHECK(hipMemcpyAsync(dO_, userO_, sizeof(T) * 3 * N_, hipMemcpyHostToDevice, s));
+            OPT_HIP_CHECK(hipMemcpyAsync(dA_, userA_, sizeof(T) * 3 * N_, hipMemcpyHostToDevice, s));
+            OPT_HIP_CHECK(hipMemcpyAsync(dU_, params[idx_U_], sizeof(float) * 3 * N_, hipMemcpyHostToDevice, s));
+            OPT_HIP_CHECK(hipMemcpyAsync(dC_, params[idx_C_], sizeof(float) * 3 * N_, hipMemcpyHostToDevice, s));
+            // the graph itself only when its host arrays change
+            if (params[idx_v0_] != host_v0_ || params[idx_v1_] != host_v1_) {
+                OPT_HIP_CHECK(hipMemcpyAsync(dv0_, params[idx_v0_], sizeof(int) * E_, hipMemcpyHostToDevice, s));
+                OPT_HIP_CHECK(hipMemcpyAsync(dv1_, params[idx_v1_], sizeof(int) * E_, hipMemcpyHostToDevice, s));
+                host_v0_ = params[idx_v0_];
+                host_v1_ = params[idx_v1_];
+                graph_v0_ = nullptr;   // force a rebuild
+            }
+            a_.O = dO_; a_.A = dA_; a_.U = dU_; a_.C = dC_;
+            v0 = dv0_;
+            v1 = dv1_;
+        }
+        if (v0 != graph_v0_ || v1 != graph_v1_) build_csr(v0, v1, s);
+        a_.N = N_;
+        a_.out_off = out_.off; a_.out_nbr = out_.nbr;
+        a_.in_off = in_.off; a_.in_nbr = in_.nbr;
+    }
+    void unbind(hipStream_t s) {
+        if (!opts_.host_buffers) return;
+        OPT_HIP_CHECK(hipMemcpyAsync(userO_, dO_, sizeof(T) * 3 * N_, hipMemcpyDeviceToHost, s));
+        OPT_HIP_CHECK(hipMemcpyAsync(userA_, dA_, sizeof(T) * 3 * N_, hipMemcpyDeviceToHost, s));
+    }
+    T* unknown(int k) { return k == 0 ? a_.O : a_.A; }
+    void precompute(hipStream_t) {}
+    void computed_planes(std::vector<HaloPlane>&) const {}
+    void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
+        a_.flags = flags;
+        hipLaunchKernelGGL((arap::arap_jtf<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, r, diag);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
+        hipLaunchKernelGGL((arap::arap_apply<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap, dadd, stop,
+                           rs);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    void cost(ReduceSlot rs, hipStream_t s) {
+        hipLaunchKernelGGL((arap::arap_cost<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, (const T*)nullptr, rs);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    void model_cost(const T* delta, ReduceSlot rs, hipStream_t s) {
+        hipLaunchKernelGGL((arap::arap_cost<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, delta, rs);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+
+private:
+    // CSR of the edges grouped by `keys` with `vals` as the neighbour: stable radix sort
+    // of (key, neighbour) pairs + histogram / exclusive scan of the head counts.
+    void csr(const int* keys, const int* vals, GraphCSR& g, hipStream_t s) {
+        g.release();
+        g.off = (int*)dmalloc(sizeof(int) * (N_ + 1));
+        g.nbr = (int*)dmalloc(sizeof(int) * std::max(E_, 1));
+        OPT_HIP_CHECK(hipMemsetAsync(g.off, 0, sizeof(int) * (N_ + 1), s));
+        if (E_ == 0) return;
+        int bits = 1;
+        while ((1LL << bits) < N_) ++bits;
+        size_t need = 0, need2 = 0;
+        OPT_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, keys, keys_tmp_, vals, g.nbr, E_, 0, bits, s));
+        OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, need2, g.off, g.off, N_ + 1, s));
+        need = std::max(need, need2);
+        if (need > scratch_bytes_) {
+            dfree(scratch_);
+            scratch_ = dmalloc(need);
+            scratch_bytes_ = need;
+        }
+        OPT_HIP_CHECK(
+            hipcub::DeviceRadixSort::SortPairs(scratch_, need, keys, keys_tmp_, vals, g.nbr, E_, 0, bits, s));
+        hipLaunchKernelGGL(arap::count_heads, dim3(std::min((E_ + 255) / 256, 4096)), dim3(256), 0, s, keys, E_,
+                           g.off);
+        size_t n2 = scratch_bytes_;
+        OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(scratch_, n2, g.off, g.off, N_ + 1, s));
+    }
+    void build_csr(const int* v0, const int* v1, hipStream_t s) {
+        if (E_ > 0) {
+            int* bad = (int*)dmalloc(sizeof(int));
+            OPT_HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(int), s));
+            hipLaunchKernelGGL(arap::check_indices, dim3(std::min((E_ + 255) / 256, 4096)), dim3(256), 0, s, v0, v1,
+                               E_, N_, bad);
+            int hbad = 0;
+            OPT_HIP_CHECK(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, s));
+            OPT_HIP_CHECK(hipStreamSynchronize(s));
+            dfree(bad);
+            if (hbad) {
+                fprintf(stderr, "[opt_amd] arap_mesh_deformation: graph vertex index outside [0, %d)\n", N_);
+                exit(1);   // fail-stop, as the reference does on invalid input (backend_cuda.t:26-40)
+            }
+            dfree(keys_tmp_);
+            keys_tmp_ = (int*)dmalloc(sizeof(int) * E_);
+        }
+        csr(v0, v1, out_, s);
+        csr(v1, v0, in_, s);
+        graph_v0_ = v0;
+        graph_v1_ = v1;
+    }
+
+    StateOptions opts_;
+    int N_ = 0, E_ = 0;
+    int idx_O_, idx_A_, idx_U_, idx_C_, idx_v0_, idx_v1_, idx_wf_, idx_wr_;
+    arap::Args<T> a_{};
+    GraphCSR out_, in_;
+    const int* graph_v0_ = nullptr;
+    const int* graph_v1_ = nullptr;
+    const void* host_v0_ = nullptr;
+    const void* host_v1_ = nullptr;
+    void* scratch_ = nullptr;
+    size_t scratch_bytes_ = 0;
+    int* keys_tmp_ = nullptr;
+    T *userO_ = nullptr, *userA_ = nullptr, *dO_ = nullptr, *dA_ = nullptr;
+    float *dU_ = nullptr, *dC_ = nullptr;
+    int *dv0_ = nullptr, *dv1_ = nullptr;
+};
+
+std::unique_ptr<Plan> make_arap_plan(const ProblemSpec& spec, const StateOptions& opts, const unsigned* dims,
+                                     std::string* err) {
+    if (spec.graphs.size() != 1 || spec.graphs[0].vertices.size() != 2 || spec.graphs[0].dims.empty()) {
+        *err = "arap_mesh_deformation: expects one graph with two vertex slots";
+        return nullptr;
+    }
+    unsigned N = 0, E = 0;
+    for (auto& d : spec.dims) {
+        if (d.name == spec.unknown(0)->dims[0]) N = dims[d.index];
+        if (d.name == spec.graphs[0].dims[0]) E = dims[d.index];
+    }
+    if (N == 0) { *err = "arap_mesh_deformation: zero vertices"; return nullptr; }
+    if (N > (1u << 30) || E > (1u << 30)) { *err = "arap_mesh_deformation: graph too large"; return nullptr; }
+    Domain dom{(int)N, 1, 0, 1, 0, 1};
+    dom.edges = (int)E;
+    if (opts.double_precision) return std::unique_ptr<Plan>(new StencilPlan<ArapOp<double>>(spec, opts, dom));
+    return std::unique_ptr<Plan>(new StencilPlan<ArapOp<float>>(spec, opts, dom));
+}
+
+}  // namespace optamd

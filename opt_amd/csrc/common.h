@@ -32,6 +32,7 @@ struct Domain {
     int W, H;
     int y_lo, y_hi;
     int y_mem0, mem_rows;
+    int edges = 0;   // graph domains (W = vertex count, H = 1): directed edge count
     __host__ __device__ long long npix_mem() const { return (long long)W * mem_rows; }
     __host__ __device__ long long off(int x, int yg) const {
         return (long long)(yg - y_mem0) * W + x;

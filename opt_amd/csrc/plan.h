@@ -140,6 +140,9 @@ std::unique_ptr<Plan> make_optical_flow_plan(const ProblemSpec&, const StateOpti
 std::unique_ptr<Plan> make_sfs_plan(const ProblemSpec&, const StateOptions&, const unsigned* dims,
                                     std::string* err);
 
+std::unique_ptr<Plan> make_arap_plan(const ProblemSpec&, const StateOptions&, const unsigned* dims,
+                                     std::string* err);
+
 // Device-memory helpers (fail-stop).
 void* dmalloc(size_t bytes);
 void dfree(void* p);

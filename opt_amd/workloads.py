@@ -208,3 +208,48 @@ def shape_from_shading(W: int, H: int, seed: int = 3, valid_frac: float = 0.6, n
         "W": W,
         "H": H,
     }
+
+
+def arap_grid(nx: int, ny: int, seed: int = 9, n_handles: int = 16, z_noise: float = 0.01,
+              handle_move: float = 0.15):
+    """arap_mesh_deformation inputs (examples/arap_mesh_deformation).
+
+    A planar nx x ny grid mesh over [0,1]^2 (seeded z-noise), each quad split into two
+    triangles; the graph holds every mesh edge in both directions, grouped by head vertex
+    as createGraphFromNeighborLists builds it (examples/shared/OptGraph.h:78-90):
+    ~6 directed edges per vertex. Constraints: the first and last grid rows pinned to
+    themselves, n_handles seeded interior vertices moved by up to handle_move, all
+    others -inf (CombinedSolver.h:84-101); Angle = 0.1 (CombinedSolver.h:166);
+    w_fit = 4, w_reg = 1 passed as square roots (main.cpp).
+    """
+    rng = np.random.default_rng(seed)
+    N = nx * ny
+    ys, xs = np.mgrid[0:ny, 0:nx]
+    P = np.stack([xs / max(nx - 1, 1), ys / max(ny - 1, 1), z_noise * rng.normal(size=(ny, nx))], -1)
+    P = P.reshape(N, 3).astype(np.float32)
+    idx = np.arange(N).reshape(ny, nx)
+    und = [np.stack([idx[:, :-1].ravel(), idx[:, 1:].ravel()], 1),      # horizontal
+           np.stack([idx[:-1, :].ravel(), idx[1:, :].ravel()], 1),      # vertical
+           np.stack([idx[:-1, :-1].ravel(), idx[1:, 1:].ravel()], 1)]   # diagonal
+    und = np.concatenate(und)
+    directed = np.concatenate([und, und[:, ::-1]])
+    order = np.lexsort((directed[:, 1], directed[:, 0]))   # by head, then tail
+    directed = directed[order]
+    C = np.full((N, 3), -np.inf, np.float32)
+    pinned = np.concatenate([idx[0, :], idx[-1, :]])
+    C[pinned] = P[pinned]
+    interior = idx[1:-1, 1:-1].ravel()
+    handles = rng.choice(interior, size=min(n_handles, interior.size), replace=False)
+    C[handles] = P[handles] + rng.uniform(-handle_move, handle_move, (handles.size, 3)).astype(np.float32)
+    return {
+        "Offset": P.reshape(-1).copy(),
+        "Angle": np.full(3 * N, 0.1, np.float32),
+        "UrShape": P.reshape(-1).copy(),
+        "Constraints": C.reshape(-1),
+        "v0": np.ascontiguousarray(directed[:, 0].astype(np.int32)),
+        "v1": np.ascontiguousarray(directed[:, 1].astype(np.int32)),
+        "w_fitSqrt": float(np.sqrt(np.float32(4.0))),
+        "w_regSqrt": float(np.sqrt(np.float32(1.0))),
+        "N": N,
+        "E": int(directed.shape[0]),
+    }

@@ -310,3 +310,66 @@ def sfs_solve(w, n_iter, l_iter, lm=True):
     costs = np.zeros(n_iter + 1, np.float64)
     k = _sfs_lib().oracle_sfs_solve(*a, int(lm), n_iter, l_iter, costs.ctypes.data_as(_D))
     return X, costs[: k + 1]
+
+
+# ------------------------------------------------------------ arap_mesh_deformation
+_I = ctypes.POINTER(ctypes.c_int)
+
+
+def _arap_lib():
+    lib = load()
+    if not getattr(lib, "_arap", False):
+        i, f, d = ctypes.c_int, ctypes.c_float, ctypes.c_double
+        base = [i, i, _F, _F, _F, _F, _I, _I, f, f]
+        lib.oracle_arap_cost.restype, lib.oracle_arap_cost.argtypes = d, base
+        lib.oracle_arap_jtf.restype, lib.oracle_arap_jtf.argtypes = None, base + [_F, _F]
+        lib.oracle_arap_apply.restype, lib.oracle_arap_apply.argtypes = d, base + [_F, _F]
+        lib.oracle_arap_model_cost.restype, lib.oracle_arap_model_cost.argtypes = d, base + [_F]
+        lib.oracle_arap_solve.restype, lib.oracle_arap_solve.argtypes = i, base + [i, i, i, _D]
+        lib._arap = True
+    return lib
+
+
+def _arap_args(w, O=None, A=None):
+    O = np.ascontiguousarray(w["Offset"] if O is None else O, np.float32)
+    A = np.ascontiguousarray(w["Angle"] if A is None else A, np.float32)
+    v0 = np.ascontiguousarray(w["v0"], np.int32)
+    v1 = np.ascontiguousarray(w["v1"], np.int32)
+    keep = (O, A, v0, v1)
+    return keep, (w["N"], w["E"], _f(O), _f(A), _f(w["UrShape"]), _f(w["Constraints"]),
+                  v0.ctypes.data_as(_I), v1.ctypes.data_as(_I), w["w_fitSqrt"], w["w_regSqrt"])
+
+
+def arap_cost(w):
+    keep, a = _arap_args(w)
+    return _arap_lib().oracle_arap_cost(*a)
+
+
+def arap_jtf(w):
+    keep, a = _arap_args(w)
+    n = 6 * w["N"]
+    r, dg = np.zeros(n, np.float32), np.zeros(n, np.float32)
+    _arap_lib().oracle_arap_jtf(*a, _f(r), _f(dg))
+    return r, dg
+
+
+def arap_apply(w, p):
+    keep, a = _arap_args(w)
+    p = np.ascontiguousarray(p, np.float32)
+    Ap = np.zeros_like(p)
+    v = _arap_lib().oracle_arap_apply(*a, _f(p), _f(Ap))
+    return Ap, v
+
+
+def arap_model_cost(w, d):
+    keep, a = _arap_args(w)
+    d = np.ascontiguousarray(d, np.float32)
+    return _arap_lib().oracle_arap_model_cost(*a, _f(d))
+
+
+def arap_solve(w, n_iter, l_iter, lm=False):
+    O, A = w["Offset"].copy(), w["Angle"].copy()
+    keep, a = _arap_args(w, O, A)
+    costs = np.zeros(n_iter + 1, np.float64)
+    k = _arap_lib().oracle_arap_solve(*a, int(lm), n_iter, l_iter, costs.ctypes.data_as(_D))
+    return O, A, costs[: k + 1]

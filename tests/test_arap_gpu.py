@@ -1,0 +1,140 @@
+"""GPU parity of the arap_mesh_deformation graph path (CSR gathers built from the edge
+list, generic GN/LM driver) against the C oracle's edge-scatter restatement, through the
+C ABI. BASELINE config 4 (1M-vertex grid mesh, fp32, GN) at full size."""
+import os
+
+import numpy as np
+import pytest
+
+from opt_amd import OptSolver, workloads
+from oracle import oracle
+from tests.iw_helpers import ROOT, rel_err
+
+pytestmark = pytest.mark.gpu
+ENERGY = os.path.join(ROOT, "energies", "arap_mesh_deformation.t")
+
+
+def params(w, host=False, double=False):
+    dt = np.float64 if double else np.float32
+    arrs = [w["Offset"].astype(dt).copy(), w["Angle"].astype(dt).copy(), w["UrShape"], w["Constraints"]]
+    graph = [w["v0"], w["v1"]]
+    if not host:
+        import torch
+        arrs = [torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in arrs]
+        graph = [torch.from_numpy(g).cuda() for g in graph]
+    return [w["w_fitSqrt"], w["w_regSqrt"]] + arrs + [None] + graph
+
+
+def to_np(t):
+    return t.detach().cpu().numpy() if hasattr(t, "detach") else t
+
+
+def solver(w, kind="gaussNewtonGPU", **kw):
+    return OptSolver([w["N"], w["E"]], ENERGY, kind, **kw)
+
+
+def perturbed(nx, ny, seed):
+    w = workloads.arap_grid(nx, ny, seed=seed)
+    rng = np.random.default_rng(seed)
+    w["Offset"] = (w["Offset"] + 0.02 * rng.normal(size=w["Offset"].size)).astype(np.float32)
+    w["Angle"] = (w["Angle"] + 0.2 * rng.normal(size=w["Angle"].size)).astype(np.float32)
+    return w
+
+
+@pytest.mark.parametrize("nx,ny", [(7, 5), (40, 30), (3, 200)])
+def test_kernels_match_oracle(nx, ny):
+    import torch
+
+    w = perturbed(nx, ny, seed=nx + ny)
+    s = solver(w)
+    assert s.family() == "arap_mesh_deformation"
+    prm = params(w)
+    assert s.eval_cost(prm) == pytest.approx(oracle.arap_cost(w), rel=1e-5)
+    n = 6 * w["N"]
+    r = torch.zeros(n, device="cuda")
+    pre = torch.zeros(n, device="cuda")
+    s.eval_jtf(prm, r, pre)
+    r_ref, dg = oracle.arap_jtf(w)
+    assert rel_err(to_np(r), r_ref) < 2e-5
+    assert rel_err(to_np(pre), 1.0 / (1.0 + np.sqrt(dg)) ** 2) < 1e-5
+    p = np.random.default_rng(4).normal(size=n).astype(np.float32)
+    Ap = torch.zeros(n, device="cuda")
+    pAp = s.apply_jtj(prm, torch.from_numpy(p).cuda(), Ap)
+    Ap_ref, pAp_ref = oracle.arap_apply(w, p)
+    assert rel_err(to_np(Ap), Ap_ref) < 2e-5
+    assert pAp == pytest.approx(pAp_ref, rel=2e-5)
+
+
+@pytest.mark.parametrize("kind,nit,lit", [("gaussNewtonGPU", 4, 20), ("LMGPU", 6, 20), ("LMGPU", 3, 25)])
+def test_solve_matches_oracle(kind, nit, lit):
+    w = perturbed(40, 30, seed=8)
+    s = solver(w, kind)
+    prm = params(w)
+    s.set_solver_params({"nIterations": nit, "lIterations": lit})
+    costs = s.profiled_solve(prm)
+    O_ref, A_ref, c_ref = oracle.arap_solve(w, nit, lit, lm=(kind == "LMGPU"))
+    assert len(costs) == len(c_ref)
+    np.testing.assert_allclose(costs, c_ref, rtol=1e-4)
+    assert rel_err(to_np(prm[2]), O_ref) < 1e-4
+    assert np.abs(to_np(prm[3]) - A_ref).max() < 1e-3
+
+
+def test_edge_order_does_not_matter():
+    """A shuffled edge list gives the same CSR up to per-vertex order (tolerance only)."""
+    w = perturbed(30, 20, seed=3)
+    s = solver(w)
+    prm = params(w)
+    s.set_solver_params({"nIterations": 3, "lIterations": 10})
+    c1 = s.profiled_solve(prm)
+    perm = np.random.default_rng(0).permutation(w["E"])
+    w2 = dict(w, v0=np.ascontiguousarray(w["v0"][perm]), v1=np.ascontiguousarray(w["v1"][perm]))
+    s2 = solver(w2)
+    prm2 = params(w2)
+    s2.set_solver_params({"nIterations": 3, "lIterations": 10})
+    c2 = s2.profiled_solve(prm2)
+    np.testing.assert_allclose(c2, c1, rtol=1e-5)
+
+
+def test_host_buffers_equal_device_path():
+    w = perturbed(25, 20, seed=6)
+    sd = solver(w, "LMGPU")
+    pd = params(w)
+    sd.set_solver_params({"nIterations": 4, "lIterations": 10})
+    cd = sd.profiled_solve(pd)
+    sh = solver(w, "LMGPU", backend="backend_cpu")
+    ph = params(w, host=True)
+    sh.set_solver_params({"nIterations": 4, "lIterations": 10})
+    ch = sh.profiled_solve(ph)
+    np.testing.assert_array_equal(cd, ch)
+    np.testing.assert_array_equal(to_np(pd[2]), ph[2])
+
+
+def test_double_precision_tracks_float():
+    w = perturbed(20, 20, seed=2)
+    c = []
+    for dbl in (False, True):
+        s = solver(w, double_precision=dbl)
+        prm = params(w, double=dbl)
+        s.set_solver_params({"nIterations": 3, "lIterations": 10})
+        c.append(s.profiled_solve(prm))
+    np.testing.assert_allclose(c[1], c[0], rtol=1e-3)
+
+
+def test_config4_one_million_vertices():
+    """BASELINE config 4: 1000x1000 grid mesh (1M vertices, ~6M directed edges), GN:
+    energy trajectory vs the oracle, descent, bitwise determinism."""
+    w = workloads.arap_grid(1000, 1000, seed=9)
+    assert w["N"] == 1000000 and 5.9e6 < w["E"] < 6.1e6
+    runs = []
+    for _ in range(2):
+        s = solver(w)
+        prm = params(w)
+        s.set_solver_params({"nIterations": 3, "lIterations": 10})
+        runs.append((s.profiled_solve(prm), to_np(prm[2])))
+        s.close()
+    c = runs[0][0]
+    assert c[-1] < c[0]
+    np.testing.assert_array_equal(runs[1][0], c)
+    np.testing.assert_array_equal(runs[1][1], runs[0][1])
+    _, _, c_ref = oracle.arap_solve(w, 3, 10)
+    np.testing.assert_allclose(c, c_ref, rtol=1e-4)
