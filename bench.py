@@ -43,6 +43,31 @@ def apply_bytes_per_px(i: int) -> int:
     return b
 
 
+# HBM traffic of the in-loop apply from the committed rocprofv3 PMC summary of the same
+# kernels (tools/measure.sh: separate --pmc FETCH_SIZE / WRITE_SIZE passes over this
+# bench). FETCH_SIZE reads exactly 1/2 of the bytes on gfx950 for 1/4/8/16-B-per-lane
+# streaming reads and WRITE_SIZE is exact (profiles/r01_fetchcal.json, 1 GiB arrays), so
+# traffic = 2 FETCH_SIZE + WRITE_SIZE, averaged over the lIterations in-loop launches.
+PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc.json")
+APPLY_VARIANT = {0: "iw_apply<float, 1, 0,", 1: "iw_apply<float, 2, 1,", 2: "iw_apply<float, 2, 2,"}
+
+
+def pmc_traffic(liter: int):
+    try:
+        with open(PMC_FILE) as f:
+            ks = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    total = 0.0
+    for i in range(liter):
+        key = APPLY_VARIANT[min(i, 2)]
+        hit = [v for k, v in ks.items() if key in k]
+        if not hit or "FETCH_SIZE" not in hit[0] or "WRITE_SIZE" not in hit[0]:
+            return None
+        total += (2.0 * hit[0]["FETCH_SIZE"] + hit[0]["WRITE_SIZE"]) * 1024.0
+    return total / liter
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -54,8 +79,8 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(w, n_unknowns):
-    """Oracle J^T J p apply on host cores (bounded: one full-image apply)."""
+def cpu_baseline(w, n_unknowns, budget_s=10.0):
+    """Oracle J^T J p apply on host cores: full-image applies repeated for ~budget_s."""
     from oracle import oracle
 
     cores = min(16, os.cpu_count() or 1)
@@ -65,16 +90,21 @@ def cpu_baseline(w, n_unknowns):
                          "Angle": w["Angle"][: w["W"] * 64], "UrShape": w["UrShape"][: 2 * w["W"] * 64],
                          "Constraints": w["Constraints"][: 2 * w["W"] * 64], "Mask": w["Mask"][: w["W"] * 64]},
                         p[: 3 * w["W"] * 64], nthreads=cores)  # warm
+    reps = 0
     t0 = time.perf_counter()
-    oracle.iw_apply_jtj(w, p, nthreads=cores)
-    dt = time.perf_counter() - t0
+    while True:
+        oracle.iw_apply_jtj(w, p, nthreads=cores)
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= budget_s:
+            break
     return {
-        "value": n_unknowns / dt,
+        "value": reps * n_unknowns / dt,
         "unit": "unknowns/s",
         "cores": cores,
         "kind": "port",
-        "sample": f"one J^T J p apply over the full {w['W']}x{w['H']} image "
-                  f"({n_unknowns} unknowns), oracle/image_warping.c, {cores} pthreads, {dt:.2f} s",
+        "sample": f"{reps} J^T J p applies over the full {w['W']}x{w['H']} image "
+                  f"({n_unknowns} unknowns each), oracle/image_warping.c, {cores} pthreads, {dt:.1f} s",
     }
 
 
@@ -186,7 +216,8 @@ def main():
             "peak": PEAK_HBM_GBS,
             "unit": "GB/s",
             "frac": achieved / PEAK_HBM_GBS,
-            "traffic": None,
+            "traffic": (pmc_traffic(args.liter) if world == 1 and args.size == 4096 else None),
+            "traffic_unit": "bytes per launch (2 FETCH_SIZE + WRITE_SIZE, profiles/r01_pmc.json)",
             "avg_us": avg_apply_s * 1e6,
             "launches": n_apply,
             "bytes_per_px": bpp,
