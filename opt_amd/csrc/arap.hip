@@ -14,8 +14,8 @@
 //   J_e p = w (p_O(v0) - p_O(v1) - K_v0 d_e),  K_v = sum_j p_A,j(v) dR/dA_j(v),  d_e = U(v0) - U(v1)
 //   (J^T J p)_O(v) = w sum_out J_e p - w sum_in J_e p (+ w_fit^2 p_O(v))
 //   (J^T J p)_A,j(v) = -w sum_out (dR_j(v) d_e) . J_e p
-// For an in-edge the neighbour's K_u is rebuilt from its angle and p_A (three sincos),
-// which costs less than storing 9 floats per vertex per apply.
+// K is computed once per vertex per apply by a first pass (arap_kdir, 36 B/vertex) so
+// the in-edge terms read the neighbour's K instead of rebuilding its rotation derivatives.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <algorithm>
@@ -138,9 +138,27 @@ __global__ __launch_bounds__(kBlock) void arap_jtf(Args<T> a, T* __restrict__ r,
 }
 
 // ------------------------------------------------------------------ J^T J p
+// First pass of the apply: K_v = sum_j p_A,j(v) dR/dA_j(v) for every vertex (9 values),
+// so the in-edge terms of the gather read a neighbour's K instead of rebuilding its
+// rotation derivatives (three sincos and ~80 FMA per in-edge).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void arap_kdir(Args<T> a, const T* __restrict__ p, T* __restrict__ Kout,
+                                                    const int* stop) {
+    if (stop && *stop) return;
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= a.N) return;
+    const long long N = a.N;
+    T R[9], dR[3][9], K[9];
+    rotation(ld3<T>(a.A, v), R, dR);
+    directional(dR, ld3<T>(p + 3 * N, v), K);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Kout[9LL * v + i] = K[i];
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
-                                                     const T* __restrict__ dadd, const int* stop, ReduceSlot rs) {
+                                                     const T* __restrict__ Kall, const T* __restrict__ dadd,
+                                                     const int* stop, ReduceSlot rs) {
     if (stop && *stop) return;
     const int v = blockIdx.x * blockDim.x + threadIdx.x;
     T dot = 0;
@@ -170,11 +188,11 @@ __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restr
         }
         for (int i = a.in_off[v]; i < a.in_off[v + 1]; ++i) {
             const int u = a.in_nbr[i];
-            const V3<T> pu = ld3<T>(p, u), pAu = ld3<T>(p + 3 * N, u), Au = ld3<T>(a.A, u);
+            const V3<T> pu = ld3<T>(p, u);
             const V3<float> Uu = ld3<float>(a.U, u);
-            T Ru[9], dRu[3][9], Ku[9];
-            rotation(Au, Ru, dRu);
-            directional(dRu, pAu, Ku);
+            T Ku[9];
+#pragma unroll
+            for (int q = 0; q < 9; ++q) Ku[q] = Kall[9LL * u + q];
             const V3<T> d = {(T)(Uu.x - Uv.x), (T)(Uu.y - Uv.y), (T)(Uu.z - Uv.z)};
             const V3<T> Kd = mv(Ku, d);
             const V3<T> jp = {wr * (pu.x - pO.x - Kd.x), wr * (pu.y - pO.y - Kd.y), wr * (pu.z - pO.z - Kd.z)};
@@ -282,6 +300,7 @@ public:
             if (p.name == "w_fitSqrt") idx_wf_ = p.index;
             if (p.name == "w_regSqrt") idx_wr_ = p.index;
         }
+        K_ = (T*)dmalloc(sizeof(T) * 9 * std::max(N_, 1));
         if (opts.host_buffers) {
             dO_ = (T*)dmalloc(sizeof(T) * 3 * N_);
             dA_ = (T*)dmalloc(sizeof(T) * 3 * N_);
@@ -294,7 +313,7 @@ public:
     ~ArapOp() {
         out_.release(); in_.release();
         dfree(dO_); dfree(dA_); dfree(dU_); dfree(dC_); dfree(dv0_); dfree(dv1_);
-        dfree(scratch_); dfree(keys_tmp_);
+        dfree(scratch_); dfree(keys_tmp_); dfree(K_);
     }
     VecLayout layout() const {
         VecLayout L{};
@@ -355,8 +374,9 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
     void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
-        hipLaunchKernelGGL((arap::arap_apply<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap, dadd, stop,
-                           rs);
+        hipLaunchKernelGGL((arap::arap_kdir<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, K_, stop);
+        hipLaunchKernelGGL((arap::arap_apply<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap,
+                           (const T*)K_, dadd, stop, rs);
         OPT_HIP_CHECK(hipGetLastError());
     }
     void cost(ReduceSlot rs, hipStream_t s) {
@@ -430,6 +450,7 @@ private:
     void* scratch_ = nullptr;
     size_t scratch_bytes_ = 0;
     int* keys_tmp_ = nullptr;
+    T* K_ = nullptr;   // per-vertex directional rotation derivative of the current p
     T *userO_ = nullptr, *userA_ = nullptr, *dO_ = nullptr, *dA_ = nullptr;
     float *dU_ = nullptr, *dC_ = nullptr;
     int *dv0_ = nullptr, *dv1_ = nullptr;

@@ -174,4 +174,32 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 
 template <typename T> struct Vec2 { T x, y; };
 
+// Persistent tile loops: a grid of at most kMaxTileBlocks blocks (a multiple of 8)
+// walks `ntiles` tiles; the blocks of one XCD (b % 8) take a contiguous range of tiles
+// so neighbouring tiles' halos meet in that XCD's L2, and every block arrives at the
+// reduction tickets once instead of once per tile.
+constexpr int kMaxTileBlocks = 2048;
+__host__ __device__ inline int tile_blocks(int ntiles) {
+    const int nb = ntiles < kMaxTileBlocks ? ntiles : kMaxTileBlocks;
+    return ((nb + 7) / 8) * 8;
+}
+struct TileRange { int first, end, step; };
+// 64 x 4 pixel tiles of a Domain's owned rows (one pixel per thread of a 256-thread block)
+struct PixGeom { int x, y; bool ok; long long i; };
+__host__ __device__ inline int pix_tiles(const Domain& d) { return ((d.W + 63) / 64) * ((d.y_hi - d.y_lo + 3) / 4); }
+__device__ __forceinline__ PixGeom tile_pix(const Domain& d, int tile) {
+    const int ntx = (d.W + 63) / 64;
+    PixGeom g;
+    g.x = (tile % ntx) * 64 + (threadIdx.x & 63);
+    g.y = d.y_lo + (tile / ntx) * 4 + (threadIdx.x >> 6);
+    g.ok = g.x < d.W && g.y < d.y_hi;
+    g.i = g.ok ? d.off(g.x, g.y) : 0;
+    return g;
+}
+__device__ __forceinline__ TileRange tile_range(int ntiles) {
+    const int nb = gridDim.x, b = blockIdx.x, xcd = b % 8, slot = b / 8, nslots = nb / 8;
+    const int lo = (int)((long long)ntiles * xcd / 8), hi = (int)((long long)ntiles * (xcd + 1) / 8);
+    return TileRange{lo + slot, hi, nslots};
+}
+
 }  // namespace optamd

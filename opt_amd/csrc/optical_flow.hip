@@ -41,7 +41,6 @@ struct Args {
     T wf, wr;
 };
 
-struct PixGeom { int x, y; bool ok; long long i; };
 __device__ __forceinline__ PixGeom pix(const Domain& d) {
     PixGeom g;
     g.x = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -131,12 +130,16 @@ __global__ __launch_bounds__(kBlock) void of_jtf(Args<T> a, T* __restrict__ r, T
 // Ap = J^T J p (+ dadd p for LM), sum p.Ap; returns at entry once *stop is set.
 // J^T J p = wf^2 G (G.p) + 2 wr^2 sum_{in-bounds t} (p_k - p_t), evaluated in the
 // reference's gather order (fit, then per direction: own instance, neighbour's).
+// Persistent: a capped grid walks 64 x 4 pixel tiles (common.h tile_range / tile_pix).
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void of_apply(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
                                                    const T* __restrict__ dadd, const int* stop, ReduceSlot rs) {
     if (stop && *stop) return;
-    const PixGeom g = pix(a.dom);
+    const TileRange tr = tile_range(pix_tiles(a.dom));
     T dot = 0;
+    for (int tile = tr.first; tile < tr.end; tile += tr.step) {
+    const PixGeom g = tile_pix(a.dom, tile);
     if (g.ok) {
         const V2<T> pk = ld2(p, g.i);
         const V2<T> gk = ld2((const T*)a.G, g.i);
@@ -164,18 +167,21 @@ __global__ __launch_bounds__(kBlock) void of_apply(Args<T> a, const T* __restric
             ay += c.y * pk.y;
         }
         st2(Ap, g.i, ax, ay);
-        dot = pk.x * ax + pk.y * ay;
+        dot += pk.x * ax + pk.y * ay;
+    }
     }
     double v[1] = {(double)dot};
-    block_reduce_publish<1>(v, rs, blockIdx.y * gridDim.x + blockIdx.x);
+    block_reduce_publish<1>(v, rs, blockIdx.x);
 }
 
 // cost 1/2 sum r^2 (delta == nullptr) or the LM model cost 1/2 sum (r + J delta)^2
 // (o.t:3119-3129, 2915-2943)
 template <typename T>
 __global__ __launch_bounds__(kBlock) void of_cost(Args<T> a, const T* __restrict__ delta, ReduceSlot rs) {
-    const PixGeom g = pix(a.dom);
+    const TileRange tr = tile_range(pix_tiles(a.dom));
     T acc = 0;
+    for (int tile = tr.first; tile < tr.end; tile += tr.step) {
+    const PixGeom g = tile_pix(a.dom, tile);
     if (g.ok) {
         const V2<T> xk = ld2((const T*)a.X, g.i);
         T xn, yn;
@@ -201,10 +207,11 @@ __global__ __launch_bounds__(kBlock) void of_cost(Args<T> a, const T* __restrict
             }
             s2 += ex * ex + ey * ey;
         }
-        acc = (T)0.5 * s2;
+        acc += (T)0.5 * s2;
+    }
     }
     double v[1] = {(double)acc};
-    block_reduce_publish<1>(v, rs, blockIdx.y * gridDim.x + blockIdx.x);
+    block_reduce_publish<1>(v, rs, blockIdx.x);
 }
 
 }  // namespace of
@@ -249,7 +256,7 @@ public:
         return L;
     }
     int halo() const { return 1; }
-    int stencil_blocks() const { return grid().x * grid().y; }
+    int stencil_blocks() const { return std::max<int>(grid().x * grid().y, tgrid()); }
     void bind(void** params, hipStream_t s) {
         a_.wf = (T)*(const float*)params[idx_wf_];
         a_.wr = (T)*(const float*)params[idx_wr_];
@@ -285,20 +292,24 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
     void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
-        hipLaunchKernelGGL((of::of_apply<T>), grid(), dim3(kBlock), 0, s, a_, p, Ap, dadd, stop, rs);
+        rs.nblocks = tgrid();
+        hipLaunchKernelGGL((of::of_apply<T>), dim3(tgrid()), dim3(kBlock), 0, s, a_, p, Ap, dadd, stop, rs);
         OPT_HIP_CHECK(hipGetLastError());
     }
     void cost(ReduceSlot rs, hipStream_t s) {
-        hipLaunchKernelGGL((of::of_cost<T>), grid(), dim3(kBlock), 0, s, a_, (const T*)nullptr, rs);
+        rs.nblocks = tgrid();
+        hipLaunchKernelGGL((of::of_cost<T>), dim3(tgrid()), dim3(kBlock), 0, s, a_, (const T*)nullptr, rs);
         OPT_HIP_CHECK(hipGetLastError());
     }
     void model_cost(const T* delta, ReduceSlot rs, hipStream_t s) {
-        hipLaunchKernelGGL((of::of_cost<T>), grid(), dim3(kBlock), 0, s, a_, delta, rs);
+        rs.nblocks = tgrid();
+        hipLaunchKernelGGL((of::of_cost<T>), dim3(tgrid()), dim3(kBlock), 0, s, a_, delta, rs);
         OPT_HIP_CHECK(hipGetLastError());
     }
 
 private:
     dim3 grid() const { return dim3((dom_.W + 63) / 64, (dom_.y_hi - dom_.y_lo + 3) / 4); }
+    int tgrid() const { return tile_blocks(pix_tiles(dom_)); }
     Domain dom_;
     StateOptions opts_;
     int idx_X_, idx_I_, idx_Ih_, idx_Ihx_, idx_Ihy_, idx_wf_, idx_wr_;

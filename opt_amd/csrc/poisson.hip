@@ -53,7 +53,6 @@ __device__ __forceinline__ V4t<T> resid(const V4t<T>& xk, const V4t<T>& xj, cons
 constexpr int DX[4] = {1, -1, 0, 0};
 constexpr int DY[4] = {0, 0, 1, -1};
 
-struct PixGeom { int x, y; bool ok; long long i; };
 __device__ __forceinline__ PixGeom pix(const Domain& d) {
     PixGeom g;
     g.x = blockIdx.x * 64 + (threadIdx.x & 63);

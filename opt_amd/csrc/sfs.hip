@@ -46,7 +46,6 @@ struct Args {
     T L[9];
 };
 
-struct PixGeom { int x, y; bool ok; long long i; };
 __device__ __forceinline__ PixGeom pix(const Domain& d) {
     PixGeom g;
     g.x = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -162,15 +161,28 @@ __device__ __forceinline__ void pvec(const Args<T>& a, int x, int y, T& px, T& p
     px = ((T)x - a.ux) / a.fx;
     py = ((T)y - a.uy) / a.fy;
 }
+// px / py of the columns / rows k-2 .. k+2 of a thread's pixel k: the divisions of
+// p(0,0) (shape_from_shading.t:26-31) are done once per thread, not once per use.
+template <typename T>
+struct PTab {
+    T x[5], y[5];
+    int kx, ky;
+    __device__ __forceinline__ void init(const Args<T>& a, int x0, int y0) {
+        kx = x0; ky = y0;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) pvec(a, x0 + j - 2, y0 + j - 2, x[j], y[j]);
+    }
+    __device__ __forceinline__ T px(int gx) const { return x[gx - kx + 2]; }
+    __device__ __forceinline__ T py(int gy) const { return y[gy - ky + 2]; }
+};
 // E_s: partial w.r.t. X(q) = ws co (px(q), py(q), 1); J p of the instance at c
 template <typename T>
-__device__ __forceinline__ void smooth_jp(const Args<T>& a, const T* p, int cx, int cy, T out[3]) {
+__device__ __forceinline__ void smooth_jp(const Args<T>& a, const PTab<T>& tb, const T* p, int cx, int cy, T out[3]) {
     constexpr int OX[5] = {0, -1, 0, 1, 0}, OY[5] = {0, 0, -1, 0, 1};
     out[0] = out[1] = out[2] = 0;
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
-        T px, py;
-        pvec(a, cx + OX[s], cy + OY[s], px, py);
+        const T px = tb.px(cx + OX[s]), py = tb.py(cy + OY[s]);
         const T co = s == 0 ? (T)4 : (T)-1;
         const T pv = pget(p, a.dom, cx + OX[s], cy + OY[s]);
         out[0] += a.ws * co * px * pv;
@@ -180,13 +192,12 @@ __device__ __forceinline__ void smooth_jp(const Args<T>& a, const T* p, int cx, 
 }
 // E_s value at c (oracle order: 4 p(0,0) - (sum of the four in order (-1,0),(0,-1),(1,0),(0,1)))
 template <typename T>
-__device__ __forceinline__ void smooth_val(const Args<T>& a, const T* X, int cx, int cy, T out[3]) {
+__device__ __forceinline__ void smooth_val(const Args<T>& a, const PTab<T>& tb, const T* X, int cx, int cy, T out[3]) {
     constexpr int OX[5] = {0, -1, 0, 1, 0}, OY[5] = {0, 0, -1, 0, 1};
     T sx = 0, sy = 0, sz = 0, x0 = 0, y0 = 0, z0 = 0;
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
-        T px, py;
-        pvec(a, cx + OX[s], cy + OY[s], px, py);
+        const T px = tb.px(cx + OX[s]), py = tb.py(cy + OY[s]);
         const T xv = get(X, a.dom, cx + OX[s], cy + OY[s]);
         if (s == 0) { x0 = px * xv; y0 = py * xv; z0 = xv; }
         else { sx += px * xv; sy += py * xv; sz += xv; }
@@ -233,13 +244,15 @@ __global__ __launch_bounds__(kBlock) void sfs_jtf(Args<T> a, T* __restrict__ r, 
             }
         }
         // E_s
-        T px, py;
-        pvec(a, x, y, px, py);
+        PTab<T> tb;
+        tb.init(a, x, y);
+        const T px = tb.px(x), py = tb.py(y);
+#pragma unroll
         for (int s = 0; s < 5; ++s) {
             const int cx = x - SX5[s], cy = y - SY5[s];
             if (!inside(a.dom, cx, cy) || a.valid[a.dom.off(cx, cy)] != 1) continue;
             T v[3];
-            smooth_val(a, a.X, cx, cy, v);
+            smooth_val(a, tb, a.X, cx, cy, v);
             const T co = s == 0 ? (T)4 : (T)-1;
             const T d0 = a.ws * co * px, d1 = a.ws * co * py, d2 = a.ws * co;
             F += d0 * v[0]; Dg += d0 * d0;
@@ -252,56 +265,169 @@ __global__ __launch_bounds__(kBlock) void sfs_jtf(Args<T> a, T* __restrict__ r, 
 }
 
 // ------------------------------------------------------------------- J^T J p
+// The shading residuals are w_g m(c) (B_I(c) - B_I(c+s)), so their Jacobian factors
+// through the directional derivative of the computed array,
+//   D(q) = J_{B_I}(q) p = G00(q) p(q) + Gm0(q) p(q-x) + G0m(q) p(q-y),
+// and J_g^T J_g p collapses to a chain of 3-point stencils:
+//   V_h(c) = w_g m_R(c) u_h(c),  u_h(c) = [inbe(c)] w_g m_R(c) (D(c) - D(c+x))   (same for v, +y)
+//   W(q)   = V_h(q) - V_h(q-x) + V_v(q) - V_v(q-y)
+//   (J_g^T J_g p)(k) = G00(k) W(k) + Gm0(k+x) W(k+x) + G0m(k+y) W(k+y).
+// The smoothness term is w_s^2 P(k).L(valid * L(Q))(k) with Q(q) = (px, py, 1)(q) p(q),
+// L = 4 centre - 4 neighbours; the fit term w_p^2 p(k). This is the reference's
+// per-unknown gather (o.t:2770-2830) re-associated; each residual is evaluated once.
+// A block owns a 64 x 8 tile; p and the gradient images are staged in LDS with a
+// 2 / 1-pixel ring, all tile loads issued before the first wait.
+constexpr int TX = 64, TY = 8;
+constexpr int PW = TX + 4, PH = TY + 4;    // p: origin (x0-2, y0-2)
+constexpr int GW = TX + 3, GH = TY + 3;    // gradient images and D: origin (x0-1, y0-1)
+constexpr int CW = TX + 2, CH = TY + 2;    // residual centres (V, u_s): origin (x0-1, y0-1)
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void sfs_apply(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
                                                     const T* __restrict__ dadd, const int* stop, ReduceSlot rs) {
     if (stop && *stop) return;
-    const PixGeom g = pix(a.dom);
+    __shared__ T sP[PH][PW];
+    __shared__ T sG00[GH][GW], sGm0[GH][GW], sG0m[GH][GW], sD[GH][GW];
+    __shared__ T sVh[CH][CW], sVv[CH][CW], sUs[3][CH][CW];
+    __shared__ uint8_t sMR[CH][CW], sMC[CH][CW], sV[CH][CW];
+    __shared__ T sPX[PW], sPY[PH];
+    const Domain& d = a.dom;
+    const int t = threadIdx.x;
+    const int ntx = (d.W + TX - 1) / TX, nty = (d.y_hi - d.y_lo + TY - 1) / TY;
+    const TileRange tr = tile_range(ntx * nty);
     T dot = 0;
-    if (g.ok) {
-        const int x = g.x, y = g.y;
-        T acc = 0;
-        if (a.flags[g.i] & 1) {
-            const T pk = p[g.i];
-            acc += a.wp * (a.wp * pk);
+    for (int tile = tr.first; tile < tr.end; tile += tr.step) {
+    const int x0 = (tile % ntx) * TX, y0 = d.y_lo + (tile / ntx) * TY;
+    constexpr int NP = (PW * PH + kBlock - 1) / kBlock;
+    constexpr int NG = (GW * GH + kBlock - 1) / kBlock;
+    constexpr int NC = (CW * CH + kBlock - 1) / kBlock;
+    T rP[NP], rG0[NG], rG1[NG], rG2[NG];
+    int rMR[NC], rMC[NC], rV[NC];
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const int sx = t == 0 ? 1 : 0;
-                for (int s = 0; s < 5; ++s) {
-                    const int ox = t == 0 ? HX[s] : VX[s], oy = t == 0 ? HY[s] : VY[s];
-                    const int cx = x - ox, cy = y - oy;
-                    if (!inbe(a.dom, cx, cy)) continue;
-                    const long long c = a.dom.off(cx, cy);
-                    const T m = (T)(t == 0 ? a.mR[c] : a.mC[c]);
-                    acc += shade_coef(a, cx, cy, sx, ox, oy, m) * shade_jp(a, p, cx, cy, sx, m);
-                }
+    for (int j = 0; j < NP; ++j) {
+        const int i = t + j * kBlock, rx = i % PW, ry = i / PW, gx = x0 - 2 + rx, gy = y0 - 2 + ry;
+        rP[j] = (i < PW * PH && inside(d, gx, gy)) ? p[d.off(gx, gy)] : (T)0;
+    }
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+        const int i = t + j * kBlock, rx = i % GW, ry = i / GW, gx = x0 - 1 + rx, gy = y0 - 1 + ry;
+        const bool in = i < GW * GH && inside(d, gx, gy);
+        const long long o = in ? d.off(gx, gy) : 0;
+        rG0[j] = in ? a.G00[o] : (T)0;
+        rG1[j] = in ? a.Gm0[o] : (T)0;
+        rG2[j] = in ? a.G0m[o] : (T)0;
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        const int i = t + j * kBlock, rx = i % CW, ry = i / CW, gx = x0 - 1 + rx, gy = y0 - 1 + ry;
+        const bool in = i < CW * CH && inbe(d, gx, gy);
+        const long long o = in ? d.off(gx, gy) : 0;
+        rMR[j] = in ? a.mR[o] : 0;
+        rMC[j] = in ? a.mC[o] : 0;
+        rV[j] = in ? a.valid[o] : 0;
+    }
+    // the tile's own flags and LM diagonal, needed only at the end
+    constexpr int NK = TX * TY / kBlock;
+    int rF[NK];
+    T rD[NK];
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+        const int i = t + j * kBlock, gx = x0 + (i % TX), gy = y0 + i / TX;
+        const bool own = gx < d.W && gy < d.y_hi;
+        const long long k = own ? d.off(gx, gy) : 0;
+        rF[j] = own ? a.flags[k] : 0;
+        rD[j] = (own && dadd) ? dadd[k] : (T)0;
+    }
+    if (t < PW) sPX[t] = ((T)(x0 - 2 + t) - a.ux) / a.fx;
+    else if (t < PW + PH) sPY[t - PW] = ((T)(y0 - 2 + (t - PW)) - a.uy) / a.fy;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const int i = t + j * kBlock;
+        if (i < PW * PH) sP[i / PW][i % PW] = rP[j];
+    }
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+        const int i = t + j * kBlock;
+        if (i < GW * GH) { sG00[i / GW][i % GW] = rG0[j]; sGm0[i / GW][i % GW] = rG1[j]; sG0m[i / GW][i % GW] = rG2[j]; }
+    }
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+        const int i = t + j * kBlock;
+        if (i < CW * CH) { sMR[i / CW][i % CW] = rMR[j]; sMC[i / CW][i % CW] = rMC[j]; sV[i / CW][i % CW] = rV[j]; }
+    }
+    __syncthreads();
+    const T wg = a.wg, ws = a.ws;
+    // D over the G region (G coords (gx, gy) = P coords - 1)
+    for (int i = t; i < GW * GH; i += kBlock) {
+        const int cx = i % GW, cy = i / GW;
+        sD[cy][cx] = sG00[cy][cx] * sP[cy + 1][cx + 1] + sGm0[cy][cx] * sP[cy + 1][cx] + sG0m[cy][cx] * sP[cy][cx + 1];
+    }
+    // u_s over the centre region (C coords = G coords)
+    for (int i = t; i < CW * CH; i += kBlock) {
+        const int cx = i % CW, cy = i / CW, px = cx + 1, py = cy + 1;
+        T q0 = 0, q1 = 0, q2 = 0;
+        if (sV[cy][cx] == 1) {
+            constexpr int OX[5] = {0, -1, 0, 1, 0}, OY[5] = {0, 0, -1, 0, 1};
+#pragma unroll
+            for (int sIdx = 0; sIdx < 5; ++sIdx) {
+                const T qx = sPX[px + OX[sIdx]], qy = sPY[py + OY[sIdx]];
+                const T co = sIdx == 0 ? (T)4 : (T)-1;
+                const T pv = sP[py + OY[sIdx]][px + OX[sIdx]];
+                q0 += ws * co * qx * pv;
+                q1 += ws * co * qy * pv;
+                q2 += ws * co * pv;
             }
-            T px, py;
-            pvec(a, x, y, px, py);
-            for (int s = 0; s < 5; ++s) {
-                const int cx = x - SX5[s], cy = y - SY5[s];
-                if (!inside(a.dom, cx, cy) || a.valid[a.dom.off(cx, cy)] != 1) continue;
-                T jp[3];
-                smooth_jp(a, p, cx, cy, jp);
-                const T co = s == 0 ? (T)4 : (T)-1;
-                acc += (a.ws * co * px) * jp[0];
-                acc += (a.ws * co * py) * jp[1];
-                acc += (a.ws * co) * jp[2];
-            }
-            if (dadd) acc += dadd[g.i] * pk;
-            dot = pk * acc;
         }
-        Ap[g.i] = acc;
+        sUs[0][cy][cx] = q0; sUs[1][cy][cx] = q1; sUs[2][cy][cx] = q2;
+    }
+    __syncthreads();
+    // V_h, V_v over the centre region (masks are 0 outside InBoundsExpanded(0,0,1))
+    for (int i = t; i < CW * CH; i += kBlock) {
+        const int cx = i % CW, cy = i / CW;
+        const T mh = (T)sMR[cy][cx], mv = (T)sMC[cy][cx];
+        const T dc = sD[cy][cx];
+        sVh[cy][cx] = wg * mh * (wg * mh * (dc - sD[cy][cx + 1]));
+        sVv[cy][cx] = wg * mv * (wg * mv * (dc - sD[cy + 1][cx]));
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+        const int i = t + j * kBlock, kx = i % TX, ky = i / TX;
+        const int gx = x0 + kx, gy = y0 + ky;
+        if (gx >= d.W || gy >= d.y_hi) continue;
+        const long long k = d.off(gx, gy);
+        T acc = 0;
+        if (rF[j] & 1) {
+            const int cx = kx + 1, cy = ky + 1;   // k in C / G coords
+            const T pk = sP[ky + 2][kx + 2];
+            auto W = [&](int qx, int qy) {
+                return (sVh[qy][qx] - sVh[qy][qx - 1]) + (sVv[qy][qx] - sVv[qy - 1][qx]);
+            };
+            T shade = sG00[cy][cx] * W(cx, cy) + sGm0[cy][cx + 1] * W(cx + 1, cy) + sG0m[cy + 1][cx] * W(cx, cy + 1);
+            T l[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                l[c] = (T)4 * sUs[c][cy][cx] -
+                       (sUs[c][cy][cx - 1] + sUs[c][cy - 1][cx] + sUs[c][cy][cx + 1] + sUs[c][cy + 1][cx]);
+            acc = a.wp * (a.wp * pk) + shade + ws * (sPX[kx + 2] * l[0] + sPY[ky + 2] * l[1] + l[2]);
+            if (dadd) acc += rD[j] * pk;
+            dot += pk * acc;
+        }
+        Ap[k] = acc;
+    }
+    __syncthreads();   // the next tile overwrites the LDS
     }
     double v[1] = {(double)dot};
-    block_reduce_publish<1>(v, rs, blockIdx.y * gridDim.x + blockIdx.x);
+    block_reduce_publish<1>(v, rs, blockIdx.x);
 }
 
 // ------------------------------------------------------- cost / model cost
 template <typename T>
 __global__ __launch_bounds__(kBlock) void sfs_cost(Args<T> a, const T* __restrict__ delta, ReduceSlot rs) {
-    const PixGeom g = pix(a.dom);
+    const TileRange tr = tile_range(pix_tiles(a.dom));
     T acc = 0;
+    for (int tile = tr.first; tile < tr.end; tile += tr.step) {
+    const PixGeom g = tile_pix(a.dom, tile);
     if (g.ok && a.D[g.i] > 0.f) {
         const int x = g.x, y = g.y;
         T s2 = 0;
@@ -322,19 +448,22 @@ __global__ __launch_bounds__(kBlock) void sfs_cost(Args<T> a, const T* __restric
             }
         }
         if (a.valid[g.i] == 1) {
+            PTab<T> tb;
+            tb.init(a, x, y);
             T v[3];
-            smooth_val(a, a.X, x, y, v);
+            smooth_val(a, tb, a.X, x, y, v);
             if (delta) {
                 T jd[3];
-                smooth_jp(a, delta, x, y, jd);
+                smooth_jp(a, tb, delta, x, y, jd);
                 v[0] += jd[0]; v[1] += jd[1]; v[2] += jd[2];
             }
             s2 += v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
         }
-        acc = (T)0.5 * s2;
+        acc += (T)0.5 * s2;
+    }
     }
     double v[1] = {(double)acc};
-    block_reduce_publish<1>(v, rs, blockIdx.y * gridDim.x + blockIdx.x);
+    block_reduce_publish<1>(v, rs, blockIdx.x);
 }
 
 }  // namespace sfs
@@ -390,7 +519,7 @@ public:
         return L;
     }
     int halo() const { return 2; }
-    int stencil_blocks() const { return grid().x * grid().y; }
+    int stencil_blocks() const { return std::max(grid().x * grid().y, tile_grid().x * tile_grid().y); }
     void bind(void** params, hipStream_t s) {
         auto pf = [&](int k) { return (T)*(const float*)params[idx_p_[k]]; };
         // w_p, w_s, w_g enter the energy as sqrt(Param) (shape_from_shading.t:4-6)
@@ -437,20 +566,28 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
     void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
-        hipLaunchKernelGGL((sfs::sfs_apply<T>), grid(), dim3(kBlock), 0, s, a_, p, Ap, dadd, stop, rs);
+        const dim3 g = tile_grid();
+        rs.nblocks = g.x * g.y;   // the reduction's arrival count is this launch's grid
+        hipLaunchKernelGGL((sfs::sfs_apply<T>), g, dim3(kBlock), 0, s, a_, p, Ap, dadd, stop, rs);
         OPT_HIP_CHECK(hipGetLastError());
     }
     void cost(ReduceSlot rs, hipStream_t s) {
-        hipLaunchKernelGGL((sfs::sfs_cost<T>), grid(), dim3(kBlock), 0, s, a_, (const T*)nullptr, rs);
+        rs.nblocks = tile_blocks(pix_tiles(dom_));
+        hipLaunchKernelGGL((sfs::sfs_cost<T>), dim3(rs.nblocks), dim3(kBlock), 0, s, a_, (const T*)nullptr, rs);
         OPT_HIP_CHECK(hipGetLastError());
     }
     void model_cost(const T* delta, ReduceSlot rs, hipStream_t s) {
-        hipLaunchKernelGGL((sfs::sfs_cost<T>), grid(), dim3(kBlock), 0, s, a_, delta, rs);
+        rs.nblocks = tile_blocks(pix_tiles(dom_));
+        hipLaunchKernelGGL((sfs::sfs_cost<T>), dim3(rs.nblocks), dim3(kBlock), 0, s, a_, delta, rs);
         OPT_HIP_CHECK(hipGetLastError());
     }
 
 private:
     dim3 grid() const { return dim3((dom_.W + 63) / 64, (dom_.y_hi - dom_.y_lo + 3) / 4); }
+    dim3 tile_grid() const {
+        const int nt = ((dom_.W + sfs::TX - 1) / sfs::TX) * ((dom_.y_hi - dom_.y_lo + sfs::TY - 1) / sfs::TY);
+        return dim3(tile_blocks(nt));
+    }
     Domain dom_;
     StateOptions opts_;
     int idx_X_, idx_D_, idx_Im_, idx_mR_, idx_mC_, idx_p_[16];
