@@ -42,6 +42,7 @@ struct Args {
 };
 
 template <typename T> struct V3 { T x, y, z; };
+constexpr int kEB = 4;   // edges gathered per batch
 template <typename T, typename S>
 __device__ __forceinline__ V3<T> ld3(const S* a, long long v) {
     return V3<T>{(T)a[3 * v], (T)a[3 * v + 1], (T)a[3 * v + 2]};
@@ -85,7 +86,7 @@ __device__ __forceinline__ bool fit_valid(const Args<T>& a, int v) { return a.C[
 // ------------------------------------------------------------------ J^T F
 template <typename T>
 __global__ __launch_bounds__(kBlock) void arap_jtf(Args<T> a, T* __restrict__ r, T* __restrict__ diag) {
-    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    const int v = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;   // contiguous vertex ranges per XCD
     if (v >= a.N) return;
     const long long N = a.N;
     const T wr = a.wr, wf = a.wf;
@@ -145,7 +146,7 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void arap_kdir(Args<T> a, const T* __restrict__ p, T* __restrict__ Kout,
                                                     const int* stop) {
     if (stop && *stop) return;
-    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    const int v = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;   // contiguous vertex ranges per XCD
     if (v >= a.N) return;
     const long long N = a.N;
     T R[9], dR[3][9], K[9];
@@ -160,7 +161,7 @@ __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restr
                                                      const T* __restrict__ Kall, const T* __restrict__ dadd,
                                                      const int* stop, ReduceSlot rs) {
     if (stop && *stop) return;
-    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    const int v = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;   // contiguous vertex ranges per XCD
     T dot = 0;
     if (v < a.N) {
         const long long N = a.N;
@@ -173,30 +174,54 @@ __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restr
         directional(dR, pA, K);
         V3<T> aO = {0, 0, 0}, aA = {0, 0, 0};
         if (fit_valid(a, v)) aO = {wf * (wf * pO.x), wf * (wf * pO.y), wf * (wf * pO.z)};
-        for (int i = a.out_off[v]; i < a.out_off[v + 1]; ++i) {
-            const int u = a.out_nbr[i];
-            const V3<T> pu = ld3<T>(p, u);
-            const V3<float> Uu = ld3<float>(a.U, u);
-            const V3<T> d = {(T)(Uv.x - Uu.x), (T)(Uv.y - Uu.y), (T)(Uv.z - Uu.z)};
-            const V3<T> Kd = mv(K, d);
-            const V3<T> jp = {wr * (pO.x - pu.x - Kd.x), wr * (pO.y - pu.y - Kd.y), wr * (pO.z - pu.z - Kd.z)};
-            aO.x += wr * jp.x; aO.y += wr * jp.y; aO.z += wr * jp.z;
-            const V3<T> c0 = mv(dR[0], d), c1 = mv(dR[1], d), c2 = mv(dR[2], d);
-            aA.x -= wr * (c0.x * jp.x + c0.y * jp.y + c0.z * jp.z);
-            aA.y -= wr * (c1.x * jp.x + c1.y * jp.y + c1.z * jp.z);
-            aA.z -= wr * (c2.x * jp.x + c2.y * jp.y + c2.z * jp.z);
-        }
-        for (int i = a.in_off[v]; i < a.in_off[v + 1]; ++i) {
-            const int u = a.in_nbr[i];
-            const V3<T> pu = ld3<T>(p, u);
-            const V3<float> Uu = ld3<float>(a.U, u);
-            T Ku[9];
+        // Edges in batches of kEB: all neighbour indices, then all neighbour data, are
+        // issued before any is used (memory-level parallelism for the dependent gathers).
+        const int ob = a.out_off[v], oe = a.out_off[v + 1], ib = a.in_off[v], ie = a.in_off[v + 1];
+        for (int i0 = ob; i0 < oe; i0 += kEB) {
+            int u[kEB];
 #pragma unroll
-            for (int q = 0; q < 9; ++q) Ku[q] = Kall[9LL * u + q];
-            const V3<T> d = {(T)(Uu.x - Uv.x), (T)(Uu.y - Uv.y), (T)(Uu.z - Uv.z)};
-            const V3<T> Kd = mv(Ku, d);
-            const V3<T> jp = {wr * (pu.x - pO.x - Kd.x), wr * (pu.y - pO.y - Kd.y), wr * (pu.z - pO.z - Kd.z)};
-            aO.x -= wr * jp.x; aO.y -= wr * jp.y; aO.z -= wr * jp.z;
+            for (int b = 0; b < kEB; ++b) u[b] = (i0 + b < oe) ? a.out_nbr[i0 + b] : v;
+            V3<T> pu[kEB];
+            V3<float> Uu[kEB];
+#pragma unroll
+            for (int b = 0; b < kEB; ++b) { pu[b] = ld3<T>(p, u[b]); Uu[b] = ld3<float>(a.U, u[b]); }
+#pragma unroll
+            for (int b = 0; b < kEB; ++b) {
+                if (i0 + b >= oe) break;
+                const V3<T> d = {(T)(Uv.x - Uu[b].x), (T)(Uv.y - Uu[b].y), (T)(Uv.z - Uu[b].z)};
+                const V3<T> Kd = mv(K, d);
+                const V3<T> jp = {wr * (pO.x - pu[b].x - Kd.x), wr * (pO.y - pu[b].y - Kd.y),
+                                  wr * (pO.z - pu[b].z - Kd.z)};
+                aO.x += wr * jp.x; aO.y += wr * jp.y; aO.z += wr * jp.z;
+                const V3<T> c0 = mv(dR[0], d), c1 = mv(dR[1], d), c2 = mv(dR[2], d);
+                aA.x -= wr * (c0.x * jp.x + c0.y * jp.y + c0.z * jp.z);
+                aA.y -= wr * (c1.x * jp.x + c1.y * jp.y + c1.z * jp.z);
+                aA.z -= wr * (c2.x * jp.x + c2.y * jp.y + c2.z * jp.z);
+            }
+        }
+        for (int i0 = ib; i0 < ie; i0 += kEB) {
+            int u[kEB];
+#pragma unroll
+            for (int b = 0; b < kEB; ++b) u[b] = (i0 + b < ie) ? a.in_nbr[i0 + b] : v;
+            V3<T> pu[kEB];
+            V3<float> Uu[kEB];
+            T Ku[kEB][9];
+#pragma unroll
+            for (int b = 0; b < kEB; ++b) {
+                pu[b] = ld3<T>(p, u[b]);
+                Uu[b] = ld3<float>(a.U, u[b]);
+#pragma unroll
+                for (int q = 0; q < 9; ++q) Ku[b][q] = Kall[9LL * u[b] + q];
+            }
+#pragma unroll
+            for (int b = 0; b < kEB; ++b) {
+                if (i0 + b >= ie) break;
+                const V3<T> d = {(T)(Uu[b].x - Uv.x), (T)(Uu[b].y - Uv.y), (T)(Uu[b].z - Uv.z)};
+                const V3<T> Kd = mv(Ku[b], d);
+                const V3<T> jp = {wr * (pu[b].x - pO.x - Kd.x), wr * (pu[b].y - pO.y - Kd.y),
+                                  wr * (pu[b].z - pO.z - Kd.z)};
+                aO.x -= wr * jp.x; aO.y -= wr * jp.y; aO.z -= wr * jp.z;
+            }
         }
         if (dadd) {
             aO.x += dadd[3 * v] * pO.x; aO.y += dadd[3 * v + 1] * pO.y; aO.z += dadd[3 * v + 2] * pO.z;
@@ -215,7 +240,7 @@ __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restr
 // Each edge residual is summed by its head vertex (the edge's out-list owner).
 template <typename T>
 __global__ __launch_bounds__(kBlock) void arap_cost(Args<T> a, const T* __restrict__ delta, ReduceSlot rs) {
-    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    const int v = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;   // contiguous vertex ranges per XCD
     T acc = 0;
     if (v < a.N) {
         const long long N = a.N;

@@ -86,7 +86,7 @@ struct ReduceSlot {
     double* out;          // K results
     int nblocks;
 };
-constexpr int kTicketShards = 8;      // one arrival counter per XCD group (b % 8)
+constexpr int kTicketShards = 32;     // arrival counters (b % 32: each fed by one XCD)
 constexpr int kTicketStride = 16;     // unsigned words between counters (64 B)
 constexpr int kTicketWords = (kTicketShards + 1) * kTicketStride;
 
@@ -98,7 +98,7 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 // Called by every thread of a kBlock-thread block exactly once, after all the
 // block's stores of the kernel's outputs. v[k] is this thread's contribution.
-// Arrivals are counted per XCD group (shard = block % 8, ~nblocks/8 adds per counter
+// Arrivals are counted per shard (shard = block % 32, ~nblocks/32 adds per counter
 // instead of nblocks on one word: a single hot counter costs ~12 ns per add,
 // MI355X_MICROARCH.md row "fanin"); the last arriver of each shard then adds to a
 // top counter, and the last of those sums every partial in block order.

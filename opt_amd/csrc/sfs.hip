@@ -92,13 +92,17 @@ __global__ __launch_bounds__(kBlock) void sfs_precompute(Args<T> a) {
         const T dBx = L[3] + L[4] * Ny + L[7] * Nz + (T)2 * Nx * (L[8] - L[6]);
         const T dBy = L[1] + L[4] * Nx + L[5] * Nz - (T)2 * Ny * (L[6] + L[8]);
         const T dBz = L[2] + L[5] * Ny + (T)4 * L[6] * Nz + L[7] * Nx;
-        const T dnx[3] = {B / fy, -B / fy, (d - A) / fy};
-        const T dny[3] = {A / fx, (d - B) / fx, -A / fx};
+        // partials of the normal (divisions by the constants done once as reciprocals:
+        // these feed the gradient images only, never the energy value)
+        const T rfx = (T)1 / fx, rfy = (T)1 / fy, rfxy = (T)1 / (fx * fy);
+        const T cx_ = (ux - i) * rfx, cy_ = (uy - j) * rfy;
+        const T dnx[3] = {B * rfy, -B * rfy, (d - A) * rfy};
+        const T dny[3] = {A * rfx, (d - B) * rfx, -A * rfx};
         const T dab[3] = {(T)0, B, A};
         T gv[3];
 #pragma unroll
         for (int v = 0; v < 3; ++v) {
-            const T dnz = dnx[v] * (ux - i) / fx + dny[v] * (uy - j) / fy - dab[v] / (fx * fy);
+            const T dnz = dnx[v] * cx_ + dny[v] * cy_ - dab[v] * rfxy;
             const T dinv = sq > (T)0 ? -(inv * inv * inv) * (nx * dnx[v] + ny * dny[v] + nz * dnz) : (T)0;
             const T dNx = dinv * nx + inv * dnx[v], dNy = dinv * ny + inv * dny[v], dNz = dinv * nz + inv * dnz;
             gv[v] = dBx * dNx + dBy * dNy + dBz * dNz;
@@ -207,62 +211,6 @@ __device__ __forceinline__ void smooth_val(const Args<T>& a, const PTab<T>& tb, 
     out[2] = a.ws * ((T)4 * z0 - sz);
 }
 
-// support offsets (where X_k sits relative to the centre) of E_g_h, E_g_v, E_s
-constexpr int HX[5] = {0, -1, 0, 1, 1}, HY[5] = {0, 0, -1, 0, -1};
-constexpr int VX[5] = {0, -1, 0, 0, -1}, VY[5] = {0, 0, -1, 1, 1};
-constexpr int SX5[5] = {0, -1, 0, 1, 0}, SY5[5] = {0, 0, -1, 0, 1};
-
-// ------------------------------------------------------------------- J^T F
-template <typename T>
-__global__ __launch_bounds__(kBlock) void sfs_jtf(Args<T> a, T* __restrict__ r, T* __restrict__ diag) {
-    const PixGeom g = pix(a.dom);
-    if (!g.ok) return;
-    const int x = g.x, y = g.y;
-    const bool act = a.D[g.i] > 0.f;
-    a.flags[g.i] = act;
-    T F = 0, Dg = 0;
-    if (act) {
-        // E_p (only offset (0,0))
-        const T ep = a.wp * (a.X[g.i] - (T)a.D[g.i]);
-        F += a.wp * ep;
-        Dg += a.wp * a.wp;
-        // E_g_h, E_g_v
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const int sx = t == 0 ? 1 : 0;
-            for (int s = 0; s < 5; ++s) {
-                const int ox = t == 0 ? HX[s] : VX[s], oy = t == 0 ? HY[s] : VY[s];
-                const int cx = x - ox, cy = y - oy;
-                if (!inbe(a.dom, cx, cy)) continue;
-                const long long c = a.dom.off(cx, cy);
-                const T m = (T)(t == 0 ? a.mR[c] : a.mC[c]);
-                const long long n = a.dom.off(cx + sx, cy + 1 - sx);
-                const T val = a.wg * (a.BI[c] - a.BI[n]) * m;
-                const T dk = shade_coef(a, cx, cy, sx, ox, oy, m);
-                F += dk * val;
-                Dg += dk * dk;
-            }
-        }
-        // E_s
-        PTab<T> tb;
-        tb.init(a, x, y);
-        const T px = tb.px(x), py = tb.py(y);
-#pragma unroll
-        for (int s = 0; s < 5; ++s) {
-            const int cx = x - SX5[s], cy = y - SY5[s];
-            if (!inside(a.dom, cx, cy) || a.valid[a.dom.off(cx, cy)] != 1) continue;
-            T v[3];
-            smooth_val(a, tb, a.X, cx, cy, v);
-            const T co = s == 0 ? (T)4 : (T)-1;
-            const T d0 = a.ws * co * px, d1 = a.ws * co * py, d2 = a.ws * co;
-            F += d0 * v[0]; Dg += d0 * d0;
-            F += d1 * v[1]; Dg += d1 * d1;
-            F += d2 * v[2]; Dg += d2 * d2;
-        }
-    }
-    r[g.i] = -F;
-    diag[g.i] = Dg;
-}
 
 // ------------------------------------------------------------------- J^T J p
 // The shading residuals are w_g m(c) (B_I(c) - B_I(c+s)), so their Jacobian factors
@@ -282,141 +230,200 @@ constexpr int PW = TX + 4, PH = TY + 4;    // p: origin (x0-2, y0-2)
 constexpr int GW = TX + 3, GH = TY + 3;    // gradient images and D: origin (x0-1, y0-1)
 constexpr int CW = TX + 2, CH = TY + 2;    // residual centres (V, u_s): origin (x0-1, y0-1)
 
-template <typename T>
-__global__ __launch_bounds__(kBlock) void sfs_apply(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
-                                                    const T* __restrict__ dadd, const int* stop, ReduceSlot rs) {
+// One tile's global data in registers: issued for tile t+1 right after tile t's copy
+// has gone to LDS, so its latency overlaps tile t's three compute phases.
+template <typename T, bool JTF>
+struct SfsTileRegs {
+    static constexpr int NP = (PW * PH + kBlock - 1) / kBlock;
+    static constexpr int NG = (GW * GH + kBlock - 1) / kBlock;
+    static constexpr int NC = (CW * CH + kBlock - 1) / kBlock;
+    static constexpr int NK = TX * TY / kBlock;
+    T P[NP], G0[NG], G1[NG], G2[NG], BI[JTF ? NG : 1];
+    int MR[NC], MC[NC], V[NC], F[NK];
+    T Dg[NK];   // apply: the LM diagonal; J^T F: D_i
+    __device__ __forceinline__ void load(const Args<T>& a, const T* p, const T* dadd, int x0, int y0) {
+        const Domain& d = a.dom;
+        const int t = threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < NP; ++j) {
+            const int i = t + j * kBlock, rx = i % PW, ry = i / PW, gx = x0 - 2 + rx, gy = y0 - 2 + ry;
+            P[j] = (i < PW * PH && inside(d, gx, gy)) ? p[d.off(gx, gy)] : (T)0;
+        }
+#pragma unroll
+        for (int j = 0; j < NG; ++j) {
+            const int i = t + j * kBlock, rx = i % GW, ry = i / GW, gx = x0 - 1 + rx, gy = y0 - 1 + ry;
+            const bool in = i < GW * GH && inside(d, gx, gy);
+            const long long o = in ? d.off(gx, gy) : 0;
+            G0[j] = in ? a.G00[o] : (T)0;
+            G1[j] = in ? a.Gm0[o] : (T)0;
+            G2[j] = in ? a.G0m[o] : (T)0;
+            if (JTF) BI[j] = in ? a.BI[o] : (T)0;
+        }
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            const int i = t + j * kBlock, rx = i % CW, ry = i / CW, gx = x0 - 1 + rx, gy = y0 - 1 + ry;
+            const bool in = i < CW * CH && inbe(d, gx, gy);
+            const long long o = in ? d.off(gx, gy) : 0;
+            MR[j] = in ? a.mR[o] : 0;
+            MC[j] = in ? a.mC[o] : 0;
+            V[j] = in ? a.valid[o] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < NK; ++j) {
+            const int i = t + j * kBlock, gx = x0 + (i % TX), gy = y0 + i / TX;
+            const bool own = gx < d.W && gy < d.y_hi;
+            const long long k = own ? d.off(gx, gy) : 0;
+            if (JTF) {
+                Dg[j] = own ? (T)a.D[k] : (T)0;
+                F[j] = own && a.D[k] > 0.f;
+            } else {
+                F[j] = own ? a.flags[k] : 0;
+                Dg[j] = (own && dadd) ? dadd[k] : (T)0;
+            }
+        }
+    }
+};
+
+// JTF = true: the same tile pipeline evaluates r = -J^T F and diag(J^T J) (evalJTF,
+// o.t:2870-2913): "p" is X, the directional derivative D is replaced by B_I itself
+// (the shading residual values), the smoothness Q by P X, the fit term by w_p (X - D_i);
+// it also writes the flag byte. Ap / dadd / reduction unused.
+template <typename T, bool JTF>
+__global__ __launch_bounds__(kBlock) void sfs_tiles(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
+                                                    T* __restrict__ diag, const T* __restrict__ dadd,
+                                                    const int* stop, ReduceSlot rs) {
     if (stop && *stop) return;
     __shared__ T sP[PH][PW];
     __shared__ T sG00[GH][GW], sGm0[GH][GW], sG0m[GH][GW], sD[GH][GW];
     __shared__ T sVh[CH][CW], sVv[CH][CW], sUs[3][CH][CW];
     __shared__ uint8_t sMR[CH][CW], sMC[CH][CW], sV[CH][CW];
     __shared__ T sPX[PW], sPY[PH];
+    using R = SfsTileRegs<T, JTF>;
     const Domain& d = a.dom;
     const int t = threadIdx.x;
     const int ntx = (d.W + TX - 1) / TX, nty = (d.y_hi - d.y_lo + TY - 1) / TY;
     const TileRange tr = tile_range(ntx * nty);
-    T dot = 0;
-    for (int tile = tr.first; tile < tr.end; tile += tr.step) {
-    const int x0 = (tile % ntx) * TX, y0 = d.y_lo + (tile / ntx) * TY;
-    constexpr int NP = (PW * PH + kBlock - 1) / kBlock;
-    constexpr int NG = (GW * GH + kBlock - 1) / kBlock;
-    constexpr int NC = (CW * CH + kBlock - 1) / kBlock;
-    T rP[NP], rG0[NG], rG1[NG], rG2[NG];
-    int rMR[NC], rMC[NC], rV[NC];
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        const int i = t + j * kBlock, rx = i % PW, ry = i / PW, gx = x0 - 2 + rx, gy = y0 - 2 + ry;
-        rP[j] = (i < PW * PH && inside(d, gx, gy)) ? p[d.off(gx, gy)] : (T)0;
-    }
-#pragma unroll
-    for (int j = 0; j < NG; ++j) {
-        const int i = t + j * kBlock, rx = i % GW, ry = i / GW, gx = x0 - 1 + rx, gy = y0 - 1 + ry;
-        const bool in = i < GW * GH && inside(d, gx, gy);
-        const long long o = in ? d.off(gx, gy) : 0;
-        rG0[j] = in ? a.G00[o] : (T)0;
-        rG1[j] = in ? a.Gm0[o] : (T)0;
-        rG2[j] = in ? a.G0m[o] : (T)0;
-    }
-#pragma unroll
-    for (int j = 0; j < NC; ++j) {
-        const int i = t + j * kBlock, rx = i % CW, ry = i / CW, gx = x0 - 1 + rx, gy = y0 - 1 + ry;
-        const bool in = i < CW * CH && inbe(d, gx, gy);
-        const long long o = in ? d.off(gx, gy) : 0;
-        rMR[j] = in ? a.mR[o] : 0;
-        rMC[j] = in ? a.mC[o] : 0;
-        rV[j] = in ? a.valid[o] : 0;
-    }
-    // the tile's own flags and LM diagonal, needed only at the end
-    constexpr int NK = TX * TY / kBlock;
-    int rF[NK];
-    T rD[NK];
-#pragma unroll
-    for (int j = 0; j < NK; ++j) {
-        const int i = t + j * kBlock, gx = x0 + (i % TX), gy = y0 + i / TX;
-        const bool own = gx < d.W && gy < d.y_hi;
-        const long long k = own ? d.off(gx, gy) : 0;
-        rF[j] = own ? a.flags[k] : 0;
-        rD[j] = (own && dadd) ? dadd[k] : (T)0;
-    }
-    if (t < PW) sPX[t] = ((T)(x0 - 2 + t) - a.ux) / a.fx;
-    else if (t < PW + PH) sPY[t - PW] = ((T)(y0 - 2 + (t - PW)) - a.uy) / a.fy;
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        const int i = t + j * kBlock;
-        if (i < PW * PH) sP[i / PW][i % PW] = rP[j];
-    }
-#pragma unroll
-    for (int j = 0; j < NG; ++j) {
-        const int i = t + j * kBlock;
-        if (i < GW * GH) { sG00[i / GW][i % GW] = rG0[j]; sGm0[i / GW][i % GW] = rG1[j]; sG0m[i / GW][i % GW] = rG2[j]; }
-    }
-#pragma unroll
-    for (int j = 0; j < NC; ++j) {
-        const int i = t + j * kBlock;
-        if (i < CW * CH) { sMR[i / CW][i % CW] = rMR[j]; sMC[i / CW][i % CW] = rMC[j]; sV[i / CW][i % CW] = rV[j]; }
-    }
-    __syncthreads();
     const T wg = a.wg, ws = a.ws;
-    // D over the G region (G coords (gx, gy) = P coords - 1)
-    for (int i = t; i < GW * GH; i += kBlock) {
-        const int cx = i % GW, cy = i / GW;
-        sD[cy][cx] = sG00[cy][cx] * sP[cy + 1][cx + 1] + sGm0[cy][cx] * sP[cy + 1][cx] + sG0m[cy][cx] * sP[cy][cx + 1];
-    }
-    // u_s over the centre region (C coords = G coords)
-    for (int i = t; i < CW * CH; i += kBlock) {
-        const int cx = i % CW, cy = i / CW, px = cx + 1, py = cy + 1;
-        T q0 = 0, q1 = 0, q2 = 0;
-        if (sV[cy][cx] == 1) {
-            constexpr int OX[5] = {0, -1, 0, 1, 0}, OY[5] = {0, 0, -1, 0, 1};
+    T dot = 0;
+    R r;
+    if (tr.first < tr.end) r.load(a, p, dadd, (tr.first % ntx) * TX, d.y_lo + (tr.first / ntx) * TY);
+    for (int tile = tr.first; tile < tr.end; tile += tr.step) {
+        const int x0 = (tile % ntx) * TX, y0 = d.y_lo + (tile / ntx) * TY;
+        if (t < PW) sPX[t] = ((T)(x0 - 2 + t) - a.ux) / a.fx;
+        else if (t < PW + PH) sPY[t - PW] = ((T)(y0 - 2 + (t - PW)) - a.uy) / a.fy;
 #pragma unroll
-            for (int sIdx = 0; sIdx < 5; ++sIdx) {
-                const T qx = sPX[px + OX[sIdx]], qy = sPY[py + OY[sIdx]];
-                const T co = sIdx == 0 ? (T)4 : (T)-1;
-                const T pv = sP[py + OY[sIdx]][px + OX[sIdx]];
-                q0 += ws * co * qx * pv;
-                q1 += ws * co * qy * pv;
-                q2 += ws * co * pv;
+        for (int j = 0; j < R::NP; ++j) {
+            const int i = t + j * kBlock;
+            if (i < PW * PH) sP[i / PW][i % PW] = r.P[j];
+        }
+#pragma unroll
+        for (int j = 0; j < R::NG; ++j) {
+            const int i = t + j * kBlock;
+            if (i < GW * GH) {
+                sG00[i / GW][i % GW] = r.G0[j]; sGm0[i / GW][i % GW] = r.G1[j]; sG0m[i / GW][i % GW] = r.G2[j];
+                if (JTF) sD[i / GW][i % GW] = r.BI[j];
             }
         }
-        sUs[0][cy][cx] = q0; sUs[1][cy][cx] = q1; sUs[2][cy][cx] = q2;
-    }
-    __syncthreads();
-    // V_h, V_v over the centre region (masks are 0 outside InBoundsExpanded(0,0,1))
-    for (int i = t; i < CW * CH; i += kBlock) {
-        const int cx = i % CW, cy = i / CW;
-        const T mh = (T)sMR[cy][cx], mv = (T)sMC[cy][cx];
-        const T dc = sD[cy][cx];
-        sVh[cy][cx] = wg * mh * (wg * mh * (dc - sD[cy][cx + 1]));
-        sVv[cy][cx] = wg * mv * (wg * mv * (dc - sD[cy + 1][cx]));
-    }
-    __syncthreads();
 #pragma unroll
-    for (int j = 0; j < NK; ++j) {
-        const int i = t + j * kBlock, kx = i % TX, ky = i / TX;
-        const int gx = x0 + kx, gy = y0 + ky;
-        if (gx >= d.W || gy >= d.y_hi) continue;
-        const long long k = d.off(gx, gy);
-        T acc = 0;
-        if (rF[j] & 1) {
-            const int cx = kx + 1, cy = ky + 1;   // k in C / G coords
-            const T pk = sP[ky + 2][kx + 2];
-            auto W = [&](int qx, int qy) {
-                return (sVh[qy][qx] - sVh[qy][qx - 1]) + (sVv[qy][qx] - sVv[qy - 1][qx]);
-            };
-            T shade = sG00[cy][cx] * W(cx, cy) + sGm0[cy][cx + 1] * W(cx + 1, cy) + sG0m[cy + 1][cx] * W(cx, cy + 1);
-            T l[3];
-#pragma unroll
-            for (int c = 0; c < 3; ++c)
-                l[c] = (T)4 * sUs[c][cy][cx] -
-                       (sUs[c][cy][cx - 1] + sUs[c][cy - 1][cx] + sUs[c][cy][cx + 1] + sUs[c][cy + 1][cx]);
-            acc = a.wp * (a.wp * pk) + shade + ws * (sPX[kx + 2] * l[0] + sPY[ky + 2] * l[1] + l[2]);
-            if (dadd) acc += rD[j] * pk;
-            dot += pk * acc;
+        for (int j = 0; j < R::NC; ++j) {
+            const int i = t + j * kBlock;
+            if (i < CW * CH) { sMR[i / CW][i % CW] = r.MR[j]; sMC[i / CW][i % CW] = r.MC[j]; sV[i / CW][i % CW] = r.V[j]; }
         }
-        Ap[k] = acc;
+        int F[R::NK];
+        T Dg[R::NK];
+#pragma unroll
+        for (int j = 0; j < R::NK; ++j) { F[j] = r.F[j]; Dg[j] = r.Dg[j]; }
+        const int next = tile + tr.step;
+        if (next < tr.end) r.load(a, p, dadd, (next % ntx) * TX, d.y_lo + (next / ntx) * TY);
+        __syncthreads();
+        // D over the G region (G coords = P coords - 1); J^T F: B_I, staged above
+        if (!JTF)
+            for (int i = t; i < GW * GH; i += kBlock) {
+                const int cx = i % GW, cy = i / GW;
+                sD[cy][cx] = sG00[cy][cx] * sP[cy + 1][cx + 1] + sGm0[cy][cx] * sP[cy + 1][cx] + sG0m[cy][cx] * sP[cy][cx + 1];
+            }
+        // u_s over the centre region (C coords = G coords)
+        for (int i = t; i < CW * CH; i += kBlock) {
+            const int cx = i % CW, cy = i / CW, px = cx + 1, py = cy + 1;
+            T q0 = 0, q1 = 0, q2 = 0;
+            if (sV[cy][cx] == 1) {
+                constexpr int OX[5] = {0, -1, 0, 1, 0}, OY[5] = {0, 0, -1, 0, 1};
+#pragma unroll
+                for (int sIdx = 0; sIdx < 5; ++sIdx) {
+                    const T qx = sPX[px + OX[sIdx]], qy = sPY[py + OY[sIdx]];
+                    const T co = sIdx == 0 ? (T)4 : (T)-1;
+                    const T pv = sP[py + OY[sIdx]][px + OX[sIdx]];
+                    q0 += ws * co * qx * pv;
+                    q1 += ws * co * qy * pv;
+                    q2 += ws * co * pv;
+                }
+            }
+            sUs[0][cy][cx] = q0; sUs[1][cy][cx] = q1; sUs[2][cy][cx] = q2;
+        }
+        __syncthreads();
+        // V_h, V_v over the centre region (masks are 0 outside InBoundsExpanded(0,0,1))
+        for (int i = t; i < CW * CH; i += kBlock) {
+            const int cx = i % CW, cy = i / CW;
+            const T mh = (T)sMR[cy][cx], mv = (T)sMC[cy][cx];
+            const T dc = sD[cy][cx];
+            sVh[cy][cx] = wg * mh * (wg * mh * (dc - sD[cy][cx + 1]));
+            sVv[cy][cx] = wg * mv * (wg * mv * (dc - sD[cy + 1][cx]));
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < R::NK; ++j) {
+            const int i = t + j * kBlock, kx = i % TX, ky = i / TX;
+            const int gx = x0 + kx, gy = y0 + ky;
+            if (gx < d.W && gy < d.y_hi) {
+                const long long k = d.off(gx, gy);
+                T acc = 0, dg = 0;
+                if (F[j] & 1) {
+                    const int cx = kx + 1, cy = ky + 1;   // k in C / G coords
+                    const T pk = sP[ky + 2][kx + 2];
+                    auto W = [&](int qx, int qy) {
+                        return (sVh[qy][qx] - sVh[qy][qx - 1]) + (sVv[qy][qx] - sVv[qy - 1][qx]);
+                    };
+                    const T shade = sG00[cy][cx] * W(cx, cy) + sGm0[cy][cx + 1] * W(cx + 1, cy) +
+                                    sG0m[cy + 1][cx] * W(cx, cy + 1);
+                    T l[3];
+#pragma unroll
+                    for (int c = 0; c < 3; ++c)
+                        l[c] = (T)4 * sUs[c][cy][cx] -
+                               (sUs[c][cy][cx - 1] + sUs[c][cy - 1][cx] + sUs[c][cy][cx + 1] + sUs[c][cy + 1][cx]);
+                    const T qx = sPX[kx + 2], qy = sPY[ky + 2];
+                    const T fit = JTF ? a.wp * (a.wp * (pk - Dg[j])) : a.wp * (a.wp * pk);
+                    acc = fit + shade + ws * (qx * l[0] + qy * l[1] + l[2]);
+                    if (JTF) {
+                        // diag: squared partials of every residual containing X_k
+                        auto sq = [](T v) { return v * v; };
+                        const T mh0 = wg * (T)sMR[cy][cx], mv0 = wg * (T)sMC[cy][cx];
+                        dg = a.wp * a.wp;
+                        dg += sq(mh0 * (sG00[cy][cx] - sGm0[cy][cx + 1])) + sq(wg * (T)sMR[cy][cx + 1] * sGm0[cy][cx + 1]) +
+                              sq(wg * (T)sMR[cy + 1][cx] * sG0m[cy + 1][cx]) + sq(wg * (T)sMR[cy][cx - 1] * sG00[cy][cx]) +
+                              sq(wg * (T)sMR[cy + 1][cx - 1] * sG0m[cy + 1][cx]);
+                        dg += sq(mv0 * (sG00[cy][cx] - sG0m[cy + 1][cx])) + sq(wg * (T)sMC[cy][cx + 1] * sGm0[cy][cx + 1]) +
+                              sq(wg * (T)sMC[cy + 1][cx] * sG0m[cy + 1][cx]) + sq(wg * (T)sMC[cy - 1][cx] * sG00[cy][cx]) +
+                              sq(wg * (T)sMC[cy - 1][cx + 1] * sGm0[cy][cx + 1]);
+                        const T nv = (T)16 * (T)(sV[cy][cx] == 1) + (T)(sV[cy][cx - 1] == 1) + (T)(sV[cy - 1][cx] == 1) +
+                                     (T)(sV[cy][cx + 1] == 1) + (T)(sV[cy + 1][cx] == 1);
+                        dg += ws * ws * (qx * qx + qy * qy + (T)1) * nv;
+                    } else {
+                        if (dadd) acc += Dg[j] * pk;
+                        dot += pk * acc;
+                    }
+                }
+                if (JTF) {
+                    Ap[k] = -acc;   // r
+                    diag[k] = dg;
+                    a.flags[k] = (uint8_t)(F[j] & 1);
+                } else {
+                    Ap[k] = acc;
+                }
+            }
+        }
+        __syncthreads();   // the next tile overwrites the LDS
     }
-    __syncthreads();   // the next tile overwrites the LDS
-    }
+    if (JTF) return;
     double v[1] = {(double)dot};
     block_reduce_publish<1>(v, rs, blockIdx.x);
 }
@@ -473,7 +480,7 @@ class ShapeFromShadingOp {
 public:
     using T = TT;
     static constexpr const char* kName = "shape_from_shading";
-    static constexpr const char* kApplyName = "sfs_apply";
+    static constexpr const char* kApplyName = "sfs_tiles";
     static constexpr bool kSlabs = true;
     ShapeFromShadingOp(const ProblemSpec& spec, const StateOptions& opts, Domain dom) : dom_(dom), opts_(opts) {
         idx_X_ = spec.unknown(0)->index;
@@ -562,13 +569,14 @@ public:
     }
     void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
         a_.flags = flags;
-        hipLaunchKernelGGL((sfs::sfs_jtf<T>), grid(), dim3(kBlock), 0, s, a_, r, diag);
+        hipLaunchKernelGGL((sfs::sfs_tiles<T, true>), tile_grid(), dim3(kBlock), 0, s, a_, (const T*)a_.X, r, diag,
+                           (const T*)nullptr, (const int*)nullptr, ReduceSlot{});
         OPT_HIP_CHECK(hipGetLastError());
     }
     void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
         const dim3 g = tile_grid();
         rs.nblocks = g.x * g.y;   // the reduction's arrival count is this launch's grid
-        hipLaunchKernelGGL((sfs::sfs_apply<T>), g, dim3(kBlock), 0, s, a_, p, Ap, dadd, stop, rs);
+        hipLaunchKernelGGL((sfs::sfs_tiles<T, false>), g, dim3(kBlock), 0, s, a_, p, Ap, (T*)nullptr, dadd, stop, rs);
         OPT_HIP_CHECK(hipGetLastError());
     }
     void cost(ReduceSlot rs, hipStream_t s) {
