@@ -139,7 +139,8 @@ __global__ __launch_bounds__(kBlock) void arap_jtf(Args<T> a, T* __restrict__ r,
 }
 
 // ------------------------------------------------------------------ J^T J p
-// First pass of the apply: K_v = sum_j p_A,j(v) dR/dA_j(v) for every vertex (9 values),
+// First pass of the apply: K_v = sum_j p_A,j(v) dR/dA_j(v) for every vertex (9 values,
+// stored structure-of-arrays),
 // so the in-edge terms of the gather read a neighbour's K instead of rebuilding its
 // rotation derivatives (three sincos and ~80 FMA per in-edge).
 template <typename T>
@@ -153,7 +154,7 @@ __global__ __launch_bounds__(kBlock) void arap_kdir(Args<T> a, const T* __restri
     rotation(ld3<T>(a.A, v), R, dR);
     directional(dR, ld3<T>(p + 3 * N, v), K);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) Kout[9LL * v + i] = K[i];
+    for (int i = 0; i < 9; ++i) Kout[i * N + v] = K[i];   // SoA: a wave's gathers of K_u hit 2 lines per entry
 }
 
 template <typename T>
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restr
                 pu[b] = ld3<T>(p, u[b]);
                 Uu[b] = ld3<float>(a.U, u[b]);
 #pragma unroll
-                for (int q = 0; q < 9; ++q) Ku[b][q] = Kall[9LL * u[b] + q];
+                for (int q = 0; q < 9; ++q) Ku[b][q] = Kall[q * N + u[b]];
             }
 #pragma unroll
             for (int b = 0; b < kEB; ++b) {
