@@ -164,3 +164,34 @@ def test_full_size_properties(W, H):
     s.set_solver_params({"nIterations": 1, "lIterations": 10})
     costs = s.profiled_solve(prm)
     assert costs[1] < costs[0]
+
+
+def test_bench_workload_trajectory_within_fp32_noise_floor():
+    """The bench generator's workload (seeded) at 1024^2, 2 GN steps x 10
+    PCG: the GPU energies must lie within the oracle's own sensitivity to a 1-ulp change
+    of the inputs (the fp32 noise floor of this energy, tests/test_oracle.py), and one
+    short-PCG step within 1e-5."""
+    import numpy as np
+    from opt_amd import workloads
+
+    W = H = 1024
+    w = workloads.image_warping(W, H, seed=1234)
+    s = solver(W, H)
+    prm = device_params(w)
+    s.set_solver_params({"nIterations": 2, "lIterations": 10})
+    c = np.array(s.profiled_solve(prm))
+    _, _, ref, _ = oracle.iw_solve(w, 2, 10, nthreads=16)
+    rng = np.random.default_rng(0)
+    w2 = dict(w)
+    w2["Offset"] = (w["Offset"] * (1 + 2.0 ** -24 * rng.standard_normal(w["Offset"].size))).astype(np.float32)
+    _, _, ref2, _ = oracle.iw_solve(w2, 2, 10, nthreads=16)
+    floor = np.abs(ref2 - ref) / ref
+    drift = np.abs(c - ref) / ref
+    assert drift[0] < 1e-6
+    assert np.all(drift[1:] <= np.maximum(floor[1:], 1e-5)), (drift, floor)
+    s1 = solver(W, H)
+    p1 = device_params(w)
+    s1.set_solver_params({"nIterations": 1, "lIterations": 1})
+    c1 = s1.profiled_solve(p1)
+    _, _, r1, _ = oracle.iw_solve(w, 1, 1, nthreads=16)
+    np.testing.assert_allclose(c1, r1, rtol=1e-5)
