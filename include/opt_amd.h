@@ -102,6 +102,44 @@ int OptAMD_PlanHalo(Opt_Plan* plan);
  * Returns 0 on success. */
 int OptAMD_PlanSetDecomposition(Opt_Plan* plan, OptAMD_Comm* comm, int y_lo, int y_hi);
 
+/* ---- materialized Jacobian path (useMaterializedJTJ / useFusedJTJ, Opt.h) --------
+ * Every array is a device pointer; CSR is zero-based with int32 indices (nnz < 2^31);
+ * values are float, or double when doublePrecision is nonzero. Synchronous. */
+
+/* Shape of the plan's assembled Jacobian: returns its nonzero count and stores the
+ * residual (row) count in *nResiduals; -1 when the energy family has no J assembly. */
+long long OptAMD_PlanJacobianShape(Opt_Plan* plan, long long* nResiduals);
+
+/* J at the current unknowns (reference kernels.saveJToCRS, solverGPUGaussNewton.t:
+ * 1004-1022, rows/columns as generateDumpJ :385-442: one block of rows per pixel,
+ * columns = unknown indices wrapped into [0, nUnknowns) and sorted inside each row).
+ * rowPtr: nResiduals+1, colInd / val: nnz. Returns 0 on success. */
+int OptAMD_EvalJacobian(Opt_State* state, Opt_Plan* plan, void** problemparams,
+                        int* rowPtr, int* colInd, void* val);
+
+/* A^T of an nRowsA x nColsA matrix: rowPtrAT (nColsA+1), colIndAT and valAT (nnz), the
+ * rows of A ascending inside each row of A^T (reference computeNnzPatternAT + computeAT,
+ * API/src/linalg_cpu.t:203-297,512-551; cusparseScsr2csc, API/src/backend_cuda.t:600-612).
+ * valA / valAT may be NULL (pattern only). */
+int OptAMD_CsrTranspose(int nRowsA, int nColsA, long long nnz, const int* rowPtrA,
+                        const int* colIndA, const void* valA, int* rowPtrAT, int* colIndAT,
+                        void* valAT, int doublePrecision);
+
+/* A^T A (nColsA x nColsA) of A with sorted columns in every row. First call with
+ * colIndATA = valATA = NULL: fills rowPtrATA (nColsA+1) and *nnzATA; second call with
+ * those arrays allocated: sorted column indices and the values, each summed over the
+ * rows of A in ascending order (reference computeNnzPatternATA + computeATA,
+ * API/src/linalg_cpu.t:300-508; cusparseXcsrgemmNnz / cusparseScsrgemm,
+ * API/src/backend_cuda.t:556-596). Nonzero return: more than 2^31 nonzeros. */
+int OptAMD_CsrATA(int nRowsA, int nColsA, long long nnz, const int* rowPtrA, const int* colIndA,
+                  const void* valA, int* rowPtrATA, int* colIndATA, void* valATA,
+                  long long* nnzATA, int doublePrecision);
+
+/* y = A x (reference applyAtoVector, API/src/linalg_cpu.t:560-600; cusparseScsrmv,
+ * API/src/backend_cuda.t:616-636). */
+int OptAMD_CsrSpMV(int nRowsA, int nColsA, long long nnz, const int* rowPtrA, const int* colIndA,
+                   const void* valA, const void* x, void* y, int doublePrecision);
+
 #ifdef __cplusplus
 }
 #endif

@@ -72,6 +72,14 @@ _SIGNATURES = [
     ("OptAMD_LocalGroupDestroy", None, [_VP]),
     ("OptAMD_PlanHalo", ctypes.c_int, [_VP]),
     ("OptAMD_PlanSetDecomposition", ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int]),
+    ("OptAMD_PlanJacobianShape", ctypes.c_longlong, [_VP, ctypes.POINTER(ctypes.c_longlong)]),
+    ("OptAMD_EvalJacobian", ctypes.c_int, [_VP, _VP, ctypes.POINTER(_VP), _VP, _VP, _VP]),
+    ("OptAMD_CsrTranspose", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_longlong, _VP, _VP, _VP, _VP, _VP,
+                                           _VP, ctypes.c_int]),
+    ("OptAMD_CsrATA", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_longlong, _VP, _VP, _VP, _VP, _VP, _VP,
+                                     ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]),
+    ("OptAMD_CsrSpMV", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_longlong, _VP, _VP, _VP, _VP, _VP,
+                                      ctypes.c_int]),
 ]
 EXPORTED_SYMBOLS = [s[0] for s in _SIGNATURES]
 
@@ -152,6 +160,8 @@ class OptSolver:
         verbosity: int = 0,
         kernel_timing: bool = False,
         numthreads: int = 1,
+        materialized: bool = False,
+        fused_jtj: bool = False,
     ):
         self.lib = load_library()
         ip = InitParams()
@@ -160,6 +170,8 @@ class OptSolver:
         ip.collectPerKernelTimingInfo = int(kernel_timing)
         ip.backend = backend.encode()
         ip.numthreads = numthreads
+        ip.useMaterializedJTJ = int(materialized)
+        ip.useFusedJTJ = int(fused_jtj)
         self.state = self.lib.Opt_NewState(ip)
         if not self.state:
             raise OptError("Opt_NewState failed")
@@ -272,6 +284,18 @@ class OptSolver:
         if self.lib.OptAMD_PlanSetDecomposition(self.plan, comm, y_lo, y_hi):
             raise OptError("OptAMD_PlanSetDecomposition failed")
 
+    def jacobian_shape(self):
+        """(residual rows, nonzeros) of the materialized J; nnz = -1 if the family has none."""
+        rows = ctypes.c_longlong()
+        nnz = self.lib.OptAMD_PlanJacobianShape(self.plan, ctypes.byref(rows))
+        return rows.value, nnz
+
+    def eval_jacobian(self, problem_params, rowPtr, colInd, val):
+        """J at the current unknowns into device arrays (rowPtr rows+1, colInd/val nnz)."""
+        pk = ParamPack(problem_params)
+        if self.lib.OptAMD_EvalJacobian(self.state, self.plan, pk.ptr, _ptr(rowPtr), _ptr(colInd), _ptr(val)):
+            raise OptError("OptAMD_EvalJacobian failed")
+
     def close(self):
         if getattr(self, "plan", None):
             self.lib.Opt_PlanFree(self.state, self.plan)
@@ -285,3 +309,50 @@ class OptSolver:
             self.close()
         except Exception:
             pass
+
+
+# ---- device CSR building blocks (include/opt_amd.h) ---------------------------------
+def csr_transpose(rows, cols, rowPtr, colInd, val=None):
+    """(rowPtrT, colIndT, valT) of a device CSR matrix given as torch tensors."""
+    import torch
+
+    lib = load_library()
+    nnz = colInd.numel()
+    rpT = torch.empty(cols + 1, dtype=torch.int32, device=rowPtr.device)
+    ciT = torch.empty(max(nnz, 1), dtype=torch.int32, device=rowPtr.device)
+    vT = torch.empty(max(nnz, 1), dtype=val.dtype, device=rowPtr.device) if val is not None else None
+    dp = int(val is not None and val.dtype == torch.float64)
+    if lib.OptAMD_CsrTranspose(rows, cols, nnz, _ptr(rowPtr), _ptr(colInd), _ptr(val), _ptr(rpT), _ptr(ciT),
+                               _ptr(vT), dp):
+        raise OptError("OptAMD_CsrTranspose failed")
+    return rpT, ciT[:nnz], (vT[:nnz] if vT is not None else None)
+
+
+def csr_ata(rows, cols, rowPtr, colInd, val):
+    """(rowPtrATA, colIndATA, valATA) of A^T A for a device CSR matrix A."""
+    import torch
+
+    lib = load_library()
+    nnz = colInd.numel()
+    dp = int(val.dtype == torch.float64)
+    rp = torch.empty(cols + 1, dtype=torch.int32, device=rowPtr.device)
+    n = ctypes.c_longlong()
+    args = (rows, cols, nnz, _ptr(rowPtr), _ptr(colInd), _ptr(val), _ptr(rp))
+    if lib.OptAMD_CsrATA(*args, None, None, ctypes.byref(n), dp):
+        raise OptError("OptAMD_CsrATA (pattern) failed")
+    ci = torch.empty(max(n.value, 1), dtype=torch.int32, device=rowPtr.device)
+    v = torch.empty(max(n.value, 1), dtype=val.dtype, device=rowPtr.device)
+    if lib.OptAMD_CsrATA(*args, _ptr(ci), _ptr(v), ctypes.byref(n), dp):
+        raise OptError("OptAMD_CsrATA failed")
+    return rp, ci[: n.value], v[: n.value]
+
+
+def csr_spmv(rows, cols, rowPtr, colInd, val, x):
+    import torch
+
+    lib = load_library()
+    y = torch.empty(rows, dtype=val.dtype, device=x.device)
+    dp = int(val.dtype == torch.float64)
+    if lib.OptAMD_CsrSpMV(rows, cols, colInd.numel(), _ptr(rowPtr), _ptr(colInd), _ptr(val), _ptr(x), _ptr(y), dp):
+        raise OptError("OptAMD_CsrSpMV failed")
+    return y

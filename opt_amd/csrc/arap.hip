@@ -497,8 +497,8 @@ std::unique_ptr<Plan> make_arap_plan(const ProblemSpec& spec, const StateOptions
     if (N > (1u << 30) || E > (1u << 30)) { *err = "arap_mesh_deformation: graph too large"; return nullptr; }
     Domain dom{(int)N, 1, 0, 1, 0, 1};
     dom.edges = (int)E;
-    if (opts.double_precision) return std::unique_ptr<Plan>(new StencilPlan<ArapOp<double>>(spec, opts, dom));
-    return std::unique_ptr<Plan>(new StencilPlan<ArapOp<float>>(spec, opts, dom));
+    if (opts.double_precision) return make_stencil_plan<ArapOp<double>>(spec, opts, dom, err);
+    return make_stencil_plan<ArapOp<float>>(spec, opts, dom, err);
 }
 
 }  // namespace optamd

@@ -39,6 +39,20 @@ struct Domain {
     }
 };
 
+// Element -> pixel map of the unknown vector [img0 (ch0 x N) | img1 (ch1 x N) | ...]
+// (reference UnknownType contiguous allocation, o.t:1056-1100).
+struct VecLayout {
+    int nimg;
+    int ch[4];
+    long long off[5];
+    long long N;       // pixels in memory
+    __host__ __device__ long long pix(long long e) const {
+        int k = 0;
+        while (k + 1 < nimg && e >= off[k + 1]) ++k;
+        return (e - off[k]) / ch[k];
+    }
+};
+
 // ---- DPP whole-wave lane shifts (gfx9 family: wave_shr:1 / wave_shl:1) ----------
 // from_left(v, e):  lane l gets v of lane l-1, lane 0 gets e.
 // from_right(v, e): lane l gets v of lane l+1, lane 63 gets e.

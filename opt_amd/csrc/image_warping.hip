@@ -702,6 +702,69 @@ __global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O
     }
 }
 
+
+// ---------------------------------------------------- materialized Jacobian
+// saveJToCRS (solverGPUGaussNewton.t:1004-1022) with generateDumpJ (:385-442): every
+// pixel (excluded ones included, as the reference) writes its 10 residual rows — for s
+// in (+x,-x,+y,-y): channel x, channel y; then the two fit channels — with
+// 3 + ... + 3 + 1 + 1 = 26 nonzeros at rowPtr = 26 k + offset. Columns are the unknown
+// indices image_offset + channels * tooffset(neighbour) + channel, wrapped into
+// [0, nUnknowns) as the reference's wrap() (:365-381), and sorted inside each row
+// (sortCol). Values are the partials of Select(valid, wr (...), 0) and wf Select(has, ...).
+template <typename T>
+__device__ __forceinline__ void sort3(int* c, T* v) {
+    auto sw = [&](int i, int j) {
+        if (c[j] < c[i]) {
+            const int tc = c[i]; c[i] = c[j]; c[j] = tc;
+            const T tv = v[i]; v[i] = v[j]; v[j] = tv;
+        }
+    };
+    sw(0, 1); sw(1, 2); sw(0, 1);
+}
+template <typename T>
+__global__ __launch_bounds__(kBlock) void iw_dump_j(Args<T> a, int* __restrict__ rowPtr, int* __restrict__ colInd,
+                                                    T* __restrict__ val) {
+    const int W = a.dom.W, H = a.dom.H;
+    const long long N = (long long)W * H, n = 3 * N;
+    constexpr int SXd[4] = {1, -1, 0, 0}, SYd[4] = {0, 0, 1, -1};
+    auto wrap = [n](long long c) -> int { return (int)(c < 0 ? c + n : (c >= n ? c - n : c)); };
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < N; k += (long long)gridDim.x * blockDim.x) {
+        const int x = (int)(k % W), y = (int)(k / W);
+        const long long rb = 10 * k, nb = 26 * k;
+        const bool mk = a.M[k] == 0.f;
+        T ck, sk;
+        sc_of(a.A[k], &ck, &sk);
+        const float ukx = a.U[2 * k], uky = a.U[2 * k + 1];
+        for (int s = 0; s < 4; ++s) {
+            const int tx = x + SXd[s], ty = y + SYd[s];
+            const bool in = tx >= 0 && tx < W && ty >= 0 && ty < H;
+            const long long t = in ? (long long)ty * W + tx : 0;
+            const bool v = in && mk && a.M[t] == 0.f;
+            const T dx = in ? (T)(ukx - a.U[2 * t]) : (T)0, dy = in ? (T)(uky - a.U[2 * t + 1]) : (T)0;
+            const T drot[2] = {-sk * dx - ck * dy, ck * dx - sk * dy};
+            const long long tn = k + SXd[s] + (long long)SYd[s] * W;   // tooffset of the (maybe outside) neighbour
+            for (int c = 0; c < 2; ++c) {
+                const int row = 2 * s + c;
+                rowPtr[rb + row] = (int)(nb + 3 * row);
+                int cc[3] = {(int)(2 * k + c), wrap(2 * tn + c), (int)(2 * N + k)};
+                T vv[3] = {v ? a.wr : (T)0, v ? -a.wr : (T)0, v ? -a.wr * drot[c] : (T)0};
+                sort3(cc, vv);
+                for (int q = 0; q < 3; ++q) {
+                    colInd[nb + 3 * row + q] = cc[q];
+                    val[nb + 3 * row + q] = vv[q];
+                }
+            }
+        }
+        const bool has = a.C[2 * k] >= 0.f && a.C[2 * k + 1] >= 0.f;
+        for (int c = 0; c < 2; ++c) {
+            rowPtr[rb + 8 + c] = (int)(nb + 24 + c);
+            colInd[nb + 24 + c] = (int)(2 * k + c);
+            val[nb + 24 + c] = has ? a.wf : (T)0;
+        }
+        if (k == N - 1) rowPtr[10 * N] = (int)(26 * N);
+    }
+}
+
 }  // namespace iw
 
 // ====================================================================== plan
@@ -1175,6 +1238,15 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
 
+    // materialized Jacobian (csr.h): 10 residual rows / 26 nonzeros per pixel
+    long long jacobian_rows() const { return 10LL * dom_.W * dom_.H; }
+    long long jacobian_nnz() const { return 26LL * dom_.W * dom_.H; }
+    void dump_j(int* rowPtr, int* colInd, T* val, hipStream_t s) {
+        hipLaunchKernelGGL(iw::iw_dump_j<T>, dim3(flat_grid((long long)dom_.W * dom_.H, 1)), dim3(kBlock), 0, s, a_,
+                           rowPtr, colInd, val);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+
 private:
     Domain dom_;
     StateOptions opts_;
@@ -1195,11 +1267,10 @@ std::unique_ptr<Plan> make_image_warping_plan(const ProblemSpec& spec, const Sta
         if (d.name == spec.unknown(0)->dims[1]) H = dims[d.index];
     }
     if (W == 0 || H == 0) { *err = "image_warping: zero-sized domain"; return nullptr; }
-    if (spec.lm()) {
+    if (spec.lm() || opts.materialized) {   // generic driver (LM; materialized J^T J)
         Domain dom{(int)W, (int)H, 0, (int)H, 0, (int)H};
-        if (opts.double_precision)
-            return std::unique_ptr<Plan>(new StencilPlan<ImageWarpingOp<double>>(spec, opts, dom));
-        return std::unique_ptr<Plan>(new StencilPlan<ImageWarpingOp<float>>(spec, opts, dom));
+        if (opts.double_precision) return make_stencil_plan<ImageWarpingOp<double>>(spec, opts, dom, err);
+        return make_stencil_plan<ImageWarpingOp<float>>(spec, opts, dom, err);
     }
     if (opts.double_precision)
         return std::unique_ptr<Plan>(new ImageWarpingPlan<double>(spec, opts, W, H));

@@ -1,6 +1,7 @@
 // opt_api.cpp — the Opt.h C ABI (reference API/release/include/Opt.h, implemented in
 // the reference by the trampolines of API/src/createwrapper.t:291-305 into
 // API/src/o.t:3301-3352) plus the opt_amd.h extension entry points.
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -10,6 +11,7 @@
 #include <vector>
 #include "../../include/Opt.h"
 #include "../../include/opt_amd.h"
+#include "csr.h"
 #include "plan.h"
 #include "problem.h"
 
@@ -58,6 +60,8 @@ Opt_State* Opt_NewState(Opt_InitializationParameters params) {
     s->opts.double_precision = params.doublePrecision != 0;
     s->opts.verbosity = params.verbosityLevel;
     s->opts.kernel_timing = params.collectPerKernelTimingInfo != 0;
+    s->opts.materialized = params.useMaterializedJTJ != 0;
+    s->opts.fused_jtj = params.useFusedJTJ != 0;
     return s;
 }
 
@@ -269,6 +273,85 @@ int OptAMD_PlanSetDecomposition(Opt_Plan* plan, OptAMD_Comm* comm, int y_lo, int
         fprintf(stderr, "[opt_amd] OptAMD_PlanSetDecomposition: %s\n", err.c_str());
         return 1;
     }
+    return 0;
+}
+
+long long OptAMD_PlanJacobianShape(Opt_Plan* plan, long long* nResiduals) {
+    if (!valid_plan(plan, "OptAMD_PlanJacobianShape")) return -1;
+    return plan->impl->jacobian_shape(nResiduals);
+}
+int OptAMD_EvalJacobian(Opt_State* state, Opt_Plan* plan, void** params, int* rowPtr, int* colInd, void* val) {
+    if (!valid_state(state, "OptAMD_EvalJacobian") || !valid_plan(plan, "OptAMD_EvalJacobian") || !rowPtr ||
+        !colInd || !val)
+        return 1;
+    return plan->impl->eval_jacobian(params, rowPtr, colInd, val);
+}
+
+// ---- sparse building blocks (synchronous, on the null stream) -------------------
+static bool csr_args_ok(const char* fn, int rows, int cols, long long nnz) {
+    if (rows < 0 || cols < 0 || nnz < 0 || nnz >= (1LL << 31) - 1) {
+        fprintf(stderr, "[opt_amd] %s: invalid CSR shape %d x %d, nnz %lld\n", fn, rows, cols, nnz);
+        return false;
+    }
+    return true;
+}
+int OptAMD_CsrTranspose(int nRowsA, int nColsA, long long nnz, const int* rowPtrA, const int* colIndA,
+                        const void* valA, int* rowPtrAT, int* colIndAT, void* valAT, int doublePrecision) {
+    if (!csr_args_ok("OptAMD_CsrTranspose", nRowsA, nColsA, nnz) || !rowPtrA || !rowPtrAT) return 1;
+    optamd::DevBuf scratch;
+    int* perm = (int*)optamd::dmalloc(sizeof(int) * std::max(nnz, 1LL));
+    optamd::csr_transpose_pattern(nRowsA, nColsA, nnz, rowPtrA, colIndA, rowPtrAT, colIndAT, perm, scratch, nullptr);
+    if (valA && valAT) {
+        if (doublePrecision) optamd::csr_gather<double>(nnz, perm, (const double*)valA, (double*)valAT, nullptr);
+        else optamd::csr_gather<float>(nnz, perm, (const float*)valA, (float*)valAT, nullptr);
+    }
+    OPT_HIP_CHECK(hipDeviceSynchronize());
+    optamd::dfree(perm);
+    return 0;
+}
+int OptAMD_CsrATA(int nRowsA, int nColsA, long long nnz, const int* rowPtrA, const int* colIndA, const void* valA,
+                  int* rowPtrATA, int* colIndATA, void* valATA, long long* nnzATA, int doublePrecision) {
+    if (!csr_args_ok("OptAMD_CsrATA", nRowsA, nColsA, nnz) || !rowPtrA || !rowPtrATA) return 1;
+    optamd::DevBuf scratch;
+    const size_t vb = doublePrecision ? sizeof(double) : sizeof(float);
+    int* rowPtrT = (int*)optamd::dmalloc(sizeof(int) * (nColsA + 1));
+    int* colIndT = (int*)optamd::dmalloc(sizeof(int) * std::max(nnz, 1LL));
+    int* perm = (int*)optamd::dmalloc(sizeof(int) * std::max(nnz, 1LL));
+    void* valT = optamd::dmalloc(vb * std::max(nnz, 1LL));
+    optamd::csr_transpose_pattern(nRowsA, nColsA, nnz, rowPtrA, colIndA, rowPtrT, colIndT, perm, scratch, nullptr);
+    long long n = optamd::csr_ata_pattern(nColsA, rowPtrA, colIndA, rowPtrT, colIndT, rowPtrATA, nullptr, scratch,
+                                          nullptr);
+    int rc = n < 0 ? 1 : 0;
+    if (!rc && colIndATA) {
+        optamd::csr_ata_pattern(nColsA, rowPtrA, colIndA, rowPtrT, colIndT, rowPtrATA, colIndATA, scratch, nullptr);
+        if (valA && valATA) {
+            if (doublePrecision) {
+                optamd::csr_gather<double>(nnz, perm, (const double*)valA, (double*)valT, nullptr);
+                optamd::csr_ata_values<double>(nColsA, rowPtrA, colIndA, (const double*)valA, rowPtrT, colIndT,
+                                               (const double*)valT, rowPtrATA, colIndATA, (double*)valATA, nullptr);
+            } else {
+                optamd::csr_gather<float>(nnz, perm, (const float*)valA, (float*)valT, nullptr);
+                optamd::csr_ata_values<float>(nColsA, rowPtrA, colIndA, (const float*)valA, rowPtrT, colIndT,
+                                              (const float*)valT, rowPtrATA, colIndATA, (float*)valATA, nullptr);
+            }
+        }
+    }
+    OPT_HIP_CHECK(hipDeviceSynchronize());
+    for (void* v : {(void*)rowPtrT, (void*)colIndT, (void*)perm, valT}) optamd::dfree(v);
+    if (nnzATA) *nnzATA = n;
+    if (rc) fprintf(stderr, "[opt_amd] OptAMD_CsrATA: A^T A exceeds 2^31 nonzeros\n");
+    return rc;
+}
+int OptAMD_CsrSpMV(int nRowsA, int nColsA, long long nnz, const int* rowPtrA, const int* colIndA, const void* valA,
+                   const void* x, void* y, int doublePrecision) {
+    if (!csr_args_ok("OptAMD_CsrSpMV", nRowsA, nColsA, nnz) || !rowPtrA || !x || !y) return 1;
+    if (doublePrecision)
+        optamd::csr_spmv<double>(nRowsA, nnz, rowPtrA, colIndA, (const double*)valA, (const double*)x, (double*)y,
+                                 nullptr);
+    else
+        optamd::csr_spmv<float>(nRowsA, nnz, rowPtrA, colIndA, (const float*)valA, (const float*)x, (float*)y,
+                                nullptr);
+    OPT_HIP_CHECK(hipDeviceSynchronize());
     return 0;
 }
 

@@ -330,8 +330,8 @@ std::unique_ptr<Plan> make_optical_flow_plan(const ProblemSpec& spec, const Stat
     if (W == 0 || H == 0) { *err = "optical_flow: zero-sized domain"; return nullptr; }
     if (spec.unknown(0)->channels != 2) { *err = "optical_flow: expects a 2-channel unknown"; return nullptr; }
     Domain dom{(int)W, (int)H, 0, (int)H, 0, (int)H};
-    if (opts.double_precision) return std::unique_ptr<Plan>(new StencilPlan<OpticalFlowOp<double>>(spec, opts, dom));
-    return std::unique_ptr<Plan>(new StencilPlan<OpticalFlowOp<float>>(spec, opts, dom));
+    if (opts.double_precision) return make_stencil_plan<OpticalFlowOp<double>>(spec, opts, dom, err);
+    return make_stencil_plan<OpticalFlowOp<float>>(spec, opts, dom, err);
 }
 
 }  // namespace optamd

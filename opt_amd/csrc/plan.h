@@ -37,6 +37,11 @@ struct StateOptions {
     bool kernel_timing = false;
     bool host_buffers = false;   // backend_cpu / backend_cpu_mt: params are host pointers
     std::string backend = "backend_cuda";
+    // useMaterializedJTJ / useFusedJTJ (Opt.h:32-34): J assembled in CSR every step and
+    // the PCG apply done as J^T J p (fused: one SpMV with the assembled J^T J) or
+    // J^T (J p) (two SpMVs) — solverGPUGaussNewton.t:1532-1757.
+    bool materialized = false;
+    bool fused_jtj = false;
 };
 
 // hipEvent-pair accounting per kernel name (reference Timer, backend_cuda.t:152-297).
@@ -97,6 +102,14 @@ public:
         return "this energy family does not support row-slab decomposition";
     }
     virtual int halo() const { return 0; }
+    // Materialized Jacobian (saveJToCRS, solverGPUGaussNewton.t:1004-1022): nonzeros
+    // (-1: the family has no J assembly) and *rows = residual count.
+    virtual long long jacobian_shape(long long* rows) const { if (rows) *rows = 0; return -1; }
+    // J at the current unknowns into caller device arrays (rowPtr rows+1, colInd/val nnz).
+    virtual int eval_jacobian(void** params, int* rowPtr, int* colInd, void* val) {
+        (void)params; (void)rowPtr; (void)colInd; (void)val;
+        return 1;
+    }
 
     void set_solver_param(const char* name, const void* value);
     int iterations() const { return n_iter_; }

@@ -159,6 +159,37 @@ __global__ __launch_bounds__(kBlock) void pie_cost(Args<T> a, const T* __restric
     block_reduce_publish<1>(v, rs, blockIdx.y * gridDim.x + blockIdx.x);
 }
 
+
+// saveJToCRS / generateDumpJ (solverGPUGaussNewton.t:385-442, 1004-1022): every pixel
+// writes 16 rows (s-major, channel-minor), each {X_c(k): b, X_c(k+s): -b} with
+// b = InBounds(k+s), columns wrapped (wrap(), :365-381) and sorted.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void pie_dump_j(Domain d, int* __restrict__ rowPtr, int* __restrict__ colInd,
+                                                     T* __restrict__ val) {
+    const long long N = (long long)d.W * d.H, n = 4 * N;
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < N; k += (long long)gridDim.x * blockDim.x) {
+        const int x = (int)(k % d.W), y = (int)(k / d.W);
+        for (int s = 0; s < 4; ++s) {
+            const bool in = inside(d, x + DX[s], y + DY[s]);
+            const long long tn = k + DX[s] + (long long)DY[s] * d.W;
+            for (int c = 0; c < 4; ++c) {
+                const long long row = 16 * k + 4 * s + c, nz = 2 * row;
+                rowPtr[row] = (int)nz;
+                long long c0 = 4 * k + c, c1 = 4 * tn + c;
+                c1 = c1 < 0 ? c1 + n : (c1 >= n ? c1 - n : c1);
+                T v0 = in ? (T)1 : (T)0, v1 = in ? (T)-1 : (T)0;
+                if (c1 < c0) {
+                    const long long tc = c0; c0 = c1; c1 = tc;
+                    const T tv = v0; v0 = v1; v1 = tv;
+                }
+                colInd[nz] = (int)c0; val[nz] = v0;
+                colInd[nz + 1] = (int)c1; val[nz + 1] = v1;
+            }
+        }
+        if (k == N - 1) rowPtr[16 * N] = (int)(32 * N);
+    }
+}
+
 }  // namespace pie
 
 template <typename TT>
@@ -230,6 +261,14 @@ public:
         hipLaunchKernelGGL((pie::pie_cost<T>), grid(), dim3(kBlock), 0, s, a_, delta, rs);
         OPT_HIP_CHECK(hipGetLastError());
     }
+    // materialized Jacobian (csr.h): 16 residual rows / 32 nonzeros per pixel
+    long long jacobian_rows() const { return 16LL * dom_.W * dom_.H; }
+    long long jacobian_nnz() const { return 32LL * dom_.W * dom_.H; }
+    void dump_j(int* rowPtr, int* colInd, T* val, hipStream_t s) {
+        hipLaunchKernelGGL(pie::pie_dump_j<T>, dim3(flat_grid((long long)dom_.W * dom_.H, 1)), dim3(kBlock), 0, s,
+                           dom_, rowPtr, colInd, val);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
 
 private:
     dim3 grid() const {
@@ -254,8 +293,8 @@ std::unique_ptr<Plan> make_poisson_plan(const ProblemSpec& spec, const StateOpti
     if (W == 0 || H == 0) { *err = "poisson_image_editing: zero-sized domain"; return nullptr; }
     if (spec.unknown(0)->channels != 4) { *err = "poisson_image_editing: expects a 4-channel unknown"; return nullptr; }
     Domain dom{(int)W, (int)H, 0, (int)H, 0, (int)H};
-    if (opts.double_precision) return std::unique_ptr<Plan>(new StencilPlan<PoissonOp<double>>(spec, opts, dom));
-    return std::unique_ptr<Plan>(new StencilPlan<PoissonOp<float>>(spec, opts, dom));
+    if (opts.double_precision) return make_stencil_plan<PoissonOp<double>>(spec, opts, dom, err);
+    return make_stencil_plan<PoissonOp<float>>(spec, opts, dom, err);
 }
 
 }  // namespace optamd

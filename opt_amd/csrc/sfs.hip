@@ -619,8 +619,8 @@ std::unique_ptr<Plan> make_sfs_plan(const ProblemSpec& spec, const StateOptions&
     if (spec.params.size() < 16) { *err = "shape_from_shading: expects 16 scalar parameters"; return nullptr; }
     Domain dom{(int)W, (int)H, 0, (int)H, 0, (int)H};
     if (opts.double_precision)
-        return std::unique_ptr<Plan>(new StencilPlan<ShapeFromShadingOp<double>>(spec, opts, dom));
-    return std::unique_ptr<Plan>(new StencilPlan<ShapeFromShadingOp<float>>(spec, opts, dom));
+        return make_stencil_plan<ShapeFromShadingOp<double>>(spec, opts, dom, err);
+    return make_stencil_plan<ShapeFromShadingOp<float>>(spec, opts, dom, err);
 }
 
 }  // namespace optamd

@@ -18,20 +18,6 @@
 
 namespace optamd {
 
-// Element -> pixel map of the unknown vector [img0 (ch0 x N) | img1 (ch1 x N) | ...]
-// (reference UnknownType contiguous allocation, o.t:1056-1100).
-struct VecLayout {
-    int nimg;
-    int ch[4];
-    long long off[5];
-    long long N;       // pixels in memory
-    __host__ __device__ long long pix(long long e) const {
-        int k = 0;
-        while (k + 1 < nimg && e >= off[k + 1]) ++k;
-        return (e - off[k]) / ch[k];
-    }
-};
-
 struct LMScalars {      // trust-region parameters the diagonal kernels need
     float radius, min_diag, max_diag;
 };

@@ -3,6 +3,8 @@
 // reference's init / step exactly (API/src/solverGPUGaussNewton.t:1766-2349),
 // including the LM trust-region update and its early exits.
 #pragma once
+#include <type_traits>
+#include "csr.h"
 #include "stencil_driver.h"
 
 namespace optamd {
@@ -57,6 +59,9 @@ __global__ __launch_bounds__(kBlock) void revert_images_kernel(VecLayout L, cons
 //                     — Ap = J^T J p (+ dadd p), sum p.Ap; returns early if *stop
 //   void cost(ReduceSlot, hipStream_t); void model_cost(const T* delta, ReduceSlot, hipStream_t)
 //   void unbind(hipStream_t)                               — copy unknowns back (host mode)
+//   optional, for the materialized path (useMaterializedJTJ, csr.h):
+//   long long jacobian_rows() const, jacobian_nnz() const;
+//   void dump_j(int* rowPtr, int* colInd, T* val, hipStream_t)  — J in CSR (saveJToCRS)
 // All stencil kernels cover the owned rows [y_lo, y_hi) of the Domain and read up to
 // halo() rows beyond them.
 //
@@ -67,6 +72,13 @@ __global__ __launch_bounds__(kBlock) void revert_images_kernel(VecLayout L, cons
 // exchanges are: unknowns after bind / update / revert, computed arrays after each
 // precompute, flags after J^T F, p before each apply (delta before an apply of delta
 // and before the model cost); every scalar is all-reduced right after its kernel.
+template <class Op, class = void>
+struct HasDumpJ : std::false_type {};
+template <class Op>
+struct HasDumpJ<Op, std::void_t<decltype(std::declval<Op&>().dump_j((int*)nullptr, (int*)nullptr,
+                                                                     (typename Op::T*)nullptr, hipStream_t{}))>>
+    : std::true_type {};
+
 template <class Op>
 class StencilPlan final : public Plan {
 public:
@@ -86,12 +98,13 @@ public:
 
     long long unknown_count() const override { return n_; }
     std::string family() const override { return Op::kName; }
-    std::string apply_kernel_name() const override { return Op::kApplyName; }
+    std::string apply_kernel_name() const override { return mat_ ? mat_->apply_name() : Op::kApplyName; }
     int halo() const override { return op_->halo(); }
 
     std::string set_decomposition(Comm* comm, int y_lo, int y_hi) override {
         if (!Op::kSlabs) return std::string(Op::kName) + ": no row-slab decomposition (data-dependent reads)";
         if (opts_.host_buffers) return "row-slab decomposition needs backend_cuda (device arrays)";
+        if (opts_.materialized) return "row-slab decomposition of the materialized Jacobian path is not supported";
         const int h = op_->halo();
         if (y_lo < 0 || y_hi > dom_.H || y_hi - y_lo < h) return "invalid slab rows";
         comm_ = comm;
@@ -160,11 +173,18 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
         allreduce(rz(0), 1);
         const int* stop = lm_ ? stop_ : nullptr;
+        if (mat_) materialize();   // cusparseOuter (:2068): J, J^T (, J^T J) at the current X
         for (int i = 0; i < Lit; ++i) {
             exchange_vec(p_);
-            tbegin(Op::kApplyName);
-            op_->apply(p_, Ap_, lm_ ? CtC_ : nullptr, stop, red_.slot(nb(), pap(i)), stream_);
-            tend();
+            if (mat_) {
+                // cusparseInner + PCGStep1_Finish (:2101-2118): the SpMV replaces PCGStep1;
+                // as in the reference, the LM CtC term is not part of this product
+                mat_apply(p_, Ap_, stop, pap(i));
+            } else {
+                tbegin(Op::kApplyName);
+                op_->apply(p_, Ap_, lm_ ? CtC_ : nullptr, stop, red_.slot(nb(), pap(i)), stream_);
+                tend();
+            }
             allreduce(pap(i), 1);
             const bool reset = lm_ && ((i + 1) % std::max(1, sp_.residual_reset_period)) == 0;
             if (reset) {
@@ -262,7 +282,12 @@ public:
         op_->jtf(r_, diag_, flags_, stream_);   // flags for the exclusion mask
         exchange({{(void*)flags_, (size_t)dom_.W}});
         exchange_vec((T*)p);
-        op_->apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
+        if (mat_) {
+            materialize();
+            mat_apply((const T*)p, (T*)Ap, nullptr, kScTmp);
+        } else {
+            op_->apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
+        }
         allreduce(kScTmp, 1);
         *pAp = read(kScTmp);
         end_call();
@@ -281,13 +306,17 @@ public:
         begin_call();
         prepare(params);
         op_->jtf(r_, diag_, flags_, stream_);
+        if (mat_) materialize();
+        auto run = [&]() {
+            if (mat_) mat_apply((const T*)p, (T*)Ap, nullptr, kScTmp);
+            else op_->apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
+        };
         hipEvent_t e0, e1;
         OPT_HIP_CHECK(hipEventCreate(&e0));
         OPT_HIP_CHECK(hipEventCreate(&e1));
-        op_->apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
+        run();
         OPT_HIP_CHECK(hipEventRecord(e0, stream_));
-        for (int i = 0; i < reps; ++i)
-            op_->apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
+        for (int i = 0; i < reps; ++i) run();
         OPT_HIP_CHECK(hipEventRecord(e1, stream_));
         OPT_HIP_CHECK(hipEventSynchronize(e1));
         float ms = 0;
@@ -296,6 +325,25 @@ public:
         (void)hipEventDestroy(e1);
         end_call();
         return 1000.0 * ms / std::max(1, reps);
+    }
+
+    long long jacobian_shape(long long* rows) const override {
+        if constexpr (HasDumpJ<Op>::value) {
+            if (rows) *rows = op_->jacobian_rows();
+            return op_->jacobian_nnz();
+        }
+        return Plan::jacobian_shape(rows);
+    }
+    int eval_jacobian(void** params, int* rowPtr, int* colInd, void* val) override {
+        if constexpr (HasDumpJ<Op>::value) {
+            if (distributed() || dom_.mem_rows != dom_.H) return 1;
+            begin_call();
+            prepare(params);
+            op_->dump_j(rowPtr, colInd, (T*)val, stream_);
+            end_call();
+            return 0;
+        }
+        return Plan::eval_jacobian(params, rowPtr, colInd, val);
     }
 
 private:
@@ -324,6 +372,11 @@ private:
         flags_ = (uint8_t*)dmalloc(dom_.npix_mem());
         OPT_HIP_CHECK(hipMemset(flags_, 0, dom_.npix_mem()));
         red_.ensure(std::max(op_->stencil_blocks(), 4096), 2, 64);
+        if constexpr (HasDumpJ<Op>::value) {
+            if (opts_.materialized)
+                mat_.reset(new MaterializedJacobian<T>(op_->jacobian_rows(), op_->jacobian_nnz(), n_,
+                                                       opts_.fused_jtj));
+        }
     }
     void release() {
         for (T** v : {&r_, &diag_, &pre_, &p_, &Ap_, &delta_, &b_, &CtC_, &SSq_, &prev_, &Adelta_}) {
@@ -332,6 +385,7 @@ private:
         }
         dfree(flags_);
         flags_ = nullptr;
+        mat_.reset();
         op_.reset();
     }
 
@@ -411,6 +465,21 @@ private:
         OPT_HIP_CHECK(hipGetLastError());
         exchange_unknowns();
     }
+    // J at the current unknowns (saveJToCRS), then J^T (+ J^T J) values (cusparseOuter)
+    void materialize() {
+        if constexpr (HasDumpJ<Op>::value) {
+            tbegin("saveJToCRS");
+            op_->dump_j(mat_->rowPtrJ(), mat_->colIndJ(), mat_->valJ(), stream_);
+            tend();
+            mat_->build([this](const char* n, bool b) { if (b) tbegin(n); else tend(); }, stream_);
+        }
+    }
+    void mat_apply(const T* p, T* Ap, const int* stop, int out) {
+        PcgMask m{L_, (const uint8_t*)flags_, pix_lo(), pix_hi(), stop};
+        mat_->apply(p, Ap, m, red_.slot(mat_->blocks(), out), [this](const char* n, bool b) {
+            if (b) tbegin(n); else tend();
+        }, stream_);
+    }
     double read(int idx) {
         double v;
         OPT_HIP_CHECK(hipMemcpyAsync(&v, red_.scalars + idx, sizeof(double), hipMemcpyDeviceToHost, stream_));
@@ -428,7 +497,20 @@ private:
     T *b_ = nullptr, *CtC_ = nullptr, *SSq_ = nullptr, *prev_ = nullptr, *Adelta_ = nullptr;
     uint8_t* flags_ = nullptr;
     int* stop_ = nullptr;
+    std::unique_ptr<MaterializedJacobian<T>> mat_;
     float radius_ = 1e4f, decrease_ = 2.0f;
 };
+
+// Plan factory for the generic driver: refuses useMaterializedJTJ for a family without
+// a J assembly (the reference returns a nil plan on compile errors, o.t:1352,1526).
+template <class Op>
+std::unique_ptr<Plan> make_stencil_plan(const ProblemSpec& spec, const StateOptions& opts, Domain dom,
+                                        std::string* err) {
+    if (opts.materialized && !HasDumpJ<Op>::value) {
+        *err = std::string(Op::kName) + ": no materialized Jacobian (useMaterializedJTJ) for this energy family";
+        return nullptr;
+    }
+    return std::unique_ptr<Plan>(new StencilPlan<Op>(spec, opts, dom));
+}
 
 }  // namespace optamd

@@ -465,3 +465,89 @@ double oracle_iw_model_cost(int W, int H, const float* O, const float* A, const 
     iw_ctx c = {{W, H, O, A, U, C, M, wf, wr}, (float*)O, (float*)A, NULL, NULL, 1};
     return iwg_model(&c, d);
 }
+
+/* ------------------------------------------- materialized Jacobian (oracle/csr.c) ---- */
+/* saveJToCRS / generateDumpJ (solverGPUGaussNewton.t:385-442, 1004-1022): every pixel
+ * k (excluded ones included) owns rows 10k..10k+9 — for s in (+x,-x,+y,-y): channel 0,
+ * channel 1 (3 nonzeros each: O_c(k), O_c(k+s), A(k)); then fit channel 0, 1 (1 each)
+ * — at nonzero offset 26k. Columns: image offset + channels * tooffset + channel,
+ * wrapped into [0, 3N) (wrap :365-381), sorted inside the row (sortCol). Values are the
+ * partials of the residual (0 where it is not valid). */
+#include "csr.h"
+static void iw_dump(void* v, int* rowPtr, int* colInd, float* val) {
+    const iw_problem* P = (const iw_problem*)v;
+    const long long N = (long long)P->W * P->H, n = 3 * N;
+    for (int y = 0; y < P->H; ++y)
+        for (int x = 0; x < P->W; ++x) {
+            const long long k = (long long)y * P->W + x, rb = 10 * k, nb = 26 * k;
+            for (int s = 0; s < 4; ++s) {
+                const long long tn = k + SX[s] + (long long)SY[s] * P->W;
+                for (int c = 0; c < 2; ++c) {
+                    reg_res r = reg_residual(P, x, y, s, c);
+                    const int row = 2 * s + c;
+                    long long cc[3] = {2 * k + c, 2 * tn + c, 2 * N + k};
+                    float vv[3] = {r.valid ? r.dOc : 0.f, r.valid ? r.dOsc : 0.f, r.valid ? r.dA : 0.f};
+                    for (int q = 0; q < 3; ++q) cc[q] = cc[q] < 0 ? cc[q] + n : (cc[q] >= n ? cc[q] - n : cc[q]);
+                    for (int a = 1; a < 3; ++a)   /* sortCol */
+                        for (int b = a; b > 0 && cc[b] < cc[b - 1]; --b) {
+                            long long tc = cc[b]; cc[b] = cc[b - 1]; cc[b - 1] = tc;
+                            float tv = vv[b]; vv[b] = vv[b - 1]; vv[b - 1] = tv;
+                        }
+                    rowPtr[rb + row] = (int)(nb + 3 * row);
+                    for (int q = 0; q < 3; ++q) { colInd[nb + 3 * row + q] = (int)cc[q]; val[nb + 3 * row + q] = vv[q]; }
+                }
+            }
+            const int has = fit_valid(P, (int)k);
+            for (int c = 0; c < 2; ++c) {
+                rowPtr[rb + 8 + c] = (int)(nb + 24 + c);
+                colInd[nb + 24 + c] = (int)(2 * k + c);
+                val[nb + 24 + c] = has ? P->wf : 0.f;
+            }
+        }
+    rowPtr[10 * N] = (int)(26 * N);
+}
+void oracle_iw_dump_j(int W, int H, const float* O, const float* A, const float* U, const float* C, const float* M,
+                      float wf, float wr, int* rowPtr, int* colInd, float* val) {
+    iw_problem P = {W, H, O, A, U, C, M, wf, wr};
+    iw_dump(&P, rowPtr, colInd, val);
+}
+
+typedef struct { iw_ctx c; oracle_mat m; } iwm_ctx;
+static void iwm_materialize(void* v) { oracle_mat_build(&((iwm_ctx*)v)->m); }
+static double iwm_apply(void* v, const float* p, float* Ap) { return oracle_mat_apply(&((iwm_ctx*)v)->m, p, Ap); }
+static void iwm_dump(void* v, int* rowPtr, int* colInd, float* val) { iw_dump(&((iw_ctx*)v)->P, rowPtr, colInd, val); }
+
+/* GN / LM solve with the materialized J^T J (fused) or J^T (J p) apply */
+int oracle_iw_solve_materialized(int W, int H, float* O, float* A, const float* U, const float* C, const float* M,
+                                 float wf, float wr, int lm, int fused, int nIter, int lIter, double* costs) {
+    const int N = W * H;
+    iwm_ctx c = {{{W, H, O, A, U, C, M, wf, wr}, O, A, NULL, NULL, 1}};
+    c.c.prevO = (float*)malloc(sizeof(float) * 2 * N);
+    c.c.prevA = (float*)malloc(sizeof(float) * N);
+    unsigned char* act = (unsigned char*)malloc((size_t)3 * N);
+    for (int k = 0; k < N; ++k) act[2 * k] = act[2 * k + 1] = act[2 * N + k] = M[k] == 0.f;
+    oracle_mat_init(&c.m, 10LL * N, 26LL * N, 3 * N, fused, act, iwm_dump, &c.c);
+    oracle_problem_float P = {3LL * N, act, 1, &c, iwg_cost, iwg_jtf, iwg_apply, iwg_model,
+                              iwg_update, iwg_save, iwg_revert, iwm_materialize, iwm_apply};
+    oracle_params sp = oracle_default_params();
+    sp.nIterations = nIter;
+    sp.lIterations = lIter;
+    const int k = oracle_solve_f32(&P, lm, &sp, costs);
+    oracle_mat_free(&c.m);
+    free(act); free(c.c.prevO); free(c.c.prevA);
+    return k;
+}
+/* one materialized apply at the given unknowns (Ap = 0 on excluded unknowns) */
+double oracle_iw_apply_materialized(int W, int H, const float* O, const float* A, const float* U, const float* C,
+                                    const float* M, float wf, float wr, int fused, const float* p, float* Ap) {
+    const int N = W * H;
+    iwm_ctx c = {{{W, H, O, A, U, C, M, wf, wr}, (float*)O, (float*)A, NULL, NULL, 1}};
+    unsigned char* act = (unsigned char*)malloc((size_t)3 * N);
+    for (int k = 0; k < N; ++k) act[2 * k] = act[2 * k + 1] = act[2 * N + k] = M[k] == 0.f;
+    oracle_mat_init(&c.m, 10LL * N, 26LL * N, 3 * N, fused, act, iwm_dump, &c.c);
+    oracle_mat_build(&c.m);
+    const double d = oracle_mat_apply(&c.m, p, Ap);
+    oracle_mat_free(&c.m);
+    free(act);
+    return d;
+}

@@ -373,3 +373,123 @@ def arap_solve(w, n_iter, l_iter, lm=False):
     costs = np.zeros(n_iter + 1, np.float64)
     k = _arap_lib().oracle_arap_solve(*a, int(lm), n_iter, l_iter, costs.ctypes.data_as(_D))
     return O, A, costs[: k + 1]
+
+
+# ------------------------------------------------------------ CSR / materialized J
+_I = ctypes.POINTER(ctypes.c_int)
+
+
+def _csr_lib():
+    lib = load()
+    if not getattr(lib, "_csr", False):
+        i, f, d = ctypes.c_int, ctypes.c_float, ctypes.c_double
+        lib.oracle_csr_pattern_at.restype = None
+        lib.oracle_csr_pattern_at.argtypes = [i, i, i, _I, _I, _I, _I]
+        lib.oracle_csr_at.restype = None
+        lib.oracle_csr_at.argtypes = [i, i, i, _F, _I, _I, _F, _I, _I]
+        lib.oracle_csr_pattern_ata.restype = i
+        lib.oracle_csr_pattern_ata.argtypes = [i, i, i, _I, _I, _I, _I]
+        lib.oracle_csr_ata.restype = None
+        lib.oracle_csr_ata.argtypes = [i, i, i, i, _F, _I, _I, _F, _I, _I, _F, _I, _I]
+        lib.oracle_csr_spmv.restype = None
+        lib.oracle_csr_spmv.argtypes = [i, i, i, _F, _I, _I, _F, _F]
+        lib.oracle_iw_dump_j.restype = None
+        lib.oracle_iw_dump_j.argtypes = [i, i, _F, _F, _F, _F, _F, f, f, _I, _I, _F]
+        lib.oracle_iw_solve_materialized.restype = i
+        lib.oracle_iw_solve_materialized.argtypes = [i, i, _F, _F, _F, _F, _F, f, f, i, i, i, i, _D]
+        lib.oracle_iw_apply_materialized.restype = d
+        lib.oracle_iw_apply_materialized.argtypes = [i, i, _F, _F, _F, _F, _F, f, f, i, _F, _F]
+        lib.oracle_pie_dump_j.restype = None
+        lib.oracle_pie_dump_j.argtypes = [i, i, _F, _F, _F, _I, _I, _F]
+        lib.oracle_pie_solve_materialized.restype = i
+        lib.oracle_pie_solve_materialized.argtypes = [i, i, _F, _F, _F, i, i, i, i, _D]
+        lib._csr = True
+    return lib
+
+
+def _i(a):
+    assert a.dtype == np.int32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_I)
+
+
+def csr_transpose(n_rows, n_cols, rowPtr, colInd, val):
+    """computeNnzPatternAT + computeAT (linalg_cpu.t:203-297, 512-551)."""
+    lib = _csr_lib()
+    nnz = len(colInd)
+    rpT = np.zeros(n_cols + 1, np.int32)
+    ciT = np.zeros(max(nnz, 1), np.int32)
+    vT = np.zeros(max(nnz, 1), np.float32)
+    lib.oracle_csr_pattern_at(n_cols, n_rows, nnz, _i(rowPtr), _i(colInd), _i(rpT), _i(ciT))
+    lib.oracle_csr_at(n_cols, n_rows, nnz, _f(val), _i(rowPtr), _i(colInd), _f(vT), _i(rpT), _i(ciT))
+    return rpT, ciT[:nnz], vT[:nnz]
+
+
+def csr_ata(n_rows, n_cols, rowPtr, colInd, val):
+    """computeNnzPatternATA + computeATA (linalg_cpu.t:300-508)."""
+    lib = _csr_lib()
+    nnz = len(colInd)
+    rp = np.zeros(n_cols + 1, np.int32)
+    m = lib.oracle_csr_pattern_ata(n_cols, n_rows, nnz, _i(rowPtr), _i(colInd), _i(rp), None)
+    ci = np.zeros(max(m, 1), np.int32)
+    lib.oracle_csr_pattern_ata(n_cols, n_rows, nnz, _i(rowPtr), _i(colInd), _i(rp), _i(ci))
+    rpT, ciT, vT = csr_transpose(n_rows, n_cols, rowPtr, colInd, val)
+    rpT = np.ascontiguousarray(rpT)
+    ciT = np.ascontiguousarray(ciT)
+    vT = np.ascontiguousarray(vT)
+    v = np.zeros(max(m, 1), np.float32)
+    lib.oracle_csr_ata(n_cols, n_rows, nnz, m, _f(val), _i(rowPtr), _i(colInd), _f(vT), _i(rpT), _i(ciT), _f(v),
+                       _i(rp), _i(ci))
+    return rp, ci[:m], v[:m]
+
+
+def csr_spmv(n_rows, n_cols, rowPtr, colInd, val, x):
+    """applyAtoVector (linalg_cpu.t:560-600)."""
+    y = np.zeros(n_rows, np.float32)
+    _csr_lib().oracle_csr_spmv(n_cols, n_rows, len(colInd), _f(val), _i(rowPtr), _i(colInd),
+                               _f(np.ascontiguousarray(x, np.float32)), _f(y))
+    return y
+
+
+def iw_dump_j(w):
+    """J of image_warping in the runtime's CSR layout: 10 rows / 26 nonzeros per pixel."""
+    N = w["W"] * w["H"]
+    rp = np.zeros(10 * N + 1, np.int32)
+    ci = np.zeros(26 * N, np.int32)
+    v = np.zeros(26 * N, np.float32)
+    _csr_lib().oracle_iw_dump_j(*_args(w), _i(rp), _i(ci), _f(v))
+    return rp, ci, v
+
+
+def iw_apply_materialized(w, p, fused=True):
+    p = np.ascontiguousarray(p, np.float32)
+    Ap = np.zeros_like(p)
+    pAp = _csr_lib().oracle_iw_apply_materialized(*_args(w), int(fused), _f(p), _f(Ap))
+    return Ap, pAp
+
+
+def iw_solve_materialized(w, n_iter, l_iter, lm=False, fused=True):
+    O = w["Offset"].copy()
+    A = w["Angle"].copy()
+    costs = np.zeros(n_iter + 1, np.float64)
+    k = _csr_lib().oracle_iw_solve_materialized(w["W"], w["H"], _f(O), _f(A), _f(w["UrShape"]),
+                                                _f(w["Constraints"]), _f(w["Mask"]), w["w_fitSqrt"],
+                                                w["w_regSqrt"], int(lm), int(fused), n_iter, l_iter,
+                                                costs.ctypes.data_as(_D))
+    return O, A, costs[: k + 1]
+
+
+def pie_dump_j(w):
+    N = w["W"] * w["H"]
+    rp = np.zeros(16 * N + 1, np.int32)
+    ci = np.zeros(32 * N, np.int32)
+    v = np.zeros(32 * N, np.float32)
+    _csr_lib().oracle_pie_dump_j(w["W"], w["H"], _f(w["X"]), _f(w["T"]), _f(w["M"]), _i(rp), _i(ci), _f(v))
+    return rp, ci, v
+
+
+def pie_solve_materialized(w, n_iter, l_iter, lm=False, fused=True):
+    X = w["X"].copy()
+    costs = np.zeros(n_iter + 1, np.float64)
+    k = _csr_lib().oracle_pie_solve_materialized(w["W"], w["H"], _f(X), _f(w["T"]), _f(w["M"]), int(lm), int(fused),
+                                                 n_iter, l_iter, costs.ctypes.data_as(_D))
+    return X, costs[: k + 1]

@@ -167,3 +167,58 @@ int oracle_pie_solve(int W, int H, float* X, const float* T, const float* M, int
     free(c.prev);
     return k;
 }
+
+/* ------------------------------------------- materialized Jacobian (oracle/csr.c) ---- */
+/* saveJToCRS / generateDumpJ (solverGPUGaussNewton.t:385-442, 1004-1022): pixel k owns
+ * rows 16k + 4s + ch, each {X_ch(k): b, X_ch(k+s): -b}, b = InBounds(k+s), columns
+ * wrapped into [0, 4N) (:365-381) and sorted (sortCol). */
+#include "csr.h"
+static void pie_dump(void* v, int* rowPtr, int* colInd, float* val) {
+    const pie_ctx* c = (const pie_ctx*)v;
+    const long long N = (long long)c->W * c->H, n = 4 * N;
+    for (int y = 0; y < c->H; ++y)
+        for (int x = 0; x < c->W; ++x) {
+            const long long k = (long long)y * c->W + x;
+            for (int s = 0; s < 4; ++s) {
+                const int in = pin(c, x + PX[s], y + PY[s]);
+                const long long tn = k + PX[s] + (long long)PY[s] * c->W;
+                for (int ch = 0; ch < 4; ++ch) {
+                    const long long row = 16 * k + 4 * s + ch, nz = 2 * row;
+                    long long c0 = 4 * k + ch, c1 = 4 * tn + ch;
+                    c1 = c1 < 0 ? c1 + n : (c1 >= n ? c1 - n : c1);
+                    float v0 = in ? 1.f : 0.f, v1 = in ? -1.f : 0.f;
+                    if (c1 < c0) { long long t = c0; c0 = c1; c1 = t; float tv = v0; v0 = v1; v1 = tv; }
+                    rowPtr[row] = (int)nz;
+                    colInd[nz] = (int)c0; val[nz] = v0;
+                    colInd[nz + 1] = (int)c1; val[nz + 1] = v1;
+                }
+            }
+        }
+    rowPtr[16 * N] = (int)(32 * N);
+}
+void oracle_pie_dump_j(int W, int H, float* X, const float* T, const float* M, int* rowPtr, int* colInd, float* val) {
+    pie_ctx c = {W, H, X, T, M, NULL};
+    pie_dump(&c, rowPtr, colInd, val);
+}
+typedef struct { pie_ctx c; oracle_mat m; } piem_ctx;
+static void piem_materialize(void* v) { oracle_mat_build(&((piem_ctx*)v)->m); }
+static double piem_apply(void* v, const float* p, float* Ap) { return oracle_mat_apply(&((piem_ctx*)v)->m, p, Ap); }
+int oracle_pie_solve_materialized(int W, int H, float* X, const float* T, const float* M, int lm, int fused, int nIter,
+                                  int lIter, double* costs) {
+    piem_ctx c = {{W, H, X, T, M, NULL}};
+    const long long n = 4LL * W * H;
+    unsigned char* act = malloc(n);
+    for (long long e = 0; e < n; ++e) act[e] = M[e / 4] == 0.f;
+    c.c.prev = malloc(sizeof(float) * n);
+    oracle_mat_init(&c.m, 16LL * W * H, 32LL * W * H, (int)n, fused, act, pie_dump, &c.c);
+    oracle_problem_float P = {n, act, 0, &c, pie_cost_fn, pie_jtf_fn, pie_apply_fn, pie_model_fn,
+                              pie_update_fn, pie_save_fn, pie_revert_fn, piem_materialize, piem_apply};
+    oracle_params sp = oracle_default_params();
+    sp.nIterations = nIter;
+    sp.lIterations = lIter;
+    const int k = oracle_solve_f32(&P, lm, &sp, costs);
+    oracle_mat_free(&c.m);
+    free(act);
+    free(c.c.prev);
+    return k;
+}

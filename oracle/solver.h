@@ -12,6 +12,11 @@ typedef struct {
     void (*update)(void* ctx, const float* delta);
     void (*save)(void* ctx);
     void (*revert)(void* ctx);
+    /* materialized-Jacobian path (NULL: matrix-free): cusparseOuter after PCGInit1, and
+     * the SpMV apply of the PCG loop, which carries no LM CtC term (solverGPUGaussNewton.t
+     * :1660-1757); the LM residual reset keeps the matrix-free apply (computeAdelta). */
+    void (*materialize)(void* ctx);
+    double (*apply_mat)(void* ctx, const float* p, float* Ap);
 } oracle_problem_float;
 typedef struct {
     long long n;
@@ -25,6 +30,11 @@ typedef struct {
     void (*update)(void* ctx, const double* delta);
     void (*save)(void* ctx);
     void (*revert)(void* ctx);
+    /* materialized-Jacobian path (NULL: matrix-free): cusparseOuter after PCGInit1, and
+     * the SpMV apply of the PCG loop, which carries no LM CtC term (solverGPUGaussNewton.t
+     * :1660-1757); the LM residual reset keeps the matrix-free apply (computeAdelta). */
+    void (*materialize)(void* ctx);
+    double (*apply_mat)(void* ctx, const double* p, double* Ap);
 } oracle_problem_double;
 typedef struct {
     int nIterations, lIterations, residual_reset_period;

@@ -64,10 +64,11 @@ static int CAT(oracle_solve_, REAL)(CAT(oracle_problem_, REAL)* P, int lm, const
                 alpha_num += (double)r[e] * p[e];
             }
         }
+        if (P->materialize) P->materialize(P->ctx);
         for (int li = 0; li < sp->lIterations; ++li) {
-            /* PCGStep1 (+ CtC p for LM) */
-            double alpha_den = P->apply(P->ctx, p, Ap);
-            if (lm) {
+            /* PCGStep1 (+ CtC p for LM), or the materialized SpMV + PCGStep1_Finish */
+            double alpha_den = P->apply_mat ? P->apply_mat(P->ctx, p, Ap) : P->apply(P->ctx, p, Ap);
+            if (lm && !P->apply_mat) {
                 for (long long e = 0; e < n; ++e) {
                     Ap[e] += CtC[e] * p[e];
                     alpha_den += (double)p[e] * (CtC[e] * p[e]);
