@@ -110,6 +110,11 @@ int OptAMD_PlanSetDecomposition(Opt_Plan* plan, OptAMD_Comm* comm, int y_lo, int
  * residual (row) count in *nResiduals; -1 when the energy family has no J assembly. */
 long long OptAMD_PlanJacobianShape(Opt_Plan* plan, long long* nResiduals);
 
+/* Nonzeros of the J and (fused) J^T J a materialized plan holds (the J^T J count is
+ * known after the first Step, 0 before and for useFusedJTJ = 0). Returns 1 for a
+ * matrix-free plan. */
+int OptAMD_PlanMaterializedNonzeros(Opt_Plan* plan, long long* nnzJ, long long* nnzJTJ);
+
 /* J at the current unknowns (reference kernels.saveJToCRS, solverGPUGaussNewton.t:
  * 1004-1022, rows/columns as generateDumpJ :385-442: one block of rows per pixel,
  * columns = unknown indices wrapped into [0, nUnknowns) and sorted inside each row).

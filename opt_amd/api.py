@@ -73,6 +73,8 @@ _SIGNATURES = [
     ("OptAMD_PlanHalo", ctypes.c_int, [_VP]),
     ("OptAMD_PlanSetDecomposition", ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_int]),
     ("OptAMD_PlanJacobianShape", ctypes.c_longlong, [_VP, ctypes.POINTER(ctypes.c_longlong)]),
+    ("OptAMD_PlanMaterializedNonzeros", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_longlong),
+                                                       ctypes.POINTER(ctypes.c_longlong)]),
     ("OptAMD_EvalJacobian", ctypes.c_int, [_VP, _VP, ctypes.POINTER(_VP), _VP, _VP, _VP]),
     ("OptAMD_CsrTranspose", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_longlong, _VP, _VP, _VP, _VP, _VP,
                                            _VP, ctypes.c_int]),
@@ -289,6 +291,13 @@ class OptSolver:
         rows = ctypes.c_longlong()
         nnz = self.lib.OptAMD_PlanJacobianShape(self.plan, ctypes.byref(rows))
         return rows.value, nnz
+
+    def materialized_nonzeros(self):
+        """(nnz J, nnz J^T J) of a materialized plan, None for a matrix-free one."""
+        a, b = ctypes.c_longlong(), ctypes.c_longlong()
+        if self.lib.OptAMD_PlanMaterializedNonzeros(self.plan, ctypes.byref(a), ctypes.byref(b)):
+            return None
+        return a.value, b.value
 
     def eval_jacobian(self, problem_params, rowPtr, colInd, val):
         """J at the current unknowns into device arrays (rowPtr rows+1, colInd/val nnz)."""

@@ -15,11 +15,13 @@
 // per-step value transpose is one coalesced gather. The A^T A pattern is built once
 // per plan (one thread per row, sorted-unique merge of the A rows the A^T row
 // touches); its values are recomputed every step in the reference's summation order
-// (rows of A ascending), so they match the CPU restatement bit for bit. The SpMV
-// gives each row a group of G lanes (G = power of two near the mean row length, <= 16)
-// so a wavefront streams 64 consecutive (value, column) pairs per load; the PCG
-// variant masks excluded unknowns and reduces p.Ap deterministically
-// (PCGStep1_Finish, solverGPUGaussNewton.t:646-663).
+// (rows of A ascending), so they match the CPU restatement bit for bit. The solver's
+// SpMVs run over a SELL-64 copy of each operator (slices of 64 rows = one wavefront,
+// column-major inside the slice): lane r owns row r, every load instruction is one
+// contiguous segment, and each row is summed in column order with rounded products —
+// bitwise the reference CPU backend's applyAtoVector. The PCG variant masks excluded
+// unknowns and reduces p.Ap deterministically (PCGStep1_Finish,
+// solverGPUGaussNewton.t:646-663).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <algorithm>
@@ -87,8 +89,68 @@ template <typename T>
 void csr_spmv_pcg(int rows, long long nnz, const int* rowPtr, const int* colInd, const T* val, const T* x, T* y,
                   const T* pv, const PcgMask& m, ReduceSlot rs, hipStream_t s);
 
+// SELL-64 (the solver's SpMV layout): rows in slices of 64 = one wavefront, slice
+// width = its longest row, entries column-major inside a slice so lane r of the wave
+// reads row r and every load instruction is one contiguous 256-B (fp32) segment. Built
+// once per pattern; pos[] maps every slot to its CSR position (-1: padding, value 0).
+struct SellMatrix {
+    int rows = 0, nslices = 0;
+    long long padded = 0;
+    int* sliceOff = nullptr;   // nslices + 1
+    int* col = nullptr;        // padded
+    int* pos = nullptr;        // padded
+    void release() {
+        dfree(sliceOff); dfree(col); dfree(pos);
+        sliceOff = col = pos = nullptr;
+        rows = nslices = 0;
+        padded = 0;
+    }
+    ~SellMatrix() { release(); }
+};
+void sell_build(int rows, const int* rowPtr, const int* colInd, SellMatrix& S, DevBuf& scratch, hipStream_t s);
+// pos[q] <- perm[pos[q]]: slots of A^T addressed directly into A's value array
+void sell_compose(SellMatrix& S, const int* perm, hipStream_t s);
+template <typename T>
+void sell_values(const SellMatrix& S, const T* csrVal, T* sellVal, hipStream_t s);
+// computeATA straight into the SELL layout of the A^T A pattern (bitwise computeATA)
+template <typename T>
+void ata_values_sell(int cols, const int* rowPtrA, const int* colIndA, const T* valA, const int* rowPtrT,
+                     const int* colIndT, const T* valT, const int* rowPtrATA, const int* colIndATA,
+                     const SellMatrix& S, T* sellVal, hipStream_t s);
+int sell_blocks(const SellMatrix& S);
+
+// A^T A product map (the solver's per-step J^T J): for every slot of the A^T A SELL-64
+// copy, the position pairs (p1, p2) into A's values with slot = sum_m A[p1_m] A[p2_m],
+// rows of A ascending — computeATA's products in its order, so the result is bitwise
+// computeATA. Stored like the SELL copy itself: the 64 slots of a slice column (group
+// g) keep their pair lists column-major at gbase[g], padded with (-1, -1), so the
+// per-step kernel streams the map with coalesced loads and writes the SELL values
+// directly.
+struct AtaProducts {
+    long long n = 0, npairs = 0, padded = 0;
+    long long* off = nullptr;     // build only
+    int2* pairs = nullptr;        // npairs (padded, grouped)
+    long long* gbase = nullptr;   // padded / 64 + 1
+    void release() {
+        dfree(off); dfree(pairs); dfree(gbase);
+        off = nullptr; pairs = nullptr; gbase = nullptr;
+        n = npairs = padded = 0;
+    }
+    ~AtaProducts() { release(); }
+};
+void ata_products_build(int cols, const int* rowPtrA, const int* colIndA, const int* rowPtrT, const int* colIndT,
+                        const int* perm, const int* rowPtrATA, const int* colIndATA, long long nnzATA,
+                        const SellMatrix& S, AtaProducts& P, DevBuf& scratch, hipStream_t s);
+template <typename T>
+void ata_values_products(const AtaProducts& P, const T* valA, T* out, hipStream_t s);
+template <typename T>
+void sell_spmv(const SellMatrix& S, const T* val, const T* x, T* y, hipStream_t s);
+template <typename T>
+void sell_spmv_pcg(const SellMatrix& S, const T* val, const T* x, T* y, const T* pv, const PcgMask& m, ReduceSlot rs,
+                   hipStream_t s);
+
 // The solver-side holder: J (filled by the family's dump_j), J^T (pattern once, values
-// every step), J^T J (fused only), and the apply.
+// every step), J^T J (fused only), the SELL-64 copies the SpMVs stream, and the apply.
 template <typename T>
 class MaterializedJacobian {
 public:
@@ -101,19 +163,23 @@ public:
         rows_ = (int)nres;
         cols_ = (int)nunk;
         nnz_ = nnz;
+        const long long nz = std::max(nnz_, 1LL);
         rowPtrJ_ = (int*)dmalloc(sizeof(int) * (rows_ + 1));
-        colIndJ_ = (int*)dmalloc(sizeof(int) * std::max(nnz_, 1LL));
-        valJ_ = (T*)dmalloc(sizeof(T) * std::max(nnz_, 1LL));
+        colIndJ_ = (int*)dmalloc(sizeof(int) * nz);
+        valJ_ = (T*)dmalloc(sizeof(T) * nz);
         rowPtrT_ = (int*)dmalloc(sizeof(int) * (cols_ + 1));
-        colIndT_ = (int*)dmalloc(sizeof(int) * std::max(nnz_, 1LL));
-        perm_ = (int*)dmalloc(sizeof(int) * std::max(nnz_, 1LL));
-        valT_ = (T*)dmalloc(sizeof(T) * std::max(nnz_, 1LL));
-        if (!fused_) Jp_ = (T*)dmalloc(sizeof(T) * std::max(rows_, 1));
-        else rowPtrATA_ = (int*)dmalloc(sizeof(int) * (cols_ + 1));
+        colIndT_ = (int*)dmalloc(sizeof(int) * nz);
+        perm_ = (int*)dmalloc(sizeof(int) * nz);
+        if (fused_) {
+            rowPtrATA_ = (int*)dmalloc(sizeof(int) * (cols_ + 1));
+        } else {
+            Jp_ = (T*)dmalloc(sizeof(T) * std::max(rows_, 1));
+        }
     }
     ~MaterializedJacobian() {
         for (void* v : {(void*)rowPtrJ_, (void*)colIndJ_, (void*)valJ_, (void*)rowPtrT_, (void*)colIndT_, (void*)perm_,
-                        (void*)valT_, (void*)Jp_, (void*)rowPtrATA_, (void*)colIndATA_, (void*)valATA_})
+                        (void*)valT_, (void*)Jp_, (void*)rowPtrATA_, (void*)colIndATA_, (void*)svJ_, (void*)svT_,
+                        (void*)svA_})
             dfree(v);
     }
     int* rowPtrJ() { return rowPtrJ_; }
@@ -124,7 +190,7 @@ public:
     long long nnz() const { return nnz_; }
     long long nnz_jtj() const { return nnz_ata_; }
     bool fused() const { return fused_; }
-    int blocks() const { return csr_pcg_blocks(cols_); }
+    int blocks() const { return sell_blocks(fused_ ? sA_ : sT_); }
     const char* apply_name() const { return fused_ ? "J^TJp" : "J^T"; }
 
     // After the family filled J: the patterns once (section 1 of cusparseOuter,
@@ -134,6 +200,13 @@ public:
         if (!patterns_) {
             tb("JT alloc", true);
             csr_transpose_pattern(rows_, cols_, nnz_, rowPtrJ_, colIndJ_, rowPtrT_, colIndT_, perm_, scratch_, s);
+            if (!fused_) {
+                sell_build(rows_, rowPtrJ_, colIndJ_, sJ_, scratch_, s);
+                sell_build(cols_, rowPtrT_, colIndT_, sT_, scratch_, s);
+                sell_compose(sT_, perm_, s);   // J^T slots read J's values directly
+                svJ_ = (T*)dmalloc(sizeof(T) * std::max(sJ_.padded, 1LL));
+                svT_ = (T*)dmalloc(sizeof(T) * std::max(sT_.padded, 1LL));
+            }
             tb("JT alloc", false);
             if (fused_) {
                 tb("J^TJ alloc", true);
@@ -144,21 +217,26 @@ public:
                     exit(1);
                 }
                 colIndATA_ = (int*)dmalloc(sizeof(int) * std::max(nnz_ata_, 1LL));
-                valATA_ = (T*)dmalloc(sizeof(T) * std::max(nnz_ata_, 1LL));
                 csr_ata_pattern(cols_, rowPtrJ_, colIndJ_, rowPtrT_, colIndT_, rowPtrATA_, colIndATA_, scratch_, s);
+                sell_build(cols_, rowPtrATA_, colIndATA_, sA_, scratch_, s);
+                ata_products_build(cols_, rowPtrJ_, colIndJ_, rowPtrT_, colIndT_, perm_, rowPtrATA_, colIndATA_,
+                                   nnz_ata_, sA_, prod_, scratch_, s);
+                svA_ = (T*)dmalloc(sizeof(T) * std::max(sA_.padded, 1LL));
+                OPT_HIP_CHECK(hipMemsetAsync(svA_, 0, sizeof(T) * std::max(sA_.padded, 1LL), s));   // padding
                 tb("J^TJ alloc", false);
             }
             scratch_.release();
             patterns_ = true;
         }
-        tb("J_transpose", true);
-        csr_gather<T>(nnz_, perm_, valJ_, valT_, s);
-        tb("J_transpose", false);
-        if (fused_) {
+        if (fused_) {   // J^T J straight from J's values (the product map holds the transpose)
             tb("JTJ multiply", true);
-            csr_ata_values<T>(cols_, rowPtrJ_, colIndJ_, valJ_, rowPtrT_, colIndT_, valT_, rowPtrATA_, colIndATA_,
-                              valATA_, s);
+            ata_values_products<T>(prod_, valJ_, svA_, s);
             tb("JTJ multiply", false);
+        } else {
+            tb("J_transpose", true);
+            sell_values<T>(sJ_, valJ_, svJ_, s);
+            sell_values<T>(sT_, valJ_, svT_, s);
+            tb("J_transpose", false);
         }
     }
     // Ap = J^T J p (fused) or J^T (J p), masked to the active unknowns, p.Ap into rs
@@ -167,14 +245,14 @@ public:
     void apply(const T* p, T* Ap, const PcgMask& m, ReduceSlot rs, Timer&& tb, hipStream_t s) {
         if (fused_) {
             tb("J^TJp", true);
-            csr_spmv_pcg<T>(cols_, nnz_ata_, rowPtrATA_, colIndATA_, valATA_, p, Ap, p, m, rs, s);
+            sell_spmv_pcg<T>(sA_, svA_, p, Ap, p, m, rs, s);
             tb("J^TJp", false);
         } else {
             tb("Jp", true);
-            csr_spmv<T>(rows_, nnz_, rowPtrJ_, colIndJ_, valJ_, p, Jp_, s);
+            sell_spmv<T>(sJ_, svJ_, p, Jp_, s);
             tb("Jp", false);
             tb("J^T", true);
-            csr_spmv_pcg<T>(cols_, nnz_, rowPtrT_, colIndT_, valT_, Jp_, Ap, p, m, rs, s);
+            sell_spmv_pcg<T>(sT_, svT_, Jp_, Ap, p, m, rs, s);
             tb("J^T", false);
         }
     }
@@ -185,7 +263,10 @@ private:
     long long nnz_ = 0, nnz_ata_ = 0;
     int *rowPtrJ_ = nullptr, *colIndJ_ = nullptr, *rowPtrT_ = nullptr, *colIndT_ = nullptr, *perm_ = nullptr;
     int *rowPtrATA_ = nullptr, *colIndATA_ = nullptr;
-    T *valJ_ = nullptr, *valT_ = nullptr, *valATA_ = nullptr, *Jp_ = nullptr;
+    T *valJ_ = nullptr, *valT_ = nullptr, *Jp_ = nullptr;
+    SellMatrix sJ_, sT_, sA_;
+    AtaProducts prod_;
+    T *svJ_ = nullptr, *svT_ = nullptr, *svA_ = nullptr;
     DevBuf scratch_;
 };
 

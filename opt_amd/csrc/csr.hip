@@ -137,30 +137,273 @@ __global__ __launch_bounds__(kBlock) void sum_counts(int n, const int* __restric
 }
 
 // computeATA (linalg_cpu.t:447-508): row i of A^T A accumulates, for every entry k of
-// A^T row i in order (rows r of A ascending), valT[k] * A(r, c) into column c; the
-// column is located by the reference's forward merge over the sorted row.
-template <typename T>
-__global__ __launch_bounds__(kBlock) void ata_values(int cols, const int* __restrict__ rowPtrA,
-                                                     const int* __restrict__ colIndA, const T* __restrict__ valA,
-                                                     const int* __restrict__ rowPtrT, const int* __restrict__ colIndT,
-                                                     const T* __restrict__ valT, const int* __restrict__ rowPtrATA,
-                                                     const int* __restrict__ colIndATA, T* __restrict__ valATA) {
+// A^T row i in order (rows r of A ascending), valT[k] * A(r, c) into column c.
+// Same sums with the row held in registers: the row's columns and accumulators are
+// WMAX-wide register arrays (unrolled compare-select, no dynamic indexing); every
+// product t * A(r, c) is rounded and added to its column's accumulator in the order of
+// the reference loop, so the result is bitwise that of computeATA. Rows longer than
+// WMAX take the merge loop above. sliceOff != nullptr writes the SELL-64 layout of the
+// A^T A pattern (sell_* below) instead of CSR.
+template <typename T, int WMAX>
+__global__ __launch_bounds__(kBlock) void ata_values_reg(int cols, const int* __restrict__ rowPtrA,
+                                                         const int* __restrict__ colIndA, const T* __restrict__ valA,
+                                                         const int* __restrict__ rowPtrT,
+                                                         const int* __restrict__ colIndT, const T* __restrict__ valT,
+                                                         const int* __restrict__ rowPtrATA,
+                                                         const int* __restrict__ colIndATA, T* __restrict__ valATA,
+                                                         const int* __restrict__ sliceOff) {
 #pragma clang fp contract(off)
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < cols; i += gridDim.x * blockDim.x) {
         const int b = rowPtrATA[i], n = rowPtrATA[i + 1] - b;
-        for (int l = 0; l < n; ++l) valATA[b + l] = (T)0;
+        // output position of the row's l-th entry
+        const long long ob = sliceOff ? (long long)sliceOff[i >> 6] + (i & 63) : b;
+        const int os = sliceOff ? 64 : 1;
+        if (n > WMAX) {
+            for (int l = 0; l < n; ++l) valATA[ob + (long long)l * os] = (T)0;
+            for (int k = rowPtrT[i]; k < rowPtrT[i + 1]; ++k) {
+                const T t = valT[k];
+                const int r = colIndT[k];
+                int ci = rowPtrA[r];
+                const int ce = rowPtrA[r + 1];
+                for (int l = 0; l < n && ci < ce; ++l) {
+                    if (colIndATA[b + l] == colIndA[ci]) {
+                        const long long o = ob + (long long)l * os;
+                        valATA[o] = valATA[o] + t * valA[ci];
+                        ++ci;
+                    }
+                }
+            }
+            continue;
+        }
+        int cix[WMAX];
+        T acc[WMAX];
+#pragma unroll
+        for (int l = 0; l < WMAX; ++l) {
+            cix[l] = l < n ? colIndATA[b + l] : -1;
+            acc[l] = (T)0;
+        }
         for (int k = rowPtrT[i]; k < rowPtrT[i + 1]; ++k) {
             const T t = valT[k];
             const int r = colIndT[k];
-            int ci = rowPtrA[r];
-            const int ce = rowPtrA[r + 1];
-            for (int l = 0; l < n && ci < ce; ++l) {
-                if (colIndATA[b + l] == colIndA[ci]) {
-                    valATA[b + l] = valATA[b + l] + t * valA[ci];
-                    ++ci;
-                }
+            for (int j = rowPtrA[r]; j < rowPtrA[r + 1]; ++j) {
+                const int c = colIndA[j];
+                const T v = t * valA[j];
+#pragma unroll
+                for (int l = 0; l < WMAX; ++l)
+                    if (cix[l] == c) acc[l] = acc[l] + v;
             }
         }
+#pragma unroll
+        for (int l = 0; l < WMAX; ++l)
+            if (l < n) valATA[ob + (long long)l * os] = acc[l];
+    }
+}
+
+// ---- A^T A product map: for every A^T A entry, the (J(r,i), J(r,c)) position pairs
+// whose products sum to it, rows r ascending (computeATA's order). Built once per
+// pattern; the per-step values are then pure gathers (no dependent index chains).
+template <int WMAX, bool FILL>
+__global__ __launch_bounds__(kBlock) void prod_map(int cols, const int* __restrict__ rowPtrA,
+                                                   const int* __restrict__ colIndA, const int* __restrict__ rowPtrT,
+                                                   const int* __restrict__ colIndT, const int* __restrict__ perm,
+                                                   const int* __restrict__ rowPtrATA,
+                                                   const int* __restrict__ colIndATA, long long* __restrict__ cnt,
+                                                   int2* __restrict__ pairs, int* __restrict__ cursor) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < cols; i += gridDim.x * blockDim.x) {
+        const int b = rowPtrATA[i], n = rowPtrATA[i + 1] - b;
+        if (n <= WMAX) {
+            int cix[WMAX], cur[WMAX];
+            long long o[WMAX];
+#pragma unroll
+            for (int l = 0; l < WMAX; ++l) {
+                cix[l] = l < n ? colIndATA[b + l] : -1;
+                cur[l] = 0;
+                o[l] = (FILL && l < n) ? cnt[b + l] : 0;
+            }
+            for (int k = rowPtrT[i]; k < rowPtrT[i + 1]; ++k) {
+                const int r = colIndT[k], p1 = perm[k];
+                for (int j = rowPtrA[r]; j < rowPtrA[r + 1]; ++j) {
+                    const int c = colIndA[j];
+#pragma unroll
+                    for (int l = 0; l < WMAX; ++l)
+                        if (cix[l] == c) {
+                            if (FILL) pairs[o[l] + cur[l]] = make_int2(p1, j);
+                            ++cur[l];
+                        }
+                }
+            }
+            if (!FILL) {
+#pragma unroll
+                for (int l = 0; l < WMAX; ++l)
+                    if (l < n) cnt[b + l] = cur[l];
+            }
+        } else {   // long rows: cursors in global memory (this thread owns the row)
+            for (int l = 0; l < n; ++l) cursor[b + l] = 0;
+            for (int k = rowPtrT[i]; k < rowPtrT[i + 1]; ++k) {
+                const int r = colIndT[k], p1 = perm[k];
+                for (int j = rowPtrA[r]; j < rowPtrA[r + 1]; ++j) {
+                    const int c = colIndA[j];
+                    int lo = 0, hi = n - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        if (colIndATA[b + mid] < c) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    if (FILL) pairs[cnt[b + lo] + cursor[b + lo]] = make_int2(p1, j);
+                    ++cursor[b + lo];
+                }
+            }
+            if (!FILL)
+                for (int l = 0; l < n; ++l) cnt[b + l] = cursor[b + l];
+        }
+    }
+}
+// SELL layout of the product map: the slots of the A^T A SELL copy come in groups of
+// 64 (one slice column); group g stores its pairs column-major, pair m of lane l at
+// gbase[g] + 64 m + l, padded to the group's deepest list with (-1, -1).
+__global__ __launch_bounds__(kBlock) void pair_depth(long long padded, const int* __restrict__ pos,
+                                                     const long long* __restrict__ off, long long* __restrict__ depth) {
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < padded;
+         q += (long long)gridDim.x * blockDim.x) {
+        const int k = pos[q];
+        int c = k >= 0 ? (int)(off[k + 1] - off[k]) : 0;
+        for (int o = 32; o > 0; o >>= 1) c = max(c, __shfl_xor(c, o, 64));
+        if ((q & 63) == 0) depth[q >> 6] = 64LL * c;
+    }
+}
+__global__ __launch_bounds__(kBlock) void pair_fill(long long padded, const int* __restrict__ pos,
+                                                    const long long* __restrict__ off, const int2* __restrict__ pairs,
+                                                    const long long* __restrict__ gbase, int2* __restrict__ out) {
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < padded;
+         q += (long long)gridDim.x * blockDim.x) {
+        const long long g = q >> 6, b = gbase[g];
+        const int d = (int)((gbase[g + 1] - b) >> 6), lane = (int)(q & 63);
+        const int k = pos[q];
+        const int c = k >= 0 ? (int)(off[k + 1] - off[k]) : 0;
+        for (int m = 0; m < d; ++m) out[b + 64LL * m + lane] = m < c ? pairs[off[k] + m] : make_int2(-1, -1);
+    }
+}
+// Per step: every SELL slot of A^T A = its products summed in order (bitwise computeATA).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void ata_from_pairs(long long padded, const long long* __restrict__ gbase,
+                                                         const int2* __restrict__ pairs, const T* __restrict__ valA,
+                                                         T* __restrict__ out) {
+#pragma clang fp contract(off)
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < padded;
+         q += (long long)gridDim.x * blockDim.x) {
+        const long long g = q >> 6, b = gbase[g];
+        const int d = (int)((gbase[g + 1] - b) >> 6), lane = (int)(q & 63);
+        const int2* pr = pairs + b + lane;
+        T acc = 0;
+        int m = 0;
+        for (; m + 2 <= d; m += 2) {
+            const int2 a0 = pr[64 * m], a1 = pr[64 * (m + 1)];
+            const T x0 = a0.x >= 0 ? valA[a0.x] : (T)0, y0 = a0.x >= 0 ? valA[a0.y] : (T)0;
+            const T x1 = a1.x >= 0 ? valA[a1.x] : (T)0, y1 = a1.x >= 0 ? valA[a1.y] : (T)0;
+            if (a0.x >= 0) acc = acc + x0 * y0;
+            if (a1.x >= 0) acc = acc + x1 * y1;
+        }
+        if (m < d) {
+            const int2 a0 = pr[64 * m];
+            if (a0.x >= 0) acc = acc + valA[a0.x] * valA[a0.y];
+        }
+        out[q] = acc;
+    }
+}
+
+// ---- SELL-64: rows in slices of one wavefront, column-major inside a slice --------
+__global__ __launch_bounds__(kBlock) void sell_widths(int rows, int nslices, const int* __restrict__ rowPtr,
+                                                      long long* __restrict__ off) {
+    for (int sl = blockIdx.x * blockDim.x + threadIdx.x; sl < nslices; sl += gridDim.x * blockDim.x) {
+        int w = 0;
+        const int r1 = min(rows, sl * 64 + 64);
+        for (int r = sl * 64; r < r1; ++r) w = max(w, rowPtr[r + 1] - rowPtr[r]);
+        off[sl] = 64LL * w;
+    }
+}
+__global__ __launch_bounds__(kBlock) void sell_fill(int rows, int nslices, const int* __restrict__ rowPtr,
+                                                    const int* __restrict__ colInd, const long long* __restrict__ off,
+                                                    int* __restrict__ sliceOff, int* __restrict__ col,
+                                                    int* __restrict__ pos) {
+    for (long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x; t < 64LL * nslices;
+         t += (long long)gridDim.x * blockDim.x) {
+        const int sl = (int)(t >> 6), lane = (int)(t & 63), r = (int)t;
+        const long long o = off[sl];
+        const int w = (int)((off[sl + 1] - o) >> 6);
+        if (lane == 0) sliceOff[sl] = (int)o;
+        if (t == 0) sliceOff[nslices] = (int)off[nslices];
+        const int b = r < rows ? rowPtr[r] : 0, len = r < rows ? rowPtr[r + 1] - b : 0;
+        for (int j = 0; j < w; ++j) {
+            const long long q = o + (long long)j * 64 + lane;
+            col[q] = j < len ? colInd[b + j] : 0;
+            pos[q] = j < len ? b + j : -1;
+        }
+    }
+}
+template <typename T>
+__global__ __launch_bounds__(kBlock) void sell_gather(long long n, const int* __restrict__ pos,
+                                                      const T* __restrict__ val, T* __restrict__ out) {
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long long)gridDim.x * blockDim.x) {
+        const int k = pos[q];
+        out[q] = k >= 0 ? val[k] : (T)0;
+    }
+}
+__global__ __launch_bounds__(kBlock) void compose(long long n, const int* __restrict__ pos,
+                                                  const int* __restrict__ perm, int* __restrict__ out) {
+    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long long)gridDim.x * blockDim.x) {
+        const int k = pos[q];
+        out[q] = k >= 0 ? perm[k] : -1;
+    }
+}
+
+// y = A x over SELL-64: one lane per row, one wavefront per slice; every row summed in
+// column order with rounded products (applyAtoVector's order: bitwise its result).
+// PCG: y masked to the active unknowns and sum pv.y reduced (PCGStep1_Finish).
+template <typename T, bool PCG>
+__global__ __launch_bounds__(kBlock) void sell_spmv(int rows, int nslices, const int* __restrict__ sliceOff,
+                                                    const int* __restrict__ col, const T* __restrict__ val,
+                                                    const T* __restrict__ x, T* __restrict__ y,
+                                                    const T* __restrict__ pv, PcgMask m, ReduceSlot rs) {
+#pragma clang fp contract(off)
+    if (PCG && stopped(m.stop)) return;
+    const int lane = threadIdx.x & 63;
+    const int nwaves = gridDim.x * (kBlock / 64);
+    T dot = 0;
+    // plain interleaved slices: an XCD-contiguous split measured slower here (the +-W
+    // neighbours are only 2W elements away and stay L2/MALL-resident either way)
+    for (int sl = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) >> 6); sl < nslices;
+         sl += nwaves) {
+        const int o = sliceOff[sl], w = (sliceOff[sl + 1] - o) >> 6;
+        const int* c = col + o + lane;
+        const T* v = val + o + lane;
+        T acc = 0;
+        int j = 0;
+        for (; j + 4 <= w; j += 4) {
+            const int c0 = c[64 * j], c1 = c[64 * (j + 1)], c2 = c[64 * (j + 2)], c3 = c[64 * (j + 3)];
+            const T v0 = v[64 * j], v1 = v[64 * (j + 1)], v2 = v[64 * (j + 2)], v3 = v[64 * (j + 3)];
+            const T x0 = x[c0], x1 = x[c1], x2 = x[c2], x3 = x[c3];
+            acc = acc + x0 * v0;
+            acc = acc + x1 * v1;
+            acc = acc + x2 * v2;
+            acc = acc + x3 * v3;
+        }
+        for (; j < w; ++j) acc = acc + x[c[64 * j]] * v[64 * j];
+        const int r = sl * 64 + lane;
+        if (r < rows) {
+            if (PCG) {
+                int k = 0;   // element -> pixel (32-bit: the vector is < 2^31 long)
+                while (k + 1 < m.L.nimg && r >= m.L.off[k + 1]) ++k;
+                const long long px = (r - (int)m.L.off[k]) / m.L.ch[k];
+                const bool act = px >= m.pix_lo && px < m.pix_hi && (m.flags[px] & 1);
+                if (!act) acc = 0;
+                dot += pv[r] * acc;
+            }
+            y[r] = acc;
+        }
+    }
+    if (PCG) {
+        double d[1] = {(double)dot};
+        block_reduce_publish<1>(d, rs, blockIdx.x);
     }
 }
 
@@ -175,12 +418,13 @@ template <typename T, int G>
 __global__ __launch_bounds__(kBlock) void spmv(int rows, const int* __restrict__ rowPtr,
                                                const int* __restrict__ colInd, const T* __restrict__ val,
                                                const T* __restrict__ x, T* __restrict__ y) {
+#pragma clang fp contract(off)
     const int lg = threadIdx.x & (G - 1);
     const long long ngroups = (long long)gridDim.x * (kBlock / G);
     for (long long r = ((long long)blockIdx.x * kBlock + threadIdx.x) / G; r < rows; r += ngroups) {
         const int b = rowPtr[r], e = rowPtr[r + 1];
         T acc = 0;
-        for (int k = b + lg; k < e; k += G) acc += val[k] * x[colInd[k]];
+        for (int k = b + lg; k < e; k += G) acc = acc + x[colInd[k]] * val[k];
         acc = group_sum(acc, G);
         if (lg == 0) y[r] = acc;
     }
@@ -355,26 +599,19 @@ template <typename T>
 void csr_ata_values(int cols, const int* rowPtrA, const int* colIndA, const T* valA, const int* rowPtrT,
                     const int* colIndT, const T* valT, const int* rowPtrATA, const int* colIndATA, T* valATA,
                     hipStream_t s) {
-    hipLaunchKernelGGL((csr::ata_values<T>), dim3(csr::grid_for(cols)), dim3(kBlock), 0, s, cols, rowPtrA, colIndA,
-                       valA, rowPtrT, colIndT, valT, rowPtrATA, colIndATA, valATA);
+    hipLaunchKernelGGL((csr::ata_values_reg<T, 16>), dim3(csr::grid_for(cols)), dim3(kBlock), 0, s, cols, rowPtrA,
+                       colIndA, valA, rowPtrT, colIndT, valT, rowPtrATA, colIndATA, valATA, (const int*)nullptr);
     OPT_HIP_CHECK(hipGetLastError());
 }
 
 template <typename T>
 void csr_spmv(int rows, long long nnz, const int* rowPtr, const int* colInd, const T* val, const T* x, T* y,
               hipStream_t s) {
+    // one lane per row, entries in order with rounded products: bitwise applyAtoVector
     if (rows == 0) return;
-    const int G = csr::group_for(rows, nnz);
-    const dim3 g(csr::grid_for((long long)rows * G)), b(kBlock);
-#define SPMV(GG) hipLaunchKernelGGL((csr::spmv<T, GG>), g, b, 0, s, rows, rowPtr, colInd, val, x, y)
-    switch (G) {
-        case 1: SPMV(1); break;
-        case 2: SPMV(2); break;
-        case 4: SPMV(4); break;
-        case 8: SPMV(8); break;
-        default: SPMV(16); break;
-    }
-#undef SPMV
+    (void)nnz;
+    hipLaunchKernelGGL((csr::spmv<T, 1>), dim3(csr::grid_for(rows)), dim3(kBlock), 0, s, rows, rowPtr, colInd, val, x,
+                       y);
     OPT_HIP_CHECK(hipGetLastError());
 }
 
@@ -398,13 +635,142 @@ void csr_spmv_pcg(int rows, long long nnz, const int* rowPtr, const int* colInd,
     OPT_HIP_CHECK(hipGetLastError());
 }
 
+// ---- SELL-64 host side ------------------------------------------------------------
+void sell_build(int rows, const int* rowPtr, const int* colInd, SellMatrix& S, DevBuf& scratch, hipStream_t s) {
+    S.release();
+    S.rows = rows;
+    S.nslices = (rows + 63) / 64;
+    long long* off = (long long*)dmalloc(sizeof(long long) * (S.nslices + 1));
+    OPT_HIP_CHECK(hipMemsetAsync(off + S.nslices, 0, sizeof(long long), s));
+    hipLaunchKernelGGL(csr::sell_widths, dim3(csr::grid_for(S.nslices)), dim3(kBlock), 0, s, rows, S.nslices, rowPtr,
+                       off);
+    size_t need = 0;
+    OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, need, off, off, S.nslices + 1, s));
+    OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(scratch.need(need), need, off, off, S.nslices + 1, s));
+    OPT_HIP_CHECK(hipMemcpyAsync(&S.padded, off + S.nslices, sizeof(long long), hipMemcpyDeviceToHost, s));
+    OPT_HIP_CHECK(hipStreamSynchronize(s));
+    if (S.padded >= (1LL << 31) - 1) {
+        fprintf(stderr, "[opt_amd] SELL-64 layout of %d rows exceeds 2^31 padded entries\n", rows);
+        exit(1);
+    }
+    S.sliceOff = (int*)dmalloc(sizeof(int) * (S.nslices + 1));
+    S.col = (int*)dmalloc(sizeof(int) * std::max(S.padded, 1LL));
+    S.pos = (int*)dmalloc(sizeof(int) * std::max(S.padded, 1LL));
+    hipLaunchKernelGGL(csr::sell_fill, dim3(csr::grid_for(64LL * S.nslices)), dim3(kBlock), 0, s, rows, S.nslices,
+                       rowPtr, colInd, (const long long*)off, S.sliceOff, S.col, S.pos);
+    OPT_HIP_CHECK(hipGetLastError());
+    OPT_HIP_CHECK(hipStreamSynchronize(s));
+    dfree(off);
+}
+void sell_compose(SellMatrix& S, const int* perm, hipStream_t s) {
+    if (S.padded == 0) return;
+    hipLaunchKernelGGL(csr::compose, dim3(csr::grid_for(S.padded)), dim3(kBlock), 0, s, S.padded, (const int*)S.pos,
+                       perm, S.pos);
+    OPT_HIP_CHECK(hipGetLastError());
+}
+template <typename T>
+void sell_values(const SellMatrix& S, const T* csrVal, T* sellVal, hipStream_t s) {
+    if (S.padded == 0) return;
+    hipLaunchKernelGGL((csr::sell_gather<T>), dim3(csr::grid_for(S.padded)), dim3(kBlock), 0, s, S.padded,
+                       (const int*)S.pos, csrVal, sellVal);
+    OPT_HIP_CHECK(hipGetLastError());
+}
+template <typename T>
+void ata_values_sell(int cols, const int* rowPtrA, const int* colIndA, const T* valA, const int* rowPtrT,
+                     const int* colIndT, const T* valT, const int* rowPtrATA, const int* colIndATA,
+                     const SellMatrix& S, T* sellVal, hipStream_t s) {
+    if (S.padded == 0) return;
+    OPT_HIP_CHECK(hipMemsetAsync(sellVal, 0, sizeof(T) * S.padded, s));   // padding stays 0
+    hipLaunchKernelGGL((csr::ata_values_reg<T, 16>), dim3(csr::grid_for(cols)), dim3(kBlock), 0, s, cols, rowPtrA,
+                       colIndA, valA, rowPtrT, colIndT, valT, rowPtrATA, colIndATA, sellVal,
+                       (const int*)S.sliceOff);
+    OPT_HIP_CHECK(hipGetLastError());
+}
+void ata_products_build(int cols, const int* rowPtrA, const int* colIndA, const int* rowPtrT, const int* colIndT,
+                        const int* perm, const int* rowPtrATA, const int* colIndATA, long long nnzATA,
+                        const SellMatrix& S, AtaProducts& P, DevBuf& scratch, hipStream_t s) {
+    P.release();
+    P.n = nnzATA;
+    P.off = (long long*)dmalloc(sizeof(long long) * (nnzATA + 1));
+    int* cursor = (int*)dmalloc(sizeof(int) * std::max(nnzATA, 1LL));
+    OPT_HIP_CHECK(hipMemsetAsync(P.off, 0, sizeof(long long) * (nnzATA + 1), s));
+    const dim3 g(csr::grid_for(cols)), b(kBlock);
+    hipLaunchKernelGGL((csr::prod_map<16, false>), g, b, 0, s, cols, rowPtrA, colIndA, rowPtrT, colIndT, perm,
+                       rowPtrATA, colIndATA, P.off, (int2*)nullptr, cursor);
+    size_t need = 0;
+    OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, need, P.off, P.off, nnzATA + 1, s));
+    OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(scratch.need(need), need, P.off, P.off, nnzATA + 1, s));
+    OPT_HIP_CHECK(hipMemcpyAsync(&P.npairs, P.off + nnzATA, sizeof(long long), hipMemcpyDeviceToHost, s));
+    OPT_HIP_CHECK(hipStreamSynchronize(s));
+    P.pairs = (int2*)dmalloc(sizeof(int2) * std::max(P.npairs, 1LL));
+    hipLaunchKernelGGL((csr::prod_map<16, true>), g, b, 0, s, cols, rowPtrA, colIndA, rowPtrT, colIndT, perm,
+                       rowPtrATA, colIndATA, P.off, P.pairs, cursor);
+    OPT_HIP_CHECK(hipGetLastError());
+    OPT_HIP_CHECK(hipStreamSynchronize(s));
+    dfree(cursor);
+    // regroup into the SELL layout of the A^T A copy (see pair_fill)
+    const long long G = S.padded / 64;
+    P.padded = S.padded;
+    P.gbase = (long long*)dmalloc(sizeof(long long) * (G + 1));
+    OPT_HIP_CHECK(hipMemsetAsync(P.gbase + G, 0, sizeof(long long), s));
+    hipLaunchKernelGGL(csr::pair_depth, dim3(csr::grid_for(S.padded)), dim3(kBlock), 0, s, S.padded,
+                       (const int*)S.pos, (const long long*)P.off, P.gbase);
+    need = 0;
+    OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, need, P.gbase, P.gbase, G + 1, s));
+    OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(scratch.need(need), need, P.gbase, P.gbase, G + 1, s));
+    long long total = 0;
+    OPT_HIP_CHECK(hipMemcpyAsync(&total, P.gbase + G, sizeof(total), hipMemcpyDeviceToHost, s));
+    OPT_HIP_CHECK(hipStreamSynchronize(s));
+    int2* sp = (int2*)dmalloc(sizeof(int2) * std::max(total, 1LL));
+    hipLaunchKernelGGL(csr::pair_fill, dim3(csr::grid_for(S.padded)), dim3(kBlock), 0, s, S.padded,
+                       (const int*)S.pos, (const long long*)P.off, (const int2*)P.pairs, (const long long*)P.gbase, sp);
+    OPT_HIP_CHECK(hipGetLastError());
+    OPT_HIP_CHECK(hipStreamSynchronize(s));
+    dfree(P.pairs);
+    dfree(P.off);
+    P.off = nullptr;
+    P.pairs = sp;
+    P.npairs = total;
+}
+template <typename T>
+void ata_values_products(const AtaProducts& P, const T* valA, T* out, hipStream_t s) {
+    if (P.padded == 0) return;
+    hipLaunchKernelGGL((csr::ata_from_pairs<T>), dim3(csr::grid_for(P.padded)), dim3(kBlock), 0, s, P.padded,
+                       (const long long*)P.gbase, (const int2*)P.pairs, valA, out);
+    OPT_HIP_CHECK(hipGetLastError());
+}
+
+int sell_blocks(const SellMatrix& S) { return csr::grid_for((long long)S.nslices, kBlock / 64); }
+template <typename T>
+void sell_spmv(const SellMatrix& S, const T* val, const T* x, T* y, hipStream_t s) {
+    if (S.rows == 0) return;
+    hipLaunchKernelGGL((csr::sell_spmv<T, false>), dim3(sell_blocks(S)), dim3(kBlock), 0, s, S.rows, S.nslices,
+                       (const int*)S.sliceOff, (const int*)S.col, val, x, y, (const T*)nullptr, PcgMask{},
+                       ReduceSlot{});
+    OPT_HIP_CHECK(hipGetLastError());
+}
+template <typename T>
+void sell_spmv_pcg(const SellMatrix& S, const T* val, const T* x, T* y, const T* pv, const PcgMask& m, ReduceSlot rs,
+                   hipStream_t s) {
+    hipLaunchKernelGGL((csr::sell_spmv<T, true>), dim3(sell_blocks(S)), dim3(kBlock), 0, s, S.rows, S.nslices,
+                       (const int*)S.sliceOff, (const int*)S.col, val, x, y, pv, m, rs);
+    OPT_HIP_CHECK(hipGetLastError());
+}
+
 #define INST(T)                                                                                                  \
     template void csr_gather<T>(long long, const int*, const T*, T*, hipStream_t);                              \
     template void csr_ata_values<T>(int, const int*, const int*, const T*, const int*, const int*, const T*,     \
                                     const int*, const int*, T*, hipStream_t);                                    \
     template void csr_spmv<T>(int, long long, const int*, const int*, const T*, const T*, T*, hipStream_t);      \
     template void csr_spmv_pcg<T>(int, long long, const int*, const int*, const T*, const T*, T*, const T*,      \
-                                  const PcgMask&, ReduceSlot, hipStream_t);
+                                  const PcgMask&, ReduceSlot, hipStream_t);                                   \
+    template void sell_values<T>(const SellMatrix&, const T*, T*, hipStream_t);                                 \
+    template void ata_values_sell<T>(int, const int*, const int*, const T*, const int*, const int*, const T*,    \
+                                     const int*, const int*, const SellMatrix&, T*, hipStream_t);                \
+    template void sell_spmv<T>(const SellMatrix&, const T*, const T*, T*, hipStream_t);                         \
+    template void ata_values_products<T>(const AtaProducts&, const T*, T*, hipStream_t);                        \
+    template void sell_spmv_pcg<T>(const SellMatrix&, const T*, const T*, T*, const T*, const PcgMask&,          \
+                                   ReduceSlot, hipStream_t);
 INST(float)
 INST(double)
 #undef INST

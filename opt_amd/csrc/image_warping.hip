@@ -721,48 +721,66 @@ __device__ __forceinline__ void sort3(int* c, T* v) {
     };
     sw(0, 1); sw(1, 2); sw(0, 1);
 }
+// A block stages the rows of 256 consecutive pixels in LDS and stores them as one
+// contiguous run (6656 nonzeros, 2560 row pointers): every global store is coalesced.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void iw_dump_j(Args<T> a, int* __restrict__ rowPtr, int* __restrict__ colInd,
                                                     T* __restrict__ val) {
+    __shared__ int s_col[kBlock * 26];
+    __shared__ T s_val[kBlock * 26];
+    __shared__ int s_row[kBlock * 10];
     const int W = a.dom.W, H = a.dom.H;
     const long long N = (long long)W * H, n = 3 * N;
     constexpr int SXd[4] = {1, -1, 0, 0}, SYd[4] = {0, 0, 1, -1};
     auto wrap = [n](long long c) -> int { return (int)(c < 0 ? c + n : (c >= n ? c - n : c)); };
-    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < N; k += (long long)gridDim.x * blockDim.x) {
-        const int x = (int)(k % W), y = (int)(k / W);
-        const long long rb = 10 * k, nb = 26 * k;
-        const bool mk = a.M[k] == 0.f;
-        T ck, sk;
-        sc_of(a.A[k], &ck, &sk);
-        const float ukx = a.U[2 * k], uky = a.U[2 * k + 1];
-        for (int s = 0; s < 4; ++s) {
-            const int tx = x + SXd[s], ty = y + SYd[s];
-            const bool in = tx >= 0 && tx < W && ty >= 0 && ty < H;
-            const long long t = in ? (long long)ty * W + tx : 0;
-            const bool v = in && mk && a.M[t] == 0.f;
-            const T dx = in ? (T)(ukx - a.U[2 * t]) : (T)0, dy = in ? (T)(uky - a.U[2 * t + 1]) : (T)0;
-            const T drot[2] = {-sk * dx - ck * dy, ck * dx - sk * dy};
-            const long long tn = k + SXd[s] + (long long)SYd[s] * W;   // tooffset of the (maybe outside) neighbour
-            for (int c = 0; c < 2; ++c) {
-                const int row = 2 * s + c;
-                rowPtr[rb + row] = (int)(nb + 3 * row);
-                int cc[3] = {(int)(2 * k + c), wrap(2 * tn + c), (int)(2 * N + k)};
-                T vv[3] = {v ? a.wr : (T)0, v ? -a.wr : (T)0, v ? -a.wr * drot[c] : (T)0};
-                sort3(cc, vv);
-                for (int q = 0; q < 3; ++q) {
-                    colInd[nb + 3 * row + q] = cc[q];
-                    val[nb + 3 * row + q] = vv[q];
+    const int t = threadIdx.x;
+    for (long long k0 = (long long)blockIdx.x * kBlock; k0 < N; k0 += (long long)gridDim.x * kBlock) {
+        const long long k = k0 + t;
+        if (k < N) {
+            const int x = (int)(k % W), y = (int)(k / W);
+            const bool mk = a.M[k] == 0.f;
+            T ck, sk;
+            sc_of(a.A[k], &ck, &sk);
+            const float ukx = a.U[2 * k], uky = a.U[2 * k + 1];
+            int* sc = s_col + 26 * t;
+            T* sv = s_val + 26 * t;
+            for (int s = 0; s < 4; ++s) {
+                const int tx = x + SXd[s], ty = y + SYd[s];
+                const bool in = tx >= 0 && tx < W && ty >= 0 && ty < H;
+                const long long tp = in ? (long long)ty * W + tx : 0;
+                const bool v = in && mk && a.M[tp] == 0.f;
+                const T dx = in ? (T)(ukx - a.U[2 * tp]) : (T)0, dy = in ? (T)(uky - a.U[2 * tp + 1]) : (T)0;
+                const T drot[2] = {-sk * dx - ck * dy, ck * dx - sk * dy};
+                const long long tn = k + SXd[s] + (long long)SYd[s] * W;   // tooffset of the (maybe outside) neighbour
+                for (int c = 0; c < 2; ++c) {
+                    const int row = 2 * s + c;
+                    s_row[10 * t + row] = (int)(26 * k + 3 * row);
+                    int cc[3] = {(int)(2 * k + c), wrap(2 * tn + c), (int)(2 * N + k)};
+                    T vv[3] = {v ? a.wr : (T)0, v ? -a.wr : (T)0, v ? -a.wr * drot[c] : (T)0};
+                    sort3(cc, vv);
+                    for (int q = 0; q < 3; ++q) {
+                        sc[3 * row + q] = cc[q];
+                        sv[3 * row + q] = vv[q];
+                    }
                 }
             }
+            const bool has = a.C[2 * k] >= 0.f && a.C[2 * k + 1] >= 0.f;
+            for (int c = 0; c < 2; ++c) {
+                s_row[10 * t + 8 + c] = (int)(26 * k + 24 + c);
+                sc[24 + c] = (int)(2 * k + c);
+                sv[24 + c] = has ? a.wf : (T)0;
+            }
         }
-        const bool has = a.C[2 * k] >= 0.f && a.C[2 * k + 1] >= 0.f;
-        for (int c = 0; c < 2; ++c) {
-            rowPtr[rb + 8 + c] = (int)(nb + 24 + c);
-            colInd[nb + 24 + c] = (int)(2 * k + c);
-            val[nb + 24 + c] = has ? a.wf : (T)0;
+        __syncthreads();
+        const int np = (int)min((long long)kBlock, N - k0);
+        for (int e = t; e < 26 * np; e += kBlock) {
+            colInd[26 * k0 + e] = s_col[e];
+            val[26 * k0 + e] = s_val[e];
         }
-        if (k == N - 1) rowPtr[10 * N] = (int)(26 * N);
+        for (int e = t; e < 10 * np; e += kBlock) rowPtr[10 * k0 + e] = s_row[e];
+        __syncthreads();
     }
+    if (blockIdx.x == 0 && t == 0) rowPtr[10 * N] = (int)(26 * N);
 }
 
 }  // namespace iw

@@ -280,6 +280,10 @@ long long OptAMD_PlanJacobianShape(Opt_Plan* plan, long long* nResiduals) {
     if (!valid_plan(plan, "OptAMD_PlanJacobianShape")) return -1;
     return plan->impl->jacobian_shape(nResiduals);
 }
+int OptAMD_PlanMaterializedNonzeros(Opt_Plan* plan, long long* nnzJ, long long* nnzJTJ) {
+    if (!valid_plan(plan, "OptAMD_PlanMaterializedNonzeros")) return 1;
+    return plan->impl->materialized_nonzeros(nnzJ, nnzJTJ) ? 0 : 1;
+}
 int OptAMD_EvalJacobian(Opt_State* state, Opt_Plan* plan, void** params, int* rowPtr, int* colInd, void* val) {
     if (!valid_state(state, "OptAMD_EvalJacobian") || !valid_plan(plan, "OptAMD_EvalJacobian") || !rowPtr ||
         !colInd || !val)

@@ -105,6 +105,12 @@ public:
     // Materialized Jacobian (saveJToCRS, solverGPUGaussNewton.t:1004-1022): nonzeros
     // (-1: the family has no J assembly) and *rows = residual count.
     virtual long long jacobian_shape(long long* rows) const { if (rows) *rows = 0; return -1; }
+    // Sizes of the plan's materialized J and J^T J (0 before the first step); false when
+    // the plan runs matrix-free.
+    virtual bool materialized_nonzeros(long long* nnzJ, long long* nnzJTJ) const {
+        (void)nnzJ; (void)nnzJTJ;
+        return false;
+    }
     // J at the current unknowns into caller device arrays (rowPtr rows+1, colInd/val nnz).
     virtual int eval_jacobian(void** params, int* rowPtr, int* colInd, void* val) {
         (void)params; (void)rowPtr; (void)colInd; (void)val;

@@ -163,31 +163,50 @@ __global__ __launch_bounds__(kBlock) void pie_cost(Args<T> a, const T* __restric
 // saveJToCRS / generateDumpJ (solverGPUGaussNewton.t:385-442, 1004-1022): every pixel
 // writes 16 rows (s-major, channel-minor), each {X_c(k): b, X_c(k+s): -b} with
 // b = InBounds(k+s), columns wrapped (wrap(), :365-381) and sorted.
+// Rows of 128 consecutive pixels staged in LDS (4096 nonzeros, 2048 row pointers) and
+// stored contiguously; two threads per pixel (channels 0-1 / 2-3).
 template <typename T>
 __global__ __launch_bounds__(kBlock) void pie_dump_j(Domain d, int* __restrict__ rowPtr, int* __restrict__ colInd,
                                                      T* __restrict__ val) {
+    constexpr int P = kBlock / 2;
+    __shared__ int s_col[P * 32];
+    __shared__ T s_val[P * 32];
+    __shared__ int s_row[P * 16];
     const long long N = (long long)d.W * d.H, n = 4 * N;
-    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < N; k += (long long)gridDim.x * blockDim.x) {
-        const int x = (int)(k % d.W), y = (int)(k / d.W);
-        for (int s = 0; s < 4; ++s) {
-            const bool in = inside(d, x + DX[s], y + DY[s]);
-            const long long tn = k + DX[s] + (long long)DY[s] * d.W;
-            for (int c = 0; c < 4; ++c) {
-                const long long row = 16 * k + 4 * s + c, nz = 2 * row;
-                rowPtr[row] = (int)nz;
-                long long c0 = 4 * k + c, c1 = 4 * tn + c;
-                c1 = c1 < 0 ? c1 + n : (c1 >= n ? c1 - n : c1);
-                T v0 = in ? (T)1 : (T)0, v1 = in ? (T)-1 : (T)0;
-                if (c1 < c0) {
-                    const long long tc = c0; c0 = c1; c1 = tc;
-                    const T tv = v0; v0 = v1; v1 = tv;
+    const int t = threadIdx.x, tp = t >> 1, half = t & 1;
+    for (long long k0 = (long long)blockIdx.x * P; k0 < N; k0 += (long long)gridDim.x * P) {
+        const long long k = k0 + tp;
+        if (k < N) {
+            const int x = (int)(k % d.W), y = (int)(k / d.W);
+            for (int s = 0; s < 4; ++s) {
+                const bool in = inside(d, x + DX[s], y + DY[s]);
+                const long long tn = k + DX[s] + (long long)DY[s] * d.W;
+                for (int cc = 0; cc < 2; ++cc) {
+                    const int c = 2 * half + cc;
+                    const int row = 4 * s + c, nz = 2 * row;
+                    s_row[16 * tp + row] = (int)(32 * k + nz);
+                    long long c0 = 4 * k + c, c1 = 4 * tn + c;
+                    c1 = c1 < 0 ? c1 + n : (c1 >= n ? c1 - n : c1);
+                    T v0 = in ? (T)1 : (T)0, v1 = in ? (T)-1 : (T)0;
+                    if (c1 < c0) {
+                        const long long tc = c0; c0 = c1; c1 = tc;
+                        const T tv = v0; v0 = v1; v1 = tv;
+                    }
+                    s_col[32 * tp + nz] = (int)c0; s_val[32 * tp + nz] = v0;
+                    s_col[32 * tp + nz + 1] = (int)c1; s_val[32 * tp + nz + 1] = v1;
                 }
-                colInd[nz] = (int)c0; val[nz] = v0;
-                colInd[nz + 1] = (int)c1; val[nz + 1] = v1;
             }
         }
-        if (k == N - 1) rowPtr[16 * N] = (int)(32 * N);
+        __syncthreads();
+        const int np = (int)min((long long)P, N - k0);
+        for (int e = t; e < 32 * np; e += kBlock) {
+            colInd[32 * k0 + e] = s_col[e];
+            val[32 * k0 + e] = s_val[e];
+        }
+        for (int e = t; e < 16 * np; e += kBlock) rowPtr[16 * k0 + e] = s_row[e];
+        __syncthreads();
     }
+    if (blockIdx.x == 0 && t == 0) rowPtr[16 * N] = (int)(32 * N);
 }
 
 }  // namespace pie
@@ -265,8 +284,8 @@ public:
     long long jacobian_rows() const { return 16LL * dom_.W * dom_.H; }
     long long jacobian_nnz() const { return 32LL * dom_.W * dom_.H; }
     void dump_j(int* rowPtr, int* colInd, T* val, hipStream_t s) {
-        hipLaunchKernelGGL(pie::pie_dump_j<T>, dim3(flat_grid((long long)dom_.W * dom_.H, 1)), dim3(kBlock), 0, s,
-                           dom_, rowPtr, colInd, val);
+        hipLaunchKernelGGL(pie::pie_dump_j<T>, dim3(flat_grid((long long)dom_.W * dom_.H * 2, 1)), dim3(kBlock), 0,
+                           s, dom_, rowPtr, colInd, val);
         OPT_HIP_CHECK(hipGetLastError());
     }
 

@@ -334,6 +334,12 @@ public:
         }
         return Plan::jacobian_shape(rows);
     }
+    bool materialized_nonzeros(long long* nnzJ, long long* nnzJTJ) const override {
+        if (!mat_) return false;
+        if (nnzJ) *nnzJ = mat_->nnz();
+        if (nnzJTJ) *nnzJTJ = mat_->nnz_jtj();
+        return true;
+    }
     int eval_jacobian(void** params, int* rowPtr, int* colInd, void* val) override {
         if constexpr (HasDumpJ<Op>::value) {
             if (distributed() || dom_.mem_rows != dom_.H) return 1;

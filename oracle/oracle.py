@@ -401,6 +401,8 @@ def _csr_lib():
         lib.oracle_iw_apply_materialized.argtypes = [i, i, _F, _F, _F, _F, _F, f, f, i, _F, _F]
         lib.oracle_pie_dump_j.restype = None
         lib.oracle_pie_dump_j.argtypes = [i, i, _F, _F, _F, _I, _I, _F]
+        lib.oracle_pie_apply_materialized.restype = d
+        lib.oracle_pie_apply_materialized.argtypes = [i, i, _F, _F, _F, i, _F, _F]
         lib.oracle_pie_solve_materialized.restype = i
         lib.oracle_pie_solve_materialized.argtypes = [i, i, _F, _F, _F, i, i, i, i, _D]
         lib._csr = True
@@ -493,3 +495,11 @@ def pie_solve_materialized(w, n_iter, l_iter, lm=False, fused=True):
     k = _csr_lib().oracle_pie_solve_materialized(w["W"], w["H"], _f(X), _f(w["T"]), _f(w["M"]), int(lm), int(fused),
                                                  n_iter, l_iter, costs.ctypes.data_as(_D))
     return X, costs[: k + 1]
+
+
+def pie_apply_materialized(w, p, fused=True):
+    p = np.ascontiguousarray(p, np.float32)
+    Ap = np.zeros_like(p)
+    pAp = _csr_lib().oracle_pie_apply_materialized(w["W"], w["H"], _f(w["X"]), _f(w["T"]), _f(w["M"]), int(fused),
+                                                   _f(p), _f(Ap))
+    return Ap, pAp

@@ -222,3 +222,16 @@ int oracle_pie_solve_materialized(int W, int H, float* X, const float* T, const 
     free(c.c.prev);
     return k;
 }
+double oracle_pie_apply_materialized(int W, int H, float* X, const float* T, const float* M, int fused,
+                                     const float* p, float* Ap) {
+    piem_ctx c = {{W, H, X, T, M, NULL}};
+    const long long n = 4LL * W * H;
+    unsigned char* act = malloc(n);
+    for (long long e = 0; e < n; ++e) act[e] = M[e / 4] == 0.f;
+    oracle_mat_init(&c.m, 16LL * W * H, 32LL * W * H, (int)n, fused, act, pie_dump, &c.c);
+    oracle_mat_build(&c.m);
+    const double d = oracle_mat_apply(&c.m, p, Ap);
+    oracle_mat_free(&c.m);
+    free(act);
+    return d;
+}

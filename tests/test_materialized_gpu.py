@@ -55,7 +55,8 @@ def test_csr_kernels_match_oracle(shape):
     np.testing.assert_array_equal(ga[2].cpu().numpy(), vA)
     x = np.random.default_rng(2).normal(size=cols).astype(np.float32)
     y = api.csr_spmv(rows, cols, dev(rp), dev(ci), dev(v), dev(x)).cpu().numpy()
-    np.testing.assert_allclose(y, oracle.csr_spmv(rows, cols, rp, ci, v, x), rtol=1e-5, atol=1e-5)
+    # entries summed in order with rounded products: bitwise applyAtoVector
+    np.testing.assert_array_equal(y, oracle.csr_spmv(rows, cols, rp, ci, v, x))
 
 
 def test_csr_fp64():
@@ -159,3 +160,21 @@ def test_pie_materialized_solve_matches_oracle(fused):
 def test_families_without_assembly_refuse_the_materialized_plan():
     with pytest.raises(api.OptError):
         OptSolver([32, 32], os.path.join(ROOT, "energies", "optical_flow.t"), "LMGPU", materialized=True)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_pie_materialized_apply_is_bitwise_the_oracle(fused):
+    """J of this energy is exact (+-1 entries), so J^T, J^T J (reference summation order)
+    and the SELL-64 SpMV (row order, rounded products) reproduce the CPU restatement of
+    the reference's CSR path bit for bit."""
+    import torch
+
+    W, H = 70, 37
+    w = workloads.poisson_image_editing(W, H, seed=8)
+    act4 = np.repeat(w["M"] == 0, 4)
+    p = (np.random.default_rng(1).normal(size=4 * W * H) * act4).astype(np.float32)
+    s = OptSolver([W, H], PIE, "gaussNewtonGPU", materialized=True, fused_jtj=fused)
+    Ap = torch.zeros(4 * W * H, device="cuda")
+    s.apply_jtj([dev(w["X"]), dev(w["T"]), dev(w["M"])], dev(p), Ap)
+    ref, _ = oracle.pie_apply_materialized(w, p, fused=fused)
+    np.testing.assert_array_equal(Ap.cpu().numpy(), ref)

@@ -72,12 +72,32 @@ def oflow():
                 double=True, prm=prm, units=3840 * 2160, unit="px", bytes_per_unit=72, dtype=torch.float64)
 
 
+def materialized(cfg, fused):
+    """The same config through the materialized-Jacobian path (useMaterializedJTJ)."""
+    cfg = dict(cfg)
+    cfg["name"] += " materialized " + ("J^T J (fused)" if fused else "J^T (J p)")
+    cfg["materialized"] = True
+    cfg["fused"] = fused
+    return cfg
+
+
 CONFIGS = {"iw4096": lambda: iw(4096), "iw2048": lambda: iw(2048), "poisson": poisson, "sfs": sfs,
-           "arap": arap, "optical_flow": oflow}
+           "arap": arap, "optical_flow": oflow,
+           "iw4096_mat_fused": lambda: materialized(iw(4096), True),
+           "iw4096_mat_split": lambda: materialized(iw(4096), False),
+           "poisson_mat_fused": lambda: materialized(poisson(), True)}
+
+
+def spmv_bytes(rows, cols, nnz, x_len):
+    """Compulsory bytes of one CSR SpMV: (value, column) per nonzero, row pointer and
+    output per row, each input element once."""
+    return 8 * nnz + 8 * rows + 4 + 4 * x_len
 
 
 def measure(cfg, steps):
-    s = OptSolver(cfg["dims"], cfg["energy"], cfg["kind"], double_precision=cfg["double"])
+    mat = cfg.get("materialized", False)
+    s = OptSolver(cfg["dims"], cfg["energy"], cfg["kind"], double_precision=cfg["double"], materialized=mat,
+                  fused_jtj=cfg.get("fused", False))
     n = s.unknown_count()
     p = torch.randn(n, device="cuda", dtype=cfg["dtype"])
     Ap = torch.empty_like(p)
@@ -96,15 +116,29 @@ def measure(cfg, steps):
         done += 1
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    gbs = cfg["bytes_per_unit"] * cfg["units"] / (apply_us * 1e-6) / 1e9
+    bytes_apply = cfg["bytes_per_unit"] * cfg["units"]
+    bpu = cfg["bytes_per_unit"]
+    if mat:
+        nres, _ = s.jacobian_shape()
+        nnzJ, nnzJTJ = s.materialized_nonzeros()
+        if cfg["fused"]:   # one SpMV over J^T J (+ p read again for p.Ap: same vector, cached)
+            bytes_apply = spmv_bytes(n, n, nnzJTJ, n)
+        else:              # J p, then J^T (J p) with p read for p.Ap
+            bytes_apply = spmv_bytes(nres, n, nnzJ, n) + spmv_bytes(n, nres, nnzJ, nres) + 4 * n
+        bpu = bytes_apply / cfg["units"]
+        apply_us = s.time_apply(cfg["prm"], p, Ap, 20)   # after the first step: steady-state J^T J
+    gbs = bytes_apply / (apply_us * 1e-6) / 1e9
     out = {
         "config": cfg["name"], "unknowns": n, "apply_kernel": s.apply_kernel_name(), "apply_us": apply_us,
         "apply_unknowns_per_s": n / (apply_us * 1e-6),
         "roofline": {"bound": "hbm", "achieved": gbs, "peak": PEAK, "unit": "GB/s", "frac": gbs / PEAK,
-                     "bytes_per_unit": cfg["bytes_per_unit"], "unit_kind": cfg["unit"]},
+                     "bytes_per_unit": bpu, "unit_kind": cfg["unit"]},
         "lIterations": liter, "timed_steps": done,
         "step_ms": 1000.0 * dt / max(done, 1), "cost_after": s.cost(),
     }
+    if mat:
+        out["nnz_J"], out["nnz_JTJ"] = s.materialized_nonzeros()
+        out["jacobian_rows"] = s.jacobian_shape()[0]
     s.close()
     return out
 
