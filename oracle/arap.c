@@ -1,7 +1,9 @@
 /*
  * oracle/arap.c — CPU restatement of the reference's arap_mesh_deformation solver.
- * TEST INFRASTRUCTURE ONLY (oracle/README.md). PARITY UNPINNED: no executable
- * reference path and no golden outputs; pinned by an independent float64 numpy
+ * TEST INFRASTRUCTURE ONLY (oracle/README.md). PINNED to the reference's own output:
+ * its end-to-end test's CUDA final cost for the small_armadillo example
+ * (examples/test_final_cost.py:55-66, 7183.464843) is reproduced within 1.2e-7
+ * (tests/test_reference_costs.py); also checked against an independent float64 numpy
  * restatement with finite differences (tests/test_oracle_arap.py).
  *
  * Energy examples/arap_mesh_deformation/arap_mesh_deformation.t:

@@ -1,8 +1,9 @@
 /*
  * oracle/optical_flow_impl.h — TEST INFRASTRUCTURE ONLY (oracle/README.md).
- * PARITY UNPINNED: the reference holds no executable path and no golden vectors for
- * this energy; pinned by finite differences + the GN quadratic identity
- * (tests/test_oracle_optical_flow.py).
+ * PINNED to the reference's own output: its end-to-end test's CUDA final cost for the
+ * dogdance example (first solve, examples/test_final_cost.py:62, 0.52119255) is
+ * reproduced within 2e-7 (tests/test_reference_costs.py); also checked by finite
+ * differences + the GN quadratic identity (tests/test_oracle_optical_flow.py).
  *
  * Energy examples/optical_flow/optical_flow.t: unknown X (opt_float2), knowns I,
  * I_hat, I_hat_dx, I_hat_dy (float); UsePreconditioner(false); no Exclude.

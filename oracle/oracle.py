@@ -1,7 +1,9 @@
 """ctypes binding of oracle/build/liboracle.so — TEST INFRASTRUCTURE ONLY.
 
 Importable only from tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
-(the checker and the timed CPU baseline). Parity status: unpinned (oracle/README.md).
+(the checker and the timed CPU baseline). Parity status: pinned to the reference's own
+known answers for image_warping, optical_flow, arap_mesh_deformation and the CSR
+algebra (oracle/README.md).
 """
 from __future__ import annotations
 

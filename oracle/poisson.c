@@ -1,8 +1,12 @@
 /*
  * oracle/poisson.c — CPU restatement of the reference's poisson_image_editing solver.
- * TEST INFRASTRUCTURE ONLY (oracle/README.md). PARITY UNPINNED (no reference golden
- * vectors; checked against an independent float64 restatement + finite differences in
- * tests/test_oracle_poisson.py).
+ * TEST INFRASTRUCTURE ONLY (oracle/README.md). PARITY UNPINNED for this energy: the
+ * reference's end-to-end test value (test_final_cost.py:63) comes from a harness run
+ * that reads its mask out of bounds (examples/poisson_image_editing/src/main.cpp:95-101
+ * at the test's stride 4), so it cannot be reproduced; checked against an independent
+ * float64 restatement + finite differences (tests/test_oracle_poisson.py) and, through
+ * the shared generic loop (solver_impl.h), by the pinned image_warping / optical_flow
+ * solves.
  *
  * Energy: examples/poisson_image_editing/poisson_image_editing.t — X float4 unknown,
  * T float4, M mask; Exclude(M != 0); UsePreconditioner(false);

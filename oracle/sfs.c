@@ -1,7 +1,7 @@
 /*
  * oracle/sfs.c — CPU restatement of the reference's shape_from_shading solver.
- * TEST INFRASTRUCTURE ONLY (oracle/README.md). PARITY UNPINNED: the reference holds no
- * executable path and no golden outputs for this energy; its own input files
+ * TEST INFRASTRUCTURE ONLY (oracle/README.md). PARITY UNPINNED for this energy: the
+ * reference's end-to-end test holds no value for it (test_final_cost.py:64, -1); its own input files
  * (examples/data/shape_from_shading/default*) are used as inputs, and this restatement
  * is pinned by an independent float64 numpy restatement with finite differences
  * (tests/test_oracle_sfs.py).

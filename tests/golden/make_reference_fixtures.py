@@ -14,7 +14,20 @@ harness loads them:
     the Constraints image from these (CombinedSolver.h:168-219); tests/reference_inputs.py
     restates that construction.
 
-Data licence: public domain (examples/data/copyright.txt).
+  optical_flow (examples/optical_flow/src/main.cpp:33-80, file = 1, stride = 16 as
+    test_final_cost.py:78 sets): the RGB pixels of dogdance0.png / dogdance1.png at
+    (16 i, 16 j). The grayscale conversion, the two Gaussian pyramid levels and the
+    derivative images are restated in tests/reference_inputs.py.
+
+  arap_mesh_deformation (examples/arap_mesh_deformation/src/main.cpp:17-70): the vertex
+    positions and triangles of small_armadillo.ply (binary PLY) and its marker file
+    small_armadillo.mrk (x y z radius vertex-index per marker). The harness's one
+    sqrt(3) subdivision (OpenMesh Sqrt3T) and graph construction are restated in
+    tests/reference_inputs.py.
+
+Data licence: public domain (cat512*), Middlebury flow data set (dogdance*), Stanford
+3D Scanning Repository, research use with credit (small_armadillo*),
+examples/data/copyright.txt.
 
     python tests/golden/make_reference_fixtures.py /root/reference
 """
@@ -36,6 +49,31 @@ def main(ref):
     out = os.path.join(here, "iw_cat512.npz")
     np.savez_compressed(out, mask=mask, constraints=cons)
     print(out, mask.shape, cons.shape)
+    stride = 16
+    rgb = []
+    for name in ("dogdance0.png", "dogdance1.png"):
+        a = np.array(Image.open(os.path.join(data, name)).convert("RGB"))
+        H, W = a.shape[0] // stride, a.shape[1] // stride
+        rgb.append(a[: H * stride: stride, : W * stride: stride].copy())
+    out = os.path.join(here, "of_dogdance_s16.npz")
+    np.savez_compressed(out, src=rgb[0], tar=rgb[1], stride=stride)
+    print(out, rgb[0].shape)
+    raw = open(os.path.join(data, "small_armadillo.ply"), "rb").read()
+    head, body = raw.split(b"end_header\n", 1)
+    nv = int(head.split(b"element vertex ")[1].split()[0])
+    nf = int(head.split(b"element face ")[1].split()[0])
+    verts = np.frombuffer(body[: 12 * nv], np.float32).reshape(nv, 3).copy()
+    rec = np.dtype([("n", np.uint8), ("v", "<i4", (3,))])
+    fr = np.frombuffer(body[12 * nv: 12 * nv + rec.itemsize * nf], rec)
+    assert np.all(fr["n"] == 3)
+    faces = fr["v"].astype(np.int32).copy()
+    tok = open(os.path.join(data, "small_armadillo.mrk")).read().split()
+    nm = int(tok[0])
+    mk = np.array([float(t) for t in tok[1:1 + 5 * nm]], np.float64).reshape(nm, 5)
+    out = os.path.join(here, "arap_armadillo.npz")
+    np.savez_compressed(out, verts=verts, faces=faces, marker_pos=mk[:, :3].astype(np.float32),
+                        marker_idx=mk[:, 4].astype(np.int32))
+    print(out, verts.shape, faces.shape, mk.shape)
 
 
 if __name__ == "__main__":

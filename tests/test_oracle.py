@@ -1,4 +1,4 @@
-"""CPU: pin the C oracle to the energy definition (parity unpinned otherwise).
+"""CPU: pin the C oracle to the energy definition (the reference known answer is in test_reference_costs.py).
 
 The reference has no executable path and no golden vectors for this energy
 (oracle/README.md), so the oracle is checked against an independent float64 numpy

@@ -2,12 +2,15 @@
 through the C ABI on every solver path the reference test exercises (matrix-free GN,
 materialized J^T (J p), materialized J^T J) plus our GN fast path / generic driver and
 the host-buffer backends, within the reference test's 1e-5 relative tolerance."""
+import os
+
 import numpy as np
 import pytest
 
 from opt_amd import OptSolver
 from tests.iw_helpers import ENERGY, device_params, host_params
-from tests.reference_inputs import REFERENCE_FINAL_COST, REFERENCE_RTOL, image_warping_cat512
+from tests.reference_inputs import (REFERENCE_FINAL_COST, REFERENCE_RTOL, arap_armadillo, image_warping_cat512,
+                                   optical_flow_dogdance)
 
 pytestmark = pytest.mark.gpu
 
@@ -36,3 +39,38 @@ def test_image_warping_cat512_fp64():
     s.set_solver_params({"nIterations": 1, "lIterations": 1})
     s.solve(device_params(w, double=True))
     assert rel(s.cost(), REFERENCE_FINAL_COST["image_warping"]) < REFERENCE_RTOL
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def dev(a):
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.parametrize("double", [False, True])
+def test_optical_flow_dogdance_final_cost(double):
+    import torch
+
+    w = optical_flow_dogdance(1)
+    s = OptSolver([w["W"], w["H"]], os.path.join(ROOT, "energies", "optical_flow.t"), "gaussNewtonGPU",
+                  double_precision=double)
+    s.set_solver_params({"nIterations": 1, "lIterations": 1})
+    X = dev(w["X"].astype(np.float64 if double else np.float32))
+    s.solve([w["w_fitSqrt"], w["w_regSqrt"], X] + [dev(w[k]) for k in ("I", "I_hat", "I_hat_dx", "I_hat_dy")])
+    assert rel(s.cost(), REFERENCE_FINAL_COST["optical_flow"]) < REFERENCE_RTOL
+
+
+@pytest.mark.parametrize("backend", ["backend_cuda", "backend_cpu"])
+def test_arap_armadillo_final_cost(backend):
+    w = arap_armadillo()
+    s = OptSolver([w["N"], w["E"]], os.path.join(ROOT, "energies", "arap_mesh_deformation.t"), "gaussNewtonGPU",
+                  backend=backend)
+    s.set_solver_params({"nIterations": 1, "lIterations": 1})
+    conv = dev if backend == "backend_cuda" else (lambda a: np.ascontiguousarray(a).copy())
+    prm = [w["w_fitSqrt"], w["w_regSqrt"]] + [conv(w[k]) for k in ("Offset", "Angle", "UrShape", "Constraints")] + \
+          [None, conv(w["v0"]), conv(w["v1"])]
+    s.solve(prm)
+    assert rel(s.cost(), REFERENCE_FINAL_COST["arap_mesh_deformation"]) < REFERENCE_RTOL
