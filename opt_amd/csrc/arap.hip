@@ -293,6 +293,62 @@ __global__ void count_heads(const int* keys, int E, int* counts) {
         atomicAdd(&counts[keys[e]], 1);
 }
 
+
+// ---------------------------------------------------- materialized Jacobian
+// saveJToCRS / saveJToCRS_Graph (solverGPUGaussNewton.t:1004-1022, 1287-1305) with
+// generateDumpJ (:385-442). Rows: the fit residuals first (centred, vertex v owns rows
+// 3v + c, one nonzero {O_c(v): wf [has target]}), then the graph residuals (edge e owns
+// rows 3N + 3e + c, five nonzeros {O_c(v0): wr, O_c(v1): -wr, A_j(v0): -wr (dR_j d_e)_c}),
+// columns = unknown indices ([Offset 3N | Angle 3N]) sorted inside each row.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void arap_dump_fit(Args<T> a, int E, int* __restrict__ rowPtr,
+                                                        int* __restrict__ colInd, T* __restrict__ val) {
+    if (E == 0 && blockIdx.x == 0 && threadIdx.x == 0) rowPtr[3LL * a.N] = 3 * a.N;
+    for (int v = blockIdx.x * blockDim.x + threadIdx.x; v < a.N; v += gridDim.x * blockDim.x) {
+        const T w = fit_valid(a, v) ? a.wf : (T)0;
+        for (int c = 0; c < 3; ++c) {
+            rowPtr[3 * v + c] = 3 * v + c;
+            colInd[3 * v + c] = 3 * v + c;
+            val[3 * v + c] = w;
+        }
+    }
+}
+template <typename T>
+__global__ __launch_bounds__(kBlock) void arap_dump_edges(Args<T> a, const int* __restrict__ v0s,
+                                                          const int* __restrict__ v1s, int E, int* __restrict__ rowPtr,
+                                                          int* __restrict__ colInd, T* __restrict__ val) {
+    const long long N = a.N;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x) {
+        const int v0 = v0s[e], v1 = v1s[e];
+        T R[9], dR[3][9];
+        rotation(ld3<T>(a.A, v0), R, dR);
+        const V3<float> U0 = ld3<float>(a.U, v0), U1 = ld3<float>(a.U, v1);
+        const V3<T> dd = {(T)(U0.x - U1.x), (T)(U0.y - U1.y), (T)(U0.z - U1.z)};
+        V3<T> col[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) col[j] = mv(dR[j], dd);
+        for (int c = 0; c < 3; ++c) {
+            const long long row = 3 * N + 3LL * e + c, nz = 3 * N + 15LL * e + 5 * c;
+            rowPtr[row] = (int)nz;
+            int cc[5] = {(int)(3 * v0 + c), (int)(3 * v1 + c), (int)(3 * N + 3 * v0), (int)(3 * N + 3 * v0 + 1),
+                         (int)(3 * N + 3 * v0 + 2)};
+            T vv[5] = {a.wr, -a.wr, -a.wr * (c == 0 ? col[0].x : c == 1 ? col[0].y : col[0].z),
+                       -a.wr * (c == 0 ? col[1].x : c == 1 ? col[1].y : col[1].z),
+                       -a.wr * (c == 0 ? col[2].x : c == 1 ? col[2].y : col[2].z)};
+            for (int i = 1; i < 5; ++i)   // sortCol
+                for (int j = i; j > 0 && cc[j] < cc[j - 1]; --j) {
+                    const int tc = cc[j]; cc[j] = cc[j - 1]; cc[j - 1] = tc;
+                    const T tv = vv[j]; vv[j] = vv[j - 1]; vv[j - 1] = tv;
+                }
+            for (int q = 0; q < 5; ++q) {
+                colInd[nz + q] = cc[q];
+                val[nz + q] = vv[q];
+            }
+        }
+        if (e == E - 1) rowPtr[3 * N + 3LL * E] = (int)(3 * N + 15LL * E);
+    }
+}
+
 }  // namespace arap
 
 // Deterministic CSR of a directed edge list grouped by `keys` (stable: edge order kept).
@@ -411,6 +467,18 @@ public:
     }
     void model_cost(const T* delta, ReduceSlot rs, hipStream_t s) {
         hipLaunchKernelGGL((arap::arap_cost<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, delta, rs);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    // materialized Jacobian (csr.h): 3 fit rows per vertex (1 nonzero each), then 3 rows
+    // per directed edge (5 nonzeros each)
+    long long jacobian_rows() const { return 3LL * N_ + 3LL * E_; }
+    long long jacobian_nnz() const { return 3LL * N_ + 15LL * E_; }
+    void dump_j(int* rowPtr, int* colInd, T* val, hipStream_t s) {
+        hipLaunchKernelGGL((arap::arap_dump_fit<T>), dim3(std::max(1, std::min((N_ + 255) / 256, 4096))), dim3(kBlock),
+                           0, s, a_, E_, rowPtr, colInd, val);
+        if (E_ > 0)
+            hipLaunchKernelGGL((arap::arap_dump_edges<T>), dim3(std::min((E_ + 255) / 256, 4096)), dim3(kBlock), 0, s,
+                               a_, graph_v0_, graph_v1_, E_, rowPtr, colInd, val);
         OPT_HIP_CHECK(hipGetLastError());
     }
 

@@ -214,6 +214,46 @@ __global__ __launch_bounds__(kBlock) void of_cost(Args<T> a, const T* __restrict
     block_reduce_publish<1>(v, rs, blockIdx.x);
 }
 
+
+// saveJToCRS / generateDumpJ (solverGPUGaussNewton.t:385-442, 1004-1022): pixel k owns
+// rows 9k.. 9k+8 — the fit residual {X0(k): -wf G.x, X1(k): -wf G.y} (the SampledImage
+// partials at the current flow, cached by of_jtf), then for s in (+x,-x,+y,-y) and each
+// channel {X_c(k): b wr, X_c(k+s): -b wr}, b = InBounds(k+s) — 18 nonzeros at 18 k,
+// columns wrapped (wrap(), :365-381) and sorted.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void of_dump_j(Args<T> a, int* __restrict__ rowPtr, int* __restrict__ colInd,
+                                                    T* __restrict__ val) {
+    const Domain& d = a.dom;
+    const long long N = (long long)d.W * d.H, n = 2 * N;
+    constexpr int SX[4] = {1, -1, 0, 0}, SY[4] = {0, 0, 1, -1};
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < N; k += (long long)gridDim.x * blockDim.x) {
+        const int x = (int)(k % d.W), y = (int)(k / d.W);
+        const V2<T> g = ld2(a.G, k);
+        const long long rb = 9 * k, nb = 18 * k;
+        rowPtr[rb] = (int)nb;
+        colInd[nb] = (int)(2 * k); val[nb] = -a.wf * g.x;
+        colInd[nb + 1] = (int)(2 * k + 1); val[nb + 1] = -a.wf * g.y;
+        for (int s = 0; s < 4; ++s) {
+            const bool in = inside(d, x + SX[s], y + SY[s]);
+            const long long tn = k + SX[s] + (long long)SY[s] * d.W;
+            for (int c = 0; c < 2; ++c) {
+                const long long row = rb + 1 + 2 * s + c, nz = nb + 2 + 4 * s + 2 * c;
+                rowPtr[row] = (int)nz;
+                long long c0 = 2 * k + c, c1 = 2 * tn + c;
+                c1 = c1 < 0 ? c1 + n : (c1 >= n ? c1 - n : c1);
+                T v0 = in ? a.wr : (T)0, v1 = in ? -a.wr : (T)0;
+                if (c1 < c0) {
+                    const long long tc = c0; c0 = c1; c1 = tc;
+                    const T tv = v0; v0 = v1; v1 = tv;
+                }
+                colInd[nz] = (int)c0; val[nz] = v0;
+                colInd[nz + 1] = (int)c1; val[nz + 1] = v1;
+            }
+        }
+        if (k == N - 1) rowPtr[9 * N] = (int)(18 * N);
+    }
+}
+
 }  // namespace of
 
 template <typename TT>
@@ -304,6 +344,15 @@ public:
     void model_cost(const T* delta, ReduceSlot rs, hipStream_t s) {
         rs.nblocks = tgrid();
         hipLaunchKernelGGL((of::of_cost<T>), dim3(tgrid()), dim3(kBlock), 0, s, a_, delta, rs);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    // materialized Jacobian (csr.h): 9 residual rows / 18 nonzeros per pixel; the fit
+    // partials come from the gradient of_jtf cached (jtf runs first in every step)
+    long long jacobian_rows() const { return 9LL * dom_.W * dom_.H; }
+    long long jacobian_nnz() const { return 18LL * dom_.W * dom_.H; }
+    void dump_j(int* rowPtr, int* colInd, T* val, hipStream_t s) {
+        hipLaunchKernelGGL(of::of_dump_j<T>, dim3(flat_grid((long long)dom_.W * dom_.H, 1)), dim3(kBlock), 0, s, a_,
+                           rowPtr, colInd, val);
         OPT_HIP_CHECK(hipGetLastError());
     }
 

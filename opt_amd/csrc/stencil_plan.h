@@ -345,6 +345,7 @@ public:
             if (distributed() || dom_.mem_rows != dom_.H) return 1;
             begin_call();
             prepare(params);
+            op_->jtf(r_, diag_, flags_, stream_);   // families whose J reuses J^T F state (optical_flow)
             op_->dump_j(rowPtr, colInd, (T*)val, stream_);
             end_call();
             return 0;

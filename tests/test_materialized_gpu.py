@@ -159,7 +159,7 @@ def test_pie_materialized_solve_matches_oracle(fused):
 
 def test_families_without_assembly_refuse_the_materialized_plan():
     with pytest.raises(api.OptError):
-        OptSolver([32, 32], os.path.join(ROOT, "energies", "optical_flow.t"), "LMGPU", materialized=True)
+        OptSolver([32, 32], os.path.join(ROOT, "energies", "shape_from_shading.t"), "LMGPU", materialized=True)
 
 
 @pytest.mark.parametrize("fused", [True, False])

@@ -50,24 +50,28 @@ def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
-@pytest.mark.parametrize("double", [False, True])
-def test_optical_flow_dogdance_final_cost(double):
-    import torch
+MODES = {"matrix_free": {}, "materialized": {"materialized": True},
+         "materialized_fused": {"materialized": True, "fused_jtj": True}}
 
+
+@pytest.mark.parametrize("mode", list(MODES))
+@pytest.mark.parametrize("double", [False, True])
+def test_optical_flow_dogdance_final_cost(double, mode):
     w = optical_flow_dogdance(1)
     s = OptSolver([w["W"], w["H"]], os.path.join(ROOT, "energies", "optical_flow.t"), "gaussNewtonGPU",
-                  double_precision=double)
+                  double_precision=double, **MODES[mode])
     s.set_solver_params({"nIterations": 1, "lIterations": 1})
     X = dev(w["X"].astype(np.float64 if double else np.float32))
     s.solve([w["w_fitSqrt"], w["w_regSqrt"], X] + [dev(w[k]) for k in ("I", "I_hat", "I_hat_dx", "I_hat_dy")])
     assert rel(s.cost(), REFERENCE_FINAL_COST["optical_flow"]) < REFERENCE_RTOL
 
 
+@pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("backend", ["backend_cuda", "backend_cpu"])
-def test_arap_armadillo_final_cost(backend):
+def test_arap_armadillo_final_cost(backend, mode):
     w = arap_armadillo()
     s = OptSolver([w["N"], w["E"]], os.path.join(ROOT, "energies", "arap_mesh_deformation.t"), "gaussNewtonGPU",
-                  backend=backend)
+                  backend=backend, **MODES[mode])
     s.set_solver_params({"nIterations": 1, "lIterations": 1})
     conv = dev if backend == "backend_cuda" else (lambda a: np.ascontiguousarray(a).copy())
     prm = [w["w_fitSqrt"], w["w_regSqrt"]] + [conv(w[k]) for k in ("Offset", "Angle", "UrShape", "Constraints")] + \
