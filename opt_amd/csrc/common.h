@@ -188,6 +188,12 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 
 template <typename T> struct Vec2 { T x, y; };
 
+// Tuning knob read from the environment (measurement sweeps), `dflt` when unset.
+inline int env_int(const char* name, int dflt) {
+    const char* v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+
 // Persistent tile loops: a grid of at most kMaxTileBlocks blocks (a multiple of 8)
 // walks `ntiles` tiles; the blocks of one XCD (b % 8) take a contiguous range of tiles
 // so neighbouring tiles' halos meet in that XCD's L2, and every block arrives at the

@@ -786,10 +786,6 @@ __global__ __launch_bounds__(kBlock) void iw_dump_j(Args<T> a, int* __restrict__
 }  // namespace iw
 
 // ====================================================================== plan
-static int env_int(const char* name, int dflt) {
-    const char* v = getenv(name);
-    return (v && *v) ? atoi(v) : dflt;
-}
 
 template <typename T>
 class ImageWarpingPlan final : public Plan {

@@ -428,6 +428,126 @@ __global__ __launch_bounds__(kBlock) void sfs_tiles(Args<T> a, const T* __restri
     block_reduce_publish<1>(v, rs, blockIdx.x);
 }
 
+// --------------------------------------------------- register-strip apply
+// The same re-associated chain as sfs_tiles (D -> V_h, V_v -> W -> shade; u_s -> L), but
+// with no LDS: a wavefront owns a 64-column strip and walks its rows top to bottom,
+// keeping the few rows each stage needs in registers; horizontal neighbours are DPP
+// lane shifts. The chain reaches two columns to either side, so a strip computes 64
+// columns and stores the middle 60 (strips overlap by 4 columns, re-read from L2). Row r
+// is loaded while row r-1 is processed; after loading row r the wave forms D(r), V_h(r),
+// then V_v(r-1), W(r-1), u_s(r-1), and stores row k = r-2. Same floating-point
+// operations in the same order as the tile kernel.
+constexpr int kStripOut = 60;
+template <typename T>
+struct SRow {   // raw loads of row r (+ flags / LM diagonal of the output row r-2)
+    T p, g0, g1, g2, dg;
+    int mr, mc, v, f;
+};
+template <typename T>
+__device__ __forceinline__ SRow<T> strip_row(const Args<T>& a, const T* __restrict__ p, const T* __restrict__ dadd,
+                                             int gx, int r) {
+    const Domain& d = a.dom;
+    SRow<T> s;
+    const bool in = inside(d, gx, r);
+    const long long o = in ? d.off(gx, r) : 0;
+    s.p = in ? p[o] : (T)0;
+    s.g0 = in ? a.G00[o] : (T)0;
+    s.g1 = in ? a.Gm0[o] : (T)0;
+    s.g2 = in ? a.G0m[o] : (T)0;
+    const bool ib = inbe(d, gx, r);
+    s.mr = ib ? a.mR[o] : 0;
+    s.mc = ib ? a.mC[o] : 0;
+    s.v = ib ? a.valid[o] : 0;
+    const int rk = r - 2;
+    const bool own = gx >= 0 && gx < d.W && rk >= d.y_lo && rk < d.y_hi;
+    const long long ok = own ? d.off(gx, rk) : 0;
+    s.f = own ? a.flags[ok] : 0;
+    s.dg = (own && dadd) ? dadd[ok] : (T)0;
+    return s;
+}
+template <typename T>
+__global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
+                                                    const T* __restrict__ dadd, const int* stop, ReduceSlot rs,
+                                                    int nstrips, int rows) {
+    if (stop && *stop) return;
+    const Domain& d = a.dom;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    const int strip = wave % nstrips, rb = wave / nstrips;
+    const int gx = strip * kStripOut - 2 + lane;
+    const int y0 = d.y_lo + rb * rows, y1 = min(y0 + rows, d.y_hi);
+    const bool out_lane = lane >= 2 && lane < 2 + kStripOut && gx < d.W;
+    const T wg = a.wg, ws = a.ws;
+    const T qxc = ((T)gx - a.ux) / a.fx, qxl = ((T)(gx - 1) - a.ux) / a.fx, qxr = ((T)(gx + 1) - a.ux) / a.fx;
+    T dot = 0;
+    if (y0 < y1) {
+        T p_m2 = 0, p_m1 = 0, D_m1 = 0, Vh_m1 = 0, Vv_m2 = 0, W_k = 0;
+        T g0_m2 = 0, g1_m2 = 0, g0_m1 = 0, g1_m1 = 0, g2_m1 = 0, qy_m1 = 0, qy_m2 = 0;
+        T us_k[3] = {0, 0, 0}, us_km1[3] = {0, 0, 0};
+        int mc_m1 = 0, v_m1 = 0;
+        SRow<T> nx = strip_row(a, p, dadd, gx, y0 - 2);
+        for (int r = y0 - 2; r <= y1 + 1; ++r) {
+            const SRow<T> cur = nx;
+            if (r + 1 <= y1 + 1) nx = strip_row(a, p, dadd, gx, r + 1);
+            const T qy = ((T)r - a.uy) / a.fy;
+            // row r: D, V_h
+            const T D = cur.g0 * cur.p + cur.g1 * from_left(cur.p, (T)0) + cur.g2 * p_m1;
+            const T mh = (T)cur.mr;
+            const T Vh = wg * mh * (wg * mh * (D - from_right(D, (T)0)));
+            // row r-1: V_v, W, u_s
+            const T mv = (T)mc_m1;
+            const T Vv = wg * mv * (wg * mv * (D_m1 - D));
+            const T W1 = (Vh_m1 - from_left(Vh_m1, (T)0)) + (Vv - Vv_m2);
+            T us[3] = {0, 0, 0};
+            {
+                const T pl = from_left(p_m1, (T)0), pr = from_right(p_m1, (T)0);
+                if (v_m1 == 1) {
+                    const T qv[5] = {qxc, qxl, qxc, qxr, qxc};
+                    const T qw[5] = {qy_m1, qy_m1, qy_m2, qy_m1, qy};
+                    const T pv[5] = {p_m1, pl, p_m2, pr, cur.p};
+#pragma unroll
+                    for (int sI = 0; sI < 5; ++sI) {
+                        const T co = sI == 0 ? (T)4 : (T)-1;
+                        us[0] += ws * co * qv[sI] * pv[sI];
+                        us[1] += ws * co * qw[sI] * pv[sI];
+                        us[2] += ws * co * pv[sI];
+                    }
+                }
+            }
+            // row k = r - 2: output
+            const int k = r - 2;
+            const T gw = g1_m2 * W_k;
+            const T shade = g0_m2 * W_k + from_right(gw, (T)0) + g2_m1 * W1;
+            T l[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c)
+                l[c] = (T)4 * us_k[c] - (from_left(us_k[c], (T)0) + us_km1[c] + from_right(us_k[c], (T)0) + us[c]);
+            if (k >= y0 && out_lane) {
+                const long long i = d.off(gx, k);
+                T acc = 0;
+                if (cur.f & 1) {
+                    const T pk = p_m2;
+                    const T fit = a.wp * (a.wp * pk);
+                    acc = fit + shade + ws * (qxc * l[0] + qy_m2 * l[1] + l[2]);
+                    if (dadd) acc += cur.dg * pk;
+                    dot += pk * acc;
+                }
+                Ap[i] = acc;
+            }
+            // roll the window
+            p_m2 = p_m1; p_m1 = cur.p;
+            D_m1 = D; Vh_m1 = Vh; Vv_m2 = Vv; W_k = W1;
+            g0_m2 = g0_m1; g1_m2 = g1_m1; g0_m1 = cur.g0; g1_m1 = cur.g1; g2_m1 = cur.g2;
+            qy_m2 = qy_m1; qy_m1 = qy;
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { us_km1[c] = us_k[c]; us_k[c] = us[c]; }
+            mc_m1 = cur.mc; v_m1 = cur.v;
+        }
+    }
+    double v[1] = {(double)dot};
+    block_reduce_publish<1>(v, rs, blockIdx.x);
+}
+
 // ------------------------------------------------------- cost / model cost
 template <typename T>
 __global__ __launch_bounds__(kBlock) void sfs_cost(Args<T> a, const T* __restrict__ delta, ReduceSlot rs) {
@@ -480,7 +600,7 @@ class ShapeFromShadingOp {
 public:
     using T = TT;
     static constexpr const char* kName = "shape_from_shading";
-    static constexpr const char* kApplyName = "sfs_tiles";
+    static constexpr const char* kApplyName = "sfs_strip";
     static constexpr bool kSlabs = true;
     ShapeFromShadingOp(const ProblemSpec& spec, const StateOptions& opts, Domain dom) : dom_(dom), opts_(opts) {
         idx_X_ = spec.unknown(0)->index;
@@ -574,9 +694,12 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
     void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
-        const dim3 g = tile_grid();
-        rs.nblocks = g.x * g.y;   // the reduction's arrival count is this launch's grid
-        hipLaunchKernelGGL((sfs::sfs_tiles<T, false>), g, dim3(kBlock), 0, s, a_, p, Ap, (T*)nullptr, dadd, stop, rs);
+        const int nstrips = (dom_.W + sfs::kStripOut - 1) / sfs::kStripOut;
+        const int nrb = (dom_.y_hi - dom_.y_lo + strip_rows_ - 1) / strip_rows_;
+        const int blocks = (nstrips * nrb + kBlock / kWave - 1) / (kBlock / kWave);
+        rs.nblocks = blocks;   // the reduction's arrival count is this launch's grid
+        hipLaunchKernelGGL((sfs::sfs_strip<T>), dim3(blocks), dim3(kBlock), 0, s, a_, p, Ap, dadd, stop, rs, nstrips,
+                           strip_rows_);
         OPT_HIP_CHECK(hipGetLastError());
     }
     void cost(ReduceSlot rs, hipStream_t s) {
@@ -600,6 +723,7 @@ private:
     StateOptions opts_;
     int idx_X_, idx_D_, idx_Im_, idx_mR_, idx_mC_, idx_p_[16];
     sfs::Args<T> a_{};
+    int strip_rows_ = env_int("OPT_AMD_SFS_ROWS", 16);
     T *BI_ = nullptr, *G00_ = nullptr, *Gm0_ = nullptr, *G0m_ = nullptr;
     uint8_t* valid_ = nullptr;
     T* userX_ = nullptr;
