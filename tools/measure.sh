@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU measurement pass (run through gpurun from the repo root):
-# bench line, kernel-trace stats, FETCH/WRITE PMC passes (bench + calibration), and the
-# per-config table. Outputs under gpurun_out/$TAG.
+# bench line, kernel-trace stats, FETCH/WRITE PMC passes over the bench, and the
+# per-config table (incl. the materialized-Jacobian rows). Outputs under gpurun_out/$TAG.
+# (The FETCH_SIZE calibration, tools/fetchcal.hip, is a one-off: profiles/r01_fetchcal.json.)
 set -e
 R=$(pwd)
 TAG=${1:-meas}
@@ -14,10 +15,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/stats -o run --output-f
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C -d $O/pmc_$C --output-format csv -- \
       python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_$C.log 2>&1
-  timeout -k 10 120 rocprofv3 --pmc $C -d $O/cal_$C --output-format csv -- $R/tools/fetchcal > $O/cal_$C.log 2>&1
 done
 cd $R
 python3 tools/pmc_summary.py $O/pmc.json $O/pmc_FETCH_SIZE $O/pmc_WRITE_SIZE > /dev/null
-python3 tools/pmc_summary.py $O/cal.json $O/cal_FETCH_SIZE $O/cal_WRITE_SIZE > /dev/null
-timeout -k 10 400 python3 tools/bench_families.py --out $O/families.json > $O/families.log 2>&1
+timeout -k 10 600 python3 tools/bench_families.py --out $O/families.json > $O/families.log 2>&1
 echo DONE
