@@ -145,6 +145,22 @@ int OptAMD_CsrATA(int nRowsA, int nColsA, long long nnz, const int* rowPtrA, con
 int OptAMD_CsrSpMV(int nRowsA, int nColsA, long long nnz, const int* rowPtrA, const int* colIndA,
                    const void* valA, const void* x, void* y, int doublePrecision);
 
+/* General energy front end (the reference's energy compiler, API/src/o.t:1295-1348 and
+ * 2669-3235): the HIP source generated for the energy file `filename` (float kernels, or
+ * double with doublePrecision = 1), copied into buf (NUL-terminated, truncated to n).
+ * Returns the full length, or -1 with the front end's message in buf. No device needed. */
+int OptAMD_GenericSource(const char* filename, int doublePrecision, char* buf, int n);
+
+/* The residual templates the front end lowered `filename` to, one line each:
+ * "<centred|graphK> <number of unknowns it reads> <expression>" (the reference's
+ * toenergyspecs / classifyexpression result, API/src/o.t:2669-2715). Returns the residual
+ * count, or -1 with the front end's message in buf. */
+int OptAMD_GenericDescribe(const char* filename, char* buf, int n);
+
+/* Compile that source for gfx950 with hiprtc (no device needed). 0 on success, -1 with
+ * the compiler log (or the front end's message) in buf. */
+int OptAMD_GenericCompileCheck(const char* filename, int doublePrecision, char* buf, int n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -82,6 +82,9 @@ _SIGNATURES = [
                                      ctypes.POINTER(ctypes.c_longlong), ctypes.c_int]),
     ("OptAMD_CsrSpMV", ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_longlong, _VP, _VP, _VP, _VP, _VP,
                                       ctypes.c_int]),
+    ("OptAMD_GenericSource", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
+    ("OptAMD_GenericDescribe", ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]),
+    ("OptAMD_GenericCompileCheck", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
 ]
 EXPORTED_SYMBOLS = [s[0] for s in _SIGNATURES]
 
@@ -365,3 +368,33 @@ def csr_spmv(rows, cols, rowPtr, colInd, val, x):
     if lib.OptAMD_CsrSpMV(rows, cols, colInd.numel(), _ptr(rowPtr), _ptr(colInd), _ptr(val), _ptr(x), _ptr(y), dp):
         raise OptError("OptAMD_CsrSpMV failed")
     return y
+
+
+# ---- general energy front end (no device needed) ----------------------------------
+def _text_call(fn, *args, cap: int = 1 << 23):
+    buf = ctypes.create_string_buffer(cap)
+    r = fn(*args, buf, cap)
+    return r, buf.value.decode(errors="replace")
+
+
+def generic_source(energy_file: str, double: bool = False) -> str:
+    """HIP source the front end generates for `energy_file` (OptAMD_GenericSource)."""
+    r, txt = _text_call(load_library().OptAMD_GenericSource, energy_file.encode(), int(double))
+    if r < 0:
+        raise OptError(txt)
+    return txt
+
+
+def generic_describe(energy_file: str) -> List[str]:
+    """Residual templates of `energy_file`: '<centred|graphK> <n unknowns> <expression>'."""
+    r, txt = _text_call(load_library().OptAMD_GenericDescribe, energy_file.encode())
+    if r < 0:
+        raise OptError(txt)
+    return txt.splitlines()
+
+
+def generic_compile_check(energy_file: str, double: bool = False) -> None:
+    """Compile the generated source for gfx950 with hiprtc; raise with the log on error."""
+    r, txt = _text_call(load_library().OptAMD_GenericCompileCheck, energy_file.encode(), int(double))
+    if r != 0:
+        raise OptError(txt)

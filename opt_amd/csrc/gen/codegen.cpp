@@ -1,0 +1,467 @@
+// gen/codegen.cpp — HIP kernels for a lowered energy (gen/model.h), compiled at plan
+// time with hiprtc (generic.hip).
+//
+// Kernel semantics follow the reference's derived functions (API/src/o.t):
+//   gen_jtf        createjtfcentered (:2870-2913): for every unknown x of a pixel, the sum
+//                  over the centred residual instances containing x of dr/dx * r and
+//                  (dr/dx)^2 (the instances are the residual templates shifted by the
+//                  inverse of each support offset, residualsincludingX00 :2723-2733);
+//                  writes r = -J^T F (0 on excluded unknowns), diag, and the exclude flags
+//   gen_apply      createjtjcentered (:2770-2830): sum over the same instances of
+//                  dr/dx * sum_u dr/du p(u); with `finish`, masks excluded unknowns, adds
+//                  the LM diagonal and reduces p.Ap (PCGStep1, solverGPUGaussNewton.t:607-632)
+//   gen_cost       createcost / createmodelcost (:3119-3129, :2915-2966): 1/2 sum r^2 (or
+//                  (r + J delta)^2) over non-excluded centres, plus every graph edge
+//   gen_*_graph    createjtfgraph / createjtjgraph (:2969-2994, :2833-2867): per edge,
+//                  scattered to the edge's vertices with atomics as the reference does
+//                  (Image:atomicAddChannel, backend_cuda.t:751-759)
+// Reads outside the index space are zero (Image:get, o.t:856-862); centred residuals are
+// wrapped in their bounding-box test at classification time.
+#include "codegen.h"
+#include <cstdio>
+#include <functional>
+#include <map>
+#include <set>
+#include <sstream>
+#include "reduce_dev_src.h"
+
+#define OPTAMD_STR2(...) #__VA_ARGS__
+#define OPTAMD_STR(x) OPTAMD_STR2(x)
+
+namespace optamd {
+namespace gen {
+namespace {
+
+std::string lit(double v) {
+    char b[64];
+    snprintf(b, sizeof(b), "%.17g", v);
+    std::string s = b;
+    if (s.find_first_of(".eEn") == std::string::npos) s += ".0";
+    return "((T)" + s + ")";
+}
+
+const char* elem_type(const std::string& e, bool unknown) {
+    if (unknown) return "T";
+    if (e == "uint8") return "unsigned char";
+    if (e == "int") return "int";
+    return "float";
+}
+
+// One kernel body's emitter: every pool node becomes at most one local temporary.
+class Body {
+public:
+    Body(GModel& m, std::ostringstream& o, int ndims, const std::vector<int>& unk_slot)
+        : M_(m), P_(m.pool), o_(o), nd_(ndims), uslot_(unk_slot) {}
+
+    std::string v(int id) {
+        auto it = done_.find(id);
+        if (it != done_.end()) return it->second;
+        const Node n = P_.at(id);
+        std::string e;
+        switch (n.op) {
+            case Op::Const: done_[id] = lit(n.c); return done_[id];
+            case Op::Param: e = "(T)a.prm[" + std::to_string(n.i) + "]"; break;
+            case Op::Read: e = read(n, nullptr); break;
+            case Op::InBox: e = "(T)(" + inbox(n.off, n.off2) + ")"; break;
+            case Op::Coord: e = "(T)(" + std::string(1, "xyz"[n.i]) + " + " + std::to_string(n.off[n.i]) + ")"; break;
+            case Op::Add: e = v(n.a) + " + " + v(n.b); break;
+            case Op::Sub: e = v(n.a) + " - " + v(n.b); break;
+            case Op::Mul: e = v(n.a) + " * " + v(n.b); break;
+            case Op::Div: e = v(n.a) + " / " + v(n.b); break;
+            case Op::Neg: e = "-" + v(n.a); break;
+            case Op::Sqrt: e = "sqrt(" + v(n.a) + ")"; break;
+            case Op::Sin: e = "sin(" + v(n.a) + ")"; break;
+            case Op::Cos: e = "cos(" + v(n.a) + ")"; break;
+            case Op::Exp: e = "exp(" + v(n.a) + ")"; break;
+            case Op::Log: e = "log(" + v(n.a) + ")"; break;
+            case Op::Abs: e = "fabs(" + v(n.a) + ")"; break;
+            case Op::Pow: e = "pow(" + v(n.a) + ", " + v(n.b) + ")"; break;
+            case Op::Select: e = "(" + v(n.a) + " != (T)0) ? " + v(n.b) + " : " + v(n.d); break;
+            case Op::Lt: e = "(T)(" + v(n.a) + " < " + v(n.b) + ")"; break;
+            case Op::Le: e = "(T)(" + v(n.a) + " <= " + v(n.b) + ")"; break;
+            case Op::Gt: e = "(T)(" + v(n.a) + " > " + v(n.b) + ")"; break;
+            case Op::Ge: e = "(T)(" + v(n.a) + " >= " + v(n.b) + ")"; break;
+            case Op::Eq: e = "(T)(" + v(n.a) + " == " + v(n.b) + ")"; break;
+            case Op::Ne: e = "(T)(" + v(n.a) + " != " + v(n.b) + ")"; break;
+            case Op::And: e = "(T)((" + v(n.a) + " != (T)0) && (" + v(n.b) + " != (T)0))"; break;
+            case Op::Or: e = "(T)((" + v(n.a) + " != (T)0) || (" + v(n.b) + " != (T)0))"; break;
+            case Op::Not: e = "(T)(" + v(n.a) + " == (T)0)"; break;
+        }
+        const std::string name = "t" + std::to_string(id);
+        o_ << "        const T " << name << " = " << e << ";\n";
+        done_[id] = name;
+        return name;
+    }
+    // the search direction / step vector at unknown access `u` (a Read of an unknown)
+    std::string vec(int u, const char* vname) {
+        const std::string key = std::string(vname) + std::to_string(u);
+        auto it = vdone_.find(key);
+        if (it != vdone_.end()) return it->second;
+        const Node n = P_.at(u);
+        const std::string name = std::string(vname) + "_" + std::to_string(u);
+        o_ << "        const T " << name << " = " << read(n, vname) << ";\n";
+        vdone_[key] = name;
+        return name;
+    }
+    void line(const std::string& s) { o_ << "        " << s << "\n"; }
+
+private:
+    std::string coord(int k, int off) const {
+        const char c = "xyz"[k];
+        return off == 0 ? std::string(1, c) : "(" + std::string(1, c) + (off > 0 ? " + " : " - ") +
+                                                   std::to_string(off > 0 ? off : -off) + ")";
+    }
+    std::string inb(const int* off) const {
+        std::string s;
+        for (int k = 0; k < nd_; ++k) {
+            if (off[k] == 0) continue;   // the thread's own coordinate is always inside
+            if (!s.empty()) s += " && ";
+            const char* dim = k == 0 ? "W" : k == 1 ? "H" : "D";
+            s += coord(k, off[k]) + " >= 0 && " + coord(k, off[k]) + " < " + dim;
+        }
+        return s.empty() ? "true" : s;
+    }
+    std::string inbox(const int* lo, const int* hi) const {
+        return "(" + inb(lo) + ") && (" + inb(hi) + ")";
+    }
+    std::string lin(const int* off) const {
+        if (nd_ == 1) return "(long long)" + coord(0, off[0]);
+        if (nd_ == 2) return "((long long)" + coord(1, off[1]) + " * W + " + coord(0, off[0]) + ")";
+        return "(((long long)" + coord(2, off[2]) + " * H + " + coord(1, off[1]) + ") * W + " + coord(0, off[0]) + ")";
+    }
+    std::string read(const Node& n, const char* vname) {
+        const GImage& im = M_.images[n.i];
+        const std::string ch = std::to_string(im.channels), c = std::to_string(n.ch);
+        std::string base, idx;
+        if (vname) {
+            base = std::string(vname) + " + a.uoff[" + std::to_string(uslot_[n.i]) + "]";
+        } else {
+            base = "((const " + std::string(elem_type(im.elem, im.unknown)) + "*)a.img[" + std::to_string(n.i) + "])";
+        }
+        if (n.slot >= 0) {
+            idx = "(long long)v" + std::to_string(n.slot) + " * " + ch + " + " + c;
+            return "(T)(" + base + ")[" + idx + "]";
+        }
+        idx = lin(n.off) + " * " + ch + " + " + c;
+        return "((" + inb(n.off) + ") ? (T)(" + base + ")[" + idx + "] : (T)0)";
+    }
+
+    GModel& M_;
+    Pool& P_;
+    std::ostringstream& o_;
+    int nd_;
+    const std::vector<int>& uslot_;
+    std::map<int, std::string> done_;
+    std::map<std::string, std::string> vdone_;
+};
+
+struct Instance {   // a centred residual shifted so that it contains unknown (image, ch) at 0
+    int res;
+    int s[3];
+};
+
+}  // namespace
+
+GenSource generate(GModel& m, bool dbl) {
+    GenSource gs;
+    Pool& P = m.pool;
+    const int nd = m.unknown_dims();
+    const std::vector<int> unk = m.unknown_images();
+    std::vector<int> uslot(m.images.size(), -1);
+    for (size_t k = 0; k < unk.size(); ++k) uslot[unk[k]] = (int)k;
+    int sb = 0;
+    for (size_t g = 0; g < m.graphs.size() && g < 4; ++g) {
+        gs.slot_base[g] = sb;
+        sb += (int)m.graphs[g].slot_names.size();
+    }
+    for (auto& r : m.residuals) (r.graph < 0 ? gs.has_centered : gs.has_graph) = true;
+
+    std::ostringstream o;
+    o << "// generated by opt_amd's energy front end (gen/codegen.cpp)\n";
+    o << "typedef " << (dbl ? "double" : "float") << " T;\n";
+    o << OPTAMD_STR(OPTAMD_GENARGS_BODY) << "\n";
+    o << kReduceDevSrc << "\n";
+    o << "#define OPT_COORDS const int W = a.dims[0], H = a.dims[1], D = a.dims[2]; (void)D;\n";
+    const char* coords =
+        "        const int x = (int)(lin % W); const int y = (int)((lin / W) % H); const int z = (int)(lin / ((long long)W * H));\n"
+        "        (void)x; (void)y; (void)z;\n";
+
+    // centred instances per output (unknown image, channel)
+    std::map<std::pair<int, int>, std::vector<std::pair<Instance, int>>> inst;   // -> (instance, support node)
+    for (size_t ri = 0; ri < m.residuals.size(); ++ri) {
+        const GResidual& r = m.residuals[ri];
+        if (r.graph >= 0) continue;
+        for (int u : r.unknowns) {
+            const Node& n = P.at(u);
+            Instance I{(int)ri, {-n.off[0], -n.off[1], -n.off[2]}};
+            inst[{n.i, n.ch}].push_back({I, u});
+        }
+    }
+    auto shifted = [&](int id, const int* s) { return P.shift(id, s); };
+    const int zero3[3] = {0, 0, 0};
+
+    // ---------------------------------------------------------------- gen_jtf
+    {
+        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_jtf(GenArgs a, T* __restrict__ r, T* __restrict__ diag) {\n"
+             "    OPT_COORDS\n"
+             "    for (long long lin = (long long)blockIdx.x * 256 + threadIdx.x; lin < a.npix; lin += (long long)gridDim.x * 256) {\n"
+          << coords;
+        Body b(m, o, nd, uslot);
+        const std::string act = m.exclude >= 0 ? "(" + b.v(m.exclude) + " == (T)0)" : "true";
+        b.line("const bool act = " + act + ";");
+        b.line("a.flags[lin] = act ? 1 : 0;");
+        for (int k : unk) {
+            const GImage& im = m.images[k];
+            for (int c = 0; c < im.channels; ++c) {
+                std::vector<std::string> F, Dg;
+                for (auto& ent : inst[{k, c}]) {
+                    const GResidual& r = m.residuals[ent.first.res];
+                    const int R = shifted(r.expr, ent.first.s);
+                    const int g = shifted(P.diff(r.expr, ent.second), ent.first.s);
+                    if (P.is_const(g)) {
+                        double gv;
+                        P.is_const(g, &gv);
+                        if (gv == 0.0) continue;
+                    }
+                    const std::string gn = b.v(g), rn = b.v(R);
+                    F.push_back(gn + " * " + rn);
+                    Dg.push_back(gn + " * " + gn);
+                }
+                const std::string e = "a.uoff[" + std::to_string(uslot[k]) + "] + lin * " + std::to_string(im.channels) +
+                                      " + " + std::to_string(c);
+                std::string fs = "(T)0", ds = "(T)0";
+                for (auto& t : F) fs += " + " + t;
+                for (auto& t : Dg) ds += " + " + t;
+                b.line("{ const T F = " + fs + "; const T Dg = " + ds + ";");
+                b.line("  r[" + e + "] = act ? -F : (T)0; diag[" + e + "] = Dg; }");
+            }
+        }
+        o << "    }\n}\n";
+    }
+
+    // -------------------------------------------------------------- gen_apply
+    {
+        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_apply(GenArgs a, const T* __restrict__ p, T* __restrict__ Ap,\n"
+             "        const T* __restrict__ dadd, const int* stop, ReduceSlot rs, int finish) {\n"
+             "    if (stop && *stop) return;\n"
+             "    OPT_COORDS\n"
+             "    T dot = 0;\n"
+             "    for (long long lin = (long long)blockIdx.x * 256 + threadIdx.x; lin < a.npix; lin += (long long)gridDim.x * 256) {\n"
+          << coords;
+        Body b(m, o, nd, uslot);
+        b.line("const bool act = (a.flags[lin] & 1) != 0;");
+        std::map<std::string, std::string> jp;   // (residual, shift) -> J p of that instance
+        for (int k : unk) {
+            const GImage& im = m.images[k];
+            for (int c = 0; c < im.channels; ++c) {
+                std::vector<std::string> terms;
+                for (auto& ent : inst[{k, c}]) {
+                    const GResidual& r = m.residuals[ent.first.res];
+                    const int* s = ent.first.s;
+                    const int g = shifted(P.diff(r.expr, ent.second), s);
+                    double gv;
+                    if (P.is_const(g, &gv) && gv == 0.0) continue;
+                    const std::string key = std::to_string(ent.first.res) + ":" + std::to_string(s[0]) + "," +
+                                            std::to_string(s[1]) + "," + std::to_string(s[2]);
+                    if (!jp.count(key)) {
+                        std::string sum = "(T)0";
+                        for (int u : r.unknowns) {
+                            const int gu = shifted(P.diff(r.expr, u), s);
+                            if (P.is_const(gu, &gv) && gv == 0.0) continue;
+                            sum += " + " + b.v(gu) + " * " + b.vec(shifted(u, s), "p");
+                        }
+                        const std::string nm = "jp" + std::to_string(jp.size());
+                        b.line("const T " + nm + " = " + sum + ";");
+                        jp[key] = nm;
+                    }
+                    terms.push_back(b.v(g) + " * " + jp[key]);
+                }
+                const std::string e = "a.uoff[" + std::to_string(uslot[k]) + "] + lin * " + std::to_string(im.channels) +
+                                      " + " + std::to_string(c);
+                std::string acc = "(T)0";
+                for (auto& t : terms) acc += " + " + t;
+                b.line("{ const long long e = " + e + "; const T acc = " + acc + ";");
+                b.line("  if (finish) { const T pe = p[e]; const T o = act ? acc + (dadd ? dadd[e] * pe : (T)0) : (T)0; Ap[e] = o; dot += pe * o; }");
+                b.line("  else Ap[e] = acc; }");
+            }
+        }
+        o << "    }\n"
+             "    if (finish) { double v[1] = {(double)dot}; block_reduce_publish<1>(v, rs, blockIdx.x); }\n}\n";
+    }
+
+    // ------------------------------------------------------- cost (centres + edges)
+    {
+        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_cost(GenArgs a, const T* __restrict__ delta, ReduceSlot rs) {\n"
+             "    OPT_COORDS\n"
+             "    T acc = 0;\n";
+        if (gs.has_centered) {
+            o << "    for (long long lin = (long long)blockIdx.x * 256 + threadIdx.x; lin < a.npix; lin += (long long)gridDim.x * 256) {\n"
+              << coords;
+            Body b(m, o, nd, uslot);
+            if (m.exclude >= 0) b.line("if (" + b.v(m.exclude) + " != (T)0) continue;");
+            std::string sum = "(T)0", msum = "(T)0";
+            for (auto& r : m.residuals) {
+                if (r.graph >= 0) continue;
+                const std::string R = b.v(r.expr);
+                sum += " + " + R + " * " + R;
+            }
+            b.line("T s = " + sum + ";");
+            b.line("if (delta) {");
+            {
+                int idx = 0;
+                std::string ms = "(T)0";
+                for (auto& r : m.residuals) {
+                    if (r.graph >= 0) continue;
+                    std::string e = b.v(r.expr);
+                    for (int u : r.unknowns) {
+                        const int gu = P.diff(r.expr, u);
+                        double gv;
+                        if (P.is_const(gu, &gv) && gv == 0.0) continue;
+                        e += " + " + b.v(gu) + " * " + b.vec(u, "delta");
+                    }
+                    b.line("  const T m" + std::to_string(idx) + " = " + e + ";");
+                    ms += " + m" + std::to_string(idx) + " * m" + std::to_string(idx);
+                    ++idx;
+                }
+                b.line("  s = " + ms + ";");
+            }
+            b.line("}");
+            b.line("acc += (T)0.5 * s;");
+            o << "    }\n";
+        }
+        for (size_t g = 0; g < m.graphs.size(); ++g) {
+            bool any = false;
+            for (auto& r : m.residuals) any |= r.graph == (int)g;
+            if (!any) continue;
+            o << "    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < a.nedge[" << g
+              << "]; e += (long long)gridDim.x * 256) {\n";
+            for (size_t s = 0; s < m.graphs[g].slot_names.size(); ++s)
+                o << "        const int v" << s << " = a.slot[" << gs.slot_base[g] + s << "][e];\n";
+            Body b(m, o, nd, uslot);
+            std::string sum = "(T)0";
+            int idx = 0;
+            for (auto& r : m.residuals) {
+                if (r.graph != (int)g) continue;
+                std::string e = b.v(r.expr);
+                b.line("T q" + std::to_string(idx) + " = " + e + ";");
+                sum += " + q" + std::to_string(idx) + " * q" + std::to_string(idx);
+                ++idx;
+            }
+            b.line("if (delta) {");
+            idx = 0;
+            for (auto& r : m.residuals) {
+                if (r.graph != (int)g) continue;
+                std::string e;
+                for (int u : r.unknowns) {
+                    const int gu = P.diff(r.expr, u);
+                    double gv;
+                    if (P.is_const(gu, &gv) && gv == 0.0) continue;
+                    e += " + " + b.v(gu) + " * " + b.vec(u, "delta");
+                }
+                if (!e.empty()) b.line("  q" + std::to_string(idx) + " = q" + std::to_string(idx) + e + ";");
+                ++idx;
+            }
+            b.line("}");
+            b.line("acc += (T)0.5 * (" + sum + ");");
+            o << "    }\n";
+        }
+        o << "    double v[1] = {(double)acc};\n    block_reduce_publish<1>(v, rs, blockIdx.x);\n}\n";
+    }
+
+    // ------------------------------------------------------------ graph scatters
+    {
+        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_jtf_graph(GenArgs a, T* __restrict__ r, T* __restrict__ diag) {\n"
+             "    OPT_COORDS\n";
+        for (size_t g = 0; g < m.graphs.size(); ++g) {
+            o << "    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < a.nedge[" << g
+              << "]; e += (long long)gridDim.x * 256) {\n";
+            for (size_t s = 0; s < m.graphs[g].slot_names.size(); ++s)
+                o << "        const int v" << s << " = a.slot[" << gs.slot_base[g] + s << "][e];\n";
+            Body b(m, o, nd, uslot);
+            for (auto& r : m.residuals) {
+                if (r.graph != (int)g) continue;
+                const std::string R = b.v(r.expr);
+                for (int u : r.unknowns) {
+                    const int gu = P.diff(r.expr, u);
+                    double gv;
+                    if (P.is_const(gu, &gv) && gv == 0.0) continue;
+                    const Node& n = P.at(u);
+                    const std::string gn = b.v(gu);
+                    const std::string idx = "a.uoff[" + std::to_string(uslot[n.i]) + "] + (long long)v" + std::to_string(n.slot) +
+                                            " * " + std::to_string(m.images[n.i].channels) + " + " + std::to_string(n.ch);
+                    b.line("atomicAdd(&r[" + idx + "], -(" + gn + " * " + R + ")); atomicAdd(&diag[" + idx + "], " + gn + " * " + gn + ");");
+                }
+            }
+            o << "    }\n";
+        }
+        o << "}\n";
+        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_apply_graph(GenArgs a, const T* __restrict__ p, T* __restrict__ Ap, const int* stop) {\n"
+             "    if (stop && *stop) return;\n"
+             "    OPT_COORDS\n";
+        for (size_t g = 0; g < m.graphs.size(); ++g) {
+            o << "    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < a.nedge[" << g
+              << "]; e += (long long)gridDim.x * 256) {\n";
+            for (size_t s = 0; s < m.graphs[g].slot_names.size(); ++s)
+                o << "        const int v" << s << " = a.slot[" << gs.slot_base[g] + s << "][e];\n";
+            Body b(m, o, nd, uslot);
+            int idx = 0;
+            for (auto& r : m.residuals) {
+                if (r.graph != (int)g) continue;
+                std::string sum = "(T)0";
+                std::vector<std::pair<int, std::string>> gs_;
+                for (int u : r.unknowns) {
+                    const int gu = P.diff(r.expr, u);
+                    double gv;
+                    if (P.is_const(gu, &gv) && gv == 0.0) continue;
+                    const std::string gn = b.v(gu);
+                    sum += " + " + gn + " * " + b.vec(u, "p");
+                    gs_.push_back({u, gn});
+                }
+                const std::string jn = "jp" + std::to_string(idx++);
+                b.line("const T " + jn + " = " + sum + ";");
+                for (auto& ug : gs_) {
+                    const Node& n = P.at(ug.first);
+                    const std::string id = "a.uoff[" + std::to_string(uslot[n.i]) + "] + (long long)v" + std::to_string(n.slot) +
+                                           " * " + std::to_string(m.images[n.i].channels) + " + " + std::to_string(n.ch);
+                    b.line("atomicAdd(&Ap[" + id + "], " + ug.second + " * " + jn + ");");
+                }
+            }
+            o << "    }\n";
+        }
+        o << "}\n";
+    }
+
+    // ------------------------------------------------- finishing passes (graphs)
+    {
+        // element -> pixel of the unknown vector
+        std::string pix = "        long long px;\n";
+        for (size_t k = 0; k < unk.size(); ++k) {
+            const int ch = m.images[unk[k]].channels;
+            pix += "        " + std::string(k ? "else " : "") + (k + 1 < unk.size() ? "if (i < a.uoff[" + std::to_string(k + 1) + "]) " : "") +
+                   "px = (i - a.uoff[" + std::to_string(k) + "]) / " + std::to_string(ch) + ";\n";
+        }
+        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_finish(GenArgs a, const T* __restrict__ p, T* __restrict__ Ap,\n"
+             "        const T* __restrict__ dadd, const int* stop, ReduceSlot rs, long long n) {\n"
+             "    if (stop && *stop) return;\n"
+             "    T dot = 0;\n"
+             "    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {\n"
+          << pix
+          << "        const T pe = p[i];\n"
+             "        const T o = (a.flags[px] & 1) ? Ap[i] + (dadd ? dadd[i] * pe : (T)0) : (T)0;\n"
+             "        Ap[i] = o;\n"
+             "        dot += pe * o;\n"
+             "    }\n"
+             "    double v[1] = {(double)dot};\n    block_reduce_publish<1>(v, rs, blockIdx.x);\n}\n";
+        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_finish_jtf(GenArgs a, T* __restrict__ r, long long n) {\n"
+             "    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {\n"
+          << pix
+          << "        if (!(a.flags[px] & 1)) r[i] = (T)0;\n"
+             "    }\n}\n";
+    }
+    (void)zero3;
+    gs.code = o.str();
+    return gs;
+}
+
+}  // namespace gen
+}  // namespace optamd

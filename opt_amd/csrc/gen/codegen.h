@@ -1,0 +1,37 @@
+// gen/codegen.h — HIP source for a lowered energy (the role of the reference's
+// createjtfcentered / createjtjcentered / createjtfgraph / createjtjgraph / createcost /
+// createmodelcost, o.t:2770-3129, and of the Terra emitter, o.t:1949-2665).
+#pragma once
+#include <string>
+#include "model.h"
+
+// Kernel argument block shared by the host (generic.hip) and the generated source: the
+// macro body is compiled on the host and pasted, stringised, into the generated code.
+#define OPTAMD_GENARGS_BODY                                                                 \
+    struct GenArgs {                                                                        \
+        int dims[3];                /* unknowns' index space, unused dims = 1 */            \
+        long long npix;             /* elements of that space */                            \
+        const void* img[16];        /* by image id: unknowns (T) and known arrays */        \
+        float prm[32];              /* by parameter id */                                   \
+        const int* slot[16];        /* graph vertex arrays, graph-major */                  \
+        int nedge[4];               /* edges per graph */                                   \
+        unsigned char* flags;       /* bit0: active (not excluded) */                       \
+        long long uoff[4];          /* offset of each unknown image in the vector */        \
+    };
+
+namespace optamd {
+OPTAMD_GENARGS_BODY
+namespace gen {
+
+struct GenSource {
+    std::string code;
+    bool has_centered = false;   // centred residuals present
+    bool has_graph = false;      // graph residuals present
+    int slot_base[4] = {0, 0, 0, 0};   // GenArgs::slot index of graph g's first vertex array
+};
+
+// Generate the kernels for `m` in float (dbl = false) or double.
+GenSource generate(GModel& m, bool dbl);
+
+}  // namespace gen
+}  // namespace optamd

@@ -84,7 +84,18 @@ Opt_Problem* Opt_ProblemDefine(Opt_State* state, const char* filename, const cha
     p->spec.filename = filename;
     p->spec.solverkind = kind;
     std::string err;
-    if (!optamd::parse_energy(ss.str(), &p->spec, &err) || !optamd::classify(&p->spec, &err)) {
+    bool ok = optamd::parse_energy(ss.str(), &p->spec, &err) && optamd::classify(&p->spec, &err);
+    // energies no hand-written family recognises (or all, with OPT_AMD_GENERIC=1) go to the
+    // general front end
+    if (!ok || optamd::env_int("OPT_AMD_GENERIC", 0)) {
+        std::string gerr;
+        if (optamd::generic_accepts(ss.str(), &p->spec, &gerr)) {
+            ok = true;
+        } else if (!ok) {
+            err += "; general front end: " + gerr;
+        }
+    }
+    if (!ok) {
         fprintf(stderr, "[opt_amd] %s\n", err.c_str());
         delete p;
         return nullptr;
@@ -360,3 +371,33 @@ int OptAMD_CsrSpMV(int nRowsA, int nColsA, long long nnz, const int* rowPtrA, co
 }
 
 }  // extern "C"
+
+static bool read_file(const char* filename, std::string* text) {
+    std::ifstream in(filename ? filename : "");
+    if (!in.good()) return false;
+    std::stringstream ss;
+    ss << in.rdbuf();
+    *text = ss.str();
+    return true;
+}
+int OptAMD_GenericSource(const char* filename, int doublePrecision, char* buf, int n) {
+    std::string text, out;
+    if (!read_file(filename, &text)) return copy_name("cannot read energy file", buf, n), -1;
+    const int r = optamd::generic_source(text, doublePrecision != 0, &out);
+    copy_name(out, buf, n);
+    return r;
+}
+int OptAMD_GenericCompileCheck(const char* filename, int doublePrecision, char* buf, int n) {
+    std::string text, log;
+    if (!read_file(filename, &text)) return copy_name("cannot read energy file", buf, n), -1;
+    const int r = optamd::generic_compile_check(text, doublePrecision != 0, &log);
+    copy_name(log, buf, n);
+    return r;
+}
+int OptAMD_GenericDescribe(const char* filename, char* buf, int n) {
+    std::string text, out;
+    if (!read_file(filename, &text)) return copy_name("cannot read energy file", buf, n), -1;
+    const int r = optamd::generic_describe(text, &out);
+    copy_name(out, buf, n);
+    return r;
+}

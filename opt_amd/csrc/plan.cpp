@@ -151,6 +151,7 @@ std::unique_ptr<Plan> make_plan(const ProblemSpec& spec, const StateOptions& opt
     if (spec.family == "optical_flow") return make_optical_flow_plan(spec, opts, dims, err);
     if (spec.family == "shape_from_shading") return make_sfs_plan(spec, opts, dims, err);
     if (spec.family == "arap_mesh_deformation") return make_arap_plan(spec, opts, dims, err);
+    if (spec.family == "generic") return make_generic_plan(spec, opts, dims, err);
     *err = "energy family '" + spec.family + "' has no kernels in this build";
     return nullptr;
 }

@@ -162,6 +162,9 @@ std::unique_ptr<Plan> make_sfs_plan(const ProblemSpec&, const StateOptions&, con
 std::unique_ptr<Plan> make_arap_plan(const ProblemSpec&, const StateOptions&, const unsigned* dims,
                                      std::string* err);
 
+std::unique_ptr<Plan> make_generic_plan(const ProblemSpec&, const StateOptions&, const unsigned* dims,
+                                        std::string* err);
+
 // Device-memory helpers (fail-stop).
 void* dmalloc(size_t bytes);
 void dfree(void* p);

@@ -46,6 +46,8 @@ struct ProblemSpec {
     std::vector<std::string> ops;     // DSL operators seen (Rotate2D, Stencil, ...)
     std::string family;               // set by classify()
     int n_params_total = 0;           // highest declared index + 1
+    std::string text;                 // the energy file (family "generic": re-lowered per plan)
+    std::vector<unsigned> dim_values; // generic plans: Opt_ProblemPlan's dimensions
 
     bool uses_op(const std::string& op) const;
     const DeclImage* unknown(int i) const;   // i-th unknown by declared index order
@@ -59,5 +61,10 @@ struct ProblemSpec {
 bool parse_energy(const std::string& text, ProblemSpec* spec, std::string* err);
 // Decide which kernel family lowers this energy; false + message if none.
 bool classify(ProblemSpec* spec, std::string* err);
+// General front end (generic.hip): accept any energy gen/ lowers; sets family "generic".
+bool generic_accepts(const std::string& text, ProblemSpec* spec, std::string* err);
+int generic_source(const std::string& text, bool dbl, std::string* out);
+int generic_describe(const std::string& text, std::string* out);
+int generic_compile_check(const std::string& text, bool dbl, std::string* log);
 
 }  // namespace optamd

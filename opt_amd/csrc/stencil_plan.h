@@ -9,21 +9,28 @@
 
 namespace optamd {
 
+// Device pointers of the unknown images (VecLayout order).
+template <typename T>
+struct UnknownPtrs {
+    T* x[4];
+};
+
 // X += delta on the active pixels (PCGLinearUpdate, :854-859); LM also keeps the
 // previous unknowns (savePreviousUnknowns :882-887) for revertUpdate (:864-869).
 template <typename T, bool SAVE>
 __global__ __launch_bounds__(kBlock) void update_images_kernel(VecLayout L, const uint8_t* __restrict__ flags,
-                                                               T* x0, T* x1, const T* __restrict__ delta,
+                                                               UnknownPtrs<T> X, const T* __restrict__ delta,
                                                                T* __restrict__ prev, long long pix_lo,
                                                                long long pix_hi) {
     const long long n = L.off[L.nimg];
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
-        const int k = (L.nimg > 1 && e >= L.off[1]) ? 1 : 0;
+        int k = 0;
+        while (k + 1 < L.nimg && e >= L.off[k + 1]) ++k;
         const long long local = e - L.off[k];
         const long long px = local / L.ch[k];
         if (px < pix_lo || px >= pix_hi || !(flags[px] & 1)) continue;
-        T* x = k ? x1 : x0;
+        T* x = X.x[k];
         const T v = x[local];
         if (SAVE) prev[e] = v;
         x[local] = v + delta[e];
@@ -31,16 +38,17 @@ __global__ __launch_bounds__(kBlock) void update_images_kernel(VecLayout L, cons
 }
 template <typename T>
 __global__ __launch_bounds__(kBlock) void revert_images_kernel(VecLayout L, const uint8_t* __restrict__ flags,
-                                                               T* x0, T* x1, const T* __restrict__ prev,
+                                                               UnknownPtrs<T> X, const T* __restrict__ prev,
                                                                long long pix_lo, long long pix_hi) {
     const long long n = L.off[L.nimg];
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
-        const int k = (L.nimg > 1 && e >= L.off[1]) ? 1 : 0;
+        int k = 0;
+        while (k + 1 < L.nimg && e >= L.off[k + 1]) ++k;
         const long long local = e - L.off[k];
         const long long px = local / L.ch[k];
         if (px < pix_lo || px >= pix_hi || !(flags[px] & 1)) continue;
-        (k ? x1 : x0)[local] = prev[e];
+        X.x[k][local] = prev[e];
     }
 }
 
@@ -451,15 +459,20 @@ private:
         else S2(false, false);
 #undef S2
     }
+    UnknownPtrs<T> unknowns() {
+        UnknownPtrs<T> X{};
+        for (int k = 0; k < L_.nimg && k < 4; ++k) X.x[k] = op_->unknown(k);
+        return X;
+    }
     void update(bool save) {
         tbegin("update");
         if (save)
             hipLaunchKernelGGL((update_images_kernel<T, true>), dim3(fg()), dim3(kBlock), 0, stream_, L_,
-                               (const uint8_t*)flags_, op_->unknown(0), op_->unknown(1), (const T*)delta_, prev_,
+                               (const uint8_t*)flags_, unknowns(), (const T*)delta_, prev_,
                                pix_lo(), pix_hi());
         else
             hipLaunchKernelGGL((update_images_kernel<T, false>), dim3(fg()), dim3(kBlock), 0, stream_, L_,
-                               (const uint8_t*)flags_, op_->unknown(0), op_->unknown(1), (const T*)delta_, prev_,
+                               (const uint8_t*)flags_, unknowns(), (const T*)delta_, prev_,
                                pix_lo(), pix_hi());
         OPT_HIP_CHECK(hipGetLastError());
         tend();
@@ -467,7 +480,7 @@ private:
     }
     void revert() {
         hipLaunchKernelGGL((revert_images_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, L_,
-                           (const uint8_t*)flags_, op_->unknown(0), op_->unknown(1), (const T*)prev_, pix_lo(),
+                           (const uint8_t*)flags_, unknowns(), (const T*)prev_, pix_lo(),
                            pix_hi());
         OPT_HIP_CHECK(hipGetLastError());
         exchange_unknowns();

@@ -61,9 +61,9 @@ def test_define_rejects_bad_input(tmp_path):
     assert not pr
     bad = tmp_path / "bad.t"
     bad.write_text('local W,H = Dim("W",0), Dim("H",1)\nlocal X = Unknown("X", opt_float,{W,H},0)\n'
-                   'Energy(X(0,0)*X(0,0))\n')
+                   'Energy(X(0,0)*X(0,0) +)\n')
     lib, st, pr = _define(str(bad))
-    assert not pr  # not a family this runtime lowers: nil, as problemPlan on error
+    assert not pr  # neither a family nor a lowerable energy: nil, as problemPlan on error
     lib, st, pr = _define(str(tmp_path / "missing.t"), kind="notASolver")
     assert not pr
 
