@@ -136,7 +136,7 @@ private:
         if (vname) {
             base = std::string(vname) + " + a.uoff[" + std::to_string(uslot_[n.i]) + "]";
         } else {
-            base = "((const " + std::string(elem_type(im.elem, im.unknown)) + "*)a.img[" + std::to_string(n.i) + "])";
+            base = "((const " + std::string(elem_type(im.elem, im.tvalued)) + "*)a.img[" + std::to_string(n.i) + "])";
         }
         if (n.slot >= 0) {
             idx = "(long long)v" + std::to_string(n.slot) + " * " + ch + " + " + c;
@@ -199,6 +199,27 @@ GenSource generate(GModel& m, bool dbl) {
     }
     auto shifted = [&](int id, const int* s) { return P.shift(id, s); };
     const int zero3[3] = {0, 0, 0};
+
+    // --------------------------------------------- gen_precompute_<k> (ComputedArrays)
+    // One kernel per ComputedArray, launched in declaration order (a later one may read an
+    // earlier one at an offset): the values and the non-constant gradient images
+    // (createprecomputed, o.t:3131-3153).
+    for (size_t k = 0; k < m.computed.size(); ++k) {
+        const GComputed& c = m.computed[k];
+        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_precompute_" << k << "(GenArgs a) {\n"
+             "    OPT_COORDS\n"
+             "    for (long long lin = (long long)blockIdx.x * 256 + threadIdx.x; lin < a.npix; lin += (long long)gridDim.x * 256) {\n"
+          << coords;
+        Body b(m, o, nd, uslot);
+        const int nch = (int)c.expr.size();
+        for (int ch = 0; ch < nch; ++ch)
+            b.line("((T*)a.img[" + std::to_string(c.image) + "])[lin * " + std::to_string(nch) + " + " + std::to_string(ch) +
+                   "] = " + b.v(c.expr[ch]) + ";");
+        for (const GGrad& g : c.grads)
+            if (g.gimg >= 0) b.line("((T*)a.img[" + std::to_string(g.gimg) + "])[lin] = " + b.v(g.expr) + ";");
+        o << "    }\n}\n";
+    }
+    gs.n_precompute = (int)m.computed.size();
 
     // ---------------------------------------------------------------- gen_jtf
     {

@@ -28,6 +28,7 @@ struct GenSource {
     bool has_centered = false;   // centred residuals present
     bool has_graph = false;      // graph residuals present
     int slot_base[4] = {0, 0, 0, 0};   // GenArgs::slot index of graph g's first vertex array
+    int n_precompute = 0;              // kernels gen_precompute_0 .. n-1 (ComputedArrays)
 };
 
 // Generate the kernels for `m` in float (dbl = false) or double.

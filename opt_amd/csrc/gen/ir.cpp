@@ -177,7 +177,16 @@ int Pool::diff(int id, int var) {
     const Node n = nodes_[id];   // copy: the pool may grow below
     int r;
     switch (n.op) {
-        case Op::Read: r = cnst(id == var ? 1.0 : 0.0); break;
+        case Op::Read: {
+            r = cnst(id == var ? 1.0 : 0.0);
+            auto it = comp_.find(n.i);
+            if (it != comp_.end() && n.slot < 0) {   // chain rule through a ComputedArray
+                r = cnst(0.0);
+                for (const auto& e : it->second)
+                    if (e[0] == n.ch && shift(e[1], n.off) == var) r = bin(Op::Add, r, shift(e[2], n.off));
+            }
+            break;
+        }
         case Op::Add: r = bin(Op::Add, diff(n.a, var), diff(n.b, var)); break;
         case Op::Sub: r = bin(Op::Sub, diff(n.a, var), diff(n.b, var)); break;
         case Op::Neg: r = un(Op::Neg, diff(n.a, var)); break;

@@ -8,6 +8,7 @@
 // subexpressions fall out of the pool), built with light algebraic simplification
 // (constant folding, 0 / 1 identities) and differentiated symbolically.
 #pragma once
+#include <array>
 #include <cstdint>
 #include <map>
 #include <string>
@@ -70,11 +71,17 @@ public:
             st.pop_back();
             if (n < 0 || seen[n]) continue;
             seen[n] = 1;
-            f(n, nodes_[n]);
-            for (int c : {nodes_[n].a, nodes_[n].b, nodes_[n].d}) st.push_back(c);
+            const Node nd = nodes_[n];   // copy: f may grow the pool
+            f(n, nd);
+            for (int c : {nd.a, nd.b, nd.d}) st.push_back(c);
         }
     }
     std::string str(int id) const;
+    // Register d(image ch)/d(u) = gnode for a ComputedArray image (ImageAccess:gradient,
+    // o.t:1551-1562): diff() of a read of that image at offset o yields gnode shifted by o
+    // for the unknown access u shifted by o.
+    void add_computed_grad(int image, int ch, int u, int gnode) { comp_[image].push_back({ch, u, gnode}); }
+    const std::map<int, std::vector<std::array<int, 3>>>& computed_grads() const { return comp_; }
 
 private:
     int intern(const Node& n);
@@ -82,6 +89,7 @@ private:
     std::unordered_map<std::string, int> index_;
     std::map<std::pair<int, int>, int> dmemo_;
     std::map<std::pair<int, std::string>, int> smemo_;
+    std::map<int, std::vector<std::array<int, 3>>> comp_;   // image -> (ch, u, gnode)
 };
 
 }  // namespace gen

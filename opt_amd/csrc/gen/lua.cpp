@@ -978,6 +978,7 @@ private:
         if (v.k != V::Dim) err("expected a Dim");
         return v.id;
     }
+    int lp_counter_ = 0;
     void note_index(int idx) { m_->n_params_total = std::max(m_->n_params_total, idx + 1); }
     int channels_of(const Value& t) {
         if (t.k == V::Type) return t.id;
@@ -993,12 +994,82 @@ private:
         for (auto& d : a[2].t->a) im.dims.push_back(dim_of(d));
         im.index = (int)a[3].n;
         im.unknown = unknown;
+        im.tvalued = unknown;
         note_index(im.index);
         m_->images.push_back(im);
         Value v;
         v.k = V::Image;
         v.id = (int)m_->images.size() - 1;
         return v;
+    }
+    // ProblemSpecAD:ComputedImage (o.t:1686-1718): a T-valued internal image holding exp,
+    // plus one gradient image per (channel, unknown access) whose derivative is not constant.
+    Value computed_array(VList& a) {
+        if (a.size() < 3 || a[1].k != V::Table) err("ComputedArray(name, {dims}, expression)");
+        GImage im;
+        im.name = a[0].s;
+        for (auto& d : a[1].t->a) im.dims.push_back(dim_of(d));
+        const std::vector<int> ex = as_expr(a[2]);
+        im.channels = (int)ex.size();
+        im.internal = im.tvalued = true;
+        m_->images.push_back(im);
+        const int id = (int)m_->images.size() - 1;
+        GComputed c;
+        c.image = id;
+        c.expr = ex;
+        bool bounds = false;
+        for (int e : ex)
+            P().visit(e, [&](int, const Node& n) {
+                if (n.op == Op::Read && n.slot < 0) {
+                    const GComputed* inner = computed_of(n.i);
+                    for (int k = 0; k < 3; ++k) {
+                        c.lo[k] = std::min(c.lo[k], n.off[k] + (inner ? inner->lo[k] : 0));
+                        c.hi[k] = std::max(c.hi[k], n.off[k] + (inner ? inner->hi[k] : 0));
+                    }
+                } else if (n.op == Op::InBox) {
+                    bounds = true;
+                }
+            });
+        if (bounds)
+            for (int k = 0; k < 3; ++k) c.lo[k] = c.hi[k] = 0;
+        for (int ch = 0; ch < (int)ex.size(); ++ch) {
+            std::set<int> unk;
+            P().visit(ex[ch], [&](int nid, const Node& n) {
+                if (n.op == Op::Read && m_->images[n.i].unknown) {
+                    if (n.slot >= 0) err("ComputedArray over a graph access is not supported (NYI in the reference)");
+                    unk.insert(nid);
+                }
+            });
+            for (int u : unk) {
+                GGrad g;
+                g.ch = ch;
+                g.u = u;
+                g.expr = P().diff(ex[ch], u);
+                int gnode = g.expr;
+                if (!P().is_const(g.expr)) {
+                    GImage gi;
+                    gi.name = im.name + "_d_" + std::to_string(u);
+                    gi.dims = m_->images[id].dims;
+                    gi.internal = gi.tvalued = true;
+                    m_->images.push_back(gi);
+                    g.gimg = (int)m_->images.size() - 1;
+                    const int z[3] = {0, 0, 0};
+                    gnode = P().read(g.gimg, 0, z);
+                }
+                P().add_computed_grad(id, ch, u, gnode);
+                c.grads.push_back(g);
+            }
+        }
+        m_->computed.push_back(c);
+        Value v;
+        v.k = V::Image;
+        v.id = id;
+        return v;
+    }
+    const GComputed* computed_of(int image) const {
+        for (auto& c : m_->computed)
+            if (c.image == image) return &c;
+        return nullptr;
     }
     Value image_access(int id, VList& a) {
         const GImage& im = m_->images[id];
@@ -1171,7 +1242,33 @@ void Interp::install() {
         return VList{};
     });
     def("Result", [](VList&) { return VList{}; });
-    for (const char* n : {"ComputedArray", "ComputedImage", "SampledImage", "L_p", "Slice"}) {
+    def("ComputedArray", [this](VList& a) { return VList{computed_array(a)}; });
+    def("ComputedImage", [this](VList& a) { return VList{computed_array(a)}; });
+    def("L_p", [this](VList& a) {   // lib.t:113-122
+        if (a.size() < 4) err("L_p(val, val_const, p, dims)");
+        const std::vector<int> vc = as_expr(a[1]);
+        int dot = P().cnst(0.0);
+        for (int c : vc) dot = P().bin(Op::Add, dot, P().bin(Op::Mul, c, c));
+        const int dist = P().un(Op::Sqrt, dot);
+        const int C = P().bin(Op::Pow, P().bin(Op::Add, dist, P().cnst(0.0000001)),
+                              P().bin(Op::Sub, comp(a[2], 0), P().cnst(2.0)));
+        VList ca{str("L_p" + std::to_string(++lp_counter_)), a[3], expr({P().un(Op::Sqrt, C)})};
+        Value im = computed_array(ca);
+        VList z;
+        for (size_t k = 0; k < m_->images[im.id].dims.size(); ++k) z.push_back(num(0));
+        return VList{zip(Op::Mul, image_access(im.id, z), a[0])};
+    });
+    def("Slice", [this](VList& a) {   // lib.t:70-82: channels [s, e) of an image access
+        if (a.size() < 3 || a[0].k != V::Image) err("Slice(image, s, e)");
+        const int id = a[0].id, s0 = (int)a[1].n, e0 = (int)a[2].n;
+        return VList{builtin([this, id, s0, e0](VList& args) {
+            const Value v = image_access(id, args);
+            std::vector<int> out;
+            for (int c = s0; c < e0; ++c) out.push_back(comp(v, c));
+            return VList{expr(out)};
+        })};
+    });
+    for (const char* n : {"SampledImage"}) {
         const std::string nm = n;
         def(nm, [this, nm](VList&) -> VList {
             unsupported(nm);
@@ -1301,6 +1398,12 @@ void Interp::install() {
 
 // Classify and finish the residual templates (classifyexpression + bbox, o.t:2669-2715).
 void Interp::finish() {
+    // an Array declared on an Unknown's parameter slot is a view of that unknown
+    // (intrinsic_image_decomposition's r_const): stored in the solver precision
+    for (auto& im : m_->images)
+        if (!im.unknown && !im.internal)
+            for (auto& u : m_->images)
+                if (u.unknown && u.index == im.index) im.tvalued = true;
     for (int e : energy_terms_) {
         GResidual r;
         bool any = false;
@@ -1314,6 +1417,15 @@ void Interp::finish() {
                 if (n.slot >= 0) {
                     if (graph >= 0 && graph != n.g) throw LuaError("residual reads from two graphs");
                     graph = n.g;
+                } else if (const GComputed* c = computed_of(n.i)) {
+                    // a ComputedArray read: its bbox moved by the access offset, and the
+                    // unknown accesses behind its gradient images (o.t:2683-2687, 1686-1700)
+                    for (int k = 0; k < 3; ++k) {
+                        lo[k] = std::min(lo[k], n.off[k] + c->lo[k]);
+                        hi[k] = std::max(hi[k], n.off[k] + c->hi[k]);
+                    }
+                    for (const GGrad& g : c->grads)
+                        if (g.ch == n.ch) unk.insert(P().shift(g.u, n.off));
                 } else {
                     for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], n.off[k]); hi[k] = std::max(hi[k], n.off[k]); }
                 }

@@ -22,6 +22,19 @@ struct GImage {
     bool unknown = false;
     std::vector<int> dims;       // GDim ids
     std::string elem = "float";  // element type of a known array ("float", "uint8", ...)
+    bool internal = false;       // ComputedArray value / gradient image: allocated by the plan
+    bool tvalued = false;        // stored in the solver precision T (unknowns, internal
+                                 // images, arrays aliasing an unknown's parameter slot)
+};
+// d(computed channel)/d(unknown access u): a gradient image (gimg) or a constant (gimg -1)
+struct GGrad { int ch = 0; int u = -1; int expr = -1; int gimg = -1; };
+// ComputedArray (ProblemSpecAD:ComputedImage, o.t:1686-1718): evaluated per pixel by the
+// precompute kernel (createprecomputed, o.t:3131-3153) with its gradient images.
+struct GComputed {
+    int image = -1;
+    std::vector<int> expr;         // per channel
+    std::vector<GGrad> grads;
+    int lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};   // bbox of the expression (bboxforexpression)
 };
 struct GParam { std::string name; std::string type; int index = -1; };
 struct GGraph {
@@ -43,6 +56,7 @@ struct GModel {
     std::vector<GParam> params;
     std::vector<GGraph> graphs;
     std::vector<GResidual> residuals;
+    std::vector<GComputed> computed;   // declaration order (= precompute order)
     int exclude = -1;              // Exclude(expr): centred scalar, -1 = none
     bool use_preconditioner = false;
     std::string unsupported;       // first construct the generic path cannot lower

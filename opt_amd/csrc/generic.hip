@@ -63,7 +63,7 @@ std::map<std::string, std::string>& code_cache() {
 }
 
 size_t elem_size(const gen::GImage& im, bool dbl) {
-    if (im.unknown) return dbl ? 8 : 4;
+    if (im.tvalued) return dbl ? 8 : 4;
     if (im.elem == "uint8") return 1;
     return 4;
 }
@@ -94,7 +94,8 @@ bool generic_accepts(const std::string& text, ProblemSpec* spec, std::string* er
         if (m.images[k].dims != m.images[unk[0]].dims) { *err = "unknowns over different index spaces"; return false; }
     for (auto& im : m.images)
         if (!im.unknown && im.dims != m.images[unk[0]].dims) {
-            *err = "array '" + im.name + "' is not over the unknowns' index space";
+            *err = std::string(im.internal ? "computed array '" : "array '") + im.name +
+                   "' is not over the unknowns' index space";
             return false;
         }
     if (m.residuals.empty()) { *err = "no Energy terms"; return false; }
@@ -136,9 +137,15 @@ public:
         n_ = off;
         src_ = gen::generate(m_, sizeof(T) == 8);
         load_module();
+        for (size_t i = 0; i < m_.images.size(); ++i)
+            if (m_.images[i].internal) {   // ComputedArray values and gradient images
+                dimg_[i] = dmalloc(std::max<size_t>(1, image_bytes(i)));
+                OPT_HIP_CHECK(hipMemset(dimg_[i], 0, image_bytes(i)));
+                a_.img[i] = dimg_[i];
+            }
         if (opts_.host_buffers) {
             for (size_t i = 0; i < m_.images.size(); ++i)
-                dimg_[i] = dmalloc(std::max<size_t>(1, image_bytes(i)));
+                if (!m_.images[i].internal) dimg_[i] = dmalloc(std::max<size_t>(1, image_bytes(i)));
             int sb = 0;
             for (size_t g = 0; g < m_.graphs.size(); ++g)
                 for (size_t s = 0; s < m_.graphs[g].slot_names.size(); ++s, ++sb)
@@ -172,6 +179,7 @@ public:
     void bind(void** params, hipStream_t s) {
         user_ = params;
         for (size_t i = 0; i < m_.images.size(); ++i) {
+            if (m_.images[i].internal) continue;
             void* p = params[m_.images[i].index];
             if (opts_.host_buffers) {
                 OPT_HIP_CHECK(hipMemcpyAsync(dimg_[i], p, image_bytes(i), hipMemcpyHostToDevice, s));
@@ -179,6 +187,11 @@ public:
             }
             a_.img[i] = p;
         }
+        // an Array on an Unknown's slot views the (device copy of the) unknown
+        for (size_t i = 0; i < m_.images.size(); ++i)
+            if (!m_.images[i].unknown && !m_.images[i].internal && m_.images[i].tvalued)
+                for (int k : unk_)
+                    if (m_.images[k].index == m_.images[i].index) a_.img[i] = a_.img[k];
         for (size_t j = 0; j < m_.params.size(); ++j) {
             const void* p = params[m_.params[j].index];
             const std::string& t = m_.params[j].type;
@@ -210,7 +223,9 @@ public:
             OPT_HIP_CHECK(hipMemcpyAsync(user_[m_.images[k].index], dimg_[k], image_bytes(k), hipMemcpyDeviceToHost, s));
     }
     T* unknown(int k) { return k < (int)unk_.size() ? (T*)a_.img[unk_[k]] : nullptr; }
-    void precompute(hipStream_t) {}
+    void precompute(hipStream_t s) {
+        for (hipFunction_t f : k_pre_) launch(f, s, {&a_});
+    }
     void computed_planes(std::vector<HaloPlane>&) const {}
 
     void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
@@ -263,6 +278,9 @@ private:
                         std::make_pair(&k_apply_graph_, "gen_apply_graph"), std::make_pair(&k_finish_, "gen_finish"),
                         std::make_pair(&k_finish_jtf_, "gen_finish_jtf")})
             OPT_HIP_CHECK(hipModuleGetFunction(kv.first, mod_, kv.second));
+        k_pre_.resize(src_.n_precompute);
+        for (int k = 0; k < src_.n_precompute; ++k)
+            OPT_HIP_CHECK(hipModuleGetFunction(&k_pre_[k], mod_, ("gen_precompute_" + std::to_string(k)).c_str()));
     }
     void launch(hipFunction_t f, hipStream_t s, std::initializer_list<const void*> args) {
         std::vector<void*> a;
@@ -303,6 +321,7 @@ private:
     int* dslot_[16] = {};
     const int* checked_[16] = {};
     hipModule_t mod_ = nullptr;
+    std::vector<hipFunction_t> k_pre_;
     hipFunction_t k_jtf_{}, k_apply_{}, k_cost_{}, k_jtf_graph_{}, k_apply_graph_{}, k_finish_{}, k_finish_jtf_{};
 };
 
