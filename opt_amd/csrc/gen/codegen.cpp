@@ -77,6 +77,10 @@ public:
             case Op::Abs: e = "fabs(" + v(n.a) + ")"; break;
             case Op::Pow: e = "pow(" + v(n.a) + ", " + v(n.b) + ")"; break;
             case Op::Select: e = "(" + v(n.a) + " != (T)0) ? " + v(n.b) + " : " + v(n.d); break;
+            case Op::Sample:
+                e = "opt_sample(" + img_ptr(n.i) + ", " + std::to_string(M_.images[n.i].channels) + ", " +
+                    std::to_string(n.ch) + ", " + v(n.a) + ", " + v(n.b) + ", W, H)";
+                break;
             case Op::Lt: e = "(T)(" + v(n.a) + " < " + v(n.b) + ")"; break;
             case Op::Le: e = "(T)(" + v(n.a) + " <= " + v(n.b) + ")"; break;
             case Op::Gt: e = "(T)(" + v(n.a) + " > " + v(n.b) + ")"; break;
@@ -128,6 +132,10 @@ private:
         if (nd_ == 1) return "(long long)" + coord(0, off[0]);
         if (nd_ == 2) return "((long long)" + coord(1, off[1]) + " * W + " + coord(0, off[0]) + ")";
         return "(((long long)" + coord(2, off[2]) + " * H + " + coord(1, off[1]) + ") * W + " + coord(0, off[0]) + ")";
+    }
+    std::string img_ptr(int i) const {
+        const GImage& im = M_.images[i];
+        return "((const " + std::string(elem_type(im.elem, im.tvalued)) + "*)a.img[" + std::to_string(i) + "])";
     }
     std::string read(const Node& n, const char* vname) {
         const GImage& im = M_.images[n.i];
@@ -182,6 +190,15 @@ GenSource generate(GModel& m, bool dbl) {
     o << OPTAMD_STR(OPTAMD_GENARGS_BODY) << "\n";
     o << kReduceDevSrc << "\n";
     o << "#define OPT_COORDS const int W = a.dims[0], H = a.dims[1], D = a.dims[2]; (void)D;\n";
+    // Image:get / Image:sample (o.t:856-876): floor / ceil taps, zero outside, lerps in T
+    o << "template <typename E> __device__ __forceinline__ T opt_tap(const E* im, int nch, int c, int x, int y, int W, int H) {\n"
+         "    return (x >= 0 && x < W && y >= 0 && y < H) ? (T)im[((long long)y * W + x) * nch + c] : (T)0;\n}\n"
+         "template <typename E> __device__ __forceinline__ T opt_sample(const E* im, int nch, int c, T x, T y, int W, int H) {\n"
+         "    const int x0 = (int)floor(x), x1 = (int)ceil(x), y0 = (int)floor(y), y1 = (int)ceil(y);\n"
+         "    const T xn = x - (T)x0, yn = y - (T)y0;\n"
+         "    const T u = ((T)1 - xn) * opt_tap(im, nch, c, x0, y0, W, H) + xn * opt_tap(im, nch, c, x1, y0, W, H);\n"
+         "    const T b = ((T)1 - xn) * opt_tap(im, nch, c, x0, y1, W, H) + xn * opt_tap(im, nch, c, x1, y1, W, H);\n"
+         "    return ((T)1 - yn) * u + yn * b;\n}\n";
     const char* coords =
         "        const int x = (int)(lin % W); const int y = (int)((lin / W) % H); const int z = (int)(lin / ((long long)W * H));\n"
         "        (void)x; (void)y; (void)z;\n";

@@ -171,6 +171,18 @@ int Pool::select(int c, int a, int b) {
     return intern(n);
 }
 
+int Pool::sample(int image, int ch, int x, int y, int dx_image, int dy_image) {
+    Node n;
+    n.op = Op::Sample;
+    n.i = image;
+    n.ch = ch;
+    n.a = x;
+    n.b = y;
+    n.off2[0] = dx_image;
+    n.off2[1] = dy_image;
+    return intern(n);
+}
+
 int Pool::diff(int id, int var) {
     auto it = dmemo_.find({id, var});
     if (it != dmemo_.end()) return it->second;
@@ -219,6 +231,13 @@ int Pool::diff(int id, int var) {
             break;
         }
         case Op::Select: r = select(n.a, diff(n.b, var), diff(n.d, var)); break;
+        case Op::Sample: {   // op:getpartials (o.t:3274-3278): the derivative images, sampled
+            const int da = diff(n.a, var), db = diff(n.b, var);
+            if (n.off2[0] < 0) { r = cnst(0.0); break; }   // rejected by the front end if used
+            r = bin(Op::Add, bin(Op::Mul, sample(n.off2[0], n.ch, n.a, n.b, -1, -1), da),
+                    bin(Op::Mul, sample(n.off2[1], n.ch, n.a, n.b, -1, -1), db));
+            break;
+        }
         default: r = cnst(0.0); break;   // constants, parameters, bounds, comparisons, logic
     }
     dmemo_[{id, var}] = r;
@@ -249,6 +268,7 @@ int Pool::shift(int id, const int* s) {
         case Op::Const:
         case Op::Param: r = id; break;
         case Op::Select: r = select(shift(n.a, s), shift(n.b, s), shift(n.d, s)); break;
+        case Op::Sample: r = sample(n.i, n.ch, shift(n.a, s), shift(n.b, s), n.off2[0], n.off2[1]); break;
         default:
             if (n.b < 0) r = un(n.op, shift(n.a, s));
             else r = bin(n.op, shift(n.a, s), shift(n.b, s));
@@ -270,8 +290,12 @@ std::string Pool::str(int id) const {
             else o << "(" << n.off[0] << "," << n.off[1] << "," << n.off[2] << ")";
             break;
         case Op::InBox: o << "inbox"; break;
-        case Op::Coord: o << "idx" << n.i; break;
+        case Op::Coord:
+            o << "idx" << n.i;
+            if (n.off[n.i]) o << (n.off[n.i] > 0 ? "+" : "") << n.off[n.i];
+            break;
         case Op::Select: o << "(" << str(n.a) << " ? " << str(n.b) << " : " << str(n.d) << ")"; break;
+        case Op::Sample: o << "sample_I" << n.i << "[" << n.ch << "](" << str(n.a) << ", " << str(n.b) << ")"; break;
         default: {
             static const char* names[] = {"", "", "", "", "", "+", "-", "*", "/", "neg", "sqrt", "sin", "cos",
                                           "exp", "log", "abs", "pow", "", "<", "<=", ">", ">=", "==", "!=", "&&",

@@ -28,6 +28,8 @@ enum class Op : uint8_t {
     Sqrt, Sin, Cos, Exp, Log, Abs, Pow,
     Select,   // a ? b : c
     Lt, Le, Gt, Ge, Eq, Ne, And, Or, Not,
+    Sample,   // bilinear sample of image i, channel ch, at (a, b); off2[0] / off2[1] = the
+              // images sampled for d/dx and d/dy (-1: none) (ad.sampledimage, o.t:3266-3280)
 };
 
 struct Node {
@@ -55,6 +57,7 @@ public:
     int un(Op op, int a);
     int bin(Op op, int a, int b);
     int select(int c, int a, int b);
+    int sample(int image, int ch, int x, int y, int dx_image, int dy_image);
 
     bool is_const(int id, double* v = nullptr) const;
     // d(id)/d(var) where var is a Read node (an unknown access)

@@ -1268,13 +1268,33 @@ void Interp::install() {
             return VList{expr(out)};
         })};
     });
-    for (const char* n : {"SampledImage"}) {
-        const std::string nm = n;
-        def(nm, [this, nm](VList&) -> VList {
-            unsupported(nm);
-            err("the general front end does not lower " + nm);
-        });
-    }
+    // ad.sampledimage (o.t:3243-3282): I(x, y[, c]) bilinear at data-dependent coordinates,
+    // differentiated through the sampled derivative images
+    def("SampledImage", [this](VList& a) {
+        if (a.empty() || a[0].k != V::Image) err("SampledImage(image[, image_dx, image_dy])");
+        const int im = a[0].id;
+        int dx = -1, dy = -1;
+        if (a.size() >= 3) {
+            if (a[1].k != V::Image || a[2].k != V::Image) err("SampledImage derivatives must be images");
+            dx = a[1].id;
+            dy = a[2].id;
+        }
+        if (m_->images[im].dims.size() != 2) err("sampled images must be 2D");
+        return VList{builtin([this, im, dx, dy](VList& args) {
+            if (args.size() < 2) err("sampled image expects (x, y[, channel])");
+            const int x = comp(args[0], 0), y = comp(args[1], 0);
+            const int nch = m_->images[im].channels;
+            std::vector<int> out;
+            if (args.size() > 2) {
+                const int c = (int)args[2].n;
+                if (c < 0 || c >= nch) err("index out of bounds");
+                out.push_back(P().sample(im, c, x, y, dx, dy));
+            } else {
+                for (int c = 0; c < nch; ++c) out.push_back(P().sample(im, c, x, y, dx, dy));
+            }
+            return VList{expr(out)};
+        })};
+    });
     // ---- expression library (lib.t, ad.t)
     def("Select", [this](VList& a) {
         if (a.size() != 3) err("Select(cond, a, b)");
@@ -1432,6 +1452,11 @@ void Interp::finish() {
                 if (m_->images[n.i].unknown) unk.insert(id);
             } else if (n.op == Op::InBox) {
                 bounds = true;
+            } else if (n.op == Op::Sample && n.off2[0] < 0) {
+                bool dep = false;
+                for (int c : {n.a, n.b})
+                    P().visit(c, [&](int, const Node& q) { dep |= q.op == Op::Read && m_->images[q.i].unknown; });
+                if (dep) throw LuaError("image derivatives are not defined for sampled image " + m_->images[n.i].name);
             }
         });
         if (!any) throw LuaError("residual must actually use some image");

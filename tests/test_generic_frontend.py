@@ -32,6 +32,7 @@ def E(name):
     ("curve_smoothing", 7),
     ("intrinsic_image_decomposition", 19),   # 4 x 3 albedo + 4 shading + 3 fit
     ("shape_from_shading", 6),               # fit, 2 shading (through B_I), 3 smoothness
+    ("optical_flow", 9),                     # 1 sampled fit + 4 x 2 regularizer rows
 ])
 def test_residual_templates(name, count):
     d = api.generic_describe(E(name))
@@ -47,7 +48,7 @@ def test_residual_templates(name, count):
 
 @pytest.mark.parametrize("name", ["image_warping", "poisson_image_editing", "arap_mesh_deformation",
                                   "volume_denoise", "curve_smoothing", "intrinsic_image_decomposition",
-                                  "shape_from_shading"])
+                                  "shape_from_shading", "optical_flow"])
 def test_generated_source_compiles(name):
     src = api.generic_source(E(name))
     for k in ("gen_jtf", "gen_apply", "gen_cost", "gen_jtf_graph", "gen_apply_graph", "gen_finish",
@@ -132,8 +133,9 @@ def test_front_end_errors_name_the_problem(tmp_path):
     with pytest.raises(api.OptError, match="line 3"):
         api.generic_describe(_write(tmp_path, "syntax.t", 'local W = Dim("W", 0)\n'
                                     'local X = Unknown("X", opt_float, {W}, 0)\nEnergy(X(0) + )\n'))
-    with pytest.raises(api.OptError, match="SampledImage"):
-        api.generic_describe(_write(tmp_path, "s.t", HEAD + "local I = SampledImage(A, A, A)\n"))
+    with pytest.raises(api.OptError, match="derivatives are not defined"):
+        api.generic_describe(_write(tmp_path, "s.t", HEAD + "local I = SampledImage(A)\n"
+                                    "Energy(A(0,0,0) - I(X(0,0,0), X(0,0,1), 0))\n"))
     with pytest.raises(api.OptError, match="accessed with"):
         api.generic_describe(_write(tmp_path, "n.t", HEAD + "Energy(X(0,0,0,0))\n"))
 
@@ -154,14 +156,14 @@ def test_define_routes_unrecognised_energies_to_the_front_end(tmp_path):
         lib.Opt_ProblemDelete(st, pr)
     lib, st, pr = _define(_write(tmp_path, "bad.t", 'local W,H = Dim("W",0), Dim("H",1)\n'
                                  'local X = Unknown("X", opt_float,{W,H},0)\nlocal A = Array("A", opt_float,{W,H},1)\n'
-                                 'Energy(X(0,0) - SampledImage(A, A)(0,0))\n'))
+                                 'Energy(X(0,0) - SampledImage(A)(X(0,0), X(0,0)))\n'))
     assert not pr
 
 
 LOWERED = ["arap_mesh_deformation", "cotangent_mesh_smoothing", "embedded_mesh_deformation", "image_warping",
            "intrinsic_image_decomposition", "poisson_image_editing", "robust_nonrigid_alignment",
-           "shape_from_shading", "volumetric_mesh_deformation"]
-REFUSED = {"optical_flow": "SampledImage"}
+           "shape_from_shading", "volumetric_mesh_deformation", "optical_flow"]
+REFUSED = {}
 
 
 @pytest.mark.skipif(not os.path.isdir(REF), reason="reference checkout not present")
