@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include "plan.h"
+#include "graph_util.h"
 #include "stencil_plan.h"
 
 namespace optamd {
@@ -395,7 +396,7 @@ public:
     ~ArapOp() {
         out_.release(); in_.release();
         dfree(dO_); dfree(dA_); dfree(dU_); dfree(dC_); dfree(dv0_); dfree(dv1_);
-        dfree(scratch_); dfree(keys_tmp_); dfree(K_);
+        dfree(scratch_); dfree(keys_tmp_); dfree(K_); dfree(fp_scratch_);
     }
     VecLayout layout() const {
         VecLayout L{};
@@ -425,19 +426,19 @@ public:
             OPT_HIP_CHECK(hipMemcpyAsync(dA_, userA_, sizeof(T) * 3 * N_, hipMemcpyHostToDevice, s));
             OPT_HIP_CHECK(hipMemcpyAsync(dU_, params[idx_U_], sizeof(float) * 3 * N_, hipMemcpyHostToDevice, s));
             OPT_HIP_CHECK(hipMemcpyAsync(dC_, params[idx_C_], sizeof(float) * 3 * N_, hipMemcpyHostToDevice, s));
-            // the graph itself only when its host arrays change
-            if (params[idx_v0_] != host_v0_ || params[idx_v1_] != host_v1_) {
-                OPT_HIP_CHECK(hipMemcpyAsync(dv0_, params[idx_v0_], sizeof(int) * E_, hipMemcpyHostToDevice, s));
-                OPT_HIP_CHECK(hipMemcpyAsync(dv1_, params[idx_v1_], sizeof(int) * E_, hipMemcpyHostToDevice, s));
-                host_v0_ = params[idx_v0_];
-                host_v1_ = params[idx_v1_];
-                graph_v0_ = nullptr;   // force a rebuild
-            }
+            OPT_HIP_CHECK(hipMemcpyAsync(dv0_, params[idx_v0_], sizeof(int) * E_, hipMemcpyHostToDevice, s));
+            OPT_HIP_CHECK(hipMemcpyAsync(dv1_, params[idx_v1_], sizeof(int) * E_, hipMemcpyHostToDevice, s));
             a_.O = dO_; a_.A = dA_; a_.U = dU_; a_.C = dC_;
             v0 = dv0_;
             v1 = dv1_;
         }
-        if (v0 != graph_v0_ || v1 != graph_v1_) build_csr(v0, v1, s);
+        // rebuild the adjacency when the edges change (content, not address: graph_util.h)
+        const int* vs[2] = {v0, v1};
+        const unsigned long long h = graph_fingerprint(vs, 2, E_, s, fp_scratch_);
+        if (v0 != graph_v0_ || v1 != graph_v1_ || h != fingerprint_) {
+            build_csr(v0, v1, s);
+            fingerprint_ = h;
+        }
         a_.N = N_;
         a_.out_off = out_.off; a_.out_nbr = out_.nbr;
         a_.in_off = in_.off; a_.in_nbr = in_.nbr;
@@ -539,8 +540,8 @@ private:
     GraphCSR out_, in_;
     const int* graph_v0_ = nullptr;
     const int* graph_v1_ = nullptr;
-    const void* host_v0_ = nullptr;
-    const void* host_v1_ = nullptr;
+    unsigned long long fingerprint_ = 0;
+    unsigned long long* fp_scratch_ = (unsigned long long*)dmalloc(sizeof(unsigned long long));
     void* scratch_ = nullptr;
     size_t scratch_bytes_ = 0;
     int* keys_tmp_ = nullptr;

@@ -406,95 +406,108 @@ GenSource generate(GModel& m, bool dbl) {
         o << "    double v[1] = {(double)acc};\n    block_reduce_publish<1>(v, rs, blockIdx.x);\n}\n";
     }
 
-    // ------------------------------------------------------------ graph scatters
+    // ------------------------------------------------------------- graph gathers
+    // The reference scatters every edge's J^T F / J^T J p contributions to the edge's
+    // vertices with float atomics (createjtfgraph / createjtjgraph, o.t:2833-2867,
+    // 2969-2994; Image:atomicAddChannel, backend_cuda.t:751-759). Here each vertex gathers
+    // them instead, over per-slot incidence lists built once per bind (a.goff / a.geid:
+    // the edges whose slot k is this vertex, ascending): no atomics, a fixed summation
+    // order (bitwise reproducible), each edge evaluated once per incident slot. The same
+    // kernel finishes the element (exclusion mask, LM diagonal, p.Ap).
+    auto graph_gather = [&](bool apply) {
+        // accumulators per output (unknown image, channel)
+        for (int k : unk)
+            for (int c = 0; c < m.images[k].channels; ++c)
+                o << "        T acc" << uslot[k] << "_" << c << " = 0, dg" << uslot[k] << "_" << c << " = 0;\n";
+        o << "        (void)0;\n";
+        for (size_t g = 0; g < m.graphs.size(); ++g) {
+            const size_t nslots = m.graphs[g].slot_names.size();
+            for (size_t k = 0; k < nslots; ++k) {
+                // residuals of graph g reading an unknown at slot k
+                bool any = false;
+                for (auto& r : m.residuals)
+                    if (r.graph == (int)g)
+                        for (int u : r.unknowns) any |= P.at(u).slot == (int)k;
+                if (!any) continue;
+                const int sbk = gs.slot_base[g] + (int)k;
+                o << "        for (int q = a.goff[" << sbk << "][vtx]; q < a.goff[" << sbk << "][vtx + 1]; ++q) {\n"
+                  << "        const int e = a.geid[" << sbk << "][q];\n";
+                for (size_t s2 = 0; s2 < nslots; ++s2)
+                    o << "        const int v" << s2 << " = " << (s2 == k ? std::string("(int)vtx") :
+                                                              "a.slot[" + std::to_string(gs.slot_base[g] + s2) + "][e]")
+                      << ";\n";
+                Body b(m, o, nd, uslot);
+                int idx = 0;
+                for (auto& r : m.residuals) {
+                    if (r.graph != (int)g) continue;
+                    std::vector<int> mine;
+                    for (int u : r.unknowns)
+                        if (P.at(u).slot == (int)k) mine.push_back(u);
+                    if (mine.empty()) continue;
+                    std::string R;
+                    if (apply) {
+                        std::string sum = "(T)0";
+                        for (int u : r.unknowns) {
+                            const int gu = P.diff(r.expr, u);
+                            double gv;
+                            if (P.is_const(gu, &gv) && gv == 0.0) continue;
+                            sum += " + " + b.v(gu) + " * " + b.vec(u, "p");
+                        }
+                        R = "jp" + std::to_string(idx++);
+                        b.line("const T " + R + " = " + sum + ";");
+                    } else {
+                        R = b.v(r.expr);
+                    }
+                    for (int u : mine) {
+                        const int gu = P.diff(r.expr, u);
+                        double gv;
+                        if (P.is_const(gu, &gv) && gv == 0.0) continue;
+                        const Node& n = P.at(u);
+                        const std::string gn = b.v(gu);
+                        const std::string a_ = "acc" + std::to_string(uslot[n.i]) + "_" + std::to_string(n.ch);
+                        const std::string d_ = "dg" + std::to_string(uslot[n.i]) + "_" + std::to_string(n.ch);
+                        b.line(a_ + " += " + gn + " * " + R + ";" + (apply ? "" : " " + d_ + " += " + gn + " * " + gn + ";"));
+                    }
+                }
+                o << "        }\n";
+            }
+        }
+    };
     {
         o << "extern \"C\" __global__ __launch_bounds__(256) void gen_jtf_graph(GenArgs a, T* __restrict__ r, T* __restrict__ diag) {\n"
-             "    OPT_COORDS\n";
-        for (size_t g = 0; g < m.graphs.size(); ++g) {
-            o << "    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < a.nedge[" << g
-              << "]; e += (long long)gridDim.x * 256) {\n";
-            for (size_t s = 0; s < m.graphs[g].slot_names.size(); ++s)
-                o << "        const int v" << s << " = a.slot[" << gs.slot_base[g] + s << "][e];\n";
-            Body b(m, o, nd, uslot);
-            for (auto& r : m.residuals) {
-                if (r.graph != (int)g) continue;
-                const std::string R = b.v(r.expr);
-                for (int u : r.unknowns) {
-                    const int gu = P.diff(r.expr, u);
-                    double gv;
-                    if (P.is_const(gu, &gv) && gv == 0.0) continue;
-                    const Node& n = P.at(u);
-                    const std::string gn = b.v(gu);
-                    const std::string idx = "a.uoff[" + std::to_string(uslot[n.i]) + "] + (long long)v" + std::to_string(n.slot) +
-                                            " * " + std::to_string(m.images[n.i].channels) + " + " + std::to_string(n.ch);
-                    b.line("atomicAdd(&r[" + idx + "], -(" + gn + " * " + R + ")); atomicAdd(&diag[" + idx + "], " + gn + " * " + gn + ");");
-                }
+             "    OPT_COORDS\n"
+             "    for (long long vtx = (long long)blockIdx.x * 256 + threadIdx.x; vtx < a.npix; vtx += (long long)gridDim.x * 256) {\n";
+        graph_gather(false);
+        o << "        const bool act = (a.flags[vtx] & 1) != 0;\n";
+        for (int k : unk)
+            for (int c = 0; c < m.images[k].channels; ++c) {
+                const std::string e = "a.uoff[" + std::to_string(uslot[k]) + "] + vtx * " +
+                                      std::to_string(m.images[k].channels) + " + " + std::to_string(c);
+                const std::string sfx = std::to_string(uslot[k]) + "_" + std::to_string(c);
+                o << "        { const long long i = " << e << "; r[i] = act ? r[i] - acc" << sfx
+                  << " : (T)0; diag[i] += dg" << sfx << "; }\n";
             }
-            o << "    }\n";
-        }
-        o << "}\n";
-        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_apply_graph(GenArgs a, const T* __restrict__ p, T* __restrict__ Ap, const int* stop) {\n"
+        o << "    }\n}\n";
+        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_apply_graph(GenArgs a, const T* __restrict__ p, T* __restrict__ Ap,\n"
+             "        const T* __restrict__ dadd, const int* stop, ReduceSlot rs, int has_centred) {\n"
              "    if (stop && *stop) return;\n"
-             "    OPT_COORDS\n";
-        for (size_t g = 0; g < m.graphs.size(); ++g) {
-            o << "    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < a.nedge[" << g
-              << "]; e += (long long)gridDim.x * 256) {\n";
-            for (size_t s = 0; s < m.graphs[g].slot_names.size(); ++s)
-                o << "        const int v" << s << " = a.slot[" << gs.slot_base[g] + s << "][e];\n";
-            Body b(m, o, nd, uslot);
-            int idx = 0;
-            for (auto& r : m.residuals) {
-                if (r.graph != (int)g) continue;
-                std::string sum = "(T)0";
-                std::vector<std::pair<int, std::string>> gs_;
-                for (int u : r.unknowns) {
-                    const int gu = P.diff(r.expr, u);
-                    double gv;
-                    if (P.is_const(gu, &gv) && gv == 0.0) continue;
-                    const std::string gn = b.v(gu);
-                    sum += " + " + gn + " * " + b.vec(u, "p");
-                    gs_.push_back({u, gn});
-                }
-                const std::string jn = "jp" + std::to_string(idx++);
-                b.line("const T " + jn + " = " + sum + ";");
-                for (auto& ug : gs_) {
-                    const Node& n = P.at(ug.first);
-                    const std::string id = "a.uoff[" + std::to_string(uslot[n.i]) + "] + (long long)v" + std::to_string(n.slot) +
-                                           " * " + std::to_string(m.images[n.i].channels) + " + " + std::to_string(n.ch);
-                    b.line("atomicAdd(&Ap[" + id + "], " + ug.second + " * " + jn + ");");
-                }
-            }
-            o << "    }\n";
-        }
-        o << "}\n";
-    }
-
-    // ------------------------------------------------- finishing passes (graphs)
-    {
-        // element -> pixel of the unknown vector
-        std::string pix = "        long long px;\n";
-        for (size_t k = 0; k < unk.size(); ++k) {
-            const int ch = m.images[unk[k]].channels;
-            pix += "        " + std::string(k ? "else " : "") + (k + 1 < unk.size() ? "if (i < a.uoff[" + std::to_string(k + 1) + "]) " : "") +
-                   "px = (i - a.uoff[" + std::to_string(k) + "]) / " + std::to_string(ch) + ";\n";
-        }
-        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_finish(GenArgs a, const T* __restrict__ p, T* __restrict__ Ap,\n"
-             "        const T* __restrict__ dadd, const int* stop, ReduceSlot rs, long long n) {\n"
-             "    if (stop && *stop) return;\n"
+             "    OPT_COORDS\n"
              "    T dot = 0;\n"
-             "    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {\n"
-          << pix
-          << "        const T pe = p[i];\n"
-             "        const T o = (a.flags[px] & 1) ? Ap[i] + (dadd ? dadd[i] * pe : (T)0) : (T)0;\n"
-             "        Ap[i] = o;\n"
-             "        dot += pe * o;\n"
-             "    }\n"
+             "    for (long long vtx = (long long)blockIdx.x * 256 + threadIdx.x; vtx < a.npix; vtx += (long long)gridDim.x * 256) {\n";
+        graph_gather(true);
+        o << "        const bool act = (a.flags[vtx] & 1) != 0;\n";
+        for (int k : unk)
+            for (int c = 0; c < m.images[k].channels; ++c) {
+                const std::string e = "a.uoff[" + std::to_string(uslot[k]) + "] + vtx * " +
+                                      std::to_string(m.images[k].channels) + " + " + std::to_string(c);
+                const std::string sfx = std::to_string(uslot[k]) + "_" + std::to_string(c);
+                o << "        { const long long i = " << e << "; const T pe = p[i];\n"
+                  << "          const T o = act ? (has_centred ? Ap[i] : (T)0) + acc" << sfx
+                  << " + (dadd ? dadd[i] * pe : (T)0) : (T)0;\n"
+                  << "          Ap[i] = o; dot += pe * o; }\n";
+            }
+        o << "    }\n"
              "    double v[1] = {(double)dot};\n    block_reduce_publish<1>(v, rs, blockIdx.x);\n}\n";
-        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_finish_jtf(GenArgs a, T* __restrict__ r, long long n) {\n"
-             "    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {\n"
-          << pix
-          << "        if (!(a.flags[px] & 1)) r[i] = (T)0;\n"
-             "    }\n}\n";
     }
     (void)zero3;
     gs.code = o.str();

@@ -14,6 +14,8 @@
         const void* img[16];        /* by image id: unknowns (T) and known arrays */        \
         float prm[32];              /* by parameter id */                                   \
         const int* slot[16];        /* graph vertex arrays, graph-major */                  \
+        const int* goff[16];        /* per slot: incidence offsets by vertex (N+1) */       \
+        const int* geid[16];        /* per slot: incident edge ids, ascending */            \
         int nedge[4];               /* edges per graph */                                   \
         unsigned char* flags;       /* bit0: active (not excluded) */                       \
         long long uoff[4];          /* offset of each unknown image in the vector */        \

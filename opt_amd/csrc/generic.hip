@@ -11,12 +11,14 @@
 // OPT_AMD_GENERIC=1 routes recognised families here too (to validate it against the
 // hand-written kernels and the reference's known answers).
 #include <hip/hiprtc.h>
+#include <hipcub/hipcub.hpp>
 #include <algorithm>
 #include <cstring>
 #include <map>
 #include <memory>
 #include <mutex>
 #include "gen/codegen.h"
+#include "graph_util.h"
 #include "stencil_plan.h"
 
 namespace optamd {
@@ -60,6 +62,14 @@ std::mutex g_mu;
 std::map<std::string, std::string>& code_cache() {
     static std::map<std::string, std::string> m;
     return m;
+}
+
+__global__ void incidence_count(const int* keys, int E, int* counts) {
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x)
+        atomicAdd(&counts[keys[e]], 1);
+}
+__global__ void iota_kernel(int* v, int n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) v[i] = i;
 }
 
 size_t elem_size(const gen::GImage& im, bool dbl) {
@@ -155,6 +165,8 @@ public:
     ~GenericOp() {
         for (void* p : dimg_) dfree(p);
         for (int* p : dslot_) dfree(p);
+        for (int k = 0; k < 16; ++k) { dfree(goff_[k]); dfree(geid_[k]); }
+        dfree(fp_scratch_);
         if (mod_) (void)hipModuleUnload(mod_);
     }
 
@@ -230,19 +242,18 @@ public:
 
     void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
         a_.flags = flags;
-        launch(k_jtf_, s, {&a_, &r, &diag});
-        if (src_.has_graph) {
-            launch(k_jtf_graph_, s, {&a_, &r, &diag});
-            if (m_.exclude >= 0) launch(k_finish_jtf_, s, {&a_, &r, &n_});
-        }
+        launch(k_jtf_, s, {&a_, &r, &diag});   // flags, and r / diag of the centred residuals
+        if (src_.has_graph) launch(k_jtf_graph_, s, {&a_, &r, &diag});
     }
     void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
-        int finish = src_.has_graph ? 0 : 1;
-        launch(k_apply_, s, {&a_, &p, &Ap, &dadd, &stop, &rs, &finish});
-        if (src_.has_graph) {
-            launch(k_apply_graph_, s, {&a_, &p, &Ap, &stop});
-            launch(k_finish_, s, {&a_, &p, &Ap, &dadd, &stop, &rs, &n_});
+        if (!src_.has_graph) {
+            int finish = 1;
+            launch(k_apply_, s, {&a_, &p, &Ap, &dadd, &stop, &rs, &finish});
+            return;
         }
+        int finish = 0, centred = src_.has_centered ? 1 : 0;
+        if (centred) launch(k_apply_, s, {&a_, &p, &Ap, &dadd, &stop, &rs, &finish});
+        launch(k_apply_graph_, s, {&a_, &p, &Ap, &dadd, &stop, &rs, &centred});
     }
     void cost(ReduceSlot rs, hipStream_t s) {
         const T* d = nullptr;
@@ -275,8 +286,7 @@ private:
         OPT_HIP_CHECK(hipModuleLoadData(&mod_, obj.data()));
         for (auto kv : {std::make_pair(&k_jtf_, "gen_jtf"), std::make_pair(&k_apply_, "gen_apply"),
                         std::make_pair(&k_cost_, "gen_cost"), std::make_pair(&k_jtf_graph_, "gen_jtf_graph"),
-                        std::make_pair(&k_apply_graph_, "gen_apply_graph"), std::make_pair(&k_finish_, "gen_finish"),
-                        std::make_pair(&k_finish_jtf_, "gen_finish_jtf")})
+                        std::make_pair(&k_apply_graph_, "gen_apply_graph")})
             OPT_HIP_CHECK(hipModuleGetFunction(kv.first, mod_, kv.second));
         k_pre_.resize(src_.n_precompute);
         for (int k = 0; k < src_.n_precompute; ++k)
@@ -289,22 +299,64 @@ private:
     }
     // vertex indices must lie in [0, N) (fail-stop, as the reference does on bad input)
     void check_graphs(hipStream_t s) {
+        if (!fp_scratch_) fp_scratch_ = (unsigned long long*)dmalloc(sizeof(unsigned long long));
         int sb = 0;
         for (size_t g = 0; g < m_.graphs.size(); ++g) {
-            for (size_t k = 0; k < m_.graphs[g].slot_names.size(); ++k, ++sb) {
-                if (a_.slot[sb] == checked_[sb] || nedge_[g] == 0) continue;
-                std::vector<int> h(nedge_[g]);
-                OPT_HIP_CHECK(hipMemcpyAsync(h.data(), a_.slot[sb], sizeof(int) * nedge_[g], hipMemcpyDeviceToHost, s));
-                OPT_HIP_CHECK(hipStreamSynchronize(s));
-                for (int v : h)
-                    if (v < 0 || v >= npix_) {
-                        fprintf(stderr, "[opt_amd] generic: graph '%s' vertex index %d outside [0, %lld)\n",
-                                m_.graphs[g].name.c_str(), v, npix_);
-                        exit(1);
+            const int ns = (int)m_.graphs[g].slot_names.size();
+            const unsigned long long h = graph_fingerprint(a_.slot + sb, ns, nedge_[g], s, fp_scratch_);
+            if (!(goff_[sb] && h == fingerprint_[g])) {
+                fingerprint_[g] = h;
+                for (int k = 0; k < ns; ++k) {
+                    if (nedge_[g] > 0) {
+                        std::vector<int> hv(nedge_[g]);
+                        OPT_HIP_CHECK(hipMemcpyAsync(hv.data(), a_.slot[sb + k], sizeof(int) * nedge_[g],
+                                                     hipMemcpyDeviceToHost, s));
+                        OPT_HIP_CHECK(hipStreamSynchronize(s));
+                        for (int v : hv)
+                            if (v < 0 || v >= npix_) {
+                                fprintf(stderr, "[opt_amd] generic: graph '%s' vertex index %d outside [0, %lld)\n",
+                                        m_.graphs[g].name.c_str(), v, npix_);
+                                exit(1);
+                            }
                     }
-                checked_[sb] = a_.slot[sb];
+                    build_incidence(sb + k, nedge_[g], s);
+                }
             }
+            sb += ns;
         }
+        for (int k = 0; k < sb; ++k) {
+            a_.goff[k] = goff_[k];
+            a_.geid[k] = geid_[k];
+        }
+    }
+    // Edges by vertex for slot array sb: a stable radix sort of (vertex, edge id) pairs and
+    // a histogram + exclusive scan of the vertex counts.
+    void build_incidence(int sb, int E, hipStream_t s) {
+        dfree(goff_[sb]);
+        dfree(geid_[sb]);
+        goff_[sb] = (int*)dmalloc(sizeof(int) * (npix_ + 1));
+        geid_[sb] = (int*)dmalloc(sizeof(int) * std::max(E, 1));
+        OPT_HIP_CHECK(hipMemsetAsync(goff_[sb], 0, sizeof(int) * (npix_ + 1), s));
+        if (E == 0) return;
+        int* keys = (int*)dmalloc(sizeof(int) * E);
+        int* ids = (int*)dmalloc(sizeof(int) * E);
+        const int grid = std::min((E + 255) / 256, 4096);
+        hipLaunchKernelGGL(iota_kernel, dim3(grid), dim3(256), 0, s, ids, E);
+        int bits = 1;
+        while ((1LL << bits) < npix_) ++bits;
+        size_t need = 0, need2 = 0;
+        OPT_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, need, a_.slot[sb], keys, ids, geid_[sb], E, 0, bits, s));
+        OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, need2, goff_[sb], goff_[sb], (int)npix_ + 1, s));
+        need = std::max(need, need2);
+        void* tmp = dmalloc(std::max<size_t>(need, 1));
+        OPT_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(tmp, need, a_.slot[sb], keys, ids, geid_[sb], E, 0, bits, s));
+        hipLaunchKernelGGL(incidence_count, dim3(grid), dim3(256), 0, s, a_.slot[sb], E, goff_[sb]);
+        size_t n2 = need;
+        OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, n2, goff_[sb], goff_[sb], (int)npix_ + 1, s));
+        OPT_HIP_CHECK(hipStreamSynchronize(s));
+        dfree(tmp);
+        dfree(keys);
+        dfree(ids);
     }
 
     StateOptions opts_;
@@ -319,10 +371,13 @@ private:
     void** user_ = nullptr;
     void* dimg_[16] = {};
     int* dslot_[16] = {};
-    const int* checked_[16] = {};
+    unsigned long long fingerprint_[4] = {0, 0, 0, 0};
+    unsigned long long* fp_scratch_ = nullptr;
+    int* goff_[16] = {};
+    int* geid_[16] = {};
     hipModule_t mod_ = nullptr;
     std::vector<hipFunction_t> k_pre_;
-    hipFunction_t k_jtf_{}, k_apply_{}, k_cost_{}, k_jtf_graph_{}, k_apply_graph_{}, k_finish_{}, k_finish_jtf_{};
+    hipFunction_t k_jtf_{}, k_apply_{}, k_cost_{}, k_jtf_graph_{}, k_apply_graph_{};
 };
 
 std::unique_ptr<Plan> make_generic_plan(const ProblemSpec& spec, const StateOptions& opts, const unsigned* dims,

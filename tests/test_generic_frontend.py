@@ -51,8 +51,7 @@ def test_residual_templates(name, count):
                                   "shape_from_shading", "optical_flow"])
 def test_generated_source_compiles(name):
     src = api.generic_source(E(name))
-    for k in ("gen_jtf", "gen_apply", "gen_cost", "gen_jtf_graph", "gen_apply_graph", "gen_finish",
-              "gen_finish_jtf", "block_reduce_publish"):
+    for k in ("gen_jtf", "gen_apply", "gen_cost", "gen_jtf_graph", "gen_apply_graph", "block_reduce_publish"):
         assert k in src
     assert "typedef float T;" in src
     assert "typedef double T;" in api.generic_source(E(name), double=True)

@@ -81,11 +81,22 @@ def materialized(cfg, fused):
     return cfg
 
 
+def generic(cfg):
+    """The same config on the kernels the general front end generates (OPT_AMD_GENERIC=1)."""
+    cfg = dict(cfg)
+    cfg["name"] += " generated kernels"
+    cfg["generic"] = True
+    return cfg
+
+
 CONFIGS = {"iw4096": lambda: iw(4096), "iw2048": lambda: iw(2048), "poisson": poisson, "sfs": sfs,
            "arap": arap, "optical_flow": oflow,
            "iw4096_mat_fused": lambda: materialized(iw(4096), True),
            "iw4096_mat_split": lambda: materialized(iw(4096), False),
-           "poisson_mat_fused": lambda: materialized(poisson(), True)}
+           "poisson_mat_fused": lambda: materialized(poisson(), True),
+           "iw4096_generic": lambda: generic(iw(4096)), "poisson_generic": lambda: generic(poisson()),
+           "sfs_generic": lambda: generic(sfs()), "arap_generic": lambda: generic(arap()),
+           "optical_flow_generic": lambda: generic(oflow())}
 
 
 def spmv_bytes(rows, cols, nnz, x_len):
@@ -96,8 +107,15 @@ def spmv_bytes(rows, cols, nnz, x_len):
 
 def measure(cfg, steps):
     mat = cfg.get("materialized", False)
-    s = OptSolver(cfg["dims"], cfg["energy"], cfg["kind"], double_precision=cfg["double"], materialized=mat,
-                  fused_jtj=cfg.get("fused", False))
+    if cfg.get("generic"):
+        os.environ["OPT_AMD_GENERIC"] = "1"
+    try:
+        s = OptSolver(cfg["dims"], cfg["energy"], cfg["kind"], double_precision=cfg["double"], materialized=mat,
+                      fused_jtj=cfg.get("fused", False))
+    finally:
+        os.environ.pop("OPT_AMD_GENERIC", None)
+    if cfg.get("generic"):
+        assert s.family() == "generic"
     n = s.unknown_count()
     p = torch.randn(n, device="cuda", dtype=cfg["dtype"])
     Ap = torch.empty_like(p)
