@@ -277,15 +277,69 @@ GenSource generate(GModel& m, bool dbl) {
         o << "    }\n}\n";
     }
 
+    // ------------------------------------------------------------ gen_apply_tiled
+    // Two-phase J^T J p over 2-D output tiles whose tile + halo region is 32 x 8 or 16 x 16.
+    // Phase 1 evaluates every centred residual ONCE per centre q of the tile and the halo
+    // its outputs gather from: the non-constant partials d(r, u)(q) and Jp_r(q) = sum_u
+    // d(r, u)(q) p(q + off(u)), kept in LDS. Phase 2 gathers each output x from
+    // d(r, u)(x - off(u)) * Jp_r(x - off(u)). The gather form of createjtjcentered
+    // (o.t:2770-2830, what gen_apply does) re-evaluates each residual instance's partials
+    // for every pixel that reads it; here each is computed once per centre (plus the halo).
+    struct Entry { int r; int u; int dnode; int slot; int ox, oy; };   // slot -1: constant partial
+    std::vector<int> cres;                                           // centred residual ids
+    std::vector<Entry> ents;
+    int nd_slots = 0;
+    int minx = 0, maxx = 0, miny = 0, maxy = 0;
+    int PX = 32, PY = 8, TX = 0, TY = 0, nf = 0;
+    size_t lds = 0;
+    bool tiled = false;
+    if (gs.has_centered && nd == 2) {
+        for (size_t ri = 0; ri < m.residuals.size(); ++ri) {
+            const GResidual& r = m.residuals[ri];
+            if (r.graph >= 0 || r.unknowns.empty()) continue;
+            cres.push_back((int)ri);
+            for (int u : r.unknowns) {
+                const Node& n = P.at(u);
+                const int d = P.diff(r.expr, u);
+                double gv;
+                if (P.is_const(d, &gv) && gv == 0.0) continue;
+                Entry e{(int)cres.size() - 1, u, d, P.is_const(d) ? -1 : nd_slots++, n.off[0], n.off[1]};
+                ents.push_back(e);
+                minx = std::min(minx, n.off[0]); maxx = std::max(maxx, n.off[0]);
+                miny = std::min(miny, n.off[1]); maxy = std::max(maxy, n.off[1]);
+            }
+        }
+        // phase 1 covers the tile + halo in exactly one pass of the 256 threads: pick the
+        // region shape (32 x 8 or 16 x 16) that leaves the most output pixels
+        const int sx = maxx - minx, sy = maxy - miny;
+        if ((16 - sx) * (16 - sy) > (32 - sx) * (8 - sy)) PX = PY = 16;
+        TX = PX - sx;
+        TY = PY - sy;
+        nf = (int)cres.size() + nd_slots;
+        lds = (size_t)nf * PX * PY * (dbl ? 8 : 4);
+        tiled = !cres.empty() && TX > 0 && TY > 0 && lds <= 64 * 1024;
+        // the gather evaluates every distinct (residual, shift) instance per pixel; the
+        // tiled form evaluates each residual once per centre (+ halo) but pays LDS traffic
+        // and barriers. Measured: the gather wins at ~2 instances per
+        // residual (image_warping, poisson, optical_flow), the tiles at ~4.7
+        // (shape_from_shading, radius-2 supports through ComputedArray gradient images).
+        std::set<std::string> inst_keys;
+        for (const Entry& e : ents)
+            inst_keys.insert(std::to_string(e.r) + ":" + std::to_string(e.ox) + "," + std::to_string(e.oy));
+        gs.instances_per_residual = cres.empty() ? 0.0 : (double)inst_keys.size() / cres.size();
+        gs.prefer_tiled = tiled && gs.instances_per_residual > 3.0;
+    }
+
+
     // -------------------------------------------------------------- gen_apply
     {
         o << "extern \"C\" __global__ __launch_bounds__(256) void gen_apply(GenArgs a, const T* __restrict__ p, T* __restrict__ Ap,\n"
              "        const T* __restrict__ dadd, const int* stop, ReduceSlot rs, int finish) {\n"
              "    if (stop && *stop) return;\n"
              "    OPT_COORDS\n"
-             "    T dot = 0;\n"
-             "    for (long long lin = (long long)blockIdx.x * 256 + threadIdx.x; lin < a.npix; lin += (long long)gridDim.x * 256) {\n"
-          << coords;
+             "    T dot = 0;\n";
+        o << "    for (long long lin = (long long)blockIdx.x * 256 + threadIdx.x; lin < a.npix; lin += (long long)gridDim.x * 256) {\n"
+              << coords;
         Body b(m, o, nd, uslot);
         b.line("const bool act = (a.flags[lin] & 1) != 0;");
         std::map<std::string, std::string> jp;   // (residual, shift) -> J p of that instance
@@ -326,6 +380,88 @@ GenSource generate(GModel& m, bool dbl) {
         o << "    }\n"
              "    if (finish) { double v[1] = {(double)dot}; block_reduce_publish<1>(v, rs, blockIdx.x); }\n}\n";
     }
+
+    if (tiled) {
+            gs.has_tiled = true;
+            gs.tiles_x = TX;
+            gs.tiles_y = TY;
+            gs.tiled_lds = lds;
+            const int PXY = PX * PY;
+            o << "extern \"C\" __global__ __launch_bounds__(256) void gen_apply_tiled(GenArgs a, const T* __restrict__ p, T* __restrict__ Ap,\n"
+                 "        const T* __restrict__ dadd, const int* stop, ReduceSlot rs, int finish) {\n"
+                 "    if (stop && *stop) return;\n"
+                 "    OPT_COORDS\n"
+                 "    __shared__ T lds[" << nf * PXY << "];\n"
+                 "    T dot = 0;\n"
+                 "    const int ntx = (W + " << TX - 1 << ") / " << TX << ", nty = (H + " << TY - 1 << ") / " << TY << ";\n"
+                 "    for (int t = blockIdx.x; t < ntx * nty; t += gridDim.x) {\n"
+                 "        const int X0 = (t % ntx) * " << TX << ", Y0 = (t / ntx) * " << TY << ";\n"
+                 "        for (int idx = threadIdx.x; idx < " << PXY << "; idx += 256) {   // one pass\n"
+                 "        const int x = X0 - " << maxx << " + idx % " << PX << ", y = Y0 - " << maxy << " + idx / " << PX << ";\n"
+                 "        const int z = 0; (void)z;\n"
+                 "        if (x >= 0 && x < W && y >= 0 && y < H) {\n";
+            {
+                Body b(m, o, nd, uslot);
+                std::vector<std::string> dname(ents.size());
+                for (size_t ci = 0; ci < cres.size(); ++ci) {
+                    const GResidual& r = m.residuals[cres[ci]];
+                    std::string sum = "(T)0";
+                    for (size_t ei = 0; ei < ents.size(); ++ei) {
+                        if (ents[ei].r != (int)ci) continue;
+                        const std::string dn = b.v(ents[ei].dnode);
+                        if (ents[ei].slot >= 0)
+                            b.line("lds[" + std::to_string((cres.size() + ents[ei].slot) * PXY) + " + idx] = " + dn + ";");
+                        sum += " + " + dn + " * " + b.vec(ents[ei].u, "p");
+                    }
+                    (void)r;
+                    b.line("lds[" + std::to_string(ci * PXY) + " + idx] = " + sum + ";");
+                }
+            }
+            o << "        } else {   // no residual is centred outside the domain (and 0 * stale LDS could be NaN)\n";
+            for (int fi = 0; fi < nf; ++fi)
+                o << "            lds[" << fi * PXY << " + idx] = (T)0;\n";
+            o << "        }\n"
+                 "        }\n"
+                 "        __syncthreads();\n"
+                 "        {\n"
+                 "        const int lx = threadIdx.x % " << TX << ", ly = threadIdx.x / " << TX << ";\n"
+                 "        const int x = X0 + lx, y = Y0 + ly;\n"
+                 "        if (threadIdx.x < " << TX * TY << " && x < W && y < H) {\n"
+                 "        const long long lin = (long long)y * W + x;\n"
+                 "        const bool act = (a.flags[lin] & 1) != 0;\n";
+            for (int k : unk) {
+                const GImage& im = m.images[k];
+                for (int c = 0; c < im.channels; ++c) {
+                    std::string acc = "(T)0";
+                    for (const Entry& e : ents) {
+                        const Node& n = P.at(e.u);
+                        if (n.i != k || n.ch != c) continue;
+                        // centre q = x - off(u), local index in the tile + halo region
+                        const std::string qi = "(lx + " + std::to_string(maxx - e.ox) + ") + (ly + " +
+                                               std::to_string(maxy - e.oy) + ") * " + std::to_string(PX);
+                        std::string dv;
+                        if (e.slot >= 0) {
+                            dv = "lds[" + std::to_string((cres.size() + e.slot) * PXY) + " + " + qi + "]";
+                        } else {
+                            double cv;
+                            P.is_const(e.dnode, &cv);
+                            dv = lit(cv);
+                        }
+                        acc += " + " + dv + " * lds[" + std::to_string(e.r * PXY) + " + " + qi + "]";
+                    }
+                    const std::string el = "a.uoff[" + std::to_string(uslot[k]) + "] + lin * " + std::to_string(im.channels) +
+                                           " + " + std::to_string(c);
+                    o << "        { const long long e = " << el << "; const T acc = " << acc << ";\n"
+                         "          if (finish) { const T pe = p[e]; const T o = act ? acc + (dadd ? dadd[e] * pe : (T)0) : (T)0; Ap[e] = o; dot += pe * o; }\n"
+                         "          else Ap[e] = acc; }\n";
+                }
+            }
+            o << "        }\n"
+                 "        }\n"
+                 "        __syncthreads();\n"
+                 "    }\n"
+                 "    if (finish) { double v[1] = {(double)dot}; block_reduce_publish<1>(v, rs, blockIdx.x); }\n}\n";
+        }
 
     // ------------------------------------------------------- cost (centres + edges)
     {
@@ -510,7 +646,10 @@ GenSource generate(GModel& m, bool dbl) {
              "    double v[1] = {(double)dot};\n    block_reduce_publish<1>(v, rs, blockIdx.x);\n}\n";
     }
     (void)zero3;
-    gs.code = o.str();
+    char note[128];
+    snprintf(note, sizeof(note), "// apply: %s (%.2f residual instances per centred residual)\n",
+             gs.prefer_tiled ? "gen_apply_tiled" : "gen_apply", gs.instances_per_residual);
+    gs.code = note + o.str();
     return gs;
 }
 

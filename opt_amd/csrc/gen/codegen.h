@@ -31,6 +31,11 @@ struct GenSource {
     bool has_graph = false;      // graph residuals present
     int slot_base[4] = {0, 0, 0, 0};   // GenArgs::slot index of graph g's first vertex array
     int n_precompute = 0;              // kernels gen_precompute_0 .. n-1 (ComputedArrays)
+    bool has_tiled = false;            // gen_apply_tiled emitted (2-D centred energies)
+    int tiles_x = 32, tiles_y = 8;     // its output tile
+    size_t tiled_lds = 0;              // its LDS bytes
+    double instances_per_residual = 0; // distinct (residual, shift) instances / centred residuals
+    bool prefer_tiled = false;         // the plan's default apply (static rule, codegen.cpp)
 };
 
 // Generate the kernels for `m` in float (dbl = false) or double.

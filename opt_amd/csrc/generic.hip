@@ -262,6 +262,7 @@ public:
     void model_cost(const T* delta, ReduceSlot rs, hipStream_t s) { launch(k_cost_, s, {&a_, &delta, &rs}); }
 
     const std::string& source() const { return src_.code; }
+    bool tiled_selected() const { return k_apply_ == k_apply_tiled_; }
 
 private:
     size_t image_bytes(size_t i) const {
@@ -288,6 +289,13 @@ private:
                         std::make_pair(&k_cost_, "gen_cost"), std::make_pair(&k_jtf_graph_, "gen_jtf_graph"),
                         std::make_pair(&k_apply_graph_, "gen_apply_graph")})
             OPT_HIP_CHECK(hipModuleGetFunction(kv.first, mod_, kv.second));
+        // the two-phase LDS-tiled apply where the front end emitted one and prefers it
+        // (prefer_tiled: many residual instances per pixel); OPT_AMD_GEN_TILED=0/1 forces
+        if (src_.has_tiled) {
+            OPT_HIP_CHECK(hipModuleGetFunction(&k_apply_tiled_, mod_, "gen_apply_tiled"));
+            const int force = env_int("OPT_AMD_GEN_TILED", -1);
+            if (force == 1 || (force < 0 && src_.prefer_tiled)) k_apply_ = k_apply_tiled_;
+        }
         k_pre_.resize(src_.n_precompute);
         for (int k = 0; k < src_.n_precompute; ++k)
             OPT_HIP_CHECK(hipModuleGetFunction(&k_pre_[k], mod_, ("gen_precompute_" + std::to_string(k)).c_str()));
@@ -377,6 +385,7 @@ private:
     int* geid_[16] = {};
     hipModule_t mod_ = nullptr;
     std::vector<hipFunction_t> k_pre_;
+    hipFunction_t k_apply_tiled_{};
     hipFunction_t k_jtf_{}, k_apply_{}, k_cost_{}, k_jtf_graph_{}, k_apply_graph_{};
 };
 

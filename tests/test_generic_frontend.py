@@ -200,3 +200,12 @@ def test_same_energy_two_spellings_of_reference_intrinsic():
     if not os.path.exists(ref):
         pytest.skip("reference checkout not present")
     assert api.generic_describe(E("intrinsic_image_decomposition")) == api.generic_describe(ref)
+
+
+@pytest.mark.parametrize("name,tiled", [("image_warping", False), ("poisson_image_editing", False),
+                                        ("optical_flow", False), ("shape_from_shading", True)])
+def test_apply_variant_rule(name, tiled):
+    """Static choice between the gather and the LDS-tiled apply (codegen.cpp): tiles when
+    the energy has many residual instances per centred residual (measured crossover)."""
+    head = api.generic_source(E(name)).splitlines()[0]
+    assert head.startswith("// apply: " + ("gen_apply_tiled" if tiled else "gen_apply "))
