@@ -299,8 +299,11 @@ __global__ void count_heads(const int* keys, int E, int* counts) {
 // saveJToCRS / saveJToCRS_Graph (solverGPUGaussNewton.t:1004-1022, 1287-1305) with
 // generateDumpJ (:385-442). Rows: the fit residuals first (centred, vertex v owns rows
 // 3v + c, one nonzero {O_c(v): wf [has target]}), then the graph residuals (edge e owns
-// rows 3N + 3e + c, five nonzeros {O_c(v0): wr, O_c(v1): -wr, A_j(v0): -wr (dR_j d_e)_c}),
-// columns = unknown indices ([Offset 3N | Angle 3N]) sorted inside each row.
+// rows 3N + 3e + c, nonzeros {O_c(v0): wr, O_c(v1): -wr, A_j(v0): -wr (dR_j d_e)_c} for
+// the angles row c of Rotate3D reads — all three for x and y, alpha and beta for z
+// (lib.t:84-97: row z is -sin b, cos b sin a, cos b cos a), so 5 + 5 + 4 per edge as the
+// template's unknown accesses), columns = unknown indices ([Offset 3N | Angle 3N]) sorted
+// inside each row.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void arap_dump_fit(Args<T> a, int E, int* __restrict__ rowPtr,
                                                         int* __restrict__ colInd, T* __restrict__ val) {
@@ -329,24 +332,25 @@ __global__ __launch_bounds__(kBlock) void arap_dump_edges(Args<T> a, const int* 
 #pragma unroll
         for (int j = 0; j < 3; ++j) col[j] = mv(dR[j], dd);
         for (int c = 0; c < 3; ++c) {
-            const long long row = 3 * N + 3LL * e + c, nz = 3 * N + 15LL * e + 5 * c;
+            const long long row = 3 * N + 3LL * e + c, nz = 3 * N + 14LL * e + 5 * c;
+            const int K = c == 2 ? 4 : 5;   // row z has no gamma access
             rowPtr[row] = (int)nz;
             int cc[5] = {(int)(3 * v0 + c), (int)(3 * v1 + c), (int)(3 * N + 3 * v0), (int)(3 * N + 3 * v0 + 1),
                          (int)(3 * N + 3 * v0 + 2)};
             T vv[5] = {a.wr, -a.wr, -a.wr * (c == 0 ? col[0].x : c == 1 ? col[0].y : col[0].z),
                        -a.wr * (c == 0 ? col[1].x : c == 1 ? col[1].y : col[1].z),
                        -a.wr * (c == 0 ? col[2].x : c == 1 ? col[2].y : col[2].z)};
-            for (int i = 1; i < 5; ++i)   // sortCol
+            for (int i = 1; i < K; ++i)   // sortCol
                 for (int j = i; j > 0 && cc[j] < cc[j - 1]; --j) {
                     const int tc = cc[j]; cc[j] = cc[j - 1]; cc[j - 1] = tc;
                     const T tv = vv[j]; vv[j] = vv[j - 1]; vv[j - 1] = tv;
                 }
-            for (int q = 0; q < 5; ++q) {
+            for (int q = 0; q < K; ++q) {
                 colInd[nz + q] = cc[q];
                 val[nz + q] = vv[q];
             }
         }
-        if (e == E - 1) rowPtr[3 * N + 3LL * E] = (int)(3 * N + 15LL * E);
+        if (e == E - 1) rowPtr[3 * N + 3LL * E] = (int)(3 * N + 14LL * E);
     }
 }
 
@@ -471,9 +475,9 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
     // materialized Jacobian (csr.h): 3 fit rows per vertex (1 nonzero each), then 3 rows
-    // per directed edge (5 nonzeros each)
+    // per directed edge (5 + 5 + 4 nonzeros)
     long long jacobian_rows() const { return 3LL * N_ + 3LL * E_; }
-    long long jacobian_nnz() const { return 3LL * N_ + 15LL * E_; }
+    long long jacobian_nnz() const { return 3LL * N_ + 14LL * E_; }
     void dump_j(int* rowPtr, int* colInd, T* val, hipStream_t s) {
         hipLaunchKernelGGL((arap::arap_dump_fit<T>), dim3(std::max(1, std::min((N_ + 255) / 256, 4096))), dim3(kBlock),
                            0, s, a_, E_, rowPtr, colInd, val);

@@ -18,6 +18,7 @@
 // Reads outside the index space are zero (Image:get, o.t:856-862); centred residuals are
 // wrapped in their bounding-box test at classification time.
 #include "codegen.h"
+#include <algorithm>
 #include <cstdio>
 #include <functional>
 #include <map>
@@ -462,6 +463,83 @@ GenSource generate(GModel& m, bool dbl) {
                  "    }\n"
                  "    if (finish) { double v[1] = {(double)dot}; block_reduce_publish<1>(v, rs, blockIdx.x); }\n}\n";
         }
+
+    // ------------------------------------------------------------ gen_dump_j_<i>
+    // saveJToCRS / saveJToCRS_Graph (solverGPUGaussNewton.t:1004-1022, 1287-1305) with
+    // generateDumpJ (:385-442): the residuals grouped into energy specs by domain in order
+    // of first appearance (toenergyspecs); element e of spec i owns rows row_base + e R_i +
+    // r and nonzeros nnz_base + e NNZ_i + ...; each row lists every unknown access of its
+    // template (zero partials included), column = image offset + channels * tooffset +
+    // channel wrapped into [0, nUnknowns) (wrap, :365-381), sorted by column (sortCol).
+    // Every element is written, excluded ones included, as the reference does.
+    {
+        std::vector<int> order;   // spec domains in order of first appearance
+        for (auto& r : m.residuals)
+            if (std::find(order.begin(), order.end(), r.graph) == order.end()) order.push_back(r.graph);
+        for (size_t si = 0; si < order.size(); ++si) {
+            const int g = order[si];
+            std::vector<const GResidual*> rs;
+            int npe = 0;
+            for (auto& r : m.residuals)
+                if (r.graph == g) { rs.push_back(&r); npe += (int)r.unknowns.size(); }
+            gs.dump.push_back({g, (int)rs.size(), npe});
+            o << "extern \"C\" __global__ __launch_bounds__(256) void gen_dump_j_" << si
+              << "(GenArgs a, int* __restrict__ rowPtr, int* __restrict__ colInd, T* __restrict__ val,\n"
+                 "        long long row_base, long long nnz_base, long long nunk) {\n"
+                 "    OPT_COORDS\n";
+            if (g < 0) {
+                o << "    for (long long lin = (long long)blockIdx.x * 256 + threadIdx.x; lin < a.npix; lin += (long long)gridDim.x * 256) {\n"
+                  << coords << "        const long long el = lin;\n";
+            } else {
+                o << "    for (long long el = (long long)blockIdx.x * 256 + threadIdx.x; el < a.nedge[" << g
+                  << "]; el += (long long)gridDim.x * 256) {\n";
+                for (size_t sl = 0; sl < m.graphs[g].slot_names.size(); ++sl)
+                    o << "        const int v" << sl << " = a.slot[" << gs.slot_base[g] + sl << "][el];\n";
+            }
+            Body b(m, o, nd, uslot);
+            int nz = 0;
+            for (size_t ri = 0; ri < rs.size(); ++ri) {
+                const GResidual& r = *rs[ri];
+                const int K = (int)r.unknowns.size();
+                b.line("rowPtr[row_base + el * " + std::to_string(rs.size()) + " + " + std::to_string(ri) +
+                       "] = (int)(nnz_base + el * " + std::to_string(npe) + " + " + std::to_string(nz) + ");");
+                if (K == 0) continue;
+                const std::string cc = "cc" + std::to_string(ri), vv = "vv" + std::to_string(ri);
+                b.line("long long " + cc + "[" + std::to_string(K) + "]; T " + vv + "[" + std::to_string(K) + "];");
+                int q = 0;
+                for (int u : r.unknowns) {
+                    const Node& n = P.at(u);
+                    const int ch = m.images[n.i].channels;
+                    std::string idx;
+                    if (n.slot >= 0) {
+                        idx = "(long long)v" + std::to_string(n.slot);
+                    } else {   // tooffset of the (possibly outside) access
+                        idx = "(el + " + std::to_string(n.off[0]) + "LL";
+                        if (nd > 1) idx += " + " + std::to_string(n.off[1]) + "LL * W";
+                        if (nd > 2) idx += " + " + std::to_string(n.off[2]) + "LL * W * H";
+                        idx += ")";
+                    }
+                    const int d = P.diff(r.expr, u);
+                    const std::string dv = b.v(d);
+                    b.line(cc + "[" + std::to_string(q) + "] = a.uoff[" + std::to_string(uslot[n.i]) + "] + " +
+                           std::to_string(ch) + " * " + idx + " + " + std::to_string(n.ch) + "; " + vv + "[" +
+                           std::to_string(q) + "] = " + dv + ";");
+                    ++q;
+                }
+                const std::string Ks = std::to_string(K);
+                b.line("for (int i = 0; i < " + Ks + "; ++i) { const long long c = " + cc + "[i]; " + cc +
+                       "[i] = c < 0 ? c + nunk : (c >= nunk ? c - nunk : c); }");
+                b.line("for (int i = 1; i < " + Ks + "; ++i) for (int j = i; j > 0 && " + cc + "[j] < " + cc +
+                       "[j - 1]; --j) { const long long tc = " + cc + "[j]; " + cc + "[j] = " + cc + "[j - 1]; " + cc +
+                       "[j - 1] = tc; const T tv = " + vv + "[j]; " + vv + "[j] = " + vv + "[j - 1]; " + vv + "[j - 1] = tv; }");
+                b.line("for (int i = 0; i < " + Ks + "; ++i) { colInd[nnz_base + el * " + std::to_string(npe) + " + " +
+                       std::to_string(nz) + " + i] = (int)" + cc + "[i]; val[nnz_base + el * " + std::to_string(npe) +
+                       " + " + std::to_string(nz) + " + i] = " + vv + "[i]; }");
+                nz += K;
+            }
+            o << "    }\n}\n";
+        }
+    }
 
     // ------------------------------------------------------- cost (centres + edges)
     {

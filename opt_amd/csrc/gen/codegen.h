@@ -3,6 +3,7 @@
 // createmodelcost, o.t:2770-3129, and of the Terra emitter, o.t:1949-2665).
 #pragma once
 #include <string>
+#include <vector>
 #include "model.h"
 
 // Kernel argument block shared by the host (generic.hip) and the generated source: the
@@ -36,6 +37,10 @@ struct GenSource {
     size_t tiled_lds = 0;              // its LDS bytes
     double instances_per_residual = 0; // distinct (residual, shift) instances / centred residuals
     bool prefer_tiled = false;         // the plan's default apply (static rule, codegen.cpp)
+    // materialized J (saveJToCRS): one kernel gen_dump_j_<i> per energy spec, in order;
+    // spec i: domain (-1 centred, else graph id), residual rows and nonzeros per element
+    struct DumpSpec { int graph; int rows; int nnz; };
+    std::vector<DumpSpec> dump;
 };
 
 // Generate the kernels for `m` in float (dbl = false) or double.

@@ -261,10 +261,32 @@ public:
     }
     void model_cost(const T* delta, ReduceSlot rs, hipStream_t s) { launch(k_cost_, s, {&a_, &delta, &rs}); }
 
+    // materialized Jacobian (useMaterializedJTJ, csr.h): the generated saveJToCRS kernels
+    long long jacobian_rows() const {
+        long long r = 0;
+        for (auto& d : src_.dump) r += elements(d.graph) * d.rows;
+        return r;
+    }
+    long long jacobian_nnz() const {
+        long long z = 0;
+        for (auto& d : src_.dump) z += elements(d.graph) * d.nnz;
+        return z;
+    }
+    void dump_j(int* rowPtr, int* colInd, T* val, hipStream_t s) {
+        long long rb = 0, zb = 0;
+        for (size_t i = 0; i < src_.dump.size(); ++i) {
+            launch(k_dump_[i], s, {&a_, &rowPtr, &colInd, &val, &rb, &zb, &n_});
+            rb += elements(src_.dump[i].graph) * src_.dump[i].rows;
+            zb += elements(src_.dump[i].graph) * src_.dump[i].nnz;
+        }
+        OPT_HIP_CHECK(hipMemsetD32Async(rowPtr + rb, (int)zb, 1, s));
+    }
+
     const std::string& source() const { return src_.code; }
     bool tiled_selected() const { return k_apply_ == k_apply_tiled_; }
 
 private:
+    long long elements(int graph) const { return graph < 0 ? npix_ : nedge_[graph]; }
     size_t image_bytes(size_t i) const {
         return (size_t)npix_ * m_.images[i].channels * elem_size(m_.images[i], sizeof(T) == 8);
     }
@@ -296,6 +318,9 @@ private:
             const int force = env_int("OPT_AMD_GEN_TILED", -1);
             if (force == 1 || (force < 0 && src_.prefer_tiled)) k_apply_ = k_apply_tiled_;
         }
+        k_dump_.resize(src_.dump.size());
+        for (size_t k = 0; k < src_.dump.size(); ++k)
+            OPT_HIP_CHECK(hipModuleGetFunction(&k_dump_[k], mod_, ("gen_dump_j_" + std::to_string(k)).c_str()));
         k_pre_.resize(src_.n_precompute);
         for (int k = 0; k < src_.n_precompute; ++k)
             OPT_HIP_CHECK(hipModuleGetFunction(&k_pre_[k], mod_, ("gen_precompute_" + std::to_string(k)).c_str()));
@@ -384,17 +409,13 @@ private:
     int* goff_[16] = {};
     int* geid_[16] = {};
     hipModule_t mod_ = nullptr;
-    std::vector<hipFunction_t> k_pre_;
+    std::vector<hipFunction_t> k_pre_, k_dump_;
     hipFunction_t k_apply_tiled_{};
     hipFunction_t k_jtf_{}, k_apply_{}, k_cost_{}, k_jtf_graph_{}, k_apply_graph_{};
 };
 
 std::unique_ptr<Plan> make_generic_plan(const ProblemSpec& spec, const StateOptions& opts, const unsigned* dims,
                                         std::string* err) {
-    if (opts.materialized) {
-        *err = "generic: no materialized Jacobian (useMaterializedJTJ) for generated energies";
-        return nullptr;
-    }
     ProblemSpec s = spec;
     gen::GModel m;
     if (!gen::build_model(spec.text, &m, err)) return nullptr;

@@ -83,6 +83,7 @@ Opt_Problem* Opt_ProblemDefine(Opt_State* state, const char* filename, const cha
     auto* p = new Opt_Problem();
     p->spec.filename = filename;
     p->spec.solverkind = kind;
+    p->spec.text = ss.str();
     std::string err;
     bool ok = optamd::parse_energy(ss.str(), &p->spec, &err) && optamd::classify(&p->spec, &err);
     // energies no hand-written family recognises (or all, with OPT_AMD_GENERIC=1) go to the
@@ -119,6 +120,17 @@ Opt_Plan* Opt_ProblemPlan(Opt_State* state, Opt_Problem* problem, unsigned int* 
     OPT_HIP_CHECK(hipGetDevice(&state->device));
     std::string err;
     auto impl = optamd::make_plan(problem->spec, state->opts, dimensions, &err);
+    if (!impl && problem->spec.family != "generic") {
+        // a hand-written family that cannot serve these options (e.g. useMaterializedJTJ
+        // for shape_from_shading): the generated kernels of the same energy can
+        optamd::ProblemSpec g = problem->spec;
+        std::string gerr;
+        if (optamd::generic_accepts(g.text, &g, &gerr)) {
+            impl = optamd::make_plan(g, state->opts, dimensions, &gerr);
+            if (impl) err.clear();
+            else err += "; generated kernels: " + gerr;
+        }
+    }
     if (!impl) {
         fprintf(stderr, "[opt_amd] plan failed: %s\n", err.c_str());
         return nullptr;
