@@ -35,7 +35,7 @@ static __global__ void graph_fingerprint_kernel(const int* __restrict__ v, int E
 inline unsigned long long graph_fingerprint(const int* const* arrays, int n, int E, hipStream_t s,
                                             unsigned long long* d) {
     OPT_HIP_CHECK(hipMemsetAsync(d, 0, sizeof(unsigned long long), s));
-    const int grid = std::max(1, std::min((E + 255) / 256, 256));   // one atomic per block
+    const int grid = std::max(1, std::min((E + 255) / 256, 1024));   // one atomic per block
     for (int k = 0; k < n; ++k)
         if (E > 0)
             hipLaunchKernelGGL(graph_fingerprint_kernel, dim3(grid), dim3(256), 0, s, arrays[k], E,
