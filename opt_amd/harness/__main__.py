@@ -105,6 +105,7 @@ def run(argv=None) -> int:
     iters = {"gn": [], "lm": []}
     final = {"gn": 0.0, "lm": 0.0}
     last = None
+    state = {"w_fit": 10.0}   # optical_flow: CombinedSolver::m_weightFit persists across solves
     for key, use, kind in (("gn", o["useOpt"], "gaussNewtonGPU"), ("lm", o["useOptLM"], "LMGPU")):
         if not use:
             continue
@@ -114,14 +115,7 @@ def run(argv=None) -> int:
         s = OptSolver(problems.dims(name, w), energy, kind, backend=o["backend"], double_precision=a.double,
                       materialized=o["useMaterializedJTJ"], fused_jtj=o["useFusedJTJ"], numthreads=o["numthreads"])
         s.set_solver_params({"nIterations": o["nIterations"], "lIterations": o["lIterations"]})
-        outer = o["oIterations"] if name == "image_warping" else 1
-        for i in range(outer):
-            if name == "image_warping" and outer > 1:   # setConstraintImage((i+1) / numIter)
-                w2 = problems.image_warping(w["Mask"].reshape(w["H"], w["W"]),
-                                            formats.read_constraints(os.path.join(
-                                                a.data, problems.FILES[name][o["file"]][1])),
-                                            (i + 1) / outer)
-                prm[3] = conv(np.ascontiguousarray(w2["Constraints"]))
+        for prm in schedule(name, a, o, w, prm, conv, state):
             its = results.profiled_solve(s, prm)
             iters[key] += its
             print("final cost=%.16f" % s.cost(), flush=True)
@@ -136,6 +130,42 @@ def run(argv=None) -> int:
             write_result(name, last[0], last[1], a.out)
     print(results.report_final_costs(name, o["useOpt"], o["useOptLM"], final["gn"], final["lm"]))
     return 0
+
+
+def schedule(name, a, o, w, prm, conv, state):
+    """The example's sequence of single solves (CombinedSolverBase::singleSolve and the
+    examples' solveAll overrides), yielding the problem parameters of each."""
+    numIter = max(1, o["oIterations"])
+    if name == "image_warping":
+        # numIter solves with the constraints blended by alpha = (i + 1) / numIter
+        # (examples/image_warping/src/CombinedSolver.h:150-160, setConstraintImage :199-219)
+        cons = formats.read_constraints(os.path.join(a.data, problems.FILES[name][o["file"]][1]))
+        for i in range(numIter):
+            if numIter > 1:
+                w2 = problems.image_warping(w["Mask"].reshape(w["H"], w["W"]), cons, (i + 1) / numIter)
+                prm[3] = conv(np.ascontiguousarray(w2["Constraints"]))
+            yield prm
+    elif name == "optical_flow":
+        # two pyramid levels (sigma 5, then 1), coarse first; before each level every flow
+        # field is reset to zero (preSingleSolve -> resetGPU), and w_fit grows by
+        # (50 - 10) / (numIter * levels) before every solve (preNonlinearSolve), the weight
+        # carried over between solvers (examples/optical_flow/src/CombinedSolver.h:40-95)
+        levels = {lv: problems.load_example(name, a.data, file=o["file"], stride=o["stride"], level=lv)
+                  for lv in (1, 0)}
+        step = np.float32(np.float32(50.0) - np.float32(10.0)) / np.float32(numIter * 2)
+        ut = np.float64 if a.double else np.float32
+        for lv in (1, 0):
+            L = levels[lv]
+            for k in ("I", "I_hat", "I_hat_dx", "I_hat_dy"):
+                prm[3 + ("I", "I_hat", "I_hat_dx", "I_hat_dy").index(k)] = conv(np.ascontiguousarray(L[k]))
+            for _ in range(numIter):
+                prm[2] = conv(np.zeros(2 * L["W"] * L["H"], ut))
+                state["w_fit"] = float(np.float32(state["w_fit"]) + step)
+                prm[0] = float(np.sqrt(np.float32(state["w_fit"]), dtype=np.float32))
+                yield prm
+    else:
+        for _ in range(numIter):
+            yield prm
 
 
 def write_result(name, w, prm, out):

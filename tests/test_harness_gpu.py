@@ -78,10 +78,33 @@ def test_harness_runs_example(tmp_path, name, solver):
     assert rc == 0
     txt = buf.getvalue()
     costs = [float(l.split("=")[1]) for l in txt.splitlines() if l.startswith("final cost=")]
-    assert len(costs) == 1
+    # optical_flow solves its two pyramid levels (coarse first, w_fit 30 then 50)
+    assert len(costs) == (2 if name == "optical_flow" else 1)
     kind = "gaussNewtonGPU" if solver == "--useOpt" else "LMGPU"
     assert costs[0] == pytest.approx(direct_cost(name, data, kind), rel=1e-12)
     lines = open(os.path.join(out, "results.csv")).read().splitlines()
     assert lines[0].startswith("Iter, Ceres Error") and len(lines) >= 3
     assert "**Final Costs**" in txt
     assert len(os.listdir(out)) == 2   # results.csv + the example's result file
+
+
+def test_optical_flow_schedule_matches_the_reference_harness(tmp_path):
+    """CombinedSolver::solveAll of examples/optical_flow: level 1 (sigma 5) with w_fit 30,
+    then level 0 (sigma 1) from a zero flow (preSingleSolve resets every level) with w_fit
+    50, w_reg 0.1; the second logged cost equals that solve run directly."""
+    import torch
+
+    data = str(tmp_path / "data")
+    write_data(data, np.random.default_rng(1))
+    buf = io.StringIO()
+    with redirect_stdout(buf):
+        run(["optical_flow", "--data", data, "--out", str(tmp_path / "o"), "--backend", "backend_cuda", "--useOpt",
+             "--nIterations", "2", "--lIterations", "5", "--config", str(tmp_path / "none")])
+    costs = [float(l.split("=")[1]) for l in buf.getvalue().splitlines() if l.startswith("final cost=")]
+    w = problems.load_example("optical_flow", data, level=0)
+    w["w_fitSqrt"] = float(np.sqrt(np.float32(50.0)))
+    prm = problems.problem_params("optical_flow", w, lambda x: torch.from_numpy(x).cuda())
+    s = OptSolver(problems.dims("optical_flow", w), os.path.join(ROOT, "energies", "optical_flow.t"))
+    s.set_solver_params({"nIterations": 2, "lIterations": 5})
+    s.solve(prm)
+    assert costs[1] == pytest.approx(s.cost(), rel=1e-12)
