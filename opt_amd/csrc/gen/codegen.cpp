@@ -131,7 +131,7 @@ private:
     }
     std::string lin(const int* off) const {
         if (nd_ == 1) return "(long long)" + coord(0, off[0]);
-        if (nd_ == 2) return "((long long)" + coord(1, off[1]) + " * W + " + coord(0, off[0]) + ")";
+        if (nd_ == 2) return "((long long)(" + coord(1, off[1]) + " - a.ymem0) * W + " + coord(0, off[0]) + ")";
         return "(((long long)" + coord(2, off[2]) + " * H + " + coord(1, off[1]) + ") * W + " + coord(0, off[0]) + ")";
     }
     std::string img_ptr(int i) const {
@@ -200,9 +200,13 @@ GenSource generate(GModel& m, bool dbl) {
          "    const T u = ((T)1 - xn) * opt_tap(im, nch, c, x0, y0, W, H) + xn * opt_tap(im, nch, c, x1, y0, W, H);\n"
          "    const T b = ((T)1 - xn) * opt_tap(im, nch, c, x0, y1, W, H) + xn * opt_tap(im, nch, c, x1, y1, W, H);\n"
          "    return ((T)1 - yn) * u + yn * b;\n}\n";
-    const char* coords =
-        "        const int x = (int)(lin % W); const int y = (int)((lin / W) % H); const int z = (int)(lin / ((long long)W * H));\n"
-        "        (void)x; (void)y; (void)z;\n";
+    // memory pixel index -> coordinates; 2-D energies may hold a row slab whose memory row 0
+    // is global row a.ymem0 (coordinates, bounds and Index(1) are global)
+    const char* coords = nd == 2
+        ? "        const int x = (int)(lin % W); const int y = (int)(lin / W) + a.ymem0; const int z = 0;\n"
+          "        (void)x; (void)y; (void)z;\n"
+        : "        const int x = (int)(lin % W); const int y = (int)((lin / W) % H); const int z = (int)(lin / ((long long)W * H));\n"
+          "        (void)x; (void)y; (void)z;\n";
 
     // centred instances per output (unknown image, channel)
     std::map<std::pair<int, int>, std::vector<std::pair<Instance, int>>> inst;   // -> (instance, support node)
@@ -226,7 +230,7 @@ GenSource generate(GModel& m, bool dbl) {
         const GComputed& c = m.computed[k];
         o << "extern \"C\" __global__ __launch_bounds__(256) void gen_precompute_" << k << "(GenArgs a) {\n"
              "    OPT_COORDS\n"
-             "    for (long long lin = (long long)blockIdx.x * 256 + threadIdx.x; lin < a.npix; lin += (long long)gridDim.x * 256) {\n"
+             "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
           << coords;
         Body b(m, o, nd, uslot);
         const int nch = (int)c.expr.size();
@@ -243,7 +247,7 @@ GenSource generate(GModel& m, bool dbl) {
     {
         o << "extern \"C\" __global__ __launch_bounds__(256) void gen_jtf(GenArgs a, T* __restrict__ r, T* __restrict__ diag) {\n"
              "    OPT_COORDS\n"
-             "    for (long long lin = (long long)blockIdx.x * 256 + threadIdx.x; lin < a.npix; lin += (long long)gridDim.x * 256) {\n"
+             "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
           << coords;
         Body b(m, o, nd, uslot);
         const std::string act = m.exclude >= 0 ? "(" + b.v(m.exclude) + " == (T)0)" : "true";
@@ -339,7 +343,7 @@ GenSource generate(GModel& m, bool dbl) {
              "    if (stop && *stop) return;\n"
              "    OPT_COORDS\n"
              "    T dot = 0;\n";
-        o << "    for (long long lin = (long long)blockIdx.x * 256 + threadIdx.x; lin < a.npix; lin += (long long)gridDim.x * 256) {\n"
+        o << "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
               << coords;
         Body b(m, o, nd, uslot);
         b.line("const bool act = (a.flags[lin] & 1) != 0;");
@@ -428,7 +432,7 @@ GenSource generate(GModel& m, bool dbl) {
                  "        const int lx = threadIdx.x % " << TX << ", ly = threadIdx.x / " << TX << ";\n"
                  "        const int x = X0 + lx, y = Y0 + ly;\n"
                  "        if (threadIdx.x < " << TX * TY << " && x < W && y < H) {\n"
-                 "        const long long lin = (long long)y * W + x;\n"
+                 "        const long long lin = (long long)(y - a.ymem0) * W + x;\n"
                  "        const bool act = (a.flags[lin] & 1) != 0;\n";
             for (int k : unk) {
                 const GImage& im = m.images[k];
@@ -488,7 +492,7 @@ GenSource generate(GModel& m, bool dbl) {
                  "        long long row_base, long long nnz_base, long long nunk) {\n"
                  "    OPT_COORDS\n";
             if (g < 0) {
-                o << "    for (long long lin = (long long)blockIdx.x * 256 + threadIdx.x; lin < a.npix; lin += (long long)gridDim.x * 256) {\n"
+                o << "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
                   << coords << "        const long long el = lin;\n";
             } else {
                 o << "    for (long long el = (long long)blockIdx.x * 256 + threadIdx.x; el < a.nedge[" << g
@@ -547,7 +551,7 @@ GenSource generate(GModel& m, bool dbl) {
              "    OPT_COORDS\n"
              "    T acc = 0;\n";
         if (gs.has_centered) {
-            o << "    for (long long lin = (long long)blockIdx.x * 256 + threadIdx.x; lin < a.npix; lin += (long long)gridDim.x * 256) {\n"
+            o << "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
               << coords;
             Body b(m, o, nd, uslot);
             if (m.exclude >= 0) b.line("if (" + b.v(m.exclude) + " != (T)0) continue;");

@@ -20,6 +20,8 @@
         int nedge[4];               /* edges per graph */                                   \
         unsigned char* flags;       /* bit0: active (not excluded) */                       \
         long long uoff[4];          /* offset of each unknown image in the vector */        \
+        int ymem0;                  /* 2-D row slabs: global row of memory row 0 */          \
+        long long own_lo, own_hi;   /* owned pixels (memory indices) */                      \
     };
 
 namespace optamd {

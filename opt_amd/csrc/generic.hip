@@ -121,9 +121,9 @@ public:
     using T = TT;
     static constexpr const char* kName = "generic";
     static constexpr const char* kApplyName = "gen_apply";
-    static constexpr bool kSlabs = false;
+    static constexpr bool kSlabs = true;   // decided per energy: slab_refusal()
 
-    GenericOp(const ProblemSpec& spec, const StateOptions& opts, Domain) : opts_(opts) {
+    GenericOp(const ProblemSpec& spec, const StateOptions& opts, Domain dom) : opts_(opts), dom_(dom) {
         std::string err;
         if (!gen::build_model(spec.text, &m_, &err)) {
             fprintf(stderr, "[opt_amd] generic: %s\n", err.c_str());
@@ -134,6 +134,15 @@ public:
         dims_[0] = dims_[1] = dims_[2] = 1;
         for (size_t k = 0; k < u0.dims.size(); ++k) dims_[k] = (int)spec.dim_values.at(m_.dims[u0.dims[k]].index);
         npix_ = (long long)dims_[0] * dims_[1] * dims_[2];
+        own_lo_ = 0;
+        own_hi_ = npix_;
+        if (u0.dims.size() == 2) {   // a row slab (StencilPlan::set_decomposition) or the whole image
+            npix_ = dom.npix_mem();
+            ymem0_ = dom.y_mem0;
+            own_lo_ = dom.off(0, dom.y_lo);
+            own_hi_ = dom.off(0, dom.y_hi);
+        }
+        halo_ = row_halo();
         for (size_t g = 0; g < m_.graphs.size(); ++g) {
             long long e = 1;
             for (int d : m_.graphs[g].dims) e *= spec.dim_values.at(m_.dims[d].index);
@@ -181,7 +190,19 @@ public:
         L.N = npix_;
         return L;
     }
-    int halo() const { return 0; }
+    int halo() const { return halo_; }
+    // Why this energy cannot run on row slabs ("" = it can). Graph and sampled reads are
+    // data-dependent (as the optical_flow / ARAP families), slabs split the 2nd dimension.
+    std::string slab_refusal() const {
+        if (m_.unknown_dims() != 2) return "generic: row-slab decomposition needs a 2-D energy";
+        if (!m_.graphs.empty()) return "generic: no row-slab decomposition for graph energies";
+        for (auto& r : m_.residuals) {
+            bool sample = false;
+            m_.pool.visit(r.expr, [&](int, const gen::Node& n) { sample |= n.op == gen::Op::Sample; });
+            if (sample) return "generic: no row-slab decomposition with sampled images (data-dependent reads)";
+        }
+        return "";
+    }
     int stencil_blocks() const {
         long long w = std::max(npix_, n_);
         for (int e : nedge_) w = std::max<long long>(w, e);
@@ -227,6 +248,9 @@ public:
         if (sb > 0) check_graphs(s);
         for (int k = 0; k < 3; ++k) a_.dims[k] = dims_[k];
         a_.npix = npix_;
+        a_.ymem0 = ymem0_;
+        a_.own_lo = own_lo_;
+        a_.own_hi = own_hi_;
         for (size_t k = 0; k < unk_.size(); ++k) a_.uoff[k] = uoff_[k];
     }
     void unbind(hipStream_t s) {
@@ -238,7 +262,12 @@ public:
     void precompute(hipStream_t s) {
         for (hipFunction_t f : k_pre_) launch(f, s, {&a_});
     }
-    void computed_planes(std::vector<HaloPlane>&) const {}
+    // ComputedArray values and gradient images: exchanged after every precompute
+    void computed_planes(std::vector<HaloPlane>& v) const {
+        for (size_t i = 0; i < m_.images.size(); ++i)
+            if (m_.images[i].internal)
+                v.push_back({dimg_[i], sizeof(T) * m_.images[i].channels * (size_t)dims_[0]});
+    }
 
     void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
         a_.flags = flags;
@@ -287,6 +316,35 @@ public:
 
 private:
     long long elements(int graph) const { return graph < 0 ? npix_ : nedge_[graph]; }
+    // Rows a slab must hold beyond its own: the widest vertical reach of any residual
+    // instance that touches an owned unknown (the span of its reads incl. ComputedArray
+    // boxes), of the ComputedArrays' own expressions, and of the exclusion test.
+    int row_halo() const {
+        if (m_.unknown_dims() != 2) return 0;
+        auto reach = [&](int e, int* lo, int* hi) {
+            m_.pool.visit(e, [&](int, const gen::Node& n) {
+                if (n.op != gen::Op::Read || n.slot >= 0) return;
+                int clo = 0, chi = 0;
+                for (auto& c : m_.computed)
+                    if (c.image == n.i) { clo = c.lo[1]; chi = c.hi[1]; }
+                *lo = std::min(*lo, n.off[1] + clo);
+                *hi = std::max(*hi, n.off[1] + chi);
+            });
+        };
+        int h = 0;
+        for (auto& r : m_.residuals) {
+            int lo = 0, hi = 0;
+            reach(r.expr, &lo, &hi);
+            h = std::max(h, hi - lo);
+        }
+        for (auto& c : m_.computed) h = std::max({h, -c.lo[1], c.hi[1]});
+        if (m_.exclude >= 0) {
+            int lo = 0, hi = 0;
+            reach(m_.exclude, &lo, &hi);
+            h = std::max({h, -lo, hi});
+        }
+        return std::max(h, 1);
+    }
     size_t image_bytes(size_t i) const {
         return (size_t)npix_ * m_.images[i].channels * elem_size(m_.images[i], sizeof(T) == 8);
     }
@@ -313,7 +371,9 @@ private:
             OPT_HIP_CHECK(hipModuleGetFunction(kv.first, mod_, kv.second));
         // the two-phase LDS-tiled apply where the front end emitted one and prefers it
         // (prefer_tiled: many residual instances per pixel); OPT_AMD_GEN_TILED=0/1 forces
-        if (src_.has_tiled) {
+        // (row slabs use the gather: its reads stay within row_halo() of the owned rows)
+        const bool slab = dom_.mem_rows != dom_.H || dom_.y_lo != 0;
+        if (src_.has_tiled && !slab) {
             OPT_HIP_CHECK(hipModuleGetFunction(&k_apply_tiled_, mod_, "gen_apply_tiled"));
             const int force = env_int("OPT_AMD_GEN_TILED", -1);
             if (force == 1 || (force < 0 && src_.prefer_tiled)) k_apply_ = k_apply_tiled_;
@@ -393,6 +453,9 @@ private:
     }
 
     StateOptions opts_;
+    Domain dom_;
+    int ymem0_ = 0, halo_ = 0;
+    long long own_lo_ = 0, own_hi_ = 0;
     gen::GModel m_;
     gen::GenSource src_;
     std::vector<int> unk_;
@@ -423,9 +486,14 @@ std::unique_ptr<Plan> make_generic_plan(const ProblemSpec& spec, const StateOpti
     for (auto& d : m.dims) maxidx = std::max(maxidx, d.index);
     s.dim_values.assign(dims, dims + maxidx + 1);
     long long npix = 1;
-    for (int d : m.images[m.unknown_images()[0]].dims) npix *= s.dim_values[m.dims[d].index];
+    const std::vector<int>& ud = m.images[m.unknown_images()[0]].dims;
+    for (int d : ud) npix *= s.dim_values[m.dims[d].index];
     if (npix <= 0 || npix > (1LL << 31) / 16) { *err = "generic: unknown index space empty or too large"; return nullptr; }
     Domain dom{(int)npix, 1, 0, 1, 0, 1};
+    if (ud.size() == 2) {   // image rows: StencilPlan may split them into slabs
+        const int W = (int)s.dim_values[m.dims[ud[0]].index], H = (int)s.dim_values[m.dims[ud[1]].index];
+        dom = Domain{W, H, 0, H, 0, H};
+    }
     if (opts.double_precision) return make_stencil_plan<GenericOp<double>>(s, opts, dom, err);
     return make_stencil_plan<GenericOp<float>>(s, opts, dom, err);
 }

@@ -54,11 +54,17 @@ __device__ __forceinline__ PixGeom pix(const Domain& d) {
     g.i = g.ok ? d.off(g.x, g.y) : 0;
     return g;
 }
+// Inside the image AND held in this rank's memory rows. On a row slab the tile loaders
+// reach past the owned rows by the tile remainder + the halo; rows beyond the memory slab
+// never feed an owned output, so they read as zero instead of past the allocation.
+__device__ __forceinline__ bool in_mem(const Domain& d, int y) {
+    return y >= d.y_mem0 && y < d.y_mem0 + d.mem_rows;
+}
 __device__ __forceinline__ bool inside(const Domain& d, int x, int y) {
-    return x >= 0 && x < d.W && y >= 0 && y < d.H;
+    return x >= 0 && x < d.W && y >= 0 && y < d.H && in_mem(d, y);
 }
 __device__ __forceinline__ bool inbe(const Domain& d, int x, int y) {
-    return x >= 1 && x < d.W - 1 && y >= 1 && y < d.H - 1;
+    return x >= 1 && x < d.W - 1 && y >= 1 && y < d.H - 1 && in_mem(d, y);
 }
 template <typename V>
 __device__ __forceinline__ V get(const V* a, const Domain& d, int x, int y) {

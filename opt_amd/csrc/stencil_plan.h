@@ -87,6 +87,11 @@ struct HasDumpJ<Op, std::void_t<decltype(std::declval<Op&>().dump_j((int*)nullpt
                                                                      (typename Op::T*)nullptr, hipStream_t{}))>>
     : std::true_type {};
 
+template <class Op, class = void>
+struct HasSlabRefusal : std::false_type {};
+template <class Op>
+struct HasSlabRefusal<Op, std::void_t<decltype(std::declval<const Op&>().slab_refusal())>> : std::true_type {};
+
 template <class Op>
 class StencilPlan final : public Plan {
 public:
@@ -111,6 +116,10 @@ public:
 
     std::string set_decomposition(Comm* comm, int y_lo, int y_hi) override {
         if (!Op::kSlabs) return std::string(Op::kName) + ": no row-slab decomposition (data-dependent reads)";
+        if constexpr (HasSlabRefusal<Op>::value) {
+            const std::string why = op_->slab_refusal();
+            if (!why.empty()) return why;
+        }
         if (opts_.host_buffers) return "row-slab decomposition needs backend_cuda (device arrays)";
         if (opts_.materialized) return "row-slab decomposition of the materialized Jacobian path is not supported";
         const int h = op_->halo();

@@ -144,3 +144,65 @@ def test_image_warping_lm_decomposed(world):
     for sv in solvers:
         sv.close()
     lib.OptAMD_LocalGroupDestroy(group)
+
+
+# ----------------------------------------- the generated kernels (general front end)
+def _intrinsic(W, H):
+    rng = np.random.default_rng(17)
+    return {"W": W, "H": H, "params": [1.5, 0.7, 0.9, 1.2],
+            "r": rng.normal(size=3 * W * H).astype(np.float32), "i": rng.normal(size=3 * W * H).astype(np.float32),
+            "s": rng.normal(size=W * H).astype(np.float32)}
+
+
+class Intrinsic(Family):
+    """energies/intrinsic_image_decomposition.t: r at slots 4 (Unknown) and 4 (its Array
+    view, the same pointer), i at 5, s at 6."""
+
+    def params(self, w, s=None):
+        sl = (lambda a, ch: a) if s is None else (lambda a, ch: dd.slice_rows(a, w["W"], ch, s))
+        r = _cuda(sl(w["r"], 3).copy())
+        return [float(v) for v in w["params"]] + [r, _cuda(sl(w["i"], 3).copy()), _cuda(sl(w["s"], 1).copy())]
+
+
+INTRINSIC = Intrinsic(os.path.join(ROOT, "energies", "intrinsic_image_decomposition.t"), "LMGPU", _intrinsic,
+                      [("r", 3), ("i", 3), ("s", 1)], ["r"])
+
+
+@pytest.mark.parametrize("fam,world,W,H", [(POISSON, 2, 96, 64), (SFS, 1, 96, 80), (SFS, 3, 96, 80),
+                                           (INTRINSIC, 1, 64, 48), (INTRINSIC, 2, 64, 48), (INTRINSIC, 4, 70, 61)])
+def test_generated_kernels_decomposed_match_single_domain(monkeypatch, fam, world, W, H):
+    """Row slabs of the generated kernels: the halo from the energy's vertical reach
+    (2 for shape_from_shading through its ComputedArray, 1 for the others), ComputedArray
+    planes exchanged after precompute, owned-row loops with global coordinates."""
+    monkeypatch.setenv("OPT_AMD_GENERIC", "1")
+    w = fam.make(W, H)
+    s = OptSolver([W, H], fam.energy, fam.kind)
+    assert s.family() == "generic"
+    assert s.halo() == (2 if fam is SFS else 1)
+    prm = fam.params(w)
+    s.set_solver_params({"nIterations": 4, "lIterations": 10})
+    ref = s.profiled_solve(prm)
+    nscal = len(w.get("params", []))
+    Xref = to_np(prm[nscal])
+    costs, X = run(fam, w, world, 4, 10)
+    for r in range(world):
+        assert costs[r] == costs[0]
+    if world == 1:
+        assert costs[0] == ref and np.array_equal(X, Xref)
+    else:
+        assert len(costs[0]) == len(ref)
+        np.testing.assert_allclose(costs[0], ref, rtol=1e-5)
+        act = np.abs(Xref) < 1e3
+        assert np.abs(X - Xref)[act].max() <= 1e-5 * np.abs(Xref[act]).max()
+
+
+def test_generated_kernels_refuse_slabs_where_reads_are_data_dependent(monkeypatch):
+    monkeypatch.setenv("OPT_AMD_GENERIC", "1")
+    lib = api.load_library()
+    group = lib.OptAMD_LocalGroupCreate(2)
+    for energy, dims in (("optical_flow", [64, 32]), ("volume_denoise", [16, 16, 8])):
+        sv = OptSolver(dims, os.path.join(ROOT, "energies", energy + ".t"), "LMGPU")
+        assert sv.family() == "generic"
+        with pytest.raises(Exception):
+            sv.set_decomposition(lib.OptAMD_LocalGroupRank(group, 0), 0, 8)
+    lib.OptAMD_LocalGroupDestroy(group)
