@@ -71,8 +71,16 @@ public:
             case Op::Div: e = v(n.a) + " / " + v(n.b); break;
             case Op::Neg: e = "-" + v(n.a); break;
             case Op::Sqrt: e = "sqrt(" + v(n.a) + ")"; break;
-            case Op::Sin: e = "sin(" + v(n.a) + ")"; break;
-            case Op::Cos: e = "cos(" + v(n.a) + ")"; break;
+            case Op::Sin:
+            case Op::Cos: {   // one sincos per angle: both halves share the range reduction
+                const std::string x = v(n.a), sn = "s" + std::to_string(n.a), cn = "c" + std::to_string(n.a);
+                if (!sincos_.count(n.a)) {
+                    o_ << "        T " << sn << ", " << cn << "; opt_sincos(" << x << ", &" << sn << ", &" << cn << ");\n";
+                    sincos_.insert(n.a);
+                }
+                done_[id] = n.op == Op::Sin ? sn : cn;
+                return done_[id];
+            }
             case Op::Exp: e = "exp(" + v(n.a) + ")"; break;
             case Op::Log: e = "log(" + v(n.a) + ")"; break;
             case Op::Abs: e = "fabs(" + v(n.a) + ")"; break;
@@ -134,6 +142,14 @@ private:
         if (nd_ == 2) return "((long long)(" + coord(1, off[1]) + " - a.ymem0) * W + " + coord(0, off[0]) + ")";
         return "(((long long)" + coord(2, off[2]) + " * H + " + coord(1, off[1]) + ") * W + " + coord(0, off[0]) + ")";
     }
+    // offset of a centred access from the thread's pixel, in pixels (32-bit: the
+    // front end limits the index space, generic_accepts)
+    std::string rel(const int* off) const {
+        std::string r = std::to_string(off[0]);
+        if (nd_ > 1 && off[1]) r += " + " + std::to_string(off[1]) + " * W";
+        if (nd_ > 2 && off[2]) r += " + " + std::to_string(off[2]) + " * W * H";
+        return "(" + r + ")";
+    }
     std::string img_ptr(int i) const {
         const GImage& im = M_.images[i];
         return "((const " + std::string(elem_type(im.elem, im.tvalued)) + "*)a.img[" + std::to_string(i) + "])";
@@ -151,7 +167,7 @@ private:
             idx = "(long long)v" + std::to_string(n.slot) + " * " + ch + " + " + c;
             return "(T)(" + base + ")[" + idx + "]";
         }
-        idx = lin(n.off) + " * " + ch + " + " + c;
+        idx = "(li + " + rel(n.off) + ") * " + ch + " + " + c;
         return "((" + inb(n.off) + ") ? (T)(" + base + ")[" + idx + "] : (T)0)";
     }
 
@@ -161,6 +177,7 @@ private:
     int nd_;
     const std::vector<int>& uslot_;
     std::map<int, std::string> done_;
+    std::set<int> sincos_;
     std::map<std::string, std::string> vdone_;
 };
 
@@ -191,6 +208,8 @@ GenSource generate(GModel& m, bool dbl) {
     o << OPTAMD_STR(OPTAMD_GENARGS_BODY) << "\n";
     o << kReduceDevSrc << "\n";
     o << "#define OPT_COORDS const int W = a.dims[0], H = a.dims[1], D = a.dims[2]; (void)D;\n";
+    o << "__device__ __forceinline__ void opt_sincos(float x, float* s, float* c) { sincosf(x, s, c); }\n"
+         "__device__ __forceinline__ void opt_sincos(double x, double* s, double* c) { sincos(x, s, c); }\n";
     // Image:get / Image:sample (o.t:856-876): floor / ceil taps, zero outside, lerps in T
     o << "template <typename E> __device__ __forceinline__ T opt_tap(const E* im, int nch, int c, int x, int y, int W, int H) {\n"
          "    return (x >= 0 && x < W && y >= 0 && y < H) ? (T)im[((long long)y * W + x) * nch + c] : (T)0;\n}\n"
@@ -204,9 +223,9 @@ GenSource generate(GModel& m, bool dbl) {
     // is global row a.ymem0 (coordinates, bounds and Index(1) are global)
     const char* coords = nd == 2
         ? "        const int x = (int)(lin % W); const int y = (int)(lin / W) + a.ymem0; const int z = 0;\n"
-          "        (void)x; (void)y; (void)z;\n"
+          "        const int li = (int)lin; (void)x; (void)y; (void)z; (void)li;\n"
         : "        const int x = (int)(lin % W); const int y = (int)((lin / W) % H); const int z = (int)(lin / ((long long)W * H));\n"
-          "        (void)x; (void)y; (void)z;\n";
+          "        const int li = (int)lin; (void)x; (void)y; (void)z; (void)li;\n";
 
     // centred instances per output (unknown image, channel)
     std::map<std::pair<int, int>, std::vector<std::pair<Instance, int>>> inst;   // -> (instance, support node)
@@ -404,6 +423,7 @@ GenSource generate(GModel& m, bool dbl) {
                  "        for (int idx = threadIdx.x; idx < " << PXY << "; idx += 256) {   // one pass\n"
                  "        const int x = X0 - " << maxx << " + idx % " << PX << ", y = Y0 - " << maxy << " + idx / " << PX << ";\n"
                  "        const int z = 0; (void)z;\n"
+                 "        const int li = (y - a.ymem0) * W + x; (void)li;\n"
                  "        if (x >= 0 && x < W && y >= 0 && y < H) {\n";
             {
                 Body b(m, o, nd, uslot);
