@@ -19,11 +19,13 @@
 // wrapped in their bounding-box test at classification time.
 #include "codegen.h"
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <functional>
 #include <map>
 #include <set>
 #include <sstream>
+#include <tuple>
 #include "reduce_dev_src.h"
 
 #define OPTAMD_STR2(...) #__VA_ARGS__
@@ -34,6 +36,7 @@ namespace gen {
 namespace {
 
 std::string lit(double v) {
+    if (std::isinf(v)) return v < 0 ? "(-(T)HUGE_VAL)" : "((T)HUGE_VAL)";
     char b[64];
     snprintf(b, sizeof(b), "%.17g", v);
     std::string s = b;
@@ -49,6 +52,21 @@ const char* elem_type(const std::string& e, bool unknown) {
 }
 
 // One kernel body's emitter: every pool node becomes at most one local temporary.
+// Per-step caches of single-pixel transcendentals: (op, image, channel) -> internal image
+// holding op(image(x).channel) for every pixel, refreshed by the last precompute kernel.
+// While set, the emitter reads f(image(x + o)) from the cache at offset o instead of
+// evaluating it (the gather evaluates each residual instance, so an angle's sin/cos would
+// otherwise be recomputed at every neighbour that reads it). Same function, same input:
+// the cached values are the bits the kernels would compute.
+using CacheMap = std::map<std::tuple<int, int, int>, int>;
+const CacheMap* g_cache = nullptr;
+
+bool cacheable(const Pool& P, const Node& n) {
+    if (n.op != Op::Sin && n.op != Op::Cos && n.op != Op::Exp && n.op != Op::Log && n.op != Op::Sqrt) return false;
+    const Node& c = P.at(n.a);
+    return c.op == Op::Read && c.slot < 0;
+}
+
 class Body {
 public:
     Body(GModel& m, std::ostringstream& o, int ndims, const std::vector<int>& unk_slot)
@@ -58,6 +76,19 @@ public:
         auto it = done_.find(id);
         if (it != done_.end()) return it->second;
         const Node n = P_.at(id);
+        if (g_cache && cacheable(P_, n)) {
+            const Node c = P_.at(n.a);
+            auto ci = g_cache->find(std::make_tuple((int)n.op, c.i, c.ch));
+            if (ci != g_cache->end()) {
+                // outside the image the argument reads 0: f(0), as the evaluated form
+                const double f0 = n.op == Op::Cos || n.op == Op::Exp ? 1.0 : n.op == Op::Log ? -HUGE_VAL : 0.0;
+                const std::string name = "k" + std::to_string(id);
+                o_ << "        const T " << name << " = (" << inb(c.off) << ") ? ((const T*)a.img[" << ci->second
+                   << "])[li + " << rel(c.off) << "] : " << lit(f0) << ";\n";
+                done_[id] = name;
+                return name;
+            }
+        }
         std::string e;
         switch (n.op) {
             case Op::Const: done_[id] = lit(n.c); return done_[id];
@@ -261,6 +292,62 @@ GenSource generate(GModel& m, bool dbl) {
         o << "    }\n}\n";
     }
     gs.n_precompute = (int)m.computed.size();
+
+    // ------------------------------------------------ transcendental caches (see g_cache)
+    // Worth it when residuals have instances at several shifts (each would re-evaluate
+    // its neighbours' transcendentals): cache every sin / cos / exp / log / sqrt of a
+    // centred read the residuals use, one internal image each, filled by one extra
+    // precompute kernel after the ComputedArrays.
+    CacheMap cache;
+    {
+        bool multi = false;
+        for (auto& r : m.residuals) {
+            if (r.graph >= 0) continue;
+            std::set<std::string> offs;
+            for (int u : r.unknowns) {
+                const Node& n = P.at(u);
+                offs.insert(std::to_string(n.off[0]) + "," + std::to_string(n.off[1]) + "," + std::to_string(n.off[2]));
+            }
+            multi |= offs.size() > 1;
+        }
+        std::vector<std::pair<std::tuple<int, int, int>, int>> want;   // key -> a node with offset 0 form
+        if (multi)
+            for (auto& r : m.residuals) {
+                if (r.graph >= 0) continue;
+                P.visit(r.expr, [&](int, const Node& n) {
+                    if (!cacheable(P, n)) return;
+                    const Node& c = P.at(n.a);
+                    auto key = std::make_tuple((int)n.op, c.i, c.ch);
+                    for (auto& w : want)
+                        if (w.first == key) return;
+                    const int z0[3] = {0, 0, 0};
+                    want.push_back({key, P.un(n.op, P.read(c.i, c.ch, z0))});
+                });
+            }
+        if (!want.empty()) {
+            o << "extern \"C\" __global__ __launch_bounds__(256) void gen_precompute_" << gs.n_precompute << "(GenArgs a) {\n"
+                 "    OPT_COORDS\n"
+                 "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
+              << coords;
+            Body b(m, o, nd, uslot);
+            const int uimg = unk.empty() ? 0 : unk[0];
+            for (auto& w : want) {
+                if (m.images.size() >= 16) break;   // GenArgs::img capacity
+                GImage ci;
+                ci.name = "cache_" + std::to_string(std::get<0>(w.first)) + "_" + std::to_string(std::get<1>(w.first)) +
+                          "_" + std::to_string(std::get<2>(w.first));
+                ci.dims = m.images[uimg].dims;
+                ci.internal = ci.tvalued = true;
+                m.images.push_back(ci);
+                const int id = (int)m.images.size() - 1;
+                cache[w.first] = id;
+                b.line("((T*)a.img[" + std::to_string(id) + "])[lin] = " + b.v(w.second) + ";");
+            }
+            o << "    }\n}\n";
+            if (!cache.empty()) ++gs.n_precompute;
+        }
+    }
+    g_cache = cache.empty() ? nullptr : &cache;
 
     // ---------------------------------------------------------------- gen_jtf
     {
@@ -748,6 +835,7 @@ GenSource generate(GModel& m, bool dbl) {
              "    double v[1] = {(double)dot};\n    block_reduce_publish<1>(v, rs, blockIdx.x);\n}\n";
     }
     (void)zero3;
+    g_cache = nullptr;
     char note[128];
     snprintf(note, sizeof(note), "// apply: %s (%.2f residual instances per centred residual)\n",
              gs.prefer_tiled ? "gen_apply_tiled" : "gen_apply", gs.instances_per_residual);
