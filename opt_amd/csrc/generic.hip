@@ -489,6 +489,23 @@ std::unique_ptr<Plan> make_generic_plan(const ProblemSpec& spec, const StateOpti
     const std::vector<int>& ud = m.images[m.unknown_images()[0]].dims;
     for (int d : ud) npix *= s.dim_values[m.dims[d].index];
     if (npix <= 0 || npix > (1LL << 31) / 16) { *err = "generic: unknown index space empty or too large"; return nullptr; }
+    // compile (and cache) the kernels here so that a compile error is a NULL plan, as the
+    // reference returns nil on errors in the energy (o.t:1526), not a fail-stop
+    {
+        gen::GModel mc;
+        std::string e2;
+        gen::build_model(spec.text, &mc, &e2);
+        const std::string code = gen::generate(mc, opts.double_precision).code;
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!code_cache().count(code)) {
+            std::string obj, log;
+            if (!rtc_compile(code, &obj, &log)) {
+                *err = "generic: generated kernels failed to compile:\n" + log;
+                return nullptr;
+            }
+            code_cache()[code] = obj;
+        }
+    }
     Domain dom{(int)npix, 1, 0, 1, 0, 1};
     if (ud.size() == 2) {   // image rows: StencilPlan may split them into slabs
         const int W = (int)s.dim_values[m.dims[ud[0]].index], H = (int)s.dim_values[m.dims[ud[1]].index];

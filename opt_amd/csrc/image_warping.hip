@@ -854,7 +854,7 @@ public:
     int step(void** params) override {
         if (!initialised_) init(params);
         if (n_iter_ >= sp_.nIterations) {
-            if (opts_.kernel_timing && opts_.verbosity > 0) fprintf(stderr, "%s", timer_.report().c_str());
+            cleanup_log();
             return 0;
         }
         begin_call();

@@ -1,4 +1,5 @@
 // plan.cpp — Plan base class, solver parameters, kernel timer, reduction scratch.
+#include <cstdarg>
 #include "plan.h"
 #include <cstring>
 #include <sstream>
@@ -139,6 +140,21 @@ void Plan::begin_call() {
     OPT_HIP_CHECK(hipStreamWaitEvent(stream_, e, 0));
     OPT_HIP_CHECK(hipEventDestroy(e));
 }
+void Plan::log_solver(const char* fmt, ...) {
+    if (opts_.verbosity <= 0) return;
+    va_list ap;
+    va_start(ap, fmt);
+    vprintf(fmt, ap);
+    va_end(ap);
+    fflush(stdout);
+}
+void Plan::cleanup_log() {
+    if (opts_.verbosity <= 0) return;
+    printf("final cost=%.16f\n", prev_cost_);
+    if (opts_.kernel_timing) printf("%s", timer_.report().c_str());
+    fflush(stdout);
+}
+
 void Plan::end_call() {
     OPT_HIP_CHECK(hipStreamSynchronize(stream_));
     OPT_HIP_CHECK(hipGetLastError());

@@ -127,6 +127,12 @@ protected:
     void begin_call();              // order after the caller's default-stream work
     void end_call();                // wait for this plan's device work
     // Launch bookkeeping: wraps a kernel launch with the timer when enabled.
+    // The reference's cleanup (solverGPUGaussNewton.t:1902-1910), run when Step returns 0:
+    // with verbosityLevel > 0 it logs "final cost=%.16f" (the line the examples' test
+    // harness parses, examples/test_final_cost.py:100-103) and the per-kernel timing table.
+    void cleanup_log();
+    // logSolver: printf to stdout when verbosityLevel > 0 (o.t:95-104)
+    void log_solver(const char* fmt, ...);
     void tbegin(const char* name) { if (timer_.mode) timer_.begin(stream_, name); }
     void tend() { if (timer_.mode) timer_.end(stream_); }
 

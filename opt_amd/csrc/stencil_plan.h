@@ -155,7 +155,10 @@ public:
 
     int step(void** params) override {
         if (!initialised_) init(params);
-        if (n_iter_ >= sp_.nIterations) return 0;
+        if (n_iter_ >= sp_.nIterations) {
+            cleanup_log();
+            return 0;
+        }
         begin_call();
         op_->bind(params, stream_);
         exchange_unknowns();
@@ -252,6 +255,9 @@ public:
         const T model_cost = (T)h[0], new_cost = (T)h[1];
         const T prev = (T)prev_cost_;
         const T model_change = prev - model_cost;
+        log_solver(" cost=%f \n", (double)prev);   // computeModelCostChange (:1505-1513)
+        log_solver(" model_cost=%f \n", (double)model_cost);
+        log_solver(" model_cost_change=%f \n", (double)model_change);
         const T cost_change = prev - new_cost;
         const T rel = cost_change / model_change;
         int ret = 1;
@@ -259,6 +265,7 @@ public:
             const T abs_tol = prev * (T)sp_.function_tolerance;
             if (cost_change <= abs_tol) {
                 ret = 0;   // function tolerance reached (prevCost is left as it was, :2254-2258)
+                log_solver("\nFunction tolerance reached, exiting\n");
             } else {
                 const T qv = rel;
                 const T min_factor = (T)(1.0 / 3.0);
@@ -272,12 +279,19 @@ public:
             if (Lit > 0) revert();
             precompute();
             radius_ = radius_ / decrease_;
+            log_solver(" trust_region_radius=%f \n", (double)radius_);
             decrease_ = 2.0f * decrease_;
-            if (radius_ <= sp_.min_trust_region_radius) ret = 0;
+            if (radius_ <= sp_.min_trust_region_radius) {
+                ret = 0;
+                log_solver("\nTrust_region_radius is less than the min, exiting\n");
+            } else {
+                log_solver("REVERT\n");
+            }
         }
         op_->unbind(stream_);
         end_call();
         if (ret) ++n_iter_;
+        else cleanup_log();
         return ret;
     }
 
