@@ -48,7 +48,9 @@ def test_residual_templates(name, count):
 
 @pytest.mark.parametrize("name", ["image_warping", "poisson_image_editing", "arap_mesh_deformation",
                                   "volume_denoise", "curve_smoothing", "intrinsic_image_decomposition",
-                                  "shape_from_shading", "optical_flow"])
+                                  "shape_from_shading", "optical_flow", "cotangent_mesh_smoothing",
+                                  "embedded_mesh_deformation", "robust_nonrigid_alignment",
+                                  "volumetric_mesh_deformation"])
 def test_generated_source_compiles(name):
     src = api.generic_source(E(name))
     for k in ("gen_jtf", "gen_apply", "gen_cost", "gen_jtf_graph", "gen_apply_graph", "block_reduce_publish"):
@@ -194,12 +196,17 @@ Energy(C(1,0) - A(0,0,0))
     assert "gen_precompute_0" in src and "gen_precompute_1" not in src
 
 
-def test_same_energy_two_spellings_of_reference_intrinsic():
-    """Our energies/intrinsic_image_decomposition.t lowers to exactly the reference's."""
-    ref = os.path.join(REF, "examples", "intrinsic_image_decomposition", "intrinsic_image_decomposition.t")
+@pytest.mark.parametrize("name", ["intrinsic_image_decomposition", "cotangent_mesh_smoothing",
+                                  "embedded_mesh_deformation", "robust_nonrigid_alignment",
+                                  "volumetric_mesh_deformation", "image_warping", "optical_flow",
+                                  "arap_mesh_deformation", "poisson_image_editing"])
+def test_our_energy_files_lower_exactly_as_the_reference_files(name):
+    """energies/<name>.t (our text) and the reference's examples/<name>/<name>.t produce
+    identical residual templates (hash-consed expressions printed canonically)."""
+    ref = os.path.join(REF, "examples", name, name + ".t")
     if not os.path.exists(ref):
         pytest.skip("reference checkout not present")
-    assert api.generic_describe(E("intrinsic_image_decomposition")) == api.generic_describe(ref)
+    assert api.generic_describe(E(name)) == api.generic_describe(ref)
 
 
 @pytest.mark.parametrize("name,tiled", [("image_warping", False), ("poisson_image_editing", False),
