@@ -1,21 +1,30 @@
--- As-rigid-as-possible mesh deformation on a vertex graph (same energy as the
--- reference's examples/arap_mesh_deformation/arap_mesh_deformation.t, same indices).
-local N = Dim("N", 0)
-local NUMEDGES = Dim("NUMEDGES", 1)
+-- As-rigid-as-possible deformation of a triangle mesh given as a vertex graph.
+-- Unknowns: the deformed position and an Euler-angle rotation per vertex. Handles pull
+-- their vertex towards a target; every directed edge (a -> b) should keep its rest
+-- vector up to the rotation of a. Declaration indices follow the reference example
+-- (examples/arap_mesh_deformation), so its problemparams bind unchanged.
+local vertexCount, edgeCount = Dim("N", 0), Dim("NUMEDGES", 1)
 
-local w_fitSqrt = Param("w_fitSqrt", float, 0)
-local w_regSqrt = Param("w_regSqrt", float, 1)
-local Offset = Unknown("Offset", opt_float3, {N}, 2)        -- deformed vertex positions
-local Angle = Unknown("Angle", opt_float3, {N}, 3)          -- per-vertex rotation (Euler)
-local UrShape = Array("UrShape", opt_float3, {N}, 4)        -- rest positions
-local Constraints = Array("Constraints", opt_float3, {N}, 5) -- targets (-inf: free)
-local G = Graph("G", {NUMEDGES}, "v0", {N}, 7, "v1", {N}, 8)
+local fitWeight = Param("w_fitSqrt", float, 0)
+local rigidWeight = Param("w_regSqrt", float, 1)
+local pos = Unknown("Offset", opt_float3, {vertexCount}, 2)
+local euler = Unknown("Angle", opt_float3, {vertexCount}, 3)
+local rest = Array("UrShape", opt_float3, {vertexCount}, 4)
+local target = Array("Constraints", opt_float3, {vertexCount}, 5)   -- x < -999999.9: free
+local edges = Graph("G", {edgeCount}, "v0", {vertexCount}, 7, "v1", {vertexCount}, 8)
 UsePreconditioner(true)
 
--- handles pull their vertex to the target
-local has_target = greatereq(Constraints(0, 0), -999999.9)
-Energy(Select(has_target, w_fitSqrt * (Offset(0) - Constraints(0)), 0))
+local function handle_term()
+    local pull = pos(0) - target(0)
+    local pinned = greatereq(target(0, 0), -999999.9)   -- (0, 0) on a 1-D array: channel 0
+    return Select(pinned, fitWeight * pull, 0)
+end
 
--- every edge keeps its rest shape up to the rotation of its first vertex
-local rigid = (Offset(G.v0) - Offset(G.v1)) - Rotate3D(Angle(G.v0), UrShape(G.v0) - UrShape(G.v1))
-Energy(w_regSqrt * rigid)
+local function rigidity_term(a, b)
+    local moved = pos(a) - pos(b)
+    local rotated = Rotate3D(euler(a), rest(a) - rest(b))
+    return rigidWeight * (moved - rotated)
+end
+
+Energy(handle_term())
+Energy(rigidity_term(edges.v0, edges.v1))

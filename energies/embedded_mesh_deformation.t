@@ -1,32 +1,30 @@
--- Embedded deformation (same energy as the reference's
--- examples/embedded_mesh_deformation; same declaration indices): every node carries an
--- affine 3x3 matrix kept close to a rotation, neighbouring nodes predict each other's
--- positions through it, and handles pull nodes to their targets.
-local N = Dim("N", 0)
-local NUMEDGES = Dim("NUMEDGES", 1)
+-- Embedded deformation: deformation-graph nodes carry an affine 3x3 matrix kept close to
+-- a rotation (orthonormal columns) and predict their neighbours' displacements through
+-- it; handle nodes are pulled to targets. Declaration indices follow the reference
+-- example (examples/embedded_mesh_deformation).
+local nv, ne = Dim("N", 0), Dim("NUMEDGES", 1)
 
-local w_fit = Param("w_fitSqrt", float, 0)
-local w_reg = Param("w_regSqrt", float, 1)
-local w_rot = Param("w_rotSqrt", float, 2)
-local Offset      = Unknown("Offset", opt_float3, {N}, 3)
-local RotMatrix   = Unknown("RotMatrix", opt_float9, {N}, 4)   -- row-major 3x3
-local UrShape     = Image("UrShape", opt_float3, {N}, 5)
-local Constraints = Image("Constraints", opt_float3, {N}, 6)   -- x < -999999.9: no handle
-local G = Graph("G", {NUMEDGES}, "v0", {N}, 8, "v1", {N}, 9)
+local handleW = Param("w_fitSqrt", float, 0)
+local smoothW = Param("w_regSqrt", float, 1)
+local orthoW  = Param("w_rotSqrt", float, 2)
+local t  = Unknown("Offset", opt_float3, {nv}, 3)
+local Mx = Unknown("RotMatrix", opt_float9, {nv}, 4)   -- row-major 3x3
+local g0 = Image("UrShape", opt_float3, {nv}, 5)
+local q  = Image("Constraints", opt_float3, {nv}, 6)
+local E  = Graph("G", {ne}, "v0", {nv}, 8, "v1", {nv}, 9)
 UsePreconditioner(true)
 
-local has_target = greatereq(Constraints(0)(0), -999999.9)
-Energy(Select(has_target, w_fit * (Offset(0) - Constraints(0)), 0))
+local pinned = greatereq(q(0)(0), -999999.9)
+Energy(Select(pinned, handleW * (t(0) - q(0)), 0))
 
--- orthonormal columns
-local M = RotMatrix(0)
-local col = { Vector(M(0), M(3), M(6)), Vector(M(1), M(4), M(7)), Vector(M(2), M(5), M(8)) }
-Energy(w_rot * Dot3(col[1], col[2]))
-Energy(w_rot * Dot3(col[1], col[3]))
-Energy(w_rot * Dot3(col[2], col[3]))
-for k = 1, 3 do
-    Energy(w_rot * (Dot3(col[k], col[k]) - 1))
+local A = Mx(0)
+local function column(k) return Vector(A(k), A(k + 3), A(k + 6)) end
+local a1, a2, a3 = column(0), column(1), column(2)
+for _, pair in ipairs({ {a1, a2}, {a1, a3}, {a2, a3} }) do
+    Energy(orthoW * Dot3(pair[1], pair[2]))
+end
+for _, col in ipairs({ a1, a2, a3 }) do
+    Energy(orthoW * (Dot3(col, col) - 1))
 end
 
-local predicted = Matrix3x3Mul(RotMatrix(G.v0), UrShape(G.v1) - UrShape(G.v0))
-Energy(w_reg * ((Offset(G.v1) - Offset(G.v0)) - predicted))
+Energy(smoothW * ((t(E.v1) - t(E.v0)) - Matrix3x3Mul(Mx(E.v0), g0(E.v1) - g0(E.v0))))

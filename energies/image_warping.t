@@ -1,25 +1,28 @@
--- As-rigid-as-possible 2-D image warping (same energy as the reference's
--- examples/image_warping/image_warping.t, without its debug printing).
-local W, H = Dim("W", 0), Dim("H", 1)
+-- As-rigid-as-possible warping of a 2-D image mesh: every pixel carries a position and
+-- a rotation angle; neighbouring pixels inside the mesh keep their rest offset up to
+-- that rotation, and handle pixels are pulled to their targets. Declaration indices
+-- follow the reference example (examples/image_warping), so its problemparams bind
+-- unchanged.
+local cols, rows = Dim("W", 0), Dim("H", 1)
 
-local Offset      = Unknown("Offset", opt_float2, {W, H}, 0)   -- warped position
-local Angle       = Unknown("Angle", opt_float, {W, H}, 1)     -- per-pixel rotation
-local UrShape     = Array("UrShape", opt_float2, {W, H}, 2)    -- rest position
-local Constraints = Array("Constraints", opt_float2, {W, H}, 3) -- handle targets (<0: none)
-local Mask        = Array("Mask", opt_float, {W, H}, 4)         -- 0 = part of the mesh
-local w_fitSqrt   = Param("w_fitSqrt", float, 5)
-local w_regSqrt   = Param("w_regSqrt", float, 6)
+local warped    = Unknown("Offset", opt_float2, {cols, rows}, 0)
+local theta     = Unknown("Angle", opt_float, {cols, rows}, 1)
+local restPos   = Array("UrShape", opt_float2, {cols, rows}, 2)
+local handles   = Array("Constraints", opt_float2, {cols, rows}, 3)   -- < 0: no handle
+local outside   = Array("Mask", opt_float, {cols, rows}, 4)           -- 0 = pixel of the mesh
+local fitW      = Param("w_fitSqrt", float, 5)
+local rigidW    = Param("w_regSqrt", float, 6)
 
 UsePreconditioner(true)
-Exclude(Not(eq(Mask(0, 0), 0)))
+Exclude(Not(eq(outside(0, 0), 0)))
 
--- rigidity of every 4-neighbour edge inside the mesh
-for x, y in Stencil { {1, 0}, {-1, 0}, {0, 1}, {0, -1} } do
-    local edge = (Offset(0, 0) - Offset(x, y)) - Rotate2D(Angle(0, 0), UrShape(0, 0) - UrShape(x, y))
-    local inside = InBounds(x, y) * eq(Mask(x, y), 0) * eq(Mask(0, 0), 0)
-    Energy(Select(inside, w_regSqrt * edge, 0))
+local neighbours = Stencil { {1, 0}, {-1, 0}, {0, 1}, {0, -1} }
+for ox, oy in neighbours do
+    local restEdge = restPos(0, 0) - restPos(ox, oy)
+    local residual = (warped(0, 0) - warped(ox, oy)) - Rotate2D(theta(0, 0), restEdge)
+    local bothInside = InBounds(ox, oy) * eq(outside(ox, oy), 0) * eq(outside(0, 0), 0)
+    Energy(Select(bothInside, rigidW * residual, 0))
 end
 
--- handle constraints
-local has = All(greatereq(Constraints(0, 0), 0))
-Energy(w_fitSqrt * Select(has, Offset(0, 0) - Constraints(0, 0), 0.0))
+local isHandle = All(greatereq(handles(0, 0), 0))
+Energy(fitW * Select(isHandle, warped(0, 0) - handles(0, 0), 0.0))

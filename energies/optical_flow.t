@@ -1,22 +1,24 @@
--- Dense optical flow: X(i,j) moves pixel (i,j) of I onto the sampled target I_hat,
--- with a 4-neighbour smoothness prior (same energy as the reference's
--- examples/optical_flow/optical_flow.t).
-local W, H = Dim("W", 0), Dim("H", 1)
-local w_fitSqrt = Param("w_fit", float, 0)
-local w_regSqrt = Param("w_reg", float, 1)
-local X = Unknown("X", opt_float2, {W, H}, 2)          -- flow vectors
-local I = Array("I", opt_float, {W, H}, 3)             -- source image
-local target = Array("I_hat", opt_float, {W, H}, 4)    -- target image
-local target_dx = Array("I_hat_dx", opt_float, {W, H}, 5)
-local target_dy = Array("I_hat_dy", opt_float, {W, H}, 6)
-local I_hat = SampledImage(target, target_dx, target_dy)   -- bilinear, with its derivatives
+-- Dense optical flow between two grey images: the flow u(i, j) carries pixel (i, j) of
+-- the source onto the bilinearly sampled target (whose derivative images give the
+-- Jacobian of the sample), plus a 4-neighbour smoothness prior on u. Declaration
+-- indices follow the reference example (examples/optical_flow).
+local cols, rows = Dim("W", 0), Dim("H", 1)
+local fitW = Param("w_fit", float, 0)
+local smoothW = Param("w_reg", float, 1)
+local flow = Unknown("X", opt_float2, {cols, rows}, 2)
+local source = Array("I", opt_float, {cols, rows}, 3)
+local tgt = Array("I_hat", opt_float, {cols, rows}, 4)
+local tgtDx = Array("I_hat_dx", opt_float, {cols, rows}, 5)
+local tgtDy = Array("I_hat_dy", opt_float, {cols, rows}, 6)
+local warpedTarget = SampledImage(tgt, tgtDx, tgtDy)
 
-local i, j = Index(0), Index(1)
+local px, py = Index(0), Index(1)
 UsePreconditioner(false)
 
-Energy(w_fitSqrt * (I(0, 0) - I_hat(i + X(0, 0, 0), j + X(0, 0, 1))))
+local brightness = source(0, 0) - warpedTarget(px + flow(0, 0, 0), py + flow(0, 0, 1))
+Energy(fitW * brightness)
 
-for dx, dy in Stencil { {1, 0}, {-1, 0}, {0, 1}, {0, -1} } do
-    local smooth = w_regSqrt * (X(0, 0) - X(dx, dy))
-    Energy(Select(InBounds(dx, dy), smooth, 0))
+for sx, sy in Stencil { {1, 0}, {-1, 0}, {0, 1}, {0, -1} } do
+    local d = smoothW * (flow(0, 0) - flow(sx, sy))
+    Energy(Select(InBounds(sx, sy), d, 0))
 end

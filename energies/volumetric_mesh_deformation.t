@@ -1,21 +1,23 @@
--- As-rigid-as-possible deformation of a regular 3-D lattice (same energy as the
--- reference's examples/volumetric_mesh_deformation; same declaration indices): every
--- lattice edge keeps its rest vector up to the rotation of its first end.
-local W, H, D = Dim("W", 0), Dim("H", 1), Dim("D", 2)
+-- As-rigid-as-possible deformation of a regular 3-D lattice: every lattice edge keeps
+-- its rest vector up to the rotation of its first end; handle nodes are pulled to their
+-- targets. Declaration indices follow the reference example
+-- (examples/volumetric_mesh_deformation).
+local nx, ny, nz = Dim("W", 0), Dim("H", 1), Dim("D", 2)
 
-local Offset      = Unknown("Offset", opt_float3, {W, H, D}, 0)
-local Angle       = Unknown("Angle", opt_float3, {W, H, D}, 1)
-local UrShape     = Array("UrShape", opt_float3, {W, H, D}, 2)
-local Constraints = Array("Constraints", opt_float3, {W, H, D}, 3)
-local w_fit = Param("w_fitSqrt", float, 4)
-local w_reg = Param("w_regSqrt", float, 5)
+local node   = Unknown("Offset", opt_float3, {nx, ny, nz}, 0)
+local turn   = Unknown("Angle", opt_float3, {nx, ny, nz}, 1)
+local lattice = Array("UrShape", opt_float3, {nx, ny, nz}, 2)
+local goal   = Array("Constraints", opt_float3, {nx, ny, nz}, 3)
+local goalW  = Param("w_fitSqrt", float, 4)
+local stiffW = Param("w_regSqrt", float, 5)
 UsePreconditioner(true)
 
-local has_target = greatereq(Constraints(0, 0, 0)(0), -999999.9)
-Energy(Select(has_target, w_fit * (Offset(0, 0, 0) - Constraints(0, 0, 0)), 0))
+local hasGoal = greatereq(goal(0, 0, 0)(0), -999999.9)
+Energy(Select(hasGoal, goalW * (node(0, 0, 0) - goal(0, 0, 0)), 0))
 
-for dx, dy, dz in Stencil { {1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1} } do
-    local edge = (Offset(0, 0, 0) - Offset(dx, dy, dz))
-               - Rotate3D(Angle(0, 0, 0), UrShape(0, 0, 0) - UrShape(dx, dy, dz))
-    Energy(w_reg * Select(InBounds(0, 0, 0), Select(InBounds(dx, dy, dz), edge, 0.0), 0.0))
+local faces = { {1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1} }
+for _, o in ipairs(faces) do
+    local a, b, c = o[1], o[2], o[3]
+    local deviation = (node(0, 0, 0) - node(a, b, c)) - Rotate3D(turn(0, 0, 0), lattice(0, 0, 0) - lattice(a, b, c))
+    Energy(stiffW * Select(InBounds(0, 0, 0), Select(InBounds(a, b, c), deviation, 0.0), 0.0))
 end
