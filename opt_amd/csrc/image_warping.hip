@@ -68,6 +68,18 @@ __device__ __forceinline__ T pre_offset(const Args<T>& a, int f) {
 }
 
 // ---------------------------------------------------------------- helpers
+// Element access of the once-touched PCG vectors; NT: streaming (nontemporal) form.
+template <bool NT, typename T>
+__device__ __forceinline__ T ld_v(const T* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void st_v(T* p, T v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 __device__ __forceinline__ void sc_of(float t, float* c, float* s) { sincosf(t, s, c); }
 __device__ __forceinline__ void sc_of(double t, double* c, double* s) { sincos(t, s, c); }
 
@@ -162,19 +174,22 @@ struct PRow {          // finished row
     T ejx, ejy;        // its residual pointing at this lane: J(edge -> this pixel)
 };
 
-template <typename T, int MODE>
+template <typename T, int MODE, bool NT = false>
 __device__ __forceinline__ void raw_p(const T* pin, const T* r, const T* pre, long long i, long long N,
                                       T& v0, T& v1, T& v2, T& w0, T& w1, T& w2, T& q0, T& q1, T& q2) {
     if (MODE == 0) {
-        v0 = pin[2 * i]; v1 = pin[2 * i + 1]; v2 = pin[2 * N + i];
+        v0 = ld_v<NT>(pin + 2 * i); v1 = ld_v<NT>(pin + 2 * i + 1); v2 = ld_v<NT>(pin + 2 * N + i);
     } else {
-        v0 = r[2 * i]; v1 = r[2 * i + 1]; v2 = r[2 * N + i];
-        w2 = pre[i];   // angle-channel preconditioner; Offset channels come from the flags
-        if (MODE == 2) { q0 = pin[2 * i]; q1 = pin[2 * i + 1]; q2 = pin[2 * N + i]; }
+        v0 = ld_v<NT>(r + 2 * i); v1 = ld_v<NT>(r + 2 * i + 1); v2 = ld_v<NT>(r + 2 * N + i);
+        w2 = ld_v<NT>(pre + i);   // angle-channel preconditioner; Offset channels come from the flags
+        if (MODE == 2) { q0 = ld_v<NT>(pin + 2 * i); q1 = ld_v<NT>(pin + 2 * i + 1); q2 = ld_v<NT>(pin + 2 * N + i); }
     }
 }
 
-template <typename T, int MODE, int DM>
+// NT: the row's own pixels use streaming loads of the PCG vectors (each is read by
+// exactly one lane of one wave, apart from the row-block boundary rows); the edge
+// pixels, re-read by the neighbouring strip, stay cached.
+template <typename T, int MODE, int DM, bool NT = false>
 __device__ __forceinline__ PRaw<T> raw_prow(const Args<T>& a, const WaveGeom& g, int y, const T* pin,
                                             const T* r, const T* pre, const T* delta) {
     PRaw<T> q;
@@ -184,8 +199,10 @@ __device__ __forceinline__ PRaw<T> raw_prow(const Args<T>& a, const WaveGeom& g,
     q.f = a.flags[i];
     q.u = reinterpret_cast<const float2*>(a.U)[i];
     q.ang = a.A[i];
-    raw_p<T, MODE>(pin, r, pre, i, N, q.v0, q.v1, q.v2, q.w0, q.w1, q.w2, q.q0, q.q1, q.q2);
-    if (MODE == 2 && DM == 2) { q.d0 = delta[2 * i]; q.d1 = delta[2 * i + 1]; q.d2 = delta[2 * N + i]; }
+    raw_p<T, MODE, NT>(pin, r, pre, i, N, q.v0, q.v1, q.v2, q.w0, q.w1, q.w2, q.q0, q.q1, q.q2);
+    if (MODE == 2 && DM == 2) {
+        q.d0 = ld_v<NT>(delta + 2 * i); q.d1 = ld_v<NT>(delta + 2 * i + 1); q.d2 = ld_v<NT>(delta + 2 * N + i);
+    }
     q.ein = 0;
     if (g.edge_lane) {
         q.ein = present(a.dom, g.ex, y);
@@ -255,7 +272,8 @@ __device__ __forceinline__ PRow<T> finish_prow(const Args<T>& a, const PRaw<T>& 
 // LMX (MODE 0 only, the generic LM driver): Ap += dadd p (the CtC term of
 // PCGStep1's LM variant, :617-622) and the whole grid returns at entry once the
 // device-side zeta test has set *stop.
-template <typename T, int MODE, int DM, int DEPTH, bool LMX = false>
+// NT bit 0: streaming loads of the PCG vectors (raw_prow); bit 1: streaming stores.
+template <typename T, int MODE, int DM, int DEPTH, bool LMX = false, int NT = 0>
 __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restrict__ pin,
                                                    const T* __restrict__ r,
                                                    const T* __restrict__ pre, T* __restrict__ pout,
@@ -272,9 +290,9 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
     const long long N = a.dom.npix_mem();
     T dot = 0;
     if (g.y0 < g.y1) {
-        PRow<T> up = finish_prow<T, MODE, DM>(a, raw_prow<T, MODE, DM>(a, g, g.y0 - 1, pin, r, pre, delta), beta, alpha);
-        PRow<T> cur = finish_prow<T, MODE, DM>(a, raw_prow<T, MODE, DM>(a, g, g.y0, pin, r, pre, delta), beta, alpha);
-        PRow<T> dn = finish_prow<T, MODE, DM>(a, raw_prow<T, MODE, DM>(a, g, g.y0 + 1, pin, r, pre, delta), beta, alpha);
+        PRow<T> up = finish_prow<T, MODE, DM>(a, raw_prow<T, MODE, DM, (NT & 1) != 0>(a, g, g.y0 - 1, pin, r, pre, delta), beta, alpha);
+        PRow<T> cur = finish_prow<T, MODE, DM>(a, raw_prow<T, MODE, DM, (NT & 1) != 0>(a, g, g.y0, pin, r, pre, delta), beta, alpha);
+        PRow<T> dn = finish_prow<T, MODE, DM>(a, raw_prow<T, MODE, DM, (NT & 1) != 0>(a, g, g.y0 + 1, pin, r, pre, delta), beta, alpha);
         // carries from the row above: J(up->cur) and J(cur->up) with its angle term
         T in_up_x, in_up_y, my_x, my_y, thm, ax, ay;
         jedge(up.px, up.py, up.pt, up.c, up.s, up.ux, up.uy, cur.px, cur.py, cur.ux, cur.uy,
@@ -283,12 +301,12 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
               up.act && cur.act, wr, my_x, my_y, ax, ay);
         thm = -wr * (ax * my_x + ay * my_y);
         PRaw<T> nx;
-        if (DEPTH == 2) nx = raw_prow<T, MODE, DM>(a, g, g.y0 + 2, pin, r, pre, delta);
+        if (DEPTH == 2) nx = raw_prow<T, MODE, DM, (NT & 1) != 0>(a, g, g.y0 + 2, pin, r, pre, delta);
         for (int y = g.y0; y < g.y1; ++y) {
             // DEPTH 1: row y+2 in flight during row y; DEPTH 2: rows y+2 and y+3
             PRaw<T> nn;
-            if (DEPTH == 1) nx = raw_prow<T, MODE, DM>(a, g, y + 2, pin, r, pre, delta);
-            else nn = raw_prow<T, MODE, DM>(a, g, y + 3, pin, r, pre, delta);
+            if (DEPTH == 1) nx = raw_prow<T, MODE, DM, (NT & 1) != 0>(a, g, y + 2, pin, r, pre, delta);
+            else nn = raw_prow<T, MODE, DM, (NT & 1) != 0>(a, g, y + 3, pin, r, pre, delta);
             // horizontal neighbours; the strip's outside columns enter at lanes 0 / 63
             const T lpx = from_left(cur.px, cur.epx), lpy = from_left(cur.py, cur.epy);
             const T rpx = from_right(cur.px, cur.epx), rpy = from_right(cur.py, cur.epy);
@@ -319,11 +337,15 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
                 if (LMX && dadd) {
                     aox += dadd[2 * i] * cur.px; aoy += dadd[2 * i + 1] * cur.py; aot += dadd[2 * N + i] * cur.pt;
                 }
-                Ap[2 * i] = aox; Ap[2 * i + 1] = aoy; Ap[2 * N + i] = aot;
-                if (MODE != 0) { pout[2 * i] = cur.px; pout[2 * i + 1] = cur.py; pout[2 * N + i] = cur.pt; }
+                st_v<(NT & 2) != 0>(Ap + 2 * i, aox); st_v<(NT & 2) != 0>(Ap + 2 * i + 1, aoy); st_v<(NT & 2) != 0>(Ap + 2 * N + i, aot);
+                if (MODE != 0) {
+                    st_v<(NT & 2) != 0>(pout + 2 * i, cur.px); st_v<(NT & 2) != 0>(pout + 2 * i + 1, cur.py);
+                    st_v<(NT & 2) != 0>(pout + 2 * N + i, cur.pt);
+                }
                 if (MODE == 2 && DM != 0) {
-                    if (cur.act) { delta[2 * i] = cur.dx; delta[2 * i + 1] = cur.dy; delta[2 * N + i] = cur.dt; }
-                    else { delta[2 * i] = 0; delta[2 * i + 1] = 0; delta[2 * N + i] = 0; }
+                    const bool on = cur.act;
+                    st_v<(NT & 2) != 0>(delta + 2 * i, on ? cur.dx : (T)0); st_v<(NT & 2) != 0>(delta + 2 * i + 1, on ? cur.dy : (T)0);
+                    st_v<(NT & 2) != 0>(delta + 2 * N + i, on ? cur.dt : (T)0);
                 }
                 dot += cur.px * aox + cur.py * aoy + cur.pt * aot;
             }
@@ -604,7 +626,7 @@ __global__ __launch_bounds__(kBlock) void iw_model_cost(Args<T> a, const T* __re
 //   r -= alpha Ap;  rz[i+1] = sum r.(pre r)  (pre = r's preconditioner; 1 when
 //   UsePreconditioner(false), :705-708). Two pixels per lane: Offset parts as one
 //   16-B access, angle parts and the angle preconditioner as 8-B, flags as 2 bytes.
-template <typename T>
+template <typename T, bool NT = false>
 __global__ __launch_bounds__(kBlock) void iw_residual(Args<T> a, const T* __restrict__ Ap,
                                                       const T* __restrict__ pre, T* __restrict__ r,
                                                       const double* __restrict__ sc, int i_num, int i_den,
@@ -618,17 +640,31 @@ __global__ __launch_bounds__(kBlock) void iw_residual(Args<T> a, const T* __rest
     const long long stride = (long long)gridDim.x * blockDim.x;
     for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < npairs; q += stride) {
         const long long i = b + 2 * q;
-        V4<T> ro = *reinterpret_cast<const V4<T>*>(r + 2 * i);
-        const V4<T> ao = *reinterpret_cast<const V4<T>*>(Ap + 2 * i);
-        Vec2<T> rt = *reinterpret_cast<const Vec2<T>*>(r + 2 * N + i);
-        const Vec2<T> at = *reinterpret_cast<const Vec2<T>*>(Ap + 2 * N + i);
-        const Vec2<T> wt = *reinterpret_cast<const Vec2<T>*>(pre + i);
+        V4<T> ro, ao;
+        Vec2<T> rt, at, wt;
+        if constexpr (NT) {   // streaming forms: every element is touched once
+            ro = ld4nt(r + 2 * i); ao = ld4nt(Ap + 2 * i);
+            rt = {ld_v<true>(r + 2 * N + i), ld_v<true>(r + 2 * N + i + 1)};
+            at = {ld_v<true>(Ap + 2 * N + i), ld_v<true>(Ap + 2 * N + i + 1)};
+            wt = {ld_v<true>(pre + i), ld_v<true>(pre + i + 1)};
+        } else {
+            ro = *reinterpret_cast<const V4<T>*>(r + 2 * i);
+            ao = *reinterpret_cast<const V4<T>*>(Ap + 2 * i);
+            rt = *reinterpret_cast<const Vec2<T>*>(r + 2 * N + i);
+            at = *reinterpret_cast<const Vec2<T>*>(Ap + 2 * N + i);
+            wt = *reinterpret_cast<const Vec2<T>*>(pre + i);
+        }
         const unsigned short ff = *reinterpret_cast<const unsigned short*>(a.flags + i);
         const int f0 = ff & 0xff, f1 = ff >> 8;
         ro.a -= alpha * ao.a; ro.b -= alpha * ao.b; ro.c -= alpha * ao.c; ro.d -= alpha * ao.d;
         rt.x -= alpha * at.x; rt.y -= alpha * at.y;
-        *reinterpret_cast<V4<T>*>(r + 2 * i) = ro;
-        *reinterpret_cast<Vec2<T>*>(r + 2 * N + i) = rt;
+        if constexpr (NT) {
+            st4nt(r + 2 * i, ro);
+            st_v<true>(r + 2 * N + i, rt.x); st_v<true>(r + 2 * N + i + 1, rt.y);
+        } else {
+            *reinterpret_cast<V4<T>*>(r + 2 * i) = ro;
+            *reinterpret_cast<Vec2<T>*>(r + 2 * N + i) = rt;
+        }
         if (a.use_pre) {
             const T w0 = pre_offset(a, f0), w1 = pre_offset(a, f1);
             acc += w0 * ro.a * ro.a + w0 * ro.b * ro.b + w1 * ro.c * ro.c + w1 * ro.d * ro.d +
@@ -809,6 +845,7 @@ public:
         }
         rows_ = env_int("OPT_AMD_ROWS", 32);
         depth_ = env_int("OPT_AMD_DEPTH", 1);
+        nt_ = env_int("OPT_AMD_IW_NT", 6);
         timer_.apply_name = apply_kernel_name();
         allocate();
     }
@@ -1105,6 +1142,18 @@ private:
             hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 2>), dim3(nb), dim3(kBlock), 0, stream_, args(), pin,
                                (const T*)r_, (const T*)pre_, pout, Ap ? Ap : Ap_, delta_, red_.scalars, ib_num,
                                ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
+        else if ((nt_ & 3) == 1)
+            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 1>), dim3(nb), dim3(kBlock), 0, stream_,
+                               args(), pin, (const T*)r_, (const T*)pre_, pout, Ap ? Ap : Ap_, delta_, red_.scalars,
+                               ib_num, ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
+        else if ((nt_ & 3) == 2)
+            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 2>), dim3(nb), dim3(kBlock), 0, stream_,
+                               args(), pin, (const T*)r_, (const T*)pre_, pout, Ap ? Ap : Ap_, delta_, red_.scalars,
+                               ib_num, ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
+        else if ((nt_ & 3) == 3)
+            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 3>), dim3(nb), dim3(kBlock), 0, stream_,
+                               args(), pin, (const T*)r_, (const T*)pre_, pout, Ap ? Ap : Ap_, delta_, red_.scalars,
+                               ib_num, ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
         else
             hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1>), dim3(nb), dim3(kBlock), 0, stream_, args(), pin,
                                (const T*)r_, (const T*)pre_, pout, Ap ? Ap : Ap_, delta_, red_.scalars, ib_num,
@@ -1113,8 +1162,12 @@ private:
     }
     void launch_residual(int i_num, int i_den, int sc_out) {
         const int nb = flat_grid(dom_.npix_mem(), 2);
-        hipLaunchKernelGGL((iw::iw_residual<T>), dim3(nb), dim3(kBlock), 0, stream_, args(), (const T*)Ap_,
-                           (const T*)pre_, r_, red_.scalars, i_num, i_den, red_.slot(nb, sc_out));
+        if (nt_ & 4)
+            hipLaunchKernelGGL((iw::iw_residual<T, true>), dim3(nb), dim3(kBlock), 0, stream_, args(), (const T*)Ap_,
+                               (const T*)pre_, r_, red_.scalars, i_num, i_den, red_.slot(nb, sc_out));
+        else
+            hipLaunchKernelGGL((iw::iw_residual<T>), dim3(nb), dim3(kBlock), 0, stream_, args(), (const T*)Ap_,
+                               (const T*)pre_, r_, red_.scalars, i_num, i_den, red_.slot(nb, sc_out));
         OPT_HIP_CHECK(hipGetLastError());
     }
     void launch_cost(int sc_out) {
@@ -1134,6 +1187,7 @@ private:
     T *r_ = nullptr, *pre_ = nullptr, *p0_ = nullptr, *p1_ = nullptr, *Ap_ = nullptr, *delta_ = nullptr;
     uint8_t* flags_ = nullptr;
     int rows_ = 16, depth_ = 1, nstrips_ = 0, nrowblocks_ = 0;
+    int nt_ = 6;   // streaming PCG-vector access: bit 0 iw_apply loads, bit 1 iw_apply stores, bit 2 iw_residual
     Comm* comm_ = nullptr;
     float wf_ = 0, wr_ = 0;
     T *user_O_ = nullptr, *user_A_ = nullptr;

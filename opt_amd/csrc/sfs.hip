@@ -78,10 +78,14 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void sfs_precompute(Args<T> a) {
     const PixGeom g = pix(a.dom);
     if (!g.ok) return;
-    const int x = g.x, y = g.y;
+    const int x = g.x, y = g.y, W = a.dom.W;
+    const long long i0 = g.i;
+    // inbe: the 3x3 neighbourhood is inside the image and in memory, plain offsets
+    const bool ib = inbe(a.dom, x, y);
+    const float* D = a.D;
     T bi = 0, g0 = 0, g1 = 0, g2 = 0;
-    if (inbe(a.dom, x, y) && DV(a, x - 1, y) && DV(a, x, y) && DV(a, x, y - 1)) {
-        const T d = a.X[g.i], A = get(a.X, a.dom, x - 1, y), B = get(a.X, a.dom, x, y - 1);
+    if (ib && D[i0 - 1] > 0.f && D[i0] > 0.f && D[i0 - W] > 0.f) {
+        const T d = a.X[i0], A = a.X[i0 - 1], B = a.X[i0 - W];
         const T fx = a.fx, fy = a.fy, ux = a.ux, uy = a.uy;
         const T i = (T)x, j = (T)y;
         const T nx = B * (d - A) / fy;
@@ -93,7 +97,7 @@ __global__ __launch_bounds__(kBlock) void sfs_precompute(Args<T> a) {
         const T* L = a.L;
         const T Bv = L[0] + L[1] * Ny + L[2] * Nz + L[3] * Nx + L[4] * Nx * Ny + L[5] * Ny * Nz +
                      L[6] * (-Nx * Nx - Ny * Ny + (T)2 * Nz * Nz) + L[7] * Nz * Nx + L[8] * (Nx * Nx - Ny * Ny);
-        const T I = (T)a.Im[g.i] * (T)0.5 + (T)0.25 * ((T)get(a.Im, a.dom, x - 1, y) + (T)get(a.Im, a.dom, x, y - 1));
+        const T I = (T)a.Im[i0] * (T)0.5 + (T)0.25 * ((T)a.Im[i0 - 1] + (T)a.Im[i0 - W]);
         bi = Bv - I;
         const T dBx = L[3] + L[4] * Ny + L[7] * Nz + (T)2 * Nx * (L[8] - L[6]);
         const T dBy = L[1] + L[4] * Nx + L[5] * Nz - (T)2 * Ny * (L[6] + L[8]);
@@ -116,99 +120,79 @@ __global__ __launch_bounds__(kBlock) void sfs_precompute(Args<T> a) {
         g0 = gv[0]; g1 = gv[1]; g2 = gv[2];
     }
     a.BI[g.i] = bi; a.G00[g.i] = g0; a.Gm0[g.i] = g1; a.G0m[g.i] = g2;
-    bool v = inbe(a.dom, x, y) && DV(a, x, y) && DV(a, x, y - 1) && DV(a, x, y + 1) && DV(a, x - 1, y) &&
-             DV(a, x + 1, y);
+    bool v = ib && D[i0] > 0.f && D[i0 - W] > 0.f && D[i0 + W] > 0.f && D[i0 - 1] > 0.f && D[i0 + 1] > 0.f;
     if (v) {
-        const T xc = a.X[g.i];
-        v = fabs(xc - get(a.X, a.dom, x, y - 1)) < (T)0.01 && fabs(xc - get(a.X, a.dom, x, y + 1)) < (T)0.01 &&
-            fabs(xc - get(a.X, a.dom, x - 1, y)) < (T)0.01 && fabs(xc - get(a.X, a.dom, x + 1, y)) < (T)0.01;
+        const T xc = a.X[i0];
+        v = fabs(xc - a.X[i0 - W]) < (T)0.01 && fabs(xc - a.X[i0 + W]) < (T)0.01 &&
+            fabs(xc - a.X[i0 - 1]) < (T)0.01 && fabs(xc - a.X[i0 + 1]) < (T)0.01;
     }
     a.valid[g.i] = v;
 }
 
 // ------------------------------------------------------- residual instances
-// Shading residual of direction (sx, sy) = (1,0) [E_g_h] or (0,1) [E_g_v] centred at c:
-// value and the partial w.r.t. X(c + o) for the five support offsets, as in the oracle
-// (the two X(c) partials combined).
+// Used by the cost / model cost at centres c with inbe(c) (shading) or valid(c) == 1
+// (smoothness, which implies inbe): every stencil point is then inside the image and in
+// this rank's memory rows, so the reads are plain offsets from the centre's index i
+// (row stride W), no per-read bounds tests.
+//
+// J p of the shading residual of direction sx (1: E_g_h, n = i + 1; 0: E_g_v, n = i + W)
+// at centre i, entries in the oracle's order (0,0), (-1,0), (0,-1), (s), and (1,-1) for
+// E_g_h / (-1,1) for E_g_v; each coefficient is the partial of w_g m (B_I(c) - B_I(c+s))
+// through the gradient images (the two X(c) partials combined).
 template <typename T>
-__device__ __forceinline__ T shade_coef(const Args<T>& a, int cx, int cy, int sx, int ox, int oy, T m) {
-    const Domain& d = a.dom;
-    const long long c = d.off(cx, cy);
-    const long long n = d.off(cx + sx, cy + (1 - sx));
+__device__ __forceinline__ T shade_jp(const Args<T>& a, const T* p, long long i, long long n, int W, int sx, T m) {
     const T wg = a.wg;
-    if (ox == 0 && oy == 0)
-        return wg * m * a.G00[c] + (sx ? -wg * m * a.Gm0[n] : -wg * m * a.G0m[n]);
-    if (ox == -1 && oy == 0) return wg * m * a.Gm0[c];
-    if (ox == 0 && oy == -1) return wg * m * a.G0m[c];
-    if (sx) {   // (1,0), (1,-1)
-        if (oy == 0) return -wg * m * a.G00[n];
-        return -wg * m * a.G0m[n];
-    }
-    // (0,1), (-1,1)
-    if (ox == 0) return -wg * m * a.G00[n];
-    return -wg * m * a.Gm0[n];
-}
-template <typename T>
-__device__ __forceinline__ T pget(const T* p, const Domain& d, int x, int y) { return get(p, d, x, y); }
-
-// J p of the shading residual at centre c (entries in the oracle's order:
-// (0,0), (-1,0), (0,-1), (s), (s) - (1,0) or (s) - (0,1))
-template <typename T>
-__device__ __forceinline__ T shade_jp(const Args<T>& a, const T* p, int cx, int cy, int sx, T m) {
-    const Domain& d = a.dom;
-    const int tx = sx, ty = 1 - sx;
-    T jp = shade_coef(a, cx, cy, sx, 0, 0, m) * pget(p, d, cx, cy);
-    jp += shade_coef(a, cx, cy, sx, -1, 0, m) * pget(p, d, cx - 1, cy);
-    jp += shade_coef(a, cx, cy, sx, 0, -1, m) * pget(p, d, cx, cy - 1);
-    jp += shade_coef(a, cx, cy, sx, tx, ty, m) * pget(p, d, cx + tx, cy + ty);
-    if (sx) jp += shade_coef(a, cx, cy, sx, 1, -1, m) * pget(p, d, cx + 1, cy - 1);
-    else jp += shade_coef(a, cx, cy, sx, -1, 1, m) * pget(p, d, cx - 1, cy + 1);
+    T jp = (wg * m * a.G00[i] + (sx ? -wg * m * a.Gm0[n] : -wg * m * a.G0m[n])) * p[i];
+    jp += (wg * m * a.Gm0[i]) * p[i - 1];
+    jp += (wg * m * a.G0m[i]) * p[i - W];
+    jp += (-wg * m * a.G00[n]) * p[n];
+    if (sx) jp += (-wg * m * a.G0m[n]) * p[n - W];   // X(c + (1,-1))
+    else jp += (-wg * m * a.Gm0[n]) * p[n - 1];      // X(c + (-1,1))
     return jp;
 }
 
-template <typename T>
-__device__ __forceinline__ void pvec(const Args<T>& a, int x, int y, T& px, T& py) {
-    px = ((T)x - a.ux) / a.fx;
-    py = ((T)y - a.uy) / a.fy;
-}
-// px / py of the columns / rows k-2 .. k+2 of a thread's pixel k: the divisions of
-// p(0,0) (shape_from_shading.t:26-31) are done once per thread, not once per use.
+// px / py of columns x-1..x+1 and rows y-1..y+1 (p(0,0) of shape_from_shading.t:26-31,
+// divisions as the reference writes them)
 template <typename T>
 struct PTab {
-    T x[5], y[5];
-    int kx, ky;
+    T x[3], y[3];
     __device__ __forceinline__ void init(const Args<T>& a, int x0, int y0) {
-        kx = x0; ky = y0;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) pvec(a, x0 + j - 2, y0 + j - 2, x[j], y[j]);
+        for (int j = 0; j < 3; ++j) {
+            x[j] = ((T)(x0 + j - 1) - a.ux) / a.fx;
+            y[j] = ((T)(y0 + j - 1) - a.uy) / a.fy;
+        }
     }
-    __device__ __forceinline__ T px(int gx) const { return x[gx - kx + 2]; }
-    __device__ __forceinline__ T py(int gy) const { return y[gy - ky + 2]; }
 };
-// E_s: partial w.r.t. X(q) = ws co (px(q), py(q), 1); J p of the instance at c
+// The five points of E_s in the oracle's order: centre, (-1,0), (0,-1), (1,0), (0,1).
+// E_s partial w.r.t. X(q) = w_s co (px(q), py(q), 1); J p of the instance at i.
 template <typename T>
-__device__ __forceinline__ void smooth_jp(const Args<T>& a, const PTab<T>& tb, const T* p, int cx, int cy, T out[3]) {
-    constexpr int OX[5] = {0, -1, 0, 1, 0}, OY[5] = {0, 0, -1, 0, 1};
+__device__ __forceinline__ void smooth_jp(const Args<T>& a, const PTab<T>& tb, const T* p, long long i, int W,
+                                          T out[3]) {
+    const int XI[5] = {1, 0, 1, 2, 1}, YI[5] = {1, 1, 0, 1, 2};
+    const long long o[5] = {i, i - 1, i - W, i + 1, i + W};
     out[0] = out[1] = out[2] = 0;
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
-        const T px = tb.px(cx + OX[s]), py = tb.py(cy + OY[s]);
+        const T px = tb.x[XI[s]], py = tb.y[YI[s]];
         const T co = s == 0 ? (T)4 : (T)-1;
-        const T pv = pget(p, a.dom, cx + OX[s], cy + OY[s]);
+        const T pv = p[o[s]];
         out[0] += a.ws * co * px * pv;
         out[1] += a.ws * co * py * pv;
         out[2] += a.ws * co * pv;
     }
 }
-// E_s value at c (oracle order: 4 p(0,0) - (sum of the four in order (-1,0),(0,-1),(1,0),(0,1)))
+// E_s value at i (oracle order: 4 p(0,0) - (the four neighbours in the order above))
 template <typename T>
-__device__ __forceinline__ void smooth_val(const Args<T>& a, const PTab<T>& tb, const T* X, int cx, int cy, T out[3]) {
-    constexpr int OX[5] = {0, -1, 0, 1, 0}, OY[5] = {0, 0, -1, 0, 1};
+__device__ __forceinline__ void smooth_val(const Args<T>& a, const PTab<T>& tb, const T* X, long long i, int W,
+                                           T out[3]) {
+    const int XI[5] = {1, 0, 1, 2, 1}, YI[5] = {1, 1, 0, 1, 2};
+    const long long o[5] = {i, i - 1, i - W, i + 1, i + W};
     T sx = 0, sy = 0, sz = 0, x0 = 0, y0 = 0, z0 = 0;
 #pragma unroll
     for (int s = 0; s < 5; ++s) {
-        const T px = tb.px(cx + OX[s]), py = tb.py(cy + OY[s]);
-        const T xv = get(X, a.dom, cx + OX[s], cy + OY[s]);
+        const T px = tb.x[XI[s]], py = tb.y[YI[s]];
+        const T xv = X[o[s]];
         if (s == 0) { x0 = px * xv; y0 = py * xv; z0 = xv; }
         else { sx += px * xv; sy += py * xv; sz += xv; }
     }
@@ -558,36 +542,39 @@ __global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restri
 template <typename T>
 __global__ __launch_bounds__(kBlock) void sfs_cost(Args<T> a, const T* __restrict__ delta, ReduceSlot rs) {
     const TileRange tr = tile_range(pix_tiles(a.dom));
+    const int W = a.dom.W;
     T acc = 0;
     for (int tile = tr.first; tile < tr.end; tile += tr.step) {
     const PixGeom g = tile_pix(a.dom, tile);
     if (g.ok && a.D[g.i] > 0.f) {
         const int x = g.x, y = g.y;
+        const long long i = g.i;
         T s2 = 0;
         {   // E_p
-            T e = a.wp * (a.X[g.i] - (T)a.D[g.i]);
-            if (delta) e += a.wp * delta[g.i];
+            T e = a.wp * (a.X[i] - (T)a.D[i]);
+            if (delta) e += a.wp * delta[i];
             s2 += e * e;
         }
         if (inbe(a.dom, x, y)) {
+            const T bi = a.BI[i];
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
                 const int sx = t == 0 ? 1 : 0;
-                const T m = (T)(t == 0 ? a.mR[g.i] : a.mC[g.i]);
-                const long long n = a.dom.off(x + sx, y + 1 - sx);
-                T e = a.wg * (a.BI[g.i] - a.BI[n]) * m;
-                if (delta) e += shade_jp(a, delta, x, y, sx, m);
+                const T m = (T)(t == 0 ? a.mR[i] : a.mC[i]);
+                const long long n = sx ? i + 1 : i + W;
+                T e = a.wg * (bi - a.BI[n]) * m;
+                if (delta) e += shade_jp(a, delta, i, n, W, sx, m);
                 s2 += e * e;
             }
         }
-        if (a.valid[g.i] == 1) {
+        if (a.valid[i] == 1) {
             PTab<T> tb;
             tb.init(a, x, y);
             T v[3];
-            smooth_val(a, tb, a.X, x, y, v);
+            smooth_val(a, tb, a.X, i, W, v);
             if (delta) {
                 T jd[3];
-                smooth_jp(a, tb, delta, x, y, jd);
+                smooth_jp(a, tb, delta, i, W, jd);
                 v[0] += jd[0]; v[1] += jd[1]; v[2] += jd[2];
             }
             s2 += v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
