@@ -63,7 +63,7 @@ const CacheMap* g_cache = nullptr;
 
 bool cacheable(const Pool& P, const Node& n) {
     if (n.op != Op::Sin && n.op != Op::Cos && n.op != Op::Exp && n.op != Op::Log && n.op != Op::Sqrt) return false;
-    const Node& c = P.at(n.a);
+    const Node c = P.at(n.a);
     return c.op == Op::Read && c.slot < 0;
 }
 
@@ -264,7 +264,7 @@ GenSource generate(GModel& m, bool dbl) {
         const GResidual& r = m.residuals[ri];
         if (r.graph >= 0) continue;
         for (int u : r.unknowns) {
-            const Node& n = P.at(u);
+            const Node n = P.at(u);
             Instance I{(int)ri, {-n.off[0], -n.off[1], -n.off[2]}};
             inst[{n.i, n.ch}].push_back({I, u});
         }
@@ -305,7 +305,7 @@ GenSource generate(GModel& m, bool dbl) {
             if (r.graph >= 0) continue;
             std::set<std::string> offs;
             for (int u : r.unknowns) {
-                const Node& n = P.at(u);
+                const Node n = P.at(u);
                 offs.insert(std::to_string(n.off[0]) + "," + std::to_string(n.off[1]) + "," + std::to_string(n.off[2]));
             }
             multi |= offs.size() > 1;
@@ -316,7 +316,7 @@ GenSource generate(GModel& m, bool dbl) {
                 if (r.graph >= 0) continue;
                 P.visit(r.expr, [&](int, const Node& n) {
                     if (!cacheable(P, n)) return;
-                    const Node& c = P.at(n.a);
+                    const Node c = P.at(n.a);
                     auto key = std::make_tuple((int)n.op, c.i, c.ch);
                     for (auto& w : want)
                         if (w.first == key) return;
@@ -410,7 +410,7 @@ GenSource generate(GModel& m, bool dbl) {
             if (r.graph >= 0 || r.unknowns.empty()) continue;
             cres.push_back((int)ri);
             for (int u : r.unknowns) {
-                const Node& n = P.at(u);
+                const Node n = P.at(u);
                 const int d = P.diff(r.expr, u);
                 double gv;
                 if (P.is_const(d, &gv) && gv == 0.0) continue;
@@ -546,7 +546,7 @@ GenSource generate(GModel& m, bool dbl) {
                 for (int c = 0; c < im.channels; ++c) {
                     std::string acc = "(T)0";
                     for (const Entry& e : ents) {
-                        const Node& n = P.at(e.u);
+                        const Node n = P.at(e.u);
                         if (n.i != k || n.ch != c) continue;
                         // centre q = x - off(u), local index in the tile + halo region
                         const std::string qi = "(lx + " + std::to_string(maxx - e.ox) + ") + (ly + " +
@@ -619,7 +619,7 @@ GenSource generate(GModel& m, bool dbl) {
                 b.line("long long " + cc + "[" + std::to_string(K) + "]; T " + vv + "[" + std::to_string(K) + "];");
                 int q = 0;
                 for (int u : r.unknowns) {
-                    const Node& n = P.at(u);
+                    const Node n = P.at(u);
                     const int ch = m.images[n.i].channels;
                     std::string idx;
                     if (n.slot >= 0) {
@@ -787,7 +787,7 @@ GenSource generate(GModel& m, bool dbl) {
                         const int gu = P.diff(r.expr, u);
                         double gv;
                         if (P.is_const(gu, &gv) && gv == 0.0) continue;
-                        const Node& n = P.at(u);
+                        const Node n = P.at(u);
                         const std::string gn = b.v(gu);
                         const std::string a_ = "acc" + std::to_string(uslot[n.i]) + "_" + std::to_string(n.ch);
                         const std::string d_ = "dg" + std::to_string(uslot[n.i]) + "_" + std::to_string(n.ch);

@@ -60,6 +60,22 @@ def test_generated_source_compiles(name):
     api.generic_compile_check(E(name))
 
 
+@pytest.mark.parametrize("name", ["image_warping", "poisson_image_editing", "arap_mesh_deformation",
+                                  "volume_denoise", "curve_smoothing", "intrinsic_image_decomposition",
+                                  "shape_from_shading", "optical_flow", "cotangent_mesh_smoothing",
+                                  "embedded_mesh_deformation", "robust_nonrigid_alignment",
+                                  "volumetric_mesh_deformation"])
+def test_dump_j_columns_name_valid_channels(name):
+    """saveJToCRS columns are uoff + channels * element + ch with ch < channels (a dangling
+    pool reference in the generator once emitted garbage channels after diff() grew the pool)."""
+    import re
+    src = api.generic_source(E(name))
+    cols = re.findall(r"cc\d+\[\d+\] = a\.uoff\[\d+\] \+ (\d+) \* .*? \+ (\d+);", src)
+    assert cols
+    for ch, c in cols:
+        assert int(c) < int(ch), (ch, c)
+
+
 def _write(tmp_path, name, text):
     p = tmp_path / name
     p.write_text(text)
