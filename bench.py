@@ -48,7 +48,7 @@ def apply_bytes_per_px(i: int) -> int:
 # bench). FETCH_SIZE reads exactly 1/2 of the bytes on gfx950 for 1/4/8/16-B-per-lane
 # streaming reads and WRITE_SIZE is exact (profiles/r01_fetchcal.json, 1 GiB arrays), so
 # traffic = 2 FETCH_SIZE + WRITE_SIZE, averaged over the lIterations in-loop launches.
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r01d_pmc.json")
 APPLY_VARIANT = {0: "iw_apply<float, 1, 0,", 1: "iw_apply<float, 2, 1,", 2: "iw_apply<float, 2, 2,"}
 
 
@@ -217,7 +217,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / PEAK_HBM_GBS,
             "traffic": (pmc_traffic(args.liter) if world == 1 and args.size == 4096 else None),
-            "traffic_unit": "bytes per launch (2 FETCH_SIZE + WRITE_SIZE, profiles/r01_pmc.json)",
+            "traffic_unit": "bytes per launch (2 FETCH_SIZE + WRITE_SIZE, profiles/r01d_pmc.json)",
             "avg_us": avg_apply_s * 1e6,
             "launches": n_apply,
             "bytes_per_px": bpp,
