@@ -3,7 +3,11 @@
 // reference's init / step exactly (API/src/solverGPUGaussNewton.t:1766-2349),
 // including the LM trust-region update and its early exits.
 #pragma once
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
+#include <vector>
 #include "csr.h"
 #include "stencil_driver.h"
 
@@ -194,6 +198,27 @@ public:
         allreduce(rz(0), 1);
         const int* stop = lm_ ? stop_ : nullptr;
         if (mat_) materialize();   // cusparseOuter (:2068): J, J^T (, J^T J) at the current X
+        if (pcg_graph_begin(params, Lit)) {
+            pcg_loop(Lit, use_pre, stop);
+            pcg_graph_end();
+        }
+        if (!lm_) {
+            if (Lit > 0) update(false);
+            precompute();
+            tbegin("cost"); op_->cost(red_.slot(nb(), kScCost), stream_); tend();
+            allreduce(kScCost, 1);
+            const double c = read(kScCost);
+            op_->unbind(stream_);
+            end_call();
+            prev_cost_ = c;
+            ++n_iter_;
+            return 1;
+        }
+        return lm_finish_step();
+    }
+
+    // PCG inner loop (PCGStep1-3, :607-845) of one step; launches only, no host sync.
+    void pcg_loop(int Lit, int use_pre, const int* stop) {
         for (int i = 0; i < Lit; ++i) {
             exchange_vec(p_);
             if (mat_) {
@@ -230,19 +255,68 @@ public:
                                    red_.scalars + kScQ0, i, sp_.q_tolerance, stop_);
             OPT_HIP_CHECK(hipGetLastError());
         }
-        if (!lm_) {
-            if (Lit > 0) update(false);
-            precompute();
-            tbegin("cost"); op_->cost(red_.slot(nb(), kScCost), stream_); tend();
-            allreduce(kScCost, 1);
-            const double c = read(kScCost);
-            op_->unbind(stream_);
-            end_call();
-            prev_cost_ = c;
-            ++n_iter_;
-            return 1;
+    }
+
+    // The PCG loop of a launch-bound (small) problem costs more in launches than in
+    // kernel time (poisson 512^2: ~30 launches of a few us each per step), so on one GPU
+    // it is captured once as a hipGraph and replayed. The graph is keyed on everything
+    // its launches bake in: the bound arrays and scalar parameter values, the plan's
+    // buffers and lIterations. Not used with timers (per-kernel events), row slabs
+    // (RCCL calls between launches), the materialized path, or graph-domain energies
+    // (their adjacency may be rebuilt on bind). OPT_AMD_NO_GRAPH=1 turns it off.
+    // Returns true when the caller must issue the launches (eagerly or under capture).
+    bool pcg_graph_begin(void** params, int Lit) {
+        if (distributed() || mat_ || timer_.mode || !spec_.graphs.empty() || Lit <= 0 || graph_off_) {
+            drop_graph();
+            return true;
         }
-        // ---- LM: model cost, speculative update, accept / reject (:2229-2292)
+        std::vector<unsigned long long> key{(unsigned long long)Lit, (unsigned long long)(uintptr_t)red_.scalars,
+                                            (unsigned long long)(uintptr_t)red_.partials,
+                                            (unsigned long long)(uintptr_t)red_.ticket,
+                                            (unsigned long long)(uintptr_t)op_.get(),
+                                            (unsigned long long)(uintptr_t)p_};
+        for (const DeclImage& im : spec_.images)   // arrays by address, scalars by value (below)
+            if (im.index >= 0 && im.index < spec_.n_params_total)
+                key.push_back((unsigned long long)(uintptr_t)params[im.index]);
+        {   // solver parameters the loop bakes in (Opt_SetSolverParameter may change them)
+            unsigned long long qt = 0;
+            memcpy(&qt, &sp_.q_tolerance, sizeof(sp_.q_tolerance) <= 8 ? sizeof(sp_.q_tolerance) : 8);
+            key.push_back(qt);
+            key.push_back((unsigned long long)sp_.residual_reset_period);
+        }
+        for (const DeclParam& d : spec_.params) {
+            unsigned long long v = 0;
+            if (d.index >= 0 && d.index < spec_.n_params_total && params[d.index]) memcpy(&v, params[d.index], d.type == "double" ? 8 : 4);
+            key.push_back(v);
+        }
+        if (graph_exec_ && key == graph_key_) {
+            OPT_HIP_CHECK(hipGraphLaunch(graph_exec_, stream_));
+            return false;
+        }
+        drop_graph();
+        graph_key_ = key;
+        OPT_HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeRelaxed));
+        capturing_ = true;
+        return true;
+    }
+    void pcg_graph_end() {
+        if (!capturing_) return;
+        capturing_ = false;
+        hipGraph_t g = nullptr;
+        OPT_HIP_CHECK(hipStreamEndCapture(stream_, &g));
+        OPT_HIP_CHECK(hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0));
+        OPT_HIP_CHECK(hipGraphDestroy(g));
+        OPT_HIP_CHECK(hipGraphLaunch(graph_exec_, stream_));
+    }
+    void drop_graph() {
+        if (graph_exec_) OPT_HIP_CHECK(hipGraphExecDestroy(graph_exec_));
+        graph_exec_ = nullptr;
+        graph_key_.clear();
+    }
+
+    // ---- LM: model cost, speculative update, accept / reject (:2229-2292)
+    int lm_finish_step() {
+        const int Lit = std::max(0, sp_.lIterations);
         exchange_vec(delta_);
         tbegin("model_cost"); op_->model_cost(delta_, red_.slot(nb(), kScModel), stream_); tend();
         if (Lit > 0) update(true);
@@ -417,6 +491,7 @@ private:
         }
     }
     void release() {
+        drop_graph();
         for (T** v : {&r_, &diag_, &pre_, &p_, &Ap_, &delta_, &b_, &CtC_, &SSq_, &prev_, &Adelta_}) {
             dfree(*v);
             *v = nullptr;
@@ -540,6 +615,10 @@ private:
     T *b_ = nullptr, *CtC_ = nullptr, *SSq_ = nullptr, *prev_ = nullptr, *Adelta_ = nullptr;
     uint8_t* flags_ = nullptr;
     int* stop_ = nullptr;
+    hipGraphExec_t graph_exec_ = nullptr;      // captured PCG loop (pcg_graph_begin)
+    std::vector<unsigned long long> graph_key_;
+    bool capturing_ = false;
+    const bool graph_off_ = getenv("OPT_AMD_NO_GRAPH") && atoi(getenv("OPT_AMD_NO_GRAPH"));
     std::unique_ptr<MaterializedJacobian<T>> mat_;
     float radius_ = 1e4f, decrease_ = 2.0f;
 };

@@ -1,0 +1,58 @@
+"""The generic driver's PCG loop replayed as a hipGraph (stencil_plan.h: pcg_graph_begin)
+gives bitwise the same iterates as eager launches (OPT_AMD_NO_GRAPH=1), for GN and for LM
+(device-side zeta exit inside the graph), and re-captures when a scalar parameter the
+launches bake in changes between steps."""
+import os
+
+import numpy as np
+import pytest
+
+from opt_amd import OptSolver, workloads
+from tests.iw_helpers import ROOT, device_params, perturbed, solver
+
+pytestmark = pytest.mark.gpu
+POISSON = os.path.join(ROOT, "energies", "poisson_image_editing.t")
+
+
+def _poisson(monkeypatch, graph, kind):
+    import torch
+
+    monkeypatch.setenv("OPT_AMD_NO_GRAPH", "0" if graph else "1")
+    w = workloads.poisson_image_editing(96, 80, seed=4)
+    prm = [torch.from_numpy(w[k].copy()).cuda() for k in ("X", "T", "M")]
+    s = OptSolver([96, 80], POISSON, kind)
+    s.set_solver_params({"nIterations": 4, "lIterations": 10})
+    costs = s.profiled_solve(prm)
+    return costs, prm[0].cpu().numpy()
+
+
+@pytest.mark.parametrize("kind", ["gaussNewtonGPU", "LMGPU"])
+def test_graph_replay_is_bitwise_eager(monkeypatch, kind):
+    c_eager, x_eager = _poisson(monkeypatch, False, kind)
+    c_graph, x_graph = _poisson(monkeypatch, True, kind)
+    assert c_graph == c_eager
+    np.testing.assert_array_equal(x_graph, x_eager)
+
+
+def _iw_lm_with_weight_change(monkeypatch, graph):
+    monkeypatch.setenv("OPT_AMD_NO_GRAPH", "0" if graph else "1")
+    w = perturbed(70, 50, seed=8)
+    s = solver(70, 50, kind="LMGPU")
+    s.set_solver_params({"nIterations": 6, "lIterations": 10})
+    prm = device_params(w)
+    s.init(prm)
+    costs = []
+    for k in range(6):
+        prm[-1] = float(w["w_regSqrt"]) * (1.0 + 0.5 * (k >= 3))   # new value from step 3 on
+        if not s.step(prm):
+            break
+        costs.append(s.cost())
+    return costs, prm[0].cpu().numpy()
+
+
+def test_graph_recaptures_on_parameter_change(monkeypatch):
+    c_eager, o_eager = _iw_lm_with_weight_change(monkeypatch, False)
+    c_graph, o_graph = _iw_lm_with_weight_change(monkeypatch, True)
+    assert len(c_eager) >= 4
+    assert c_graph == c_eager
+    np.testing.assert_array_equal(o_graph, o_eager)
