@@ -24,7 +24,7 @@ local function has_depth(dx, dy) return greater(Z_in(dx, dy), 0) end
 -- back-projected point of pixel (x+dx, y+dy)
 local function point(dx, dy)
     local z = Z(dx, dy)
-    return Vector(((x + dx - cx) / fx) * z, ((y + dy - cy) / fy) * z, z)
+    return Vector(((dx + x - cx) / fx) * z, ((dy + y - cy) / fy) * z, z)
 end
 
 -- unit normal from the left / upper neighbours
@@ -50,7 +50,7 @@ local function target(dx, dy)
 end
 
 local shading_error = ComputedArray("B_I", {W, H},
-    Select(InBoundsExpanded(0, 0, 1) * has_depth(-1, 0) * has_depth(0, 0) * has_depth(0, -1),
+    Select(InBoundsExpanded(0, 0, 1) * (has_depth(-1, 0) * has_depth(0, 0) * has_depth(0, -1)),
            shading(0, 0) - target(0, 0), 0))
 
 Exclude(Not(has_depth(0, 0)))
@@ -58,9 +58,9 @@ Exclude(Not(has_depth(0, 0)))
 Energy(Select(has_depth(0, 0), sqrt_wp * (Z(0, 0) - Z_in(0, 0)), 0))
 
 Energy(Select(InBoundsExpanded(0, 0, 1),
-              sqrt_wg * (shading_error(0, 0) - shading_error(1, 0)) * edge_row(0, 0), 0))
+              sqrt_wg * ((shading_error(0, 0) - shading_error(1, 0)) * edge_row(0, 0)), 0))
 Energy(Select(InBoundsExpanded(0, 0, 1),
-              sqrt_wg * (shading_error(0, 0) - shading_error(0, 1)) * edge_col(0, 0), 0))
+              sqrt_wg * ((shading_error(0, 0) - shading_error(0, 1)) * edge_col(0, 0)), 0))
 
 local function smooth_to(dx, dy) return less(abs(Z(0, 0) - Z(dx, dy)), 0.01) end
 local smooth_ok = ComputedArray("valid", {W, H},

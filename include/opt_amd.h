@@ -27,6 +27,17 @@ long long OptAMD_PlanUnknownCount(Opt_Plan* plan);
  * ...); writes a NUL-terminated name into buf. Returns the name length. */
 int OptAMD_PlanFamily(Opt_Plan* plan, char* buf, int buflen);
 
+/* Kernel family Opt_ProblemDefine chose for the energy file: a hand-written family
+ * only when the file lowers to exactly that family's residual templates, else
+ * "generic" (kernels generated from the file at plan time). No device needed. */
+int OptAMD_ProblemFamily(Opt_Problem* problem, char* buf, int buflen);
+
+/* Structural signature of an energy file as the front end lowers it (declaration
+ * kinds/types/indices, ComputedArray, Exclude and residual templates; names dropped):
+ * two files with equal signatures define the same problem. Returns the length, or -1
+ * with the error message in buf. No device needed. */
+int OptAMD_GenericSignature(const char* filename, char* buf, int buflen);
+
 /* r = -J^T F and the CERES-guarded Jacobi preconditioner pre = 1/(1+sqrt(diag J^TJ))^2
  * (or the reference's forced value when UsePreconditioner(false)) at the current
  * unknowns; *r_dot_pre_r = sum r.(pre*r) (reference kernels.PCGInit1,

@@ -54,6 +54,8 @@ _SIGNATURES = [
     ("Opt_ProblemCurrentCost", ctypes.c_double, [_VP, _VP]),
     ("OptAMD_PlanUnknownCount", ctypes.c_longlong, [_VP]),
     ("OptAMD_PlanFamily", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int]),
+    ("OptAMD_ProblemFamily", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int]),
+    ("OptAMD_GenericSignature", ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]),
     ("OptAMD_EvalJTF", ctypes.c_int, [_VP, _VP, ctypes.POINTER(_VP), _VP, _VP, ctypes.POINTER(ctypes.c_double)]),
     ("OptAMD_ApplyJTJ", ctypes.c_int, [_VP, _VP, ctypes.POINTER(_VP), _VP, _VP, ctypes.POINTER(ctypes.c_double)]),
     ("OptAMD_EvalCost", ctypes.c_double, [_VP, _VP, ctypes.POINTER(_VP)]),
@@ -89,11 +91,13 @@ _SIGNATURES = [
 EXPORTED_SYMBOLS = [s[0] for s in _SIGNATURES]
 
 
-def load_library(path: str = LIB_PATH):
-    """Load libopt_amd.so; raise if it is missing (no fallback path exists)."""
+def load_library(path: str = None):
+    """Load libopt_amd.so (OPT_AMD_LIB overrides the in-tree path, for A/B builds);
+    raise if it is missing (no fallback path exists)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("OPT_AMD_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise OptError(
             f"{path} not found: build the HIP runtime first "
@@ -391,6 +395,30 @@ def generic_describe(energy_file: str) -> List[str]:
     if r < 0:
         raise OptError(txt)
     return txt.splitlines()
+
+
+def generic_signature(energy_file: str) -> str:
+    """Structural signature of the lowered energy (OptAMD_GenericSignature)."""
+    r, txt = _text_call(load_library().OptAMD_GenericSignature, energy_file.encode())
+    if r < 0:
+        raise OptError(txt)
+    return txt
+
+
+def problem_family(energy_file: str, solver_kind: str = "gaussNewtonGPU") -> str:
+    """Kernel family Opt_ProblemDefine picks for `energy_file` (OptAMD_ProblemFamily):
+    a hand-written family only if the file lowers to exactly its residual templates."""
+    lib = load_library()
+    ip = InitParams()
+    ip.backend = b"backend_cuda"
+    st = lib.Opt_NewState(ip)
+    pr = lib.Opt_ProblemDefine(st, energy_file.encode(), solver_kind.encode())
+    if not pr:
+        raise OptError(f"Opt_ProblemDefine refused {energy_file}")
+    buf = ctypes.create_string_buffer(64)
+    lib.OptAMD_ProblemFamily(pr, buf, 64)
+    lib.Opt_ProblemDelete(st, pr)
+    return buf.value.decode()
 
 
 def generic_compile_check(energy_file: str, double: bool = False) -> None:

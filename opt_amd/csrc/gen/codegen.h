@@ -13,7 +13,7 @@
         int dims[3];                /* unknowns' index space, unused dims = 1 */            \
         long long npix;             /* elements of that space */                            \
         const void* img[16];        /* by image id: unknowns (T) and known arrays */        \
-        float prm[32];              /* by parameter id */                                   \
+        double prm[32];             /* by parameter id, at full width (cast to T on use) */ \
         const int* slot[16];        /* graph vertex arrays, graph-major */                  \
         const int* goff[16];        /* per slot: incidence offsets by vertex (N+1) */       \
         const int* geid[16];        /* per slot: incident edge ids, ascending */            \

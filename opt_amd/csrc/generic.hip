@@ -115,6 +115,86 @@ bool generic_accepts(const std::string& text, ProblemSpec* spec, std::string* er
     return true;
 }
 
+// Structural signature of a lowered energy: every declaration (kind, element type,
+// channels, index space, problemparams index — names dropped) and every residual,
+// ComputedArray and exclusion template as the hash-consed pool prints it. Two energy
+// files with equal signatures define the same problem and the same derivatives
+// (the reference derives all kernels from exactly these, o.t:1295-1348, 2669-2715).
+bool generic_signature(const std::string& text, std::string* sig, bool* use_pre, std::string* err) {
+    gen::GModel m;
+    if (!gen::build_model(text, &m, err)) return false;
+    if (!m.unsupported.empty()) { *err = "unsupported: " + m.unsupported; return false; }
+    std::string s;
+    auto ids = [](const std::vector<int>& v) {
+        std::string o;
+        for (int x : v) o += std::to_string(x) + ",";
+        return o;
+    };
+    for (auto& d : m.dims) s += "D" + std::to_string(d.index) + ";";
+    for (auto& im : m.images)
+        s += "I" + std::to_string(im.index) + ":" + std::to_string(im.channels) + (im.unknown ? "u" : "a") +
+             (im.internal ? "i" : "") + (im.tvalued ? "t" : "") + im.elem + "{" + ids(im.dims) + "};";
+    for (auto& p : m.params) s += "P" + std::to_string(p.index) + ":" + p.type + ";";
+    for (auto& g : m.graphs) s += "G{" + ids(g.dims) + "}{" + ids(g.slot_index) + "};";
+    for (auto& c : m.computed) {
+        s += "C" + std::to_string(c.image) + ":";
+        for (int e : c.expr) s += m.pool.str(e) + "|";
+        std::vector<std::string> gs;   // a set: its order follows traversal, not meaning
+        for (auto& g : c.grads)
+            gs.push_back("g" + std::to_string(g.ch) + "," + (g.u >= 0 ? m.pool.str(g.u) : std::string("-")) + "," +
+                         (g.gimg >= 0 ? "img," : "const,") + (g.expr >= 0 ? m.pool.str(g.expr) : std::string("-")) + "|");
+        std::sort(gs.begin(), gs.end());
+        for (auto& g : gs) s += g;
+        for (int k = 0; k < 3; ++k) s += std::to_string(c.lo[k]) + ":" + std::to_string(c.hi[k]) + ",";
+        s += ";";
+    }
+    s += "X" + (m.exclude >= 0 ? m.pool.str(m.exclude) : std::string("-")) + ";";
+    for (auto& r : m.residuals)
+        s += "R" + std::to_string(r.graph) + ":" + std::to_string(r.unknowns.size()) + ":" + m.pool.str(r.expr) + ";";
+    *sig = s;
+    if (use_pre) *use_pre = m.use_preconditioner;
+    return true;
+}
+
+namespace {
+// The energy each hand-written family implements: energies/<family>.t, embedded at build
+// time (Makefile: build/gen/family_energies_src.h). Each lowers to exactly the reference
+// example's templates (tests/test_generic_frontend.py).
+const std::pair<const char*, const char*> kFamilyEnergies[] = {
+#include "family_energies_src.h"
+};
+}  // namespace
+
+bool family_is_canonical(ProblemSpec* spec, std::string* why) {
+    static std::mutex mu;
+    static std::map<std::string, std::string> canon;   // family -> signature
+    std::lock_guard<std::mutex> lk(mu);
+    if (!canon.count(spec->family)) {
+        for (auto& fe : kFamilyEnergies) {
+            if (spec->family != fe.first) continue;
+            std::string sig, err;
+            if (!generic_signature(fe.second, &sig, nullptr, &err)) {
+                *why = "canonical energy of family " + spec->family + " does not lower: " + err;
+                return false;
+            }
+            canon[spec->family] = sig;
+        }
+        if (!canon.count(spec->family)) { *why = "no canonical energy for family " + spec->family; return false; }
+    }
+    std::string sig, err;
+    bool use_pre = false;
+    if (!generic_signature(spec->text, &sig, &use_pre, &err)) {
+        *why = err;
+        return false;
+    }
+    if (sig != canon[spec->family]) {
+        *why = "the energy's residuals differ from the " + spec->family + " family's";
+        return false;
+    }
+    spec->use_preconditioner = use_pre;
+    return true;
+}
+
 template <typename TT>
 class GenericOp {
 public:
@@ -228,10 +308,10 @@ public:
         for (size_t j = 0; j < m_.params.size(); ++j) {
             const void* p = params[m_.params[j].index];
             const std::string& t = m_.params[j].type;
-            a_.prm[j] = t == "double" ? (float)*(const double*)p
-                        : (t == "int" || t == "int32") ? (float)*(const int*)p
-                        : t == "uint" || t == "uint32" ? (float)*(const unsigned*)p
-                                                       : *(const float*)p;
+            a_.prm[j] = t == "double" ? *(const double*)p
+                        : (t == "int" || t == "int32") ? (double)*(const int*)p
+                        : t == "uint" || t == "uint32" ? (double)*(const unsigned*)p
+                                                       : (double)*(const float*)p;
         }
         int sb = 0;
         for (size_t g = 0; g < m_.graphs.size(); ++g) {
@@ -252,6 +332,17 @@ public:
         a_.own_lo = own_lo_;
         a_.own_hi = own_hi_;
         for (size_t k = 0; k < unk_.size(); ++k) a_.uoff[k] = uoff_[k];
+    }
+    // hipGraph replay gate + key (StencilPlan::pcg_graph_begin), from the lowered model:
+    // no capture for graph energies (adjacency rebuilt on bind); the key is the argument
+    // block every captured launch receives — image / slot / incidence pointers and
+    // parameter values as bound by bind().
+    bool capture_key(std::vector<unsigned long long>* key) const {
+        if (!m_.graphs.empty()) return false;
+        unsigned long long w[(sizeof(GenArgs) + 7) / 8] = {};
+        memcpy(w, &a_, sizeof(GenArgs));
+        key->insert(key->end(), w, w + (sizeof(GenArgs) + 7) / 8);
+        return true;
     }
     void unbind(hipStream_t s) {
         if (!opts_.host_buffers) return;

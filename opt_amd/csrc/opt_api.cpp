@@ -86,8 +86,20 @@ Opt_Problem* Opt_ProblemDefine(Opt_State* state, const char* filename, const cha
     p->spec.text = ss.str();
     std::string err;
     bool ok = optamd::parse_energy(ss.str(), &p->spec, &err) && optamd::classify(&p->spec, &err);
-    // energies no hand-written family recognises (or all, with OPT_AMD_GENERIC=1) go to the
-    // general front end
+    // A hand-written family serves the file only if the file lowers to exactly that
+    // family's residual templates (the reference derives every kernel from the file,
+    // o.t:1295-1348); any other energy, and every energy with OPT_AMD_GENERIC=1, goes to
+    // the general front end.
+    if (ok) {
+        std::string why;
+        if (!optamd::family_is_canonical(&p->spec, &why)) {
+            if (state->opts.verbosity > 0)
+                fprintf(stderr, "[opt_amd] %s: not the %s family's energy (%s); using generated kernels\n",
+                        filename, p->spec.family.c_str(), why.c_str());
+            err = why;
+            ok = false;
+        }
+    }
     if (!ok || optamd::env_int("OPT_AMD_GENERIC", 0)) {
         std::string gerr;
         if (optamd::generic_accepts(ss.str(), &p->spec, &gerr)) {
@@ -184,6 +196,10 @@ static int copy_name(const std::string& s, char* buf, int n) {
 }
 int OptAMD_PlanFamily(Opt_Plan* plan, char* buf, int n) {
     return valid_plan(plan, "OptAMD_PlanFamily") ? copy_name(plan->impl->family(), buf, n) : -1;
+}
+int OptAMD_ProblemFamily(Opt_Problem* problem, char* buf, int n) {
+    if (!problem) { fprintf(stderr, "[opt_amd] OptAMD_ProblemFamily: null Opt_Problem\n"); return -1; }
+    return copy_name(problem->spec.family, buf, n);
 }
 int OptAMD_EvalJTF(Opt_State* state, Opt_Plan* plan, void** params, void* r, void* pre, double* rz) {
     if (!valid_state(state, "OptAMD_EvalJTF") || !valid_plan(plan, "OptAMD_EvalJTF") || !r || !pre)
@@ -412,4 +428,10 @@ int OptAMD_GenericDescribe(const char* filename, char* buf, int n) {
     const int r = optamd::generic_describe(text, &out);
     copy_name(out, buf, n);
     return r;
+}
+int OptAMD_GenericSignature(const char* filename, char* buf, int n) {
+    std::string text, sig, err;
+    if (!read_file(filename, &text)) return copy_name("cannot read energy file", buf, n), -1;
+    if (!optamd::generic_signature(text, &sig, nullptr, &err)) return copy_name(err, buf, n), -1;
+    return copy_name(sig, buf, n);
 }

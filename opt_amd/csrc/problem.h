@@ -66,5 +66,11 @@ bool generic_accepts(const std::string& text, ProblemSpec* spec, std::string* er
 int generic_source(const std::string& text, bool dbl, std::string* out);
 int generic_describe(const std::string& text, std::string* out);
 int generic_compile_check(const std::string& text, bool dbl, std::string* log);
+// Structural signature of the lowered energy (declarations + residual templates, names
+// dropped); false + message if the front end cannot lower it.
+bool generic_signature(const std::string& text, std::string* sig, bool* use_pre, std::string* err);
+// true iff spec->text lowers to exactly the energy spec->family's kernels implement
+// (then also takes UsePreconditioner from the lowered model); else false + reason.
+bool family_is_canonical(ProblemSpec* spec, std::string* why);
 
 }  // namespace optamd

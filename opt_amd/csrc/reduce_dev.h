@@ -23,6 +23,18 @@ struct ReduceSlot {
     double* out;          // K results
     int nblocks;
 };
+// Ordering of the hand-off. The partials go out as sc1 (write-through) stores, every
+// storing lane drains them (s_waitcnt vmcnt(0)) before its agent-scope ticket add, and
+// the last block reads them back with sc1 loads after an agent acquire: the guide's
+// validated "one lane per workgroup, agent-scope add, last adder" row
+// (MI355X_MICROARCH.md, Valid forms). A release on every ticket add
+// (-DOPTAMD_REDUCE_ORDER=__ATOMIC_ACQ_REL: buffer_wbl2 sc1 per block) writes back the
+// XCD L2's freshly dirtied output lines before each add; measured on MI355X it takes
+// the image_warping JᵀJ·p apply from 142 to 236 µs and the GN step from 4.76 to
+// 7.04 ms (profiles/r02b_reduce_order.json), so the tickets stay relaxed.
+#ifndef OPTAMD_REDUCE_ORDER
+#define OPTAMD_REDUCE_ORDER __ATOMIC_RELAXED
+#endif
 constexpr int kTicketShards = 32;     // arrival counters (b % 32: each fed by one XCD)
 constexpr int kTicketStride = 16;     // unsigned words between counters (64 B)
 constexpr int kTicketWords = (kTicketShards + 1) * kTicketStride;
@@ -66,12 +78,12 @@ __device__ __forceinline__ void block_reduce_publish(const double (&v)[K], const
         const int shards = rs.nblocks < kTicketShards ? rs.nblocks : kTicketShards;
         const unsigned in_shard = (unsigned)((rs.nblocks - shard + kTicketShards - 1) / kTicketShards);
         unsigned* sc = rs.ticket + shard * kTicketStride;
-        const unsigned t = __hip_atomic_fetch_add(sc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned t = __hip_atomic_fetch_add(sc, 1u, OPTAMD_REDUCE_ORDER, __HIP_MEMORY_SCOPE_AGENT);
         int last = 0;
         if (t == in_shard - 1) {
             __hip_atomic_store(sc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             unsigned* top = rs.ticket + kTicketShards * kTicketStride;
-            const unsigned t2 = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned t2 = __hip_atomic_fetch_add(top, 1u, OPTAMD_REDUCE_ORDER, __HIP_MEMORY_SCOPE_AGENT);
             if (t2 == (unsigned)(shards - 1)) {
                 __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 last = 1;
@@ -81,6 +93,8 @@ __device__ __forceinline__ void block_reduce_publish(const double (&v)[K], const
     }
     __syncthreads();
     if (!last_flag) return;
+    // one block per launch: the agent acquire (buffer_inv sc1) is cheap here
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // Last arriver: fixed-order sum of all partials (sc1 loads bypass the stale L1).
     __shared__ double acc[kBlock];
 #pragma unroll

@@ -96,6 +96,14 @@ struct HasSlabRefusal : std::false_type {};
 template <class Op>
 struct HasSlabRefusal<Op, std::void_t<decltype(std::declval<const Op&>().slab_refusal())>> : std::true_type {};
 
+// Ops that describe their own hipGraph capture gate and key (GenericOp: the kernel
+// argument block the generated launches receive) instead of the declaration parser's.
+template <class Op, class = void>
+struct HasCaptureKey : std::false_type {};
+template <class Op>
+struct HasCaptureKey<Op, std::void_t<decltype(std::declval<const Op&>().capture_key(
+                             (std::vector<unsigned long long>*)nullptr))>> : std::true_type {};
+
 template <class Op>
 class StencilPlan final : public Plan {
 public:
@@ -261,12 +269,17 @@ public:
     // kernel time (poisson 512^2: ~30 launches of a few us each per step), so on one GPU
     // it is captured once as a hipGraph and replayed. The graph is keyed on everything
     // its launches bake in: the bound arrays and scalar parameter values, the plan's
-    // buffers and lIterations. Not used with timers (per-kernel events), row slabs
-    // (RCCL calls between launches), the materialized path, or graph-domain energies
-    // (their adjacency may be rebuilt on bind). OPT_AMD_NO_GRAPH=1 turns it off.
+    // buffers and lIterations; for generated kernels, the whole argument block they
+    // receive (Op::capture_key, built from the lowered model, not the declaration
+    // parser). Not used with timers (per-kernel events), row slabs (RCCL calls between
+    // launches), the materialized path, or graph-domain energies (their adjacency may be
+    // rebuilt on bind). OPT_AMD_NO_GRAPH=1 turns it off.
     // Returns true when the caller must issue the launches (eagerly or under capture).
     bool pcg_graph_begin(void** params, int Lit) {
-        if (distributed() || mat_ || timer_.mode || !spec_.graphs.empty() || Lit <= 0 || graph_off_) {
+        bool graphs = !spec_.graphs.empty();
+        std::vector<unsigned long long> op_key;
+        if constexpr (HasCaptureKey<Op>::value) graphs = !op_->capture_key(&op_key);
+        if (distributed() || mat_ || timer_.mode || graphs || Lit <= 0 || graph_off_) {
             drop_graph();
             return true;
         }
@@ -275,19 +288,23 @@ public:
                                             (unsigned long long)(uintptr_t)red_.ticket,
                                             (unsigned long long)(uintptr_t)op_.get(),
                                             (unsigned long long)(uintptr_t)p_};
-        for (const DeclImage& im : spec_.images)   // arrays by address, scalars by value (below)
-            if (im.index >= 0 && im.index < spec_.n_params_total)
-                key.push_back((unsigned long long)(uintptr_t)params[im.index]);
+        key.insert(key.end(), op_key.begin(), op_key.end());
+        if constexpr (!HasCaptureKey<Op>::value) {
+            for (const DeclImage& im : spec_.images)   // arrays by address, scalars by value (below)
+                if (im.index >= 0 && im.index < spec_.n_params_total)
+                    key.push_back((unsigned long long)(uintptr_t)params[im.index]);
+            for (const DeclParam& d : spec_.params) {
+                unsigned long long v = 0;
+                if (d.index >= 0 && d.index < spec_.n_params_total && params[d.index])
+                    memcpy(&v, params[d.index], d.type == "double" ? 8 : 4);
+                key.push_back(v);
+            }
+        }
         {   // solver parameters the loop bakes in (Opt_SetSolverParameter may change them)
             unsigned long long qt = 0;
             memcpy(&qt, &sp_.q_tolerance, sizeof(sp_.q_tolerance) <= 8 ? sizeof(sp_.q_tolerance) : 8);
             key.push_back(qt);
             key.push_back((unsigned long long)sp_.residual_reset_period);
-        }
-        for (const DeclParam& d : spec_.params) {
-            unsigned long long v = 0;
-            if (d.index >= 0 && d.index < spec_.n_params_total && params[d.index]) memcpy(&v, params[d.index], d.type == "double" ? 8 : 4);
-            key.push_back(v);
         }
         if (graph_exec_ && key == graph_key_) {
             OPT_HIP_CHECK(hipGraphLaunch(graph_exec_, stream_));

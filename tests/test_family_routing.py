@@ -1,0 +1,183 @@
+"""Opt_ProblemDefine honours the energy file it is given.
+
+A hand-written kernel family serves an energy file only when the file lowers to exactly
+that family's residual templates (declarations, ComputedArrays, Exclude and every
+residual expression, names aside: generic.hip family_is_canonical). The reference
+derives every kernel from the file (API/src/o.t:1295-1348, 2669-2715, 3173-3235), so an
+edited energy — an extra stencil point, a scaled term, an extra residual — with the
+family's declaration signature must run on kernels generated from that file.
+
+CPU: routing of canonical files, the reference's own files and perturbed variants.
+GPU: each variant solves on generated kernels, -J^T F equals the central-difference
+gradient of its own cost, and the cost differs from the unperturbed family's."""
+import os
+
+import numpy as np
+import pytest
+
+from opt_amd import api
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference"
+FAMILIES = ["image_warping", "poisson_image_editing", "optical_flow", "shape_from_shading",
+            "arap_mesh_deformation"]
+
+
+def E(name):
+    return os.path.join(ROOT, "energies", name + ".t")
+
+
+def _sub(text, old, new):
+    assert old in text, old
+    return text.replace(old, new, 1)
+
+
+# (family, variant id) -> list of (old, new) substitutions on energies/<family>.t
+VARIANTS = {
+    ("image_warping", "six_point_stencil"): [("{0, 1}, {0, -1} }", "{0, 1}, {0, -1}, {1, 1}, {-1, -1} }")],
+    ("image_warping", "scaled_fit"): [("Energy(fitW * Select", "Energy(3 * fitW * Select")],
+    ("image_warping", "extra_residual"): [("local isHandle", "Energy(0.5 * theta(0, 0))\nlocal isHandle")],
+    ("poisson_image_editing", "scaled_guidance"): [("- gradient(insert, ox, oy)", "- 2 * gradient(insert, ox, oy)")],
+    ("poisson_image_editing", "extra_residual"): [("    Energy(Select(InBounds(ox, oy)",
+                                                   "    Energy(0.25 * result(ox, oy))\n    Energy(Select(InBounds(ox, oy)")],
+    ("optical_flow", "scaled_fit"): [("Energy(fitW * brightness)", "Energy(2 * fitW * brightness)")],
+    ("optical_flow", "diagonal_neighbours"): [("{0, 1}, {0, -1} }", "{0, 1}, {0, -1}, {1, 1} }")],
+    ("shape_from_shading", "scaled_smoothness"): [("sqrt_ws * laplacian", "2 * sqrt_ws * laplacian")],
+    ("shape_from_shading", "changed_target"): [("intensity(dx, dy) * 0.5", "intensity(dx, dy) * 0.4")],
+    ("arap_mesh_deformation", "scaled_fit"): [("Energy(handle_term())", "Energy(2 * handle_term())")],
+    ("arap_mesh_deformation", "extra_residual"): [("Energy(handle_term())",
+                                                   "Energy(handle_term())\nEnergy(0.1 * euler(0))")],
+}
+
+
+def variant_file(tmp_path, family, vid):
+    text = open(E(family)).read()
+    for old, new in VARIANTS[(family, vid)]:
+        text = _sub(text, old, new)
+    p = tmp_path / f"{family}_{vid}.t"
+    p.write_text(text)
+    return str(p)
+
+
+@pytest.mark.parametrize("family", FAMILIES)
+def test_canonical_energies_select_their_family(family):
+    assert api.problem_family(E(family)) == family
+    assert api.problem_family(E(family), "LMGPU") == family
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference checkout not present")
+@pytest.mark.parametrize("family", FAMILIES)
+def test_reference_energy_files_select_their_family(family):
+    assert api.problem_family(os.path.join(REF, "examples", family, family + ".t")) == family
+
+
+@pytest.mark.parametrize("family,vid", sorted(VARIANTS))
+def test_perturbed_energies_go_to_generated_kernels(tmp_path, family, vid):
+    assert api.problem_family(variant_file(tmp_path, family, vid)) == "generic"
+
+
+def test_renamed_declarations_keep_the_family(tmp_path):
+    """Names are not part of the problem: renaming locals and the declared names keeps
+    the same residual templates, hence the hand-written family."""
+    text = open(E("image_warping")).read().replace("warped", "moved").replace('"Offset"', '"Pos"')
+    p = tmp_path / "renamed.t"
+    p.write_text(text)
+    assert api.problem_family(str(p)) == "image_warping"
+
+
+def test_energies_with_other_declaration_types_go_generic(tmp_path):
+    text = _sub(open(E("poisson_image_editing")).read(), 'Array("M", opt_float,', 'Array("M", uint8,')
+    p = tmp_path / "u8mask.t"
+    p.write_text(text)
+    assert api.problem_family(str(p)) == "generic"
+
+
+# ----------------------------------------------------------------------------- GPU
+def _cuda(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _problem(family, rng):
+    """(dims, problemparams, unknown tensors) for a small fp64 instance of `family`."""
+    from opt_amd import workloads
+    if family == "image_warping":
+        W, H = 14, 11
+        w = workloads.image_warping(W, H, seed=3, n_handles=4, max_move=0.1)
+        O = _cuda(w["Offset"].astype(np.float64) + 0.3 * rng.normal(size=w["Offset"].size))
+        A = _cuda(0.05 * rng.normal(size=W * H))
+        return [W, H], [O, A, _cuda(w["UrShape"]), _cuda(w["Constraints"]), _cuda(w["Mask"]),
+                        w["w_fitSqrt"], w["w_regSqrt"]], [O, A]
+    if family == "poisson_image_editing":
+        W, H = 12, 10
+        w = workloads.poisson_image_editing(W, H, seed=4)
+        X = _cuda(w["X"].astype(np.float64) + rng.normal(size=w["X"].size))
+        return [W, H], [X, _cuda(w["T"]), _cuda(w["M"])], [X]
+    if family == "optical_flow":
+        W, H = 16, 12
+        w = workloads.optical_flow(W, H, seed=5, sigma=2.0, max_flow=1.0)
+        X = _cuda(0.4 * rng.normal(size=2 * W * H))
+        return [W, H], [w["w_fitSqrt"], w["w_regSqrt"], X] + [_cuda(w[k]) for k in
+                                                             ("I", "I_hat", "I_hat_dx", "I_hat_dy")], [X]
+    if family == "shape_from_shading":
+        W, H = 16, 12
+        w = workloads.shape_from_shading(W, H, seed=6, valid_frac=0.8)
+        X = _cuda(w["X"].astype(np.float64))
+        return [W, H], [float(v) for v in w["params"]] + [X] + [_cuda(w[k]) for k in
+                                                               ("D_i", "Im", "edgeMaskR", "edgeMaskC")], [X]
+    w = workloads.arap_grid(5, 4, seed=7)
+    O = _cuda(w["Offset"].astype(np.float64) + 0.02 * rng.normal(size=w["Offset"].size))
+    A = _cuda(w["Angle"].astype(np.float64) + 0.2 * rng.normal(size=w["Angle"].size))
+    return [w["N"], w["E"]], [w["w_fitSqrt"], w["w_regSqrt"], O, A, _cuda(w["UrShape"]), _cuda(w["Constraints"]),
+                              None, _cuda(w["v0"]), _cuda(w["v1"])], [O, A]
+
+
+GPU_VARIANTS = [("image_warping", "six_point_stencil"), ("image_warping", "scaled_fit"),
+                ("poisson_image_editing", "extra_residual"), ("optical_flow", "diagonal_neighbours"),
+                ("shape_from_shading", "changed_target"), ("arap_mesh_deformation", "extra_residual")]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("family,vid", GPU_VARIANTS)
+def test_perturbed_energy_solves_its_own_energy(tmp_path, family, vid):
+    import torch
+    from opt_amd import OptSolver
+
+    dims, prm, unk = _problem(family, np.random.default_rng(11))
+    s = OptSolver(dims, variant_file(tmp_path, family, vid), "gaussNewtonGPU", double_precision=True)
+    assert s.family() == "generic"
+    fam = OptSolver(dims, E(family), "gaussNewtonGPU", double_precision=True)
+    assert fam.family() == family
+    c_var, c_fam = s.eval_cost(prm), fam.eval_cost(prm)
+    assert abs(c_var - c_fam) > 1e-6 * max(abs(c_fam), 1.0), (c_var, c_fam)
+    # -J^T F of the generated kernels = central-difference gradient of the variant's cost
+    n = s.unknown_count()
+    r = torch.zeros(n, dtype=torch.float64, device="cuda")
+    pre = torch.zeros_like(r)
+    s.eval_jtf(prm, r, pre)
+    rr = r.cpu().numpy()
+    rng = np.random.default_rng(2)
+    offs = np.cumsum([0] + [u.numel() for u in unk])
+    # excluded unknowns have r = 0 by definition (PCGInit1): check the free ones
+    cand = np.flatnonzero(rr != 0)
+    assert cand.size >= min(n, 16)
+    picks = rng.choice(cand, size=min(cand.size, 48), replace=False)
+    h = 1e-6
+    g, got = [], []
+    for k in picks:
+        j = int(np.searchsorted(offs, k, side="right") - 1)
+        flat = unk[j].view(-1)
+        i = int(k - offs[j])
+        x0 = flat[i].item()
+        flat[i] = x0 + h
+        cp = s.eval_cost(prm)
+        flat[i] = x0 - h
+        cm = s.eval_cost(prm)
+        flat[i] = x0
+        g.append((cp - cm) / (2 * h))
+        got.append(rr[k])
+    g, got = np.array(g), np.array(got)
+    assert np.abs(got + g).max() <= 1e-5 * max(np.abs(g).max(), 1.0)
+    s.set_solver_params({"nIterations": 2, "lIterations": 10})
+    costs = s.profiled_solve(prm)
+    assert costs[-1] < costs[0]

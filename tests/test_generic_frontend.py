@@ -212,7 +212,7 @@ Energy(C(1,0) - A(0,0,0))
     assert "gen_precompute_0" in src and "gen_precompute_1" not in src
 
 
-@pytest.mark.parametrize("name", ["intrinsic_image_decomposition", "cotangent_mesh_smoothing",
+@pytest.mark.parametrize("name", ["intrinsic_image_decomposition", "cotangent_mesh_smoothing", "shape_from_shading",
                                   "embedded_mesh_deformation", "robust_nonrigid_alignment",
                                   "volumetric_mesh_deformation", "image_warping", "optical_flow",
                                   "arap_mesh_deformation", "poisson_image_editing"])

@@ -56,3 +56,66 @@ def test_graph_recaptures_on_parameter_change(monkeypatch):
     assert len(c_eager) >= 4
     assert c_graph == c_eager
     np.testing.assert_array_equal(o_graph, o_eager)
+
+
+def _generated_iw_rebinding(monkeypatch, graph):
+    """Generated kernels (OPT_AMD_GENERIC=1): new buffers for every array from step 3 on,
+    so a replay keyed on stale pointers would read freed / old memory."""
+    import torch
+
+    monkeypatch.setenv("OPT_AMD_NO_GRAPH", "0" if graph else "1")
+    monkeypatch.setenv("OPT_AMD_GENERIC", "1")
+    w = perturbed(60, 40, seed=9)
+    s = solver(60, 40, kind="LMGPU")
+    assert s.family() == "generic"
+    s.set_solver_params({"nIterations": 6, "lIterations": 10})
+    prm = device_params(w)
+    s.init(prm)
+    costs = []
+    for k in range(6):
+        if k == 3:
+            prm = [p.clone() if isinstance(p, torch.Tensor) else p for p in prm]
+        if not s.step(prm):
+            break
+        costs.append(s.cost())
+    return costs, prm[0].cpu().numpy()
+
+
+def test_generated_graph_replay_follows_rebound_buffers(monkeypatch):
+    c_eager, o_eager = _generated_iw_rebinding(monkeypatch, False)
+    c_graph, o_graph = _generated_iw_rebinding(monkeypatch, True)
+    assert len(c_eager) >= 4
+    assert c_graph == c_eager
+    np.testing.assert_array_equal(o_graph, o_eager)
+
+
+def _embedded_rebinding(monkeypatch, graph):
+    """A graph energy whose declarations the simple parser cannot read (RotMatrix): new
+    edge arrays in a different order, on new buffers, between steps."""
+    import torch
+    from tests.test_generic_examples_gpu import E, problem
+
+    monkeypatch.setenv("OPT_AMD_NO_GRAPH", "0" if graph else "1")
+    dims, prm, _ = problem("embedded_mesh_deformation", np.random.default_rng(3))
+    s = OptSolver(dims, E("embedded_mesh_deformation"), "gaussNewtonGPU", double_precision=True)
+    s.set_solver_params({"nIterations": 5, "lIterations": 10})
+    s.init(prm)
+    costs = []
+    perm = np.random.default_rng(4).permutation(prm[-1].numel())
+    for k in range(5):
+        if k == 2:
+            prm = list(prm)
+            prm[-2] = torch.from_numpy(prm[-2].cpu().numpy()[perm].copy()).cuda()
+            prm[-1] = torch.from_numpy(prm[-1].cpu().numpy()[perm].copy()).cuda()
+        if not s.step(prm):
+            break
+        costs.append(s.cost())
+    return costs, prm[3].cpu().numpy()
+
+
+def test_graph_energy_rebinding_edges_matches_eager(monkeypatch):
+    c_eager, o_eager = _embedded_rebinding(monkeypatch, False)
+    c_graph, o_graph = _embedded_rebinding(monkeypatch, True)
+    assert len(c_eager) >= 3
+    assert c_graph == c_eager
+    np.testing.assert_array_equal(o_graph, o_eager)
