@@ -248,6 +248,180 @@ def shape_from_shading(sfs_params: dict, X0, D, Im, mask_edge) -> dict:
             "edgeMaskC": np.ascontiguousarray(mask_edge[H:2 * H]).reshape(-1).astype(np.uint8)}
 
 
+# ------------------------------------------------------ meshes: neighbour fans
+def vertex_fans(faces: np.ndarray, nv: int):
+    """Each vertex's neighbours in the cyclic order of its triangle fan, as OpenMesh's
+    vertex-vertex circulator visits them (the examples' initializeConnectivity loops).
+    Only the cyclic order matters to the energies built from it (prev / next of each
+    neighbour), not the start or the direction. A boundary vertex's fan is open: its
+    neighbours run from one boundary neighbour to the other and close cyclically."""
+    succ = [dict() for _ in range(nv)]
+    for f in np.asarray(faces, np.int64):
+        for i in range(len(f)):
+            v, a, b = int(f[i]), int(f[(i + 1) % len(f)]), int(f[(i - 1) % len(f)])
+            succ[v][a] = b      # around v: a then b (the face's orientation)
+    fans = []
+    for v in range(nv):
+        nxt = succ[v]
+        if not nxt:
+            fans.append([])
+            continue
+        has_pred = set(nxt.values())
+        starts = [a for a in nxt if a not in has_pred]
+        if len(starts) > 1:
+            raise ValueError("vertex %d is not manifold (%d fan pieces)" % (v, len(starts)))
+        a = starts[0] if starts else min(nxt)
+        ring = [a]
+        while a in nxt and nxt[a] != ring[0]:
+            a = nxt[a]
+            ring.append(a)
+        if len(set(ring)) != len(ring) or len(ring) != len(set(nxt) | has_pred):
+            raise ValueError("vertex %d: inconsistent fan" % v)
+        fans.append(ring)
+    return fans
+
+
+# ---------------------------------------------------- cotangent_mesh_smoothing
+def cotangent_mesh_smoothing(verts, faces) -> dict:
+    """examples/cotangent_mesh_smoothing/src/main.cpp:17-70 and CombinedSolver.h:16-160:
+    X = A = the vertex positions (float3); the graph has one edge per (vertex, fan
+    neighbour) as (head, curr, prev, next) with prev / next the cyclic fan neighbours of
+    curr (initializeConnectivity :78-125, grouped by head); w_fit = 1, w_reg = 0.5,
+    square-rooted (main.cpp:57-58)."""
+    P = np.asarray(verts, np.float32)
+    fans = vertex_fans(faces, len(P))
+    e = [[], [], [], []]
+    for h, ring in enumerate(fans):
+        n = len(ring)
+        for i, c in enumerate(ring):
+            e[0].append(h)
+            e[1].append(c)
+            e[2].append(ring[(i + n - 1) % n])
+            e[3].append(ring[(i + 1) % n])
+    v = [np.array(x, np.int32) for x in e]
+    return {"N": len(P), "E": len(v[0]), "X": P.reshape(-1).copy(), "A": P.reshape(-1).copy(),
+            "v0": v[0], "v1": v[1], "v2": v[2], "v3": v[3],
+            "w_fitSqrt": float(np.sqrt(f32(1.0))), "w_regSqrt": float(np.sqrt(f32(0.5)))}
+
+
+# --------------------------------------------------- embedded_mesh_deformation
+def _rot_axis(axis: str, deg) -> np.ndarray:
+    """mLib Matrix3x3::setRotation{X,Y,Z} (float, angle in degrees,
+    core-math/matrix3x3.h:126-170; degreesToRadians = x * (PIf / 180), utility.h:18)."""
+    rad = f32(deg) * (f32(3.14159265358979323846) / f32(180.0))
+    c, s = np.cos(rad, dtype=f32), np.sin(rad, dtype=f32)
+    o, z = f32(1), f32(0)
+    if axis == "x":
+        m = [o, z, z, z, c, -s, z, s, c]
+    elif axis == "y":
+        m = [c, z, s, z, o, z, -s, z, c]
+    else:
+        m = [c, -s, z, s, c, z, z, z, o]
+    return np.array(m, f32).reshape(3, 3)
+
+
+def _matmul_f32(a, b):
+    """mLib Matrix3x3 product in float, its summation order (matrix3x3.h:256-268)."""
+    r = np.zeros((3, 3), f32)
+    for i in range(3):
+        for j in range(3):
+            r[i, j] = (a[i, 0] * b[0, j] + a[i, 1] * b[1, j]) + a[i, 2] * b[2, j]
+    return r
+
+
+def embedded_mesh_deformation(verts, faces, marker_pos, marker_idx) -> dict:
+    """examples/embedded_mesh_deformation/src/main.cpp:17-90 and CombinedSolver.h:16-170:
+    Offset = UrShape = positions, RotMatrix = rotation(1e-3, 1e-3, 1e-3) degrees
+    (yaw/pitch/roll: R_y R_x R_z, row-major) for every vertex, Constraints = marker
+    targets (setConstraints(1): (1 - 1) p + 1 t) on the marker vertices and -inf
+    elsewhere, the graph = every mesh edge in both directions grouped by head
+    (createGraphFromNeighborLists), w_fit = 3, w_reg = 12, w_rot = 5 square-rooted."""
+    P = np.asarray(verts, np.float32)
+    N = len(P)
+    R = _matmul_f32(_matmul_f32(_rot_axis("y", 1e-3), _rot_axis("x", 1e-3)), _rot_axis("z", 1e-3))
+    und = np.array(mesh_edges(faces), np.int64)
+    directed = np.concatenate([und, und[:, ::-1]])
+    directed = directed[np.lexsort((directed[:, 1], directed[:, 0]))]
+    C = np.full((N, 3), -np.inf, np.float32)
+    for pos, i in zip(marker_pos, marker_idx):
+        C[i] = (f32(1) - f32(1)) * P[i] + f32(1) * np.asarray(pos, f32)
+    return {"N": N, "E": int(len(directed)), "Offset": P.reshape(-1).copy(),
+            "RotMatrix": np.tile(R.reshape(1, 9), (N, 1)).reshape(-1).copy(), "UrShape": P.reshape(-1).copy(),
+            "Constraints": C.reshape(-1), "v0": np.ascontiguousarray(directed[:, 0].astype(np.int32)),
+            "v1": np.ascontiguousarray(directed[:, 1].astype(np.int32)),
+            "w_fitSqrt": float(np.sqrt(f32(3.0))), "w_regSqrt": float(np.sqrt(f32(12.0))),
+            "w_rotSqrt": float(np.sqrt(f32(5.0)))}
+
+
+# ----------------------------------------------- intrinsic_image_decomposition
+def intrinsic_image_decomposition(rgb: np.ndarray, stride: int = 1) -> dict:
+    """examples/intrinsic_image_decomposition/src/main.cpp:19-40 (pixels (stride x,
+    stride y) of the image) and CombinedSolver.h resetGPUMemory: v = rgb / 255,
+    intensity = (r + g + b) / 3, i = log2(v + 0.01), r (albedo) = log2(v / intensity +
+    0.01), s (shading) = log2(intensity + 0.01), in float; w_fit = 500, w_regAlbedo = 1000,
+    w_regShading = 10000 square-rooted, pNorm = 0.8."""
+    img = np.asarray(rgb)[..., :3]
+    H, W = img.shape[0] // stride, img.shape[1] // stride
+    v = img[: H * stride: stride, : W * stride: stride].astype(f32) / f32(255.0)
+    inten = ((v[..., 0] + v[..., 1]) + v[..., 2]) / f32(3.0)
+    eps = f32(0.01)
+    chroma = v / inten[..., None]
+    return {"W": W, "H": H,
+            "r": np.log2(chroma + eps, dtype=f32).reshape(-1).copy(),
+            "i": np.log2(v + eps, dtype=f32).reshape(-1).copy(),
+            "s": np.log2(inten + eps, dtype=f32).reshape(-1).copy(),
+            "w_fitSqrt": float(np.sqrt(f32(500.0))), "w_regSqrtAlbedo": float(np.sqrt(f32(1000.0))),
+            "w_regSqrtShading": float(np.sqrt(f32(10000.0))), "pNorm": float(f32(0.8))}
+
+
+# ------------------------------------------------- volumetric_mesh_deformation
+def volumetric_mesh_deformation(verts, subdivisions: int = 0) -> dict:
+    """examples/volumetric_mesh_deformation/src/main.cpp:17-45 and CombinedSolver.h: a
+    lattice of (5 (s+1)) x (20 (s+1)) x (5 (s+1)) cells over the mesh's bounding box grown
+    by 1e-6 (computeBoundingBox, resetGPUMemory), node (i, j, k) at min + (i, j, k) * delta,
+    Angle = 0, Constraints = the node itself on the j = 0 layer, the top layer (j = dims.y)
+    rotated by -90 degrees about z around its centre and moved by (2.5, -2.5, 0), -inf
+    elsewhere (setConstraints(1)); w_fit = 1, w_reg = 0.05 square-rooted.
+
+    The harness stores node (i, j, k) at i (Y+1)(Z+1) + j (Z+1) + k (getIndex1D), which
+    the energy's x-fastest {X+1, Y+1, Z+1} image reads as coordinate (k, j, i): the
+    lattice is laid out the same way here (the stencil energy is symmetric under that
+    relabelling of axes; positions keep their own x, y, z)."""
+    P = np.asarray(verts, np.float32)
+    dx, dy, dz = 5 * (subdivisions + 1), 20 * (subdivisions + 1), 5 * (subdivisions + 1)
+    mn = P.min(0).astype(f32) - f32(0.000001)
+    mx = P.max(0).astype(f32) + f32(0.000001)
+    delta = (mx - mn) / np.array([dx, dy, dz], f32)
+    nx, ny, nz = dx + 1, dy + 1, dz + 1
+    n = nx * ny * nz
+    U = np.zeros((n, 3), f32)
+    C = np.full((n, 3), -np.inf, f32)
+    R = _rot_axis("z", -90.0)
+    for i in range(nx):
+        for j in range(ny):
+            for k in range(nz):
+                idx = i * (ny * nz) + j * nz + k
+                v = mn + np.array([i, j, k], f32) * delta
+                U[idx] = v
+                # mat3f::diag(i, j, k) * delta: each row adds two zero products
+                vc = mn + np.array([(f32(i) * delta[0] + f32(0) * delta[1]) + f32(0) * delta[2],
+                                    (f32(0) * delta[0] + f32(j) * delta[1]) + f32(0) * delta[2],
+                                    (f32(0) * delta[0] + f32(0) * delta[1]) + f32(k) * delta[2]], f32)
+                if j == 0:
+                    C[idx] = vc
+                elif j == dy:
+                    fd = np.array([f32(dx) / f32(2.0), f32(dy), f32(dz) / f32(2.0)], f32)
+                    mid = mn + np.array([(fd[0] * delta[0] + f32(0) * delta[1]) + f32(0) * delta[2],
+                                         (f32(0) * delta[0] + fd[1] * delta[1]) + f32(0) * delta[2],
+                                         (f32(0) * delta[0] + f32(0) * delta[1]) + fd[2] * delta[2]], f32)
+                    d = vc - mid
+                    rv = np.array([(R[r, 0] * d[0] + R[r, 1] * d[1]) + R[r, 2] * d[2] for r in range(3)], f32)
+                    C[idx] = (rv + mid) + np.array([2.5, -2.5, 0.0], f32)
+    return {"W": nz, "H": ny, "D": nx, "Offset": U.reshape(-1).copy(), "Angle": np.zeros(3 * n, f32),
+            "UrShape": U.reshape(-1).copy(), "Constraints": C.reshape(-1),
+            "w_fitSqrt": float(np.sqrt(f32(1.0))), "w_regSqrt": float(np.sqrt(f32(0.05)))}
+
+
 # --------------------------------------------------------- from the data folder
 FILES = {  # file = 1 / 2 as the examples' main.cpp choose
     "image_warping": {1: ("cat512_mask.png", "cat512.constraints"), 2: ("cat4096_mask.png", "cat4096.constraints")},
@@ -256,12 +430,27 @@ FILES = {  # file = 1 / 2 as the examples' main.cpp choose
     "arap_mesh_deformation": {1: ("small_armadillo.ply", "small_armadillo.mrk"),
                               2: ("raptor_simplify2k.off", "raptor_simplify2k.mrk")},
     "shape_from_shading": {1: ("shape_from_shading/default",)},
+    "cotangent_mesh_smoothing": {1: ("head.ply",)},
+    "embedded_mesh_deformation": {1: ("raptor_simplify2k.off", "raptor_simplify2k.mrk")},
+    "intrinsic_image_decomposition": {1: ("ye_high2.png",)},
+    "volumetric_mesh_deformation": {1: ("head.ply",)},
 }
 
 
+def _read_mesh(path):
+    return formats.read_ply(path) if path.endswith(".ply") else formats.read_off(path)
+
+
 def load_example(name: str, data: str, file: int = 1, stride: int = 1, level: int = 1,
-                 subdivisions: int = 1, alpha: float = 1.0) -> dict:
-    """Build example `name`'s problem from the reference's examples/data folder."""
+                 subdivisions=None, alpha: float = 1.0) -> dict:
+    """Build example `name`'s problem from the reference's examples/data folder
+    (subdivisions: numSubdivides; default 1 for arap, whose harness raises it to 1, else 0)."""
+    if subdivisions is None:
+        subdivisions = 1 if name == "arap_mesh_deformation" else 0
+    if subdivisions and name in ("cotangent_mesh_smoothing", "embedded_mesh_deformation",
+                                 "volumetric_mesh_deformation"):
+        raise ValueError(name + ": numSubdivides > 0 is not mirrored (open meshes need OpenMesh's "
+                         "boundary sqrt(3) rules)")
     fs = [os.path.join(data, f) for f in FILES[name][file]]
     if name == "image_warping":
         return image_warping(formats.read_png(fs[0])[..., 0], formats.read_constraints(fs[1]), alpha)
@@ -283,11 +472,28 @@ def load_example(name: str, data: str, file: int = 1, stride: int = 1, level: in
                                   formats.read_imagedump(pre + "_targetDepth.imagedump"),
                                   formats.read_imagedump(pre + "_targetIntensity.imagedump"),
                                   formats.read_imagedump(pre + "_maskEdgeMap.imagedump"))
+    if name == "cotangent_mesh_smoothing":
+        return cotangent_mesh_smoothing(*_read_mesh(fs[0]))
+    if name == "embedded_mesh_deformation":
+        v, f = _read_mesh(fs[0])
+        pos, _, idx = formats.read_mrk(fs[1])
+        return embedded_mesh_deformation(v, f, pos, idx)
+    if name == "intrinsic_image_decomposition":
+        return intrinsic_image_decomposition(formats.read_png(fs[0]), stride=stride)
+    if name == "volumetric_mesh_deformation":
+        return volumetric_mesh_deformation(_read_mesh(fs[0])[0], subdivisions=max(0, subdivisions))
     raise KeyError(name)
 
 
+GRAPH_EXAMPLES = ("arap_mesh_deformation", "cotangent_mesh_smoothing", "embedded_mesh_deformation")
+
+
 def dims(name: str, w: dict):
-    return [w["N"], w["E"]] if name == "arap_mesh_deformation" else [w["W"], w["H"]]
+    if name in GRAPH_EXAMPLES:
+        return [w["N"], w["E"]]
+    if name == "volumetric_mesh_deformation":
+        return [w["W"], w["H"], w["D"]]
+    return [w["W"], w["H"]]
 
 
 def problem_params(name: str, w: dict, conv=lambda a: a, double: bool = False) -> list:
@@ -307,9 +513,20 @@ def problem_params(name: str, w: dict, conv=lambda a: a, double: bool = False) -
                 A("v0"), A("v1")]
     if name == "shape_from_shading":
         return [float(v) for v in w["params"]] + [U("X"), A("D_i"), A("Im"), A("edgeMaskR"), A("edgeMaskC")]
+    if name == "cotangent_mesh_smoothing":
+        return [w["w_fitSqrt"], w["w_regSqrt"], U("X"), A("A"), None, A("v0"), A("v1"), A("v2"), A("v3")]
+    if name == "embedded_mesh_deformation":
+        return [w["w_fitSqrt"], w["w_regSqrt"], w["w_rotSqrt"], U("Offset"), U("RotMatrix"), A("UrShape"),
+                A("Constraints"), None, A("v0"), A("v1")]
+    if name == "intrinsic_image_decomposition":
+        return [w["w_fitSqrt"], w["w_regSqrtAlbedo"], w["w_regSqrtShading"], w["pNorm"], U("r"), A("i"), U("s")]
+    if name == "volumetric_mesh_deformation":
+        return [U("Offset"), U("Angle"), A("UrShape"), A("Constraints"), w["w_fitSqrt"], w["w_regSqrt"]]
     raise KeyError(name)
 
 
 # index of the (first) unknown in problem_params, for reading results back
 UNKNOWN_INDEX = {"image_warping": 0, "poisson_image_editing": 0, "optical_flow": 2,
-                 "arap_mesh_deformation": 2, "shape_from_shading": 16}
+                 "arap_mesh_deformation": 2, "shape_from_shading": 16, "cotangent_mesh_smoothing": 2,
+                 "embedded_mesh_deformation": 3, "intrinsic_image_decomposition": 4,
+                 "volumetric_mesh_deformation": 0}

@@ -25,8 +25,20 @@ harness loads them:
     sqrt(3) subdivision (OpenMesh Sqrt3T) and graph construction are restated in
     tests/reference_inputs.py.
 
+  cotangent_mesh_smoothing / volumetric_mesh_deformation (their main.cpp read
+    ../data/head.ply, numSubdivides 0): head.ply's vertex positions and triangles.
+
+  embedded_mesh_deformation (main.cpp:17-45): raptor_simplify2k.off (positions,
+    triangles) and raptor_simplify2k.mrk (markers).
+
+  intrinsic_image_decomposition (main.cpp:19-40, stride 12 as test_final_cost.py:85
+    sets): the RGB pixels of ye_high2.png at (12 x, 12 y).
+
+The problem construction of each (harness mirror, opt_amd/harness/problems.py) runs on
+these at test time.
+
 Data licence: public domain (cat512*), Middlebury flow data set (dogdance*), Stanford
-3D Scanning Repository, research use with credit (small_armadillo*),
+3D Scanning Repository, research use with credit (small_armadillo*, head, raptor),
 examples/data/copyright.txt.
 
     python tests/golden/make_reference_fixtures.py /root/reference
@@ -74,6 +86,23 @@ def main(ref):
     np.savez_compressed(out, verts=verts, faces=faces, marker_pos=mk[:, :3].astype(np.float32),
                         marker_idx=mk[:, 4].astype(np.int32))
     print(out, verts.shape, faces.shape, mk.shape)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(here)))
+    from opt_amd.harness import formats
+    v, f = formats.read_ply(os.path.join(data, "head.ply"))
+    out = os.path.join(here, "mesh_head.npz")
+    np.savez_compressed(out, verts=v, faces=f)
+    print(out, v.shape, f.shape)
+    v, f = formats.read_off(os.path.join(data, "raptor_simplify2k.off"))
+    pos, _, idx = formats.read_mrk(os.path.join(data, "raptor_simplify2k.mrk"))
+    out = os.path.join(here, "mesh_raptor2k.npz")
+    np.savez_compressed(out, verts=v, faces=f, marker_pos=pos, marker_idx=idx)
+    print(out, v.shape, f.shape, pos.shape)
+    stride = 12
+    a = np.array(Image.open(os.path.join(data, "ye_high2.png")).convert("RGB"))
+    H, W = a.shape[0] // stride, a.shape[1] // stride
+    out = os.path.join(here, "iid_ye_s12.npz")
+    np.savez_compressed(out, rgb=a[: H * stride: stride, : W * stride: stride].copy(), stride=stride)
+    print(out, (H, W))
 
 
 if __name__ == "__main__":

@@ -15,7 +15,14 @@ REFERENCE_FINAL_COST = {
     "image_warping": 1774.3405,
     "optical_flow": 0.52119255,     # cost of the first solve (the coarse level, sigma 5)
     "arap_mesh_deformation": 7183.464843,
+    # the energies with no hand-written family (generated kernels)
+    "cotangent_mesh_smoothing": 2091.86303,
+    "embedded_mesh_deformation": 0.367129057645,      # LM (its args.config)
+    "intrinsic_image_decomposition": 3.3105300000e6,  # stride 12 (53 x 30 px)
+    "volumetric_mesh_deformation": 189.74081,
 }
+# solver kind each example's args.config selects (useOpt / useOptLM)
+REFERENCE_KIND = {"embedded_mesh_deformation": "LMGPU"}
 # Not reproducible from the reference's files: poisson_image_editing (its harness reads
 # the strided mask at (stride x, stride y) of the already-strided image,
 # examples/poisson_image_editing/src/main.cpp:95-101, i.e. out of bounds for the
@@ -42,3 +49,31 @@ def arap_armadillo():
     (opt_amd/harness/problems.py: arap)."""
     z = np.load(os.path.join(GOLDEN, "arap_armadillo.npz"))
     return problems.arap(z["verts"].astype(np.float32), z["faces"], z["marker_pos"], z["marker_idx"], 1)
+
+
+def cotangent_head():
+    """examples/cotangent_mesh_smoothing on head.ply (opt_amd/harness/problems.py)."""
+    z = np.load(os.path.join(GOLDEN, "mesh_head.npz"))
+    return problems.cotangent_mesh_smoothing(z["verts"], z["faces"])
+
+
+def volumetric_head():
+    """examples/volumetric_mesh_deformation: the lattice over head.ply's bounding box."""
+    z = np.load(os.path.join(GOLDEN, "mesh_head.npz"))
+    return problems.volumetric_mesh_deformation(z["verts"], 0)
+
+
+def embedded_raptor():
+    """examples/embedded_mesh_deformation on raptor_simplify2k (.off + .mrk)."""
+    z = np.load(os.path.join(GOLDEN, "mesh_raptor2k.npz"))
+    return problems.embedded_mesh_deformation(z["verts"], z["faces"], z["marker_pos"], z["marker_idx"])
+
+
+def intrinsic_ye():
+    """examples/intrinsic_image_decomposition on ye_high2.png at stride 12."""
+    z = np.load(os.path.join(GOLDEN, "iid_ye_s12.npz"))
+    return problems.intrinsic_image_decomposition(z["rgb"], 1)
+
+
+GENERATED_EXAMPLES = {"cotangent_mesh_smoothing": cotangent_head, "embedded_mesh_deformation": embedded_raptor,
+                      "intrinsic_image_decomposition": intrinsic_ye, "volumetric_mesh_deformation": volumetric_head}

@@ -109,7 +109,7 @@ def _problem(family, rng):
         return [W, H], [O, A, _cuda(w["UrShape"]), _cuda(w["Constraints"]), _cuda(w["Mask"]),
                         w["w_fitSqrt"], w["w_regSqrt"]], [O, A]
     if family == "poisson_image_editing":
-        W, H = 12, 10
+        W, H = 20, 16
         w = workloads.poisson_image_editing(W, H, seed=4)
         X = _cuda(w["X"].astype(np.float64) + rng.normal(size=w["X"].size))
         return [W, H], [X, _cuda(w["T"]), _cuda(w["M"])], [X]
@@ -150,7 +150,15 @@ def test_perturbed_energy_solves_its_own_energy(tmp_path, family, vid):
     assert fam.family() == family
     c_var, c_fam = s.eval_cost(prm), fam.eval_cost(prm)
     assert abs(c_var - c_fam) > 1e-6 * max(abs(c_fam), 1.0), (c_var, c_fam)
-    # -J^T F of the generated kernels = central-difference gradient of the variant's cost
+    # -J^T F of the generated kernels = central-difference gradient of the variant's cost.
+    # Two reference semantics make that identity approximate, so the check avoids them:
+    # a SampledImage's derivative is its derivative images, not the bilinear slope
+    # (o.t:3274-3278) — the optical_flow check zeroes the brightness weight; and the cost
+    # skips residuals centred on excluded pixels while J^T F keeps them (o.t:971-997 vs
+    # the residualsincludingX00 gathers) — only unknowns 2+ pixels from every excluded one
+    # are compared.
+    if family == "optical_flow":
+        prm = [0.0] + prm[1:]
     n = s.unknown_count()
     r = torch.zeros(n, dtype=torch.float64, device="cuda")
     pre = torch.zeros_like(r)
@@ -158,8 +166,15 @@ def test_perturbed_energy_solves_its_own_energy(tmp_path, family, vid):
     rr = r.cpu().numpy()
     rng = np.random.default_rng(2)
     offs = np.cumsum([0] + [u.numel() for u in unk])
-    # excluded unknowns have r = 0 by definition (PCGInit1): check the free ones
-    cand = np.flatnonzero(rr != 0)
+    ok = rr != 0
+    if len(dims) == 2 and family != "arap_mesh_deformation":
+        from scipy import ndimage
+        W, H = dims
+        ch = unk[0].numel() // (W * H)
+        excl = ~ok[: W * H * ch].reshape(H, W, ch).any(-1)
+        far = ~ndimage.binary_dilation(excl, np.ones((5, 5), bool))
+        ok = np.concatenate([np.repeat(far.reshape(-1), u.numel() // (W * H)) for u in unk]) & ok
+    cand = np.flatnonzero(ok)
     assert cand.size >= min(n, 16)
     picks = rng.choice(cand, size=min(cand.size, 48), replace=False)
     h = 1e-6

@@ -78,3 +78,33 @@ def test_arap_armadillo_final_cost(backend, mode):
           [None, conv(w["v0"]), conv(w["v1"])]
     s.solve(prm)
     assert rel(s.cost(), REFERENCE_FINAL_COST["arap_mesh_deformation"]) < REFERENCE_RTOL
+
+
+# ---- the reference's example energies with no hand-written family, on kernels the
+# general front end generates for energies/<name>.t
+from opt_amd.harness import problems  # noqa: E402
+from tests.reference_inputs import GENERATED_EXAMPLES, REFERENCE_KIND  # noqa: E402
+
+
+@pytest.mark.parametrize("name", sorted(GENERATED_EXAMPLES))
+@pytest.mark.parametrize("double", [False, True])
+def test_generated_example_known_answers(name, double):
+    w = GENERATED_EXAMPLES[name]()
+    s = OptSolver(problems.dims(name, w), os.path.join(ROOT, "energies", name + ".t"),
+                  REFERENCE_KIND.get(name, "gaussNewtonGPU"), double_precision=double)
+    assert s.family() == "generic"
+    s.set_solver_params({"nIterations": 1, "lIterations": 1})
+    s.solve(problems.problem_params(name, w, dev, double=double))
+    assert rel(s.cost(), REFERENCE_FINAL_COST[name]) < REFERENCE_RTOL, (s.cost(), REFERENCE_FINAL_COST[name])
+
+
+@pytest.mark.parametrize("name", ["cotangent_mesh_smoothing", "volumetric_mesh_deformation"])
+@pytest.mark.parametrize("mode", ["materialized", "materialized_fused"])
+def test_generated_example_known_answers_materialized(name, mode):
+    """useMaterializedJTJ (test_final_cost.py:91-93 runs every example this way too)"""
+    w = GENERATED_EXAMPLES[name]()
+    s = OptSolver(problems.dims(name, w), os.path.join(ROOT, "energies", name + ".t"), "gaussNewtonGPU",
+                  **MODES[mode])
+    s.set_solver_params({"nIterations": 1, "lIterations": 1})
+    s.solve(problems.problem_params(name, w, dev))
+    assert rel(s.cost(), REFERENCE_FINAL_COST[name]) < REFERENCE_RTOL, (s.cost(), REFERENCE_FINAL_COST[name])
