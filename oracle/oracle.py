@@ -252,65 +252,77 @@ def _sfs_lib():
     lib = load()
     if not getattr(lib, "_sfs", False):
         i, d = ctypes.c_int, ctypes.c_double
-        base = [i, i, _F, _F, _F, _U8, _U8, _F]
-        lib.oracle_sfs_precompute.restype, lib.oracle_sfs_precompute.argtypes = None, base + [_F]
-        lib.oracle_sfs_cost.restype, lib.oracle_sfs_cost.argtypes = d, base
-        lib.oracle_sfs_jtf.restype, lib.oracle_sfs_jtf.argtypes = None, base + [_F, _F]
-        lib.oracle_sfs_apply.restype, lib.oracle_sfs_apply.argtypes = d, base + [_F, _F]
-        lib.oracle_sfs_model_cost.restype, lib.oracle_sfs_model_cost.argtypes = d, base + [_F]
-        lib.oracle_sfs_solve.restype, lib.oracle_sfs_solve.argtypes = i, base + [i, i, i, _D]
+        for suf, R in (("", _F), ("_double", _D)):
+            base = [i, i, R, _F, _F, _U8, _U8, _F]
+            for name, res, extra in (("precompute", None, [R]), ("cost", d, []), ("jtf", None, [R, R]),
+                                     ("apply", d, [R, R]), ("model_cost", d, [R]), ("solve", i, [i, i, i, _D])):
+                fn = getattr(lib, "oracle_sfs_" + name + suf)
+                fn.restype, fn.argtypes = res, base + extra
         lib._sfs = True
     return lib
 
 
-def _sfs_args(w, X):
-    X = np.ascontiguousarray(X, np.float32)
-    u8 = lambda a: np.ascontiguousarray(a, np.uint8).ctypes.data_as(_U8)
+def _real(double):
+    """(numpy dtype, ctypes pointer type, entry-point suffix) of opt_float"""
+    return (np.float64, _D, "_double") if double else (np.float32, _F, "")
+
+
+def _sfs_args(w, X, double=False):
+    dt, R, _ = _real(double)
+    X = np.ascontiguousarray(X, dt)
     keep = [np.ascontiguousarray(w["edgeMaskR"], np.uint8), np.ascontiguousarray(w["edgeMaskC"], np.uint8),
             np.ascontiguousarray(w["params"], np.float32)]
-    return X, keep, (w["W"], w["H"], _f(X), _f(w["D_i"]), _f(w["Im"]), keep[0].ctypes.data_as(_U8),
+    return X, keep, (w["W"], w["H"], X.ctypes.data_as(R), _f(w["D_i"]), _f(w["Im"]), keep[0].ctypes.data_as(_U8),
                      keep[1].ctypes.data_as(_U8), _f(keep[2]))
 
 
-def sfs_precompute(w, X=None):
+def _sfs_fn(name, double):
+    return getattr(_sfs_lib(), "oracle_sfs_" + name + _real(double)[2])
+
+
+def sfs_precompute(w, X=None, double=False):
     """[B_I, dB_I/dX(0,0), dB_I/dX(-1,0), dB_I/dX(0,-1), valid], each W*H."""
-    X, keep, a = _sfs_args(w, w["X"] if X is None else X)
-    out = np.zeros(5 * w["W"] * w["H"], np.float32)
-    _sfs_lib().oracle_sfs_precompute(*a, _f(out))
+    dt, R, _ = _real(double)
+    X, keep, a = _sfs_args(w, w["X"] if X is None else X, double)
+    out = np.zeros(5 * w["W"] * w["H"], dt)
+    _sfs_fn("precompute", double)(*a, out.ctypes.data_as(R))
     return out.reshape(5, -1)
 
 
-def sfs_cost(w, X=None):
-    X, keep, a = _sfs_args(w, w["X"] if X is None else X)
-    return _sfs_lib().oracle_sfs_cost(*a)
+def sfs_cost(w, X=None, double=False):
+    X, keep, a = _sfs_args(w, w["X"] if X is None else X, double)
+    return _sfs_fn("cost", double)(*a)
 
 
-def sfs_jtf(w, X=None):
-    X, keep, a = _sfs_args(w, w["X"] if X is None else X)
+def sfs_jtf(w, X=None, double=False):
+    dt, R, _ = _real(double)
+    X, keep, a = _sfs_args(w, w["X"] if X is None else X, double)
     n = w["W"] * w["H"]
-    r, dg = np.zeros(n, np.float32), np.zeros(n, np.float32)
-    _sfs_lib().oracle_sfs_jtf(*a, _f(r), _f(dg))
+    r, dg = np.zeros(n, dt), np.zeros(n, dt)
+    _sfs_fn("jtf", double)(*a, r.ctypes.data_as(R), dg.ctypes.data_as(R))
     return r, dg
 
 
-def sfs_apply(w, p, X=None):
-    X, keep, a = _sfs_args(w, w["X"] if X is None else X)
-    p = np.ascontiguousarray(p, np.float32)
+def sfs_apply(w, p, X=None, double=False):
+    dt, R, _ = _real(double)
+    X, keep, a = _sfs_args(w, w["X"] if X is None else X, double)
+    p = np.ascontiguousarray(p, dt)
     Ap = np.zeros_like(p)
-    v = _sfs_lib().oracle_sfs_apply(*a, _f(p), _f(Ap))
+    v = _sfs_fn("apply", double)(*a, p.ctypes.data_as(R), Ap.ctypes.data_as(R))
     return Ap, v
 
 
-def sfs_model_cost(w, d, X=None):
-    X, keep, a = _sfs_args(w, w["X"] if X is None else X)
-    d = np.ascontiguousarray(d, np.float32)
-    return _sfs_lib().oracle_sfs_model_cost(*a, _f(d))
+def sfs_model_cost(w, d, X=None, double=False):
+    dt, R, _ = _real(double)
+    X, keep, a = _sfs_args(w, w["X"] if X is None else X, double)
+    d = np.ascontiguousarray(d, dt)
+    return _sfs_fn("model_cost", double)(*a, d.ctypes.data_as(R))
 
 
-def sfs_solve(w, n_iter, l_iter, lm=True):
-    X, keep, a = _sfs_args(w, w["X"].copy())
+def sfs_solve(w, n_iter, l_iter, lm=True, double=False):
+    X, keep, a = _sfs_args(w, w["X"].copy(), double)
     costs = np.zeros(n_iter + 1, np.float64)
-    k = _sfs_lib().oracle_sfs_solve(*a, int(lm), n_iter, l_iter, costs.ctypes.data_as(_D))
+    k = _sfs_fn("solve", double)(*a, int(lm), n_iter, l_iter, costs.ctypes.data_as(_D))
     return X, costs[: k + 1]
 
 
@@ -322,58 +334,67 @@ def _arap_lib():
     lib = load()
     if not getattr(lib, "_arap", False):
         i, f, d = ctypes.c_int, ctypes.c_float, ctypes.c_double
-        base = [i, i, _F, _F, _F, _F, _I, _I, f, f]
-        lib.oracle_arap_cost.restype, lib.oracle_arap_cost.argtypes = d, base
-        lib.oracle_arap_jtf.restype, lib.oracle_arap_jtf.argtypes = None, base + [_F, _F]
-        lib.oracle_arap_apply.restype, lib.oracle_arap_apply.argtypes = d, base + [_F, _F]
-        lib.oracle_arap_model_cost.restype, lib.oracle_arap_model_cost.argtypes = d, base + [_F]
-        lib.oracle_arap_solve.restype, lib.oracle_arap_solve.argtypes = i, base + [i, i, i, _D]
+        for suf, R in (("", _F), ("_double", _D)):
+            base = [i, i, R, R, _F, _F, _I, _I, f, f]
+            for name, res, extra in (("cost", d, []), ("jtf", None, [R, R]), ("apply", d, [R, R]),
+                                     ("model_cost", d, [R]), ("solve", i, [i, i, i, _D])):
+                fn = getattr(lib, "oracle_arap_" + name + suf)
+                fn.restype, fn.argtypes = res, base + extra
         lib._arap = True
     return lib
 
 
-def _arap_args(w, O=None, A=None):
-    O = np.ascontiguousarray(w["Offset"] if O is None else O, np.float32)
-    A = np.ascontiguousarray(w["Angle"] if A is None else A, np.float32)
+def _arap_fn(name, double):
+    return getattr(_arap_lib(), "oracle_arap_" + name + _real(double)[2])
+
+
+def _arap_args(w, O=None, A=None, double=False):
+    dt, R, _ = _real(double)
+    O = np.ascontiguousarray(w["Offset"] if O is None else O, dt)
+    A = np.ascontiguousarray(w["Angle"] if A is None else A, dt)
     v0 = np.ascontiguousarray(w["v0"], np.int32)
     v1 = np.ascontiguousarray(w["v1"], np.int32)
     keep = (O, A, v0, v1)
-    return keep, (w["N"], w["E"], _f(O), _f(A), _f(w["UrShape"]), _f(w["Constraints"]),
+    return keep, (w["N"], w["E"], O.ctypes.data_as(R), A.ctypes.data_as(R), _f(w["UrShape"]), _f(w["Constraints"]),
                   v0.ctypes.data_as(_I), v1.ctypes.data_as(_I), w["w_fitSqrt"], w["w_regSqrt"])
 
 
-def arap_cost(w):
-    keep, a = _arap_args(w)
-    return _arap_lib().oracle_arap_cost(*a)
+def arap_cost(w, double=False):
+    keep, a = _arap_args(w, double=double)
+    return _arap_fn("cost", double)(*a)
 
 
-def arap_jtf(w):
-    keep, a = _arap_args(w)
+def arap_jtf(w, double=False):
+    dt, R, _ = _real(double)
+    keep, a = _arap_args(w, double=double)
     n = 6 * w["N"]
-    r, dg = np.zeros(n, np.float32), np.zeros(n, np.float32)
-    _arap_lib().oracle_arap_jtf(*a, _f(r), _f(dg))
+    r, dg = np.zeros(n, dt), np.zeros(n, dt)
+    _arap_fn("jtf", double)(*a, r.ctypes.data_as(R), dg.ctypes.data_as(R))
     return r, dg
 
 
-def arap_apply(w, p):
-    keep, a = _arap_args(w)
-    p = np.ascontiguousarray(p, np.float32)
+def arap_apply(w, p, double=False):
+    dt, R, _ = _real(double)
+    keep, a = _arap_args(w, double=double)
+    p = np.ascontiguousarray(p, dt)
     Ap = np.zeros_like(p)
-    v = _arap_lib().oracle_arap_apply(*a, _f(p), _f(Ap))
+    v = _arap_fn("apply", double)(*a, p.ctypes.data_as(R), Ap.ctypes.data_as(R))
     return Ap, v
 
 
-def arap_model_cost(w, d):
-    keep, a = _arap_args(w)
-    d = np.ascontiguousarray(d, np.float32)
-    return _arap_lib().oracle_arap_model_cost(*a, _f(d))
+def arap_model_cost(w, d, double=False):
+    dt, R, _ = _real(double)
+    keep, a = _arap_args(w, double=double)
+    d = np.ascontiguousarray(d, dt)
+    return _arap_fn("model_cost", double)(*a, d.ctypes.data_as(R))
 
 
-def arap_solve(w, n_iter, l_iter, lm=False):
-    O, A = w["Offset"].copy(), w["Angle"].copy()
-    keep, a = _arap_args(w, O, A)
+def arap_solve(w, n_iter, l_iter, lm=False, double=False):
+    dt = _real(double)[0]
+    O, A = w["Offset"].astype(dt), w["Angle"].astype(dt)
+    keep, a = _arap_args(w, O, A, double)
     costs = np.zeros(n_iter + 1, np.float64)
-    k = _arap_lib().oracle_arap_solve(*a, int(lm), n_iter, l_iter, costs.ctypes.data_as(_D))
+    k = _arap_fn("solve", double)(*a, int(lm), n_iter, l_iter, costs.ctypes.data_as(_D))
     return O, A, costs[: k + 1]
 
 

@@ -49,23 +49,28 @@ def jac(w):
     return F, J
 
 
-def test_cost_jtf_apply_model_match_numpy():
+@pytest.mark.parametrize("double", [False, True])
+def test_cost_jtf_apply_model_match_numpy(double):
+    """float: within fp32 error; double (the checker of the fp64 GPU path): within 1e-6
+    (the oracle, like the kernels, forms UrShape differences in float)."""
+    t = 1e-6 if double else 1.0
+    dt = np.float64 if double else np.float32
     w = small()
     F, J = jac(w)
-    assert oracle.arap_cost(w) == pytest.approx(0.5 * F @ F, rel=1e-5)
-    r, dg = oracle.arap_jtf(w)
+    assert oracle.arap_cost(w, double=double) == pytest.approx(0.5 * F @ F, rel=min(1e-5, t))
+    r, dg = oracle.arap_jtf(w, double=double)
     g = J.T @ F
-    np.testing.assert_allclose(r, -g, atol=2e-5 * np.abs(g).max())
-    np.testing.assert_allclose(dg, np.sum(J * J, axis=0), rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(r, -g, atol=min(2e-5, t) * np.abs(g).max())
+    np.testing.assert_allclose(dg, np.sum(J * J, axis=0), rtol=min(1e-4, t), atol=min(1e-6, t))
     rng = np.random.default_rng(5)
-    p = rng.normal(size=J.shape[1]).astype(np.float32)
-    Ap, pAp = oracle.arap_apply(w, p)
+    p = rng.normal(size=J.shape[1]).astype(dt)
+    Ap, pAp = oracle.arap_apply(w, p, double=double)
     ref = J.T @ (J @ p.astype(np.float64))
-    np.testing.assert_allclose(Ap, ref, atol=2e-5 * np.abs(ref).max())
-    assert pAp == pytest.approx(float(p @ ref), rel=1e-5)
-    d = (0.01 * rng.normal(size=J.shape[1])).astype(np.float32)
+    np.testing.assert_allclose(Ap, ref, atol=min(2e-5, t) * np.abs(ref).max())
+    assert pAp == pytest.approx(float(p @ ref), rel=min(1e-5, t))
+    d = (0.01 * rng.normal(size=J.shape[1])).astype(dt)
     m = F + J @ d
-    assert oracle.arap_model_cost(w, d) == pytest.approx(0.5 * m @ m, rel=1e-5)
+    assert oracle.arap_model_cost(w, d, double=double) == pytest.approx(0.5 * m @ m, rel=min(1e-5, t))
 
 
 @pytest.mark.parametrize("lm", [False, True])

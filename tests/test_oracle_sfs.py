@@ -112,34 +112,48 @@ def test_precomputed_gradient_images_match_finite_differences():
     del B0
 
 
-def test_cost_jtf_apply_model_match_numpy():
+@pytest.mark.parametrize("double", [False, True])
+def test_cost_jtf_apply_model_match_numpy(double):
+    """float: the fp32 oracle within fp32 + finite-difference error; double: the fp64
+    instantiation (the checker of the fp64 GPU path) within 1e-6."""
+    t = 1e-6 if double else 1.0
+    dt = np.float64 if double else np.float32
     w = small()
     valid = oracle.sfs_precompute(w)[4]
     F, excl, J = jacobian(w, valid)
     Fc = F.copy()
     Fc[excl] = 0          # cost / model cost skip excluded centres
-    assert oracle.sfs_cost(w) == pytest.approx(0.5 * np.sum(Fc ** 2), rel=1e-4)
+    assert oracle.sfs_cost(w, double=double) == pytest.approx(0.5 * np.sum(Fc ** 2), rel=min(1e-4, t))
     Jf = J.reshape(F.shape[0], 6, -1)
     Jall = Jf.reshape(-1, J.shape[1])
     g = Jall.T @ F.reshape(-1)   # gathers include residuals of excluded centres
-    r, dg = oracle.sfs_jtf(w)
+    r, dg = oracle.sfs_jtf(w, double=double)
     act = ~excl
-    np.testing.assert_allclose(r[act], -g[act], atol=2e-3 * np.abs(g).max())
+    np.testing.assert_allclose(r[act], -g[act], atol=min(2e-3, t) * np.abs(g).max())
     assert np.all(r[excl] == 0)
-    np.testing.assert_allclose(dg[act], np.sum(Jall ** 2, axis=0)[act], rtol=5e-3, atol=1e-3 * dg.max())
+    np.testing.assert_allclose(dg[act], np.sum(Jall ** 2, axis=0)[act], rtol=min(5e-3, t), atol=min(1e-3, t) * dg.max())
     rng = np.random.default_rng(1)
-    pvec = rng.normal(size=J.shape[1]).astype(np.float32)
+    pvec = rng.normal(size=J.shape[1]).astype(dt)
     pvec[excl] = 0
-    Ap, pAp = oracle.sfs_apply(w, pvec)
+    Ap, pAp = oracle.sfs_apply(w, pvec, double=double)
     ref = Jall.T @ (Jall @ pvec.astype(np.float64))
-    np.testing.assert_allclose(Ap[act], ref[act], atol=3e-3 * np.abs(ref).max())
-    assert pAp == pytest.approx(float(pvec @ ref), rel=3e-3)
-    d = (1e-3 * rng.normal(size=J.shape[1])).astype(np.float32)
+    np.testing.assert_allclose(Ap[act], ref[act], atol=min(3e-3, t) * np.abs(ref).max())
+    assert pAp == pytest.approx(float(pvec @ ref), rel=min(3e-3, t))
+    d = (1e-3 * rng.normal(size=J.shape[1])).astype(dt)
     d[excl] = 0
     Jc = Jf.copy()
     Jc[excl] = 0
     m = Fc.reshape(-1) + Jc.reshape(-1, J.shape[1]) @ d
-    assert oracle.sfs_model_cost(w, d) == pytest.approx(0.5 * m @ m, rel=1e-4)
+    assert oracle.sfs_model_cost(w, d, double=double) == pytest.approx(0.5 * m @ m, rel=min(1e-4, t))
+
+
+@pytest.mark.parametrize("lm", [False, True])
+def test_double_and_float_oracles_agree(lm):
+    w = small(23, 17, seed=2)
+    _, c32 = oracle.sfs_solve(w, 3, 10, lm=lm)
+    X64, c64 = oracle.sfs_solve(w, 3, 10, lm=lm, double=True)
+    assert X64.dtype == np.float64 and len(c32) == len(c64)
+    np.testing.assert_allclose(c32, c64, rtol=1e-3)
 
 
 def test_lm_and_gn_decrease_cost_on_reference_inputs():
