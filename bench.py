@@ -79,32 +79,70 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(w, n_unknowns, budget_s=10.0):
-    """Oracle J^T J p apply on host cores: full-image applies repeated for ~budget_s."""
+def host_cores():
+    """CPUs this process may actually run on: the affinity mask, capped by the cgroup
+    CPU quota (the GPU box grants a share of a larger machine; os.cpu_count() shows the
+    whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(-(-int(quota) // int(period)))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(w, n_unknowns, liter):
+    """The oracle (oracle/image_warping.c, the reference's GN/PCG restated in C with
+    pthreads over rows, as backend_cpu_mt splits its kernels, backend_cpu_mt.t:350-414)
+    on the host: one whole GN step (JᵀF + preconditioner, `liter` PCG iterations, update,
+    cost) on every available core, in the headline's unit (unknowns x lIterations per
+    second), plus the JᵀJ·p apply alone on all cores and on one core (a 512-row sample)."""
     from oracle import oracle
 
-    cores = min(16, os.cpu_count() or 1)
+    cores = host_cores()
+    t0 = time.perf_counter()
+    oracle.iw_solve(w, 1, liter, nthreads=cores)
+    t_step = time.perf_counter() - t0
     rng = np.random.default_rng(0)
     p = rng.normal(size=n_unknowns).astype(np.float32)
-    oracle.iw_apply_jtj({**w, "H": 64, "Offset": w["Offset"][: 2 * w["W"] * 64],
-                         "Angle": w["Angle"][: w["W"] * 64], "UrShape": w["UrShape"][: 2 * w["W"] * 64],
-                         "Constraints": w["Constraints"][: 2 * w["W"] * 64], "Mask": w["Mask"][: w["W"] * 64]},
-                        p[: 3 * w["W"] * 64], nthreads=cores)  # warm
-    reps = 0
-    t0 = time.perf_counter()
-    while True:
+    reps, t0 = 0, time.perf_counter()
+    while reps < 3 or time.perf_counter() - t0 < 3.0:
         oracle.iw_apply_jtj(w, p, nthreads=cores)
         reps += 1
-        dt = time.perf_counter() - t0
-        if dt >= budget_s:
-            break
+    t_apply = (time.perf_counter() - t0) / reps
+    rows = 512
+    ws = {**w, "H": rows, "Offset": w["Offset"][: 2 * w["W"] * rows], "Angle": w["Angle"][: w["W"] * rows],
+          "UrShape": w["UrShape"][: 2 * w["W"] * rows], "Constraints": w["Constraints"][: 2 * w["W"] * rows],
+          "Mask": w["Mask"][: w["W"] * rows]}
+    n1 = 3 * w["W"] * rows
+    reps1, t0 = 0, time.perf_counter()
+    while reps1 < 2 or time.perf_counter() - t0 < 2.0:
+        oracle.iw_apply_jtj(ws, p[:n1], nthreads=1)
+        reps1 += 1
+    t_apply1 = (time.perf_counter() - t0) / reps1
     return {
-        "value": reps * n_unknowns / dt,
+        "value": n_unknowns * liter / t_step,
         "unit": "unknowns/s",
         "cores": cores,
         "kind": "port",
-        "sample": f"{reps} J^T J p applies over the full {w['W']}x{w['H']} image "
-                  f"({n_unknowns} unknowns each), oracle/image_warping.c, {cores} pthreads, {dt:.1f} s",
+        "sample": f"one GN step ({liter} PCG iterations, incl. the init cost) of the full {w['W']}x{w['H']} "
+                  f"problem, oracle/image_warping.c on {cores} threads: {t_step:.2f} s",
+        "gn_iters_per_s": 1.0 / t_step,
+        "apply_unknowns_per_s": n_unknowns / t_apply,
+        "apply_unknowns_per_s_1core": n1 / t_apply1,
+        "cpu_model": cpu_model(),
     }
 
 
@@ -224,7 +262,7 @@ def main():
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(w, n_unknowns)
+        result["cpu_baseline"] = cpu_baseline(w, n_unknowns, args.liter)
     if rank == 0:
         print(json.dumps(result), flush=True)
     s.close()
