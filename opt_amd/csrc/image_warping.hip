@@ -337,7 +337,10 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
                 if (LMX && dadd) {
                     aox += dadd[2 * i] * cur.px; aoy += dadd[2 * i + 1] * cur.py; aot += dadd[2 * N + i] * cur.pt;
                 }
-                st_v<(NT & 2) != 0>(Ap + 2 * i, aox); st_v<(NT & 2) != 0>(Ap + 2 * i + 1, aoy); st_v<(NT & 2) != 0>(Ap + 2 * N + i, aot);
+                if (Ap) {   // null in the last PCG iteration: nothing reads that Ap
+                    st_v<(NT & 2) != 0>(Ap + 2 * i, aox); st_v<(NT & 2) != 0>(Ap + 2 * i + 1, aoy);
+                    st_v<(NT & 2) != 0>(Ap + 2 * N + i, aot);
+                }
                 if (MODE != 0) {
                     st_v<(NT & 2) != 0>(pout + 2 * i, cur.px); st_v<(NT & 2) != 0>(pout + 2 * i + 1, cur.py);
                     st_v<(NT & 2) != 0>(pout + 2 * N + i, cur.pt);
@@ -433,13 +436,17 @@ __device__ __forceinline__ VRow<T> finish_vrow(const VRaw<T>& r) {
 // OUT 1: all three preconditioner channels (OptAMD_EvalJTF layout);
 // OUT 2: diag(J^T J) in all three channels instead of pre, no reduction (the generic
 //        GN/LM driver, which forms pre / the LM diagonal itself).
-template <typename T, int OUT>
+// COST: also sc[rs.out + 1] = the cost (iw_cost's sum, same per-pixel expression and
+// block geometry) from the residuals this kernel evaluates anyway: the end of a GN step
+// evaluates the cost at the updated unknowns and, speculatively, the next step's
+// PCGInit1 there in one pass (ImageWarpingPlan::step).
+template <typename T, int OUT, bool COST = false>
 __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T* __restrict__ pre,
                                                  ReduceSlot rs) {
     const WaveGeom g = geom(a);
     const T wr = a.wr, wf = a.wf, wr2 = a.wr * a.wr;
     const long long N = a.dom.npix_mem();
-    T dot = 0;
+    T dot = 0, cacc = 0;
     if (g.y0 < g.y1) {
         VRow<T> up = finish_vrow<T, true>(raw_vrow<T, true>(a, g, g.y0 - 1)),
                 cur = finish_vrow<T, true>(raw_vrow<T, true>(a, g, g.y0)),
@@ -488,6 +495,18 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
                 fx += wf * wf * (cur.ox - (T)cur.cx);
                 fy += wf * wf * (cur.oy - (T)cur.cy);
             }
+            if (COST && g.out_lane && cur.act) {
+                T sum = 0;
+                sum += epx_x * epx_x + epx_y * epx_y;
+                sum += emx_x * emx_x + emx_y * emx_y;
+                sum += epy_x * epy_x + epy_y * epy_y;
+                sum += my_x * my_x + my_y * my_y;
+                if (cur.fit) {
+                    const T cfx = wf * (cur.ox - (T)cur.cx), cfy = wf * (cur.oy - (T)cur.cy);
+                    sum += cfx * cfx + cfy * cfy;
+                }
+                cacc += (T)0.5 * sum;
+            }
             if (g.out_lane) {
                 const long long i = a.dom.off(g.x, y);
                 const int f = cur.act | (cur.fit << 1) | (nv << 2);
@@ -528,8 +547,13 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
         }
     }
     if (OUT == 2) return;
-    double v[1] = {(double)dot};
-    block_reduce_publish<1>(v, rs, blockIdx.x);
+    if constexpr (COST) {
+        double v[2] = {(double)dot, (double)cacc};
+        block_reduce_publish<2>(v, rs, blockIdx.x);
+    } else {
+        double v[1] = {(double)dot};
+        block_reduce_publish<1>(v, rs, blockIdx.x);
+    }
 }
 
 // ----------------------------------------------------------------- cost kernel
@@ -846,6 +870,7 @@ public:
         rows_ = env_int("OPT_AMD_ROWS", 32);
         depth_ = env_int("OPT_AMD_DEPTH", 1);
         nt_ = env_int("OPT_AMD_IW_NT", 6);
+        spec_on_ = env_int("OPT_AMD_IW_SPEC", 1) != 0;
         timer_.apply_name = apply_kernel_name();
         allocate();
     }
@@ -860,6 +885,7 @@ public:
         if (opts_.host_buffers) return "row-slab decomposition needs backend_cuda (device arrays)";
         if (y_lo < 0 || y_hi > dom_.H || y_hi - y_lo < halo()) return "invalid slab rows";
         comm_ = comm;
+        spec_valid_ = false;
         OPT_HIP_CHECK(hipStreamSynchronize(stream_));
         release();
         dom_.y_lo = y_lo;
@@ -884,6 +910,7 @@ public:
         prev_cost_ = read_scalar(kScCost);
         n_iter_ = 0;
         initialised_ = true;
+        spec_valid_ = false;
         end_call();
         if (opts_.verbosity > 0) fprintf(stderr, "[opt_amd] init cost %.9g\n", prev_cost_);
     }
@@ -898,9 +925,17 @@ public:
         bind(params, false);
         exchange_unknowns();
         const int L = std::max(0, sp_.lIterations);
-        red_.ensure(std::max(stencil_blocks(), 2048), 1, kScBase + 2 * (L + 2));
-        // PCGInit1: r, pre, flags, rz[0]
-        tbegin("iw_jtf"); launch_jtf(r_, pre_, rz(0)); tend();
+        red_.ensure(std::max(stencil_blocks(), 2048), 2, kScBase + 2 * (L + 2));
+        // PCGInit1: r, pre, flags, rz[0] — unless the previous step already evaluated
+        // them at these unknowns (its cost pass, below) with the same bound arrays and
+        // parameters (problemparams are re-read every step, :2001)
+        if (spec_valid_ && spec_key_ == bind_key()) {
+            rz0_ = kScSpecRz;
+        } else {
+            rz0_ = kScBase;
+            tbegin("iw_jtf"); launch_jtf(r_, pre_, rz(0)); tend();
+        }
+        spec_valid_ = false;
         allreduce(rz(0));
         if (distributed()) {
             std::vector<HaloPlane> pl;
@@ -914,11 +949,15 @@ public:
         for (int i = 0; i < L; ++i) {
             std::swap(pcur, pprev);   // pcur <- new p, pprev <- old p
             tbegin("iw_apply");
-            if (i == 0) launch_apply<1, 0>(nullptr, pcur, pap(i), 0, 0, 0, 0);
-            else if (i == 1) launch_apply<2, 1>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1));
-            else launch_apply<2, 2>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1));
+            const bool last = i + 1 == L;
+            if (i == 0) launch_apply<1, 0>(nullptr, pcur, pap(i), 0, 0, 0, 0, nullptr, last);
+            else if (i == 1) launch_apply<2, 1>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1), nullptr, last);
+            else launch_apply<2, 2>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1), nullptr, last);
             tend();
             allreduce(pap(i));
+            // the last iteration's residual update only feeds a beta nobody reads
+            // (the update below takes alpha from rz[L-1] / pAp[L-1])
+            if (i + 1 == L) break;
             tbegin("iw_residual");
             launch_residual(rz(i), pap(i), rz(i + 1));
             tend();
@@ -944,9 +983,19 @@ public:
             tend();
             exchange_unknowns();
         }
-        tbegin("iw_cost"); launch_cost(kScCost); tend();
-        allreduce(kScCost);
-        const double c = read_scalar(kScCost);
+        // cost at the updated unknowns; on one GPU with device arrays, fused with the next
+        // step's J^T F + preconditioner + flags (same unknowns, same residuals)
+        double c;
+        if (spec_on_ && !distributed() && !opts_.host_buffers && n_iter_ + 1 < sp_.nIterations) {
+            tbegin("iw_jtf_cost"); launch_jtf_cost(r_, pre_, kScSpecRz); tend();
+            c = read_scalar(kScSpecCost);
+            spec_valid_ = true;
+            spec_key_ = bind_key();
+        } else {
+            tbegin("iw_cost"); launch_cost(kScCost); tend();
+            allreduce(kScCost);
+            c = read_scalar(kScCost);
+        }
         unbind_after_step();
         end_call();
         prev_cost_ = c;
@@ -957,6 +1006,7 @@ public:
 
     int eval_jtf(void** params, void* r, void* pre, double* rzv) override {
         begin_call();
+        spec_valid_ = false;
         bind(params, false);
         exchange_unknowns();
         launch_jtf((T*)r, (T*)pre, kScTmp, true);
@@ -967,6 +1017,7 @@ public:
     }
     int apply_jtj(void** params, const void* p, void* Ap, double* pAp) override {
         begin_call();
+        spec_valid_ = false;
         bind(params, false);
         exchange_unknowns();
         if (distributed()) {
@@ -993,6 +1044,7 @@ public:
     }
     double time_apply(void** params, const void* p, void* Ap, int reps) override {
         begin_call();
+        spec_valid_ = false;
         bind(params, false);
         launch_flags();
         hipEvent_t e0, e1;
@@ -1061,10 +1113,15 @@ private:
         exchange({{(void*)cur_O_, sizeof(T) * 2 * dom_.W}, {(void*)cur_A_, sizeof(T) * dom_.W}});
     }
 
-    // scalar slots in red_.scalars
-    static constexpr int kScCost = 0, kScTmp = 1, kScBase = 4;
-    int rz(int i) const { return kScBase + 2 * i; }
+    // scalar slots in red_.scalars (kScSpecRz / kScSpecCost: the fused end-of-step pass)
+    static constexpr int kScCost = 0, kScTmp = 1, kScSpecRz = 2, kScSpecCost = 3, kScBase = 4;
+    int rz(int i) const { return i == 0 ? rz0_ : kScBase + 2 * i; }
     int pap(int i) const { return kScBase + 2 * i + 1; }
+    // what the speculative J^T F depends on besides the unknowns it computed them from
+    std::vector<double> bind_key() const {
+        return {(double)(uintptr_t)cur_O_, (double)(uintptr_t)cur_A_, (double)(uintptr_t)cur_U_,
+                (double)(uintptr_t)cur_C_, (double)(uintptr_t)cur_M_, (double)wf_, (double)wr_};
+    }
 
     int stencil_blocks() const { return nstrips_ * nrowblocks_; }
 
@@ -1134,29 +1191,36 @@ private:
                                red_.slot(nb, sc_out));
         OPT_HIP_CHECK(hipGetLastError());
     }
+    void launch_jtf_cost(T* r, T* pre, int sc_out) {
+        const int nb = stencil_blocks();
+        hipLaunchKernelGGL((iw::iw_jtf<T, 0, true>), dim3(nb), dim3(kBlock), 0, stream_, args(), r, pre,
+                           red_.slot(nb, sc_out));
+        OPT_HIP_CHECK(hipGetLastError());
+    }
     template <int MODE, int DM>
     void launch_apply(const T* pin, T* pout, int sc_out, int ib_num, int ib_den, int ia_num, int ia_den,
-                      T* Ap = nullptr) {
+                      T* Ap = nullptr, bool no_ap = false) {
         const int nb = stencil_blocks();
+        Ap = no_ap ? nullptr : (Ap ? Ap : Ap_);
         if (depth_ == 2)
             hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 2>), dim3(nb), dim3(kBlock), 0, stream_, args(), pin,
-                               (const T*)r_, (const T*)pre_, pout, Ap ? Ap : Ap_, delta_, red_.scalars, ib_num,
+                               (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars, ib_num,
                                ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
         else if ((nt_ & 3) == 1)
             hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 1>), dim3(nb), dim3(kBlock), 0, stream_,
-                               args(), pin, (const T*)r_, (const T*)pre_, pout, Ap ? Ap : Ap_, delta_, red_.scalars,
+                               args(), pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
                                ib_num, ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
         else if ((nt_ & 3) == 2)
             hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 2>), dim3(nb), dim3(kBlock), 0, stream_,
-                               args(), pin, (const T*)r_, (const T*)pre_, pout, Ap ? Ap : Ap_, delta_, red_.scalars,
+                               args(), pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
                                ib_num, ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
         else if ((nt_ & 3) == 3)
             hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 3>), dim3(nb), dim3(kBlock), 0, stream_,
-                               args(), pin, (const T*)r_, (const T*)pre_, pout, Ap ? Ap : Ap_, delta_, red_.scalars,
+                               args(), pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
                                ib_num, ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
         else
             hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1>), dim3(nb), dim3(kBlock), 0, stream_, args(), pin,
-                               (const T*)r_, (const T*)pre_, pout, Ap ? Ap : Ap_, delta_, red_.scalars, ib_num,
+                               (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars, ib_num,
                                ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
         OPT_HIP_CHECK(hipGetLastError());
     }
@@ -1186,6 +1250,10 @@ private:
     long long nvec_ = 0;
     T *r_ = nullptr, *pre_ = nullptr, *p0_ = nullptr, *p1_ = nullptr, *Ap_ = nullptr, *delta_ = nullptr;
     uint8_t* flags_ = nullptr;
+    int rz0_ = kScBase;                 // slot of rz[0] this step
+    bool spec_valid_ = false;           // r_, pre_, flags_, sc[kScSpecRz] hold the next PCGInit1
+    bool spec_on_ = true;               // OPT_AMD_IW_SPEC=0: separate cost and J^T F passes
+    std::vector<double> spec_key_;
     int rows_ = 16, depth_ = 1, nstrips_ = 0, nrowblocks_ = 0;
     int nt_ = 6;   // streaming PCG-vector access: bit 0 iw_apply loads, bit 1 iw_apply stores, bit 2 iw_residual
     Comm* comm_ = nullptr;

@@ -195,3 +195,40 @@ def test_bench_workload_trajectory_within_fp32_noise_floor():
     c1 = s1.profiled_solve(p1)
     _, _, r1, _ = oracle.iw_solve(w, 1, 1, nthreads=16)
     np.testing.assert_allclose(c1, r1, rtol=1e-5)
+
+
+# ---- the fused end-of-step pass (cost + the next step's J^T F, image_warping.hip
+# ImageWarpingPlan::step) against separate passes (OPT_AMD_IW_SPEC=0)
+def _stepwise(monkeypatch, spec, change):
+    import torch
+
+    monkeypatch.setenv("OPT_AMD_IW_SPEC", "1" if spec else "0")
+    w = perturbed(150, 110, seed=21)
+    s = solver(150, 110)
+    s.set_solver_params({"nIterations": 6, "lIterations": 8})
+    prm = device_params(w)
+    s.init(prm)
+    costs = []
+    for k in range(6):
+        if change == "weight" and k == 2:
+            prm[-1] = float(w["w_regSqrt"]) * 1.7
+        if change == "rebind" and k == 3:
+            prm = [p.clone() if isinstance(p, torch.Tensor) else p for p in prm]
+        if change == "constraints" and k == 2:
+            C = prm[3].clone()
+            C[C >= 0] += 3.0
+            prm[3] = C
+        if not s.step(prm):
+            break
+        costs.append(s.cost())
+    return costs, prm[0].cpu().numpy(), prm[1].cpu().numpy()
+
+
+@pytest.mark.parametrize("change", ["none", "weight", "rebind", "constraints"])
+def test_fused_step_end_equals_separate_passes(monkeypatch, change):
+    c0, o0, a0 = _stepwise(monkeypatch, False, change)
+    c1, o1, a1 = _stepwise(monkeypatch, True, change)
+    assert len(c0) == 6
+    np.testing.assert_allclose(c1, c0, rtol=1e-6)
+    np.testing.assert_allclose(o1, o0, rtol=1e-6, atol=1e-5)
+    np.testing.assert_allclose(a1, a0, rtol=1e-5, atol=1e-6)
