@@ -5,15 +5,20 @@ lIterations x {fused p-update + J^T J p apply + p.Ap, PCG vector update + r.z},
 X += delta, cost). Inputs are resident in HBM before the timed region starts.
 
   value       PCG unknowns processed per second over the whole job:
-              n_unknowns * lIterations * steps * ranks / wall time of the timed steps
+              n_unknowns * lIterations * steps / wall time of the timed steps
   roofline    the dominant kernel (the J^T J p apply), HIP events on the plan's stream
-  cpu_baseline the oracle's (C restatement of the reference CPU-MT backend) J^T J p
-              apply on this host's cores, bounded sample, rank 0 at N=1 only
+  cpu_baseline the oracle (C restatement of the reference's GN/PCG, pthreads over rows
+              as backend_cpu_mt) timing one whole GN step on this host's cores, in the
+              same unit, plus apply-only rates on all cores and on one; rank 0 at N=1
 
 Multi-GPU (--gpus N under torch.distributed.run): the 4096² image is split into N
 row slabs, one per rank (OptAMD_PlanSetDecomposition over an RCCL communicator):
 per PCG iteration two scalar all-reduces (p.Ap, r.z) and one halo-row exchange.
 Total work is fixed, so the scaling is strong.
+
+--workload shape_from_shading: BASELINE config 3 (4096² fp32 LM + PCG, the config
+north_star tiles across the node) through the same slabs (halo 2, ComputedArray planes
+exchanged after each precompute, r.z and q all-reduced together).
 """
 import argparse
 import ctypes
@@ -29,17 +34,21 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 METRIC = "PCG JᵀJ·p throughput (unknowns/s) + GN iters/s, image_warping 4096² fp32"
+METRIC_SFS = "PCG JᵀJ·p throughput (unknowns/s) + LM iters/s, shape_from_shading 4096² fp32"
+SFS_APPLY_BYTES_PER_PX = 34
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # Compulsory HBM bytes per pixel of the in-loop apply kernel iw_apply:
 # always Angle 4 + UrShape 8 + flag 1 + r 12 + angle-channel pre 4 read, p 12 + Ap 12 written;
 # from PCG iteration 1 on also p_old 12 read and delta 12 written; from iteration 2 on
 # also delta 12 read.
-def apply_bytes_per_px(i: int) -> int:
+def apply_bytes_per_px(i: int, liter: int = 10) -> int:
     b = 4 + 8 + 1 + 12 + 4 + 12 + 12
     if i >= 1:
         b += 12 + 12
     if i >= 2:
         b += 12
+    if i == liter - 1:
+        b -= 12   # the last iteration's Ap is not stored (nothing reads it)
     return b
 
 
@@ -76,6 +85,7 @@ def parse():
     ap.add_argument("--size", type=int, default=4096)
     ap.add_argument("--liter", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", default="image_warping", choices=["image_warping", "shape_from_shading"])
     return ap.parse_args()
 
 
@@ -163,11 +173,17 @@ def main():
     from opt_amd import distributed as dd
 
     W = H = args.size
-    w = workloads.image_warping(W, H, seed=1234)
-    s = OptSolver([W, H], os.path.join(ROOT, "energies", "image_warping.t"), "gaussNewtonGPU")
+    sfs = args.workload == "shape_from_shading"
+    if sfs:
+        w = workloads.shape_from_shading(W, H, seed=3)
+        s = OptSolver([W, H], os.path.join(ROOT, "energies", "shape_from_shading.t"), "LMGPU")
+    else:
+        w = workloads.image_warping(W, H, seed=1234)
+        s = OptSolver([W, H], os.path.join(ROOT, "energies", "image_warping.t"), "gaussNewtonGPU")
     n_unknowns = s.unknown_count()   # global
     comm = None
     lw = w
+    sl = None
     if world > 1:
         lib = api.load_library()
         idbuf = torch.zeros(128, dtype=torch.uint8)
@@ -182,16 +198,13 @@ def main():
         assert comm, "RCCL communicator"
         sl = dd.slab(H, rank, world, s.halo())
         s.set_decomposition(comm, sl.y_lo, sl.y_hi)
-        lw = dd.local_image_warping(w, sl)
-    prm = [
-        torch.from_numpy(lw["Offset"]).cuda(),
-        torch.from_numpy(lw["Angle"]).cuda(),
-        torch.from_numpy(lw["UrShape"]).cuda(),
-        torch.from_numpy(lw["Constraints"]).cuda(),
-        torch.from_numpy(lw["Mask"]).cuda(),
-        w["w_fitSqrt"],
-        w["w_regSqrt"],
-    ]
+        lw = dd.local_image(w, sl, dd.SFS_CHANNELS if sfs else dd.IW_CHANNELS)
+    if sfs:
+        prm = [float(v) for v in w["params"]] + [torch.from_numpy(np.ascontiguousarray(lw[k])).cuda()
+                                                 for k in ("X", "D_i", "Im", "edgeMaskR", "edgeMaskC")]
+    else:
+        prm = [torch.from_numpy(lw[k]).cuda() for k in ("Offset", "Angle", "UrShape", "Constraints", "Mask")] + \
+              [w["w_fitSqrt"], w["w_regSqrt"]]
     total_steps = args.warmup + args.steps
     s.set_solver_params({"nIterations": total_steps + 1, "lIterations": args.liter})
     s.init(prm)
@@ -217,16 +230,21 @@ def main():
     n_apply, apply_ms = s.kernel_stat(kname)
     s.set_kernel_timing(0)
     avg_apply_s = (apply_ms / 1e3) / max(1, n_apply)
-    npx = W * (H // world if world > 1 else H)
-    bpp = sum(apply_bytes_per_px(i) for i in range(args.liter)) / args.liter
+    npx = W * (sl.rows if sl else H)
+    ch = 1 if sfs else 3          # unknowns per pixel
+    if sfs:   # sfs_strip: SURVEY.md §8d's per-pixel apply bytes
+        bpp = SFS_APPLY_BYTES_PER_PX
+    else:
+        bpp = sum(apply_bytes_per_px(i, args.liter) for i in range(args.liter)) / args.liter
     achieved = bpp * npx / avg_apply_s / 1e9
     # the pure apply (reads p) timed separately for the kernel-only unknowns/s
-    n_local = 3 * W * (lw["H"])
+    n_local = ch * W * (sl.mem_rows if sl else H)
     p = torch.randn(n_local, device="cuda")
     Ap = torch.empty_like(p)
     pure_us = s.time_apply(prm, p, Ap, 20)
+    kind = "LM" if sfs else "GN"
     result = {
-        "metric": METRIC,
+        "metric": METRIC_SFS if sfs else METRIC,
         "value": n_unknowns * args.liter * args.steps / dt,
         "unit": "unknowns/s",
         "n_gpus": world,
@@ -237,16 +255,16 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seeded image_warping inputs, SURVEY.md §8d)",
+        "data": f"synthetic (seeded {args.workload} inputs, SURVEY.md §8d)",
         "config": {
-            "workload": f"image_warping {W}x{H} fp32 GN+PCG, lIterations={args.liter}",
+            "workload": f"{args.workload} {W}x{H} fp32 {kind}+PCG, lIterations={args.liter}",
             "unknowns": n_unknowns,
             "parallelism": f"row-slabs x{world} (RCCL: 2 allreduce + 1 halo exchange per PCG iteration)" if world > 1 else "single",
         },
-        "gn_iters_per_s": args.steps / dt,
-        "apply_unknowns_per_s": 3 * npx * world / avg_apply_s,
+        f"{kind.lower()}_iters_per_s": args.steps / dt,
+        "apply_unknowns_per_s": ch * npx * world / avg_apply_s,
         "pure_apply_us": pure_us,
-        "pure_apply_unknowns_per_s": 3 * npx * world / (pure_us * 1e-6),
+        "pure_apply_unknowns_per_s": ch * npx * world / (pure_us * 1e-6),
         "roofline": {
             "kernel": kname,
             "bound": "hbm",
@@ -254,14 +272,14 @@ def main():
             "peak": PEAK_HBM_GBS,
             "unit": "GB/s",
             "frac": achieved / PEAK_HBM_GBS,
-            "traffic": (pmc_traffic(args.liter) if world == 1 and args.size == 4096 else None),
-            "traffic_unit": "bytes per launch (2 FETCH_SIZE + WRITE_SIZE, profiles/r01d_pmc.json)",
+            "traffic": (pmc_traffic(args.liter) if world == 1 and args.size == 4096 and not sfs else None),
+            "traffic_unit": f"bytes per launch (2 FETCH_SIZE + WRITE_SIZE, {os.path.relpath(PMC_FILE, ROOT)})",
             "avg_us": avg_apply_s * 1e6,
             "launches": n_apply,
             "bytes_per_px": bpp,
         },
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not sfs:
         result["cpu_baseline"] = cpu_baseline(w, n_unknowns, args.liter)
     if rank == 0:
         print(json.dumps(result), flush=True)

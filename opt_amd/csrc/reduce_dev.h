@@ -47,13 +47,16 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 // Called by every thread of a kBlock-thread block exactly once, after all the
 // block's stores of the kernel's outputs. v[k] is this thread's contribution.
+// Returns 1 in thread 0 of the block that summed the partials (after it stored the K
+// results; with `tot`, also copied there), 0 elsewhere: an epilogue that needs the
+// launch's totals (the LM zeta test) runs there once every block has published.
 // Arrivals are counted per shard (shard = block % 32, ~nblocks/32 adds per counter
 // instead of nblocks on one word: a single hot counter costs ~12 ns per add,
 // MI355X_MICROARCH.md row "fanin"); the last arriver of each shard then adds to a
 // top counter, and the last of those sums every partial in block order.
 template <int K>
-__device__ __forceinline__ void block_reduce_publish(const double (&v)[K], const ReduceSlot& rs,
-                                                     int block_linear) {
+__device__ __forceinline__ int block_reduce_publish(const double (&v)[K], const ReduceSlot& rs,
+                                                    int block_linear, double* tot = nullptr) {
     __shared__ double red[kBlock / kWave][K];
     __shared__ int last_flag;
     const int lane = threadIdx.x & (kWave - 1);
@@ -92,7 +95,7 @@ __device__ __forceinline__ void block_reduce_publish(const double (&v)[K], const
         last_flag = last;
     }
     __syncthreads();
-    if (!last_flag) return;
+    if (!last_flag) return 0;
     // one block per launch: the agent acquire (buffer_inv sc1) is cheap here
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // Last arriver: fixed-order sum of all partials (sc1 loads bypass the stale L1).
@@ -109,9 +112,12 @@ __device__ __forceinline__ void block_reduce_publish(const double (&v)[K], const
             if (threadIdx.x < stride) acc[threadIdx.x] += acc[threadIdx.x + stride];
             __syncthreads();
         }
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {
             __hip_atomic_store(&rs.out[k], acc[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (tot) tot[k] = acc[0];
+        }
         __syncthreads();
     }
+    return threadIdx.x == 0;
 }
 

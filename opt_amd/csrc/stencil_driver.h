@@ -102,6 +102,25 @@ __global__ __launch_bounds__(kBlock) void lm_init_kernel(VecLayout L, const uint
     block_reduce_publish<1>(v, rs, blockIdx.x);
 }
 
+// LM inner-loop exit test (:2211-2220) folded into the kernel that reduces q (one GPU:
+// the local q is the global one): zeta = (lIter+1) (Q1 - Q0) / Q1 in opt_float
+// arithmetic; stop if zeta < q_tolerance, else Q0 = Q1. on = 0: the driver launches
+// zeta_kernel after the all-reduce instead (row slabs).
+struct ZetaArgs {
+    double* q0;
+    int* stop;
+    int liter;
+    float q_tol;
+    int on;
+};
+template <typename T>
+__device__ __forceinline__ void zeta_test(const ZetaArgs& z, double q1) {
+    const T Q1 = (T)q1, Q0 = (T)*z.q0;
+    const T zeta = (T)(z.liter + 1) * (Q1 - Q0) / Q1;
+    if (zeta < (T)z.q_tol) *z.stop = 1;
+    else *z.q0 = (double)Q1;
+}
+
 // PCGStep2 (:665-731): alpha = sc[i_num]/sc[i_den]; delta (+)= alpha p; r -= alpha Ap;
 // z = pre r (r when UsePreconditioner(false)); out[0] = sum z.r; LM: out[1] = q =
 // sum 1/2 delta.(r + b).
@@ -111,7 +130,7 @@ __global__ __launch_bounds__(kBlock) void step2_kernel(long long n, const T* __r
                                                        const T* __restrict__ b, T* __restrict__ r,
                                                        T* __restrict__ delta, const double* __restrict__ sc,
                                                        int i_num, int i_den, int use_pre, const int* stop,
-                                                       ReduceSlot rs) {
+                                                       ReduceSlot rs, ZetaArgs z = {}) {
     if (stopped(stop)) return;
     const T alpha = (T)(sc[i_num] / sc[i_den]);
     T acc = 0, accq = 0;
@@ -126,8 +145,13 @@ __global__ __launch_bounds__(kBlock) void step2_kernel(long long n, const T* __r
         if (LM) accq += (T)0.5 * (d * (rr + b[e]));
     }
     double v[2] = {(double)acc, (double)accq};
-    if (LM) block_reduce_publish<2>(v, rs, blockIdx.x);
-    else { double v1[1] = {v[0]}; block_reduce_publish<1>(v1, rs, blockIdx.x); }
+    if (LM) {
+        double tot[2];
+        if (block_reduce_publish<2>(v, rs, blockIdx.x, tot) && z.on) zeta_test<T>(z, tot[1]);
+    } else {
+        double v1[1] = {v[0]};
+        block_reduce_publish<1>(v1, rs, blockIdx.x);
+    }
 }
 
 // PCGStep3 (:814-845): beta = sc[i_num]/sc[i_den]; p = z + beta p.
@@ -161,7 +185,8 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void half2_kernel(long long n, const T* __restrict__ Adelta,
                                                        const T* __restrict__ b, const T* __restrict__ pre,
                                                        const T* __restrict__ delta, T* __restrict__ r,
-                                                       int use_pre, const int* stop, ReduceSlot rs) {
+                                                       int use_pre, const int* stop, ReduceSlot rs,
+                                                       ZetaArgs z = {}) {
     if (stopped(stop)) return;
     T acc = 0, accq = 0;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
@@ -173,7 +198,8 @@ __global__ __launch_bounds__(kBlock) void half2_kernel(long long n, const T* __r
         accq += (T)0.5 * (delta[e] * (rr + b[e]));
     }
     double v[2] = {(double)acc, (double)accq};
-    block_reduce_publish<2>(v, rs, blockIdx.x);
+    double tot[2];
+    if (block_reduce_publish<2>(v, rs, blockIdx.x, tot) && z.on) zeta_test<T>(z, tot[1]);
 }
 
 // LM inner-loop exit test (:2211-2220), in opt_float arithmetic:

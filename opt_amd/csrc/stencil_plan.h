@@ -228,6 +228,8 @@ public:
     // PCG inner loop (PCGStep1-3, :607-845) of one step; launches only, no host sync.
     void pcg_loop(int Lit, int use_pre, const int* stop) {
         for (int i = 0; i < Lit; ++i) {
+            // the zeta test rides in the kernel that reduces q (one GPU), else its own launch
+            const ZetaArgs z{red_.scalars + kScQ0, stop_, i, sp_.q_tolerance, (lm_ && !distributed()) ? 1 : 0};
             exchange_vec(p_);
             if (mat_) {
                 // cusparseInner + PCGStep1_Finish (:2101-2118): the SpMV replaces PCGStep1;
@@ -247,10 +249,10 @@ public:
                 op_->apply(delta_, Adelta_, CtC_, stop, red_.slot(nb(), kScTmp), stream_);
                 hipLaunchKernelGGL((half2_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)Adelta_,
                                    (const T*)b_, (const T*)pre_, (const T*)delta_, r_, use_pre, stop,
-                                   red_.slot(fg(), rz(i + 1)));
+                                   red_.slot(fg(), rz(i + 1)), z);
             } else {
                 tbegin("step2");
-                launch_step2(i == 0, rz(i), pap(i), rz(i + 1), stop);
+                launch_step2(i == 0, rz(i), pap(i), rz(i + 1), stop, z);
                 tend();
             }
             allreduce(rz(i + 1), lm_ ? 2 : 1);   // rz and q sit side by side
@@ -258,7 +260,7 @@ public:
             hipLaunchKernelGGL((step3_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)pre_,
                                (const T*)r_, p_, red_.scalars, rz(i + 1), rz(i), use_pre, stop);
             tend();
-            if (lm_)
+            if (lm_ && !z.on)
                 hipLaunchKernelGGL((zeta_kernel<T>), dim3(1), dim3(1), 0, stream_, red_.scalars, q(i + 1),
                                    red_.scalars + kScQ0, i, sp_.q_tolerance, stop_);
             OPT_HIP_CHECK(hipGetLastError());
@@ -560,14 +562,14 @@ private:
         exchange(pl);
     }
 
-    void launch_step2(bool first, int i_num, int i_den, int out, const int* stop) {
+    void launch_step2(bool first, int i_num, int i_den, int out, const int* stop, ZetaArgs z = {}) {
         const int g = fg();
         const int use_pre = spec_.use_preconditioner ? 1 : 0;
         auto slot = red_.slot(g, out);
 #define S2(F, LMV)                                                                                     \
     hipLaunchKernelGGL((step2_kernel<T, F, LMV>), dim3(g), dim3(kBlock), 0, stream_, n_, (const T*)p_,   \
                        (const T*)Ap_, (const T*)pre_, (const T*)b_, r_, delta_, red_.scalars, i_num,    \
-                       i_den, use_pre, stop, slot)
+                       i_den, use_pre, stop, slot, z)
         if (first && lm_) S2(true, true);
         else if (first) S2(true, false);
         else if (lm_) S2(false, true);

@@ -45,14 +45,23 @@ def slice_rows(arr, W: int, channels: int, s: Slab):
     return arr[s.mem_lo * W * channels: s.mem_hi * W * channels]
 
 
-def local_image_warping(w: Dict, s: Slab) -> Dict:
-    """The image_warping problem arrays of one slab (memory rows incl. halo)."""
+IW_CHANNELS = (("Offset", 2), ("Angle", 1), ("UrShape", 2), ("Constraints", 2), ("Mask", 1))
+SFS_CHANNELS = (("X", 1), ("D_i", 1), ("Im", 1), ("edgeMaskR", 1), ("edgeMaskC", 1))
+
+
+def local_image(w: Dict, s: Slab, arrays) -> Dict:
+    """The per-pixel arrays (name, channels) of one slab (memory rows incl. halo)."""
     W = w["W"]
     out = dict(w)
-    for name, ch in (("Offset", 2), ("Angle", 1), ("UrShape", 2), ("Constraints", 2), ("Mask", 1)):
+    for name, ch in arrays:
         out[name] = slice_rows(w[name], W, ch, s).copy()
     out["H"] = s.mem_rows
     return out
+
+
+def local_image_warping(w: Dict, s: Slab) -> Dict:
+    """The image_warping problem arrays of one slab (memory rows incl. halo)."""
+    return local_image(w, s, IW_CHANNELS)
 
 
 def owned(arr, W: int, channels: int, s: Slab):

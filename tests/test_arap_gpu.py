@@ -182,3 +182,48 @@ def test_fp32_trajectory_within_the_fp32_noise_floor(kind, nit, lit):
                                   w, "Offset")
     drift = np.abs(costs - c64) / c64
     assert np.all(drift <= 2 * floor + 1e-7), (drift, floor)
+
+
+# ---- irregular graphs: hubs of up to 1000 edges, isolated vertices, one-way edges
+def irregular(seed=13):
+    rng = np.random.default_rng(seed)
+    w = workloads.arap_grid(60, 50, seed=seed)
+    N = w["N"]
+    e0, e1 = list(w["v0"]), list(w["v1"])
+    for hub, deg in ((17, 700), (63, 300), (64, 129), (2500, 1000)):
+        nb = rng.choice(N, size=deg, replace=False)
+        nb = nb[nb != hub]
+        e0 += [hub] * len(nb) + list(nb[: deg // 3])
+        e1 += list(nb) + [hub] * len(nb[: deg // 3])
+    keep = np.array([not (a in (5, 6, 7) or b in (5, 6, 7)) for a, b in zip(e0, e1)])
+    e0, e1 = np.array(e0)[keep], np.array(e1)[keep]
+    perm = rng.permutation(len(e0))
+    w["v0"] = np.ascontiguousarray(e0[perm].astype(np.int32))
+    w["v1"] = np.ascontiguousarray(e1[perm].astype(np.int32))
+    w["E"] = len(e0)
+    w["Offset"] = (w["Offset"] + 0.02 * rng.normal(size=w["Offset"].size)).astype(np.float32)
+    w["Angle"] = (w["Angle"] + 0.3 * rng.normal(size=w["Angle"].size)).astype(np.float32)
+    return w
+
+
+@pytest.mark.parametrize("double", [False, True])
+def test_apply_on_irregular_graphs(double):
+    import torch
+
+    w = irregular()
+    dt = torch.float64 if double else torch.float32
+    n = 6 * w["N"]
+    p = torch.from_numpy(np.random.default_rng(3).normal(size=n)).to(dt).cuda()
+    s = solver(w, double_precision=double)
+    prm = params(w, double=double)
+    Ap = torch.zeros(n, dtype=dt, device="cuda")
+    pAp = s.apply_jtj(prm, p, Ap)
+    Ap_ref, pAp_ref = oracle.arap_apply(w, to_np(p), double=double)
+    tol = 1e-10 if double else 2e-5
+    assert rel_err(to_np(Ap), Ap_ref) < tol
+    assert pAp == pytest.approx(pAp_ref, rel=tol)
+    r = torch.zeros(n, dtype=dt, device="cuda")
+    pre = torch.zeros_like(r)
+    s.eval_jtf(prm, r, pre)
+    r_ref, _ = oracle.arap_jtf(w, double=double)
+    assert rel_err(to_np(r), r_ref) < (1e-10 if double else 5e-5)
