@@ -158,7 +158,7 @@ __global__ __launch_bounds__(kBlock) void arap_kdir(Args<T> a, const T* __restri
     for (int i = 0; i < 9; ++i) Kout[i * N + v] = K[i];   // SoA: a wave's gathers of K_u hit 2 lines per entry
 }
 
-template <typename T>
+template <typename T, int EBO = kEB, int EBI = kEB>
 __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
                                                      const T* __restrict__ Kall, const T* __restrict__ dadd,
                                                      const int* stop, ReduceSlot rs) {
@@ -171,52 +171,66 @@ __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restr
         const V3<T> pO = ld3<T>(p, v), pA = ld3<T>(p + 3 * N, v);
         const V3<T> Av = ld3<T>(a.A, v);
         const V3<float> Uv = ld3<float>(a.U, v);
-        T R[9], dR[3][9], K[9];
-        rotation(Av, R, dR);
-        directional(dR, pA, K);
+        T K[9];
+        {
+            T R[9], dR[3][9];
+            rotation(Av, R, dR);
+            directional(dR, pA, K);
+        }
+        // Angle rows: sum_e (dR_j d_e) . Jp_e = <dR_j, M>, M = sum_e Jp_e d_e^T, so the 27
+        // rotation derivatives are rebuilt once after the out-edges instead of held live
+        // through the gathers (register pressure: more waves in flight)
+        T M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         V3<T> aO = {0, 0, 0}, aA = {0, 0, 0};
         if (fit_valid(a, v)) aO = {wf * (wf * pO.x), wf * (wf * pO.y), wf * (wf * pO.z)};
-        // Edges in batches of kEB: all neighbour indices, then all neighbour data, are
+        // Edges in batches (EBO / EBI; 4 / 4, 8 / 4, 4 / 2 and 8 / 2 measured within 4 %): all neighbour indices, then all neighbour data, are
         // issued before any is used (memory-level parallelism for the dependent gathers).
         const int ob = a.out_off[v], oe = a.out_off[v + 1], ib = a.in_off[v], ie = a.in_off[v + 1];
-        for (int i0 = ob; i0 < oe; i0 += kEB) {
-            int u[kEB];
+        for (int i0 = ob; i0 < oe; i0 += EBO) {
+            int u[EBO];
 #pragma unroll
-            for (int b = 0; b < kEB; ++b) u[b] = (i0 + b < oe) ? a.out_nbr[i0 + b] : v;
-            V3<T> pu[kEB];
-            V3<float> Uu[kEB];
+            for (int b = 0; b < EBO; ++b) u[b] = (i0 + b < oe) ? a.out_nbr[i0 + b] : v;
+            V3<T> pu[EBO];
+            V3<float> Uu[EBO];
 #pragma unroll
-            for (int b = 0; b < kEB; ++b) { pu[b] = ld3<T>(p, u[b]); Uu[b] = ld3<float>(a.U, u[b]); }
+            for (int b = 0; b < EBO; ++b) { pu[b] = ld3<T>(p, u[b]); Uu[b] = ld3<float>(a.U, u[b]); }
 #pragma unroll
-            for (int b = 0; b < kEB; ++b) {
+            for (int b = 0; b < EBO; ++b) {
                 if (i0 + b >= oe) break;
                 const V3<T> d = {(T)(Uv.x - Uu[b].x), (T)(Uv.y - Uu[b].y), (T)(Uv.z - Uu[b].z)};
                 const V3<T> Kd = mv(K, d);
                 const V3<T> jp = {wr * (pO.x - pu[b].x - Kd.x), wr * (pO.y - pu[b].y - Kd.y),
                                   wr * (pO.z - pu[b].z - Kd.z)};
                 aO.x += wr * jp.x; aO.y += wr * jp.y; aO.z += wr * jp.z;
-                const V3<T> c0 = mv(dR[0], d), c1 = mv(dR[1], d), c2 = mv(dR[2], d);
-                aA.x -= wr * (c0.x * jp.x + c0.y * jp.y + c0.z * jp.z);
-                aA.y -= wr * (c1.x * jp.x + c1.y * jp.y + c1.z * jp.z);
-                aA.z -= wr * (c2.x * jp.x + c2.y * jp.y + c2.z * jp.z);
+                M[0] += jp.x * d.x; M[1] += jp.x * d.y; M[2] += jp.x * d.z;
+                M[3] += jp.y * d.x; M[4] += jp.y * d.y; M[5] += jp.y * d.z;
+                M[6] += jp.z * d.x; M[7] += jp.z * d.y; M[8] += jp.z * d.z;
             }
         }
-        for (int i0 = ib; i0 < ie; i0 += kEB) {
-            int u[kEB];
+        {
+            T R[9], dR[3][9];
+            rotation(Av, R, dR);
+            T s0 = 0, s1 = 0, s2 = 0;
 #pragma unroll
-            for (int b = 0; b < kEB; ++b) u[b] = (i0 + b < ie) ? a.in_nbr[i0 + b] : v;
-            V3<T> pu[kEB];
-            V3<float> Uu[kEB];
-            T Ku[kEB][9];
+            for (int q = 0; q < 9; ++q) { s0 += dR[0][q] * M[q]; s1 += dR[1][q] * M[q]; s2 += dR[2][q] * M[q]; }
+            aA = {-wr * s0, -wr * s1, -wr * s2};
+        }
+        for (int i0 = ib; i0 < ie; i0 += EBI) {
+            int u[EBI];
 #pragma unroll
-            for (int b = 0; b < kEB; ++b) {
+            for (int b = 0; b < EBI; ++b) u[b] = (i0 + b < ie) ? a.in_nbr[i0 + b] : v;
+            V3<T> pu[EBI];
+            V3<float> Uu[EBI];
+            T Ku[EBI][9];
+#pragma unroll
+            for (int b = 0; b < EBI; ++b) {
                 pu[b] = ld3<T>(p, u[b]);
                 Uu[b] = ld3<float>(a.U, u[b]);
 #pragma unroll
                 for (int q = 0; q < 9; ++q) Ku[b][q] = Kall[q * N + u[b]];
             }
 #pragma unroll
-            for (int b = 0; b < kEB; ++b) {
+            for (int b = 0; b < EBI; ++b) {
                 if (i0 + b >= ie) break;
                 const V3<T> d = {(T)(Uu[b].x - Uv.x), (T)(Uu[b].y - Uv.y), (T)(Uu[b].z - Uv.z)};
                 const V3<T> Kd = mv(Ku[b], d);
