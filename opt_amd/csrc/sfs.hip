@@ -586,6 +586,143 @@ __global__ __launch_bounds__(kBlock) void sfs_cost(Args<T> a, const T* __restric
     block_reduce_publish<1>(v, rs, blockIdx.x);
 }
 
+// Register-strip form of the cost / model cost: a wavefront owns 64 columns (the middle
+// 62 are its output; neighbours at x +- 1 are DPP lane shifts of the rows in registers)
+// and walks rows y0..y1 keeping rows y-1, y, y+1. Every value, the order of the sums and
+// the expressions are sfs_cost's (the shading J delta term as shade_jp, the smoothness
+// term as smooth_val / smooth_jp); the strip only replaces the per-pixel neighbour loads
+// by register / lane reads and forms the PTab quotients once per column and per row.
+constexpr int kCostOut = 62;
+template <typename T, bool DELTA>
+struct CRow {
+    T x, dl, bi, g0, g1, g2;
+    float D;
+    int mr, mc, v;
+};
+template <typename T, bool DELTA>
+__device__ __forceinline__ CRow<T, DELTA> cost_row(const Args<T>& a, const T* __restrict__ delta, int gx, int r) {
+    const Domain& d = a.dom;
+    CRow<T, DELTA> q;
+    const bool in = inside(d, gx, r);
+    const long long o = in ? d.off(gx, r) : 0;
+    q.x = in ? a.X[o] : (T)0;
+    q.bi = in ? a.BI[o] : (T)0;
+    q.D = in ? a.D[o] : 0.f;
+    if (DELTA) {
+        q.dl = in ? delta[o] : (T)0;
+        q.g0 = in ? a.G00[o] : (T)0;
+        q.g1 = in ? a.Gm0[o] : (T)0;
+        q.g2 = in ? a.G0m[o] : (T)0;
+    } else {
+        q.dl = q.g0 = q.g1 = q.g2 = (T)0;
+    }
+    const bool ib = inbe(d, gx, r);
+    q.mr = ib ? a.mR[o] : 0;
+    q.mc = ib ? a.mC[o] : 0;
+    q.v = ib ? a.valid[o] : 0;
+    return q;
+}
+template <typename T, bool DELTA>
+__global__ __launch_bounds__(kBlock) void sfs_cost_strip(Args<T> a, const T* __restrict__ delta, ReduceSlot rs,
+                                                         int nstrips, int rows) {
+    const Domain& d = a.dom;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    const int strip = wave % nstrips, rb = wave / nstrips;
+    const int gx = strip * kCostOut - 1 + lane;
+    const int y0 = d.y_lo + rb * rows, y1 = min(y0 + rows, d.y_hi);
+    const bool out_lane = lane >= 1 && lane < 1 + kCostOut && gx < d.W;
+    const T wp = a.wp, wg = a.wg, ws = a.ws;
+    // PTab of the column: px(x-1), px(x), px(x+1)
+    const T qxl = ((T)(gx - 1) - a.ux) / a.fx, qxc = ((T)gx - a.ux) / a.fx, qxr = ((T)(gx + 1) - a.ux) / a.fx;
+    T acc = 0;
+    if (y0 < y1) {
+        CRow<T, DELTA> up = cost_row<T, DELTA>(a, delta, gx, y0 - 1);
+        CRow<T, DELTA> cur = cost_row<T, DELTA>(a, delta, gx, y0);
+        CRow<T, DELTA> dn = cost_row<T, DELTA>(a, delta, gx, y0 + 1);
+        T qyu = ((T)(y0 - 1) - a.uy) / a.fy, qyc = ((T)y0 - a.uy) / a.fy;
+        for (int y = y0; y < y1; ++y) {
+            const CRow<T, DELTA> nx = cost_row<T, DELTA>(a, delta, gx, y + 2);
+            const T qyd = ((T)(y + 1) - a.uy) / a.fy;
+            // neighbour values by lane shifts (every lane, before the divergent branch)
+            const T xl = from_left(cur.x, (T)0), xr = from_right(cur.x, (T)0);
+            const T bir = from_right(cur.bi, (T)0);
+            T dll = 0, dlr = 0, dlur = 0, dldl = 0, g0r = 0, g1r = 0, g2r = 0;
+            if (DELTA) {
+                dll = from_left(cur.dl, (T)0); dlr = from_right(cur.dl, (T)0);
+                dlur = from_right(up.dl, (T)0); dldl = from_left(dn.dl, (T)0);
+                g0r = from_right(cur.g0, (T)0); g1r = from_right(cur.g1, (T)0); g2r = from_right(cur.g2, (T)0);
+            }
+            if (out_lane && cur.D > 0.f) {
+                T s2 = 0;
+                {   // E_p
+                    T e = wp * (cur.x - (T)cur.D);
+                    if (DELTA) e += wp * cur.dl;
+                    s2 += e * e;
+                }
+                if (inbe(d, gx, y)) {
+                    const T bi = cur.bi;
+                    {   // E_g_h: n = c + (1, 0)
+                        const T m = (T)cur.mr;
+                        T e = wg * (bi - bir) * m;
+                        if (DELTA) {
+                            T jp = (wg * m * cur.g0 + -wg * m * g1r) * cur.dl;
+                            jp += (wg * m * cur.g1) * dll;
+                            jp += (wg * m * cur.g2) * up.dl;
+                            jp += (-wg * m * g0r) * dlr;
+                            jp += (-wg * m * g2r) * dlur;
+                            e += jp;
+                        }
+                        s2 += e * e;
+                    }
+                    {   // E_g_v: n = c + (0, 1)
+                        const T m = (T)cur.mc;
+                        T e = wg * (bi - dn.bi) * m;
+                        if (DELTA) {
+                            T jp = (wg * m * cur.g0 + -wg * m * dn.g2) * cur.dl;
+                            jp += (wg * m * cur.g1) * dll;
+                            jp += (wg * m * cur.g2) * up.dl;
+                            jp += (-wg * m * dn.g0) * dn.dl;
+                            jp += (-wg * m * dn.g1) * dldl;
+                            e += jp;
+                        }
+                        s2 += e * e;
+                    }
+                }
+                if (cur.v == 1) {   // E_s: centre, (-1,0), (0,-1), (1,0), (0,1)
+                    const T px[5] = {qxc, qxl, qxc, qxr, qxc}, py[5] = {qyc, qyc, qyu, qyc, qyd};
+                    const T xv[5] = {cur.x, xl, up.x, xr, dn.x};
+                    T sx = 0, sy = 0, sz = 0, x0 = 0, y0v = 0, z0 = 0;
+#pragma unroll
+                    for (int sI = 0; sI < 5; ++sI) {
+                        if (sI == 0) { x0 = px[0] * xv[0]; y0v = py[0] * xv[0]; z0 = xv[0]; }
+                        else { sx += px[sI] * xv[sI]; sy += py[sI] * xv[sI]; sz += xv[sI]; }
+                    }
+                    T v3[3] = {ws * ((T)4 * x0 - sx), ws * ((T)4 * y0v - sy), ws * ((T)4 * z0 - sz)};
+                    if (DELTA) {
+                        const T pv[5] = {cur.dl, dll, up.dl, dlr, dn.dl};
+                        T jd[3] = {0, 0, 0};
+#pragma unroll
+                        for (int sI = 0; sI < 5; ++sI) {
+                            const T co = sI == 0 ? (T)4 : (T)-1;
+                            jd[0] += ws * co * px[sI] * pv[sI];
+                            jd[1] += ws * co * py[sI] * pv[sI];
+                            jd[2] += ws * co * pv[sI];
+                        }
+                        v3[0] += jd[0]; v3[1] += jd[1]; v3[2] += jd[2];
+                    }
+                    s2 += v3[0] * v3[0] + v3[1] * v3[1] + v3[2] * v3[2];
+                }
+                acc += (T)0.5 * s2;
+            }
+            up = cur; cur = dn; dn = nx;
+            qyu = qyc; qyc = qyd;
+        }
+    }
+    double v[1] = {(double)acc};
+    block_reduce_publish<1>(v, rs, blockIdx.x);
+}
+
 }  // namespace sfs
 
 template <typename TT>
@@ -696,11 +833,28 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
     void cost(ReduceSlot rs, hipStream_t s) {
+        if (cost_strip_) {
+            launch_cost_strip<false>(nullptr, rs, s);
+            return;
+        }
         rs.nblocks = tile_blocks(pix_tiles(dom_));
         hipLaunchKernelGGL((sfs::sfs_cost<T>), dim3(rs.nblocks), dim3(kBlock), 0, s, a_, (const T*)nullptr, rs);
         OPT_HIP_CHECK(hipGetLastError());
     }
+    template <bool DELTA>
+    void launch_cost_strip(const T* delta, ReduceSlot rs, hipStream_t s) {
+        const int nstrips = (dom_.W + sfs::kCostOut - 1) / sfs::kCostOut;
+        const int nrb = (dom_.y_hi - dom_.y_lo + cost_rows_ - 1) / cost_rows_;
+        rs.nblocks = (nstrips * nrb + kBlock / kWave - 1) / (kBlock / kWave);
+        hipLaunchKernelGGL((sfs::sfs_cost_strip<T, DELTA>), dim3(rs.nblocks), dim3(kBlock), 0, s, a_, delta, rs,
+                           nstrips, cost_rows_);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
     void model_cost(const T* delta, ReduceSlot rs, hipStream_t s) {
+        if (cost_strip_) {
+            launch_cost_strip<true>(delta, rs, s);
+            return;
+        }
         rs.nblocks = tile_blocks(pix_tiles(dom_));
         hipLaunchKernelGGL((sfs::sfs_cost<T>), dim3(rs.nblocks), dim3(kBlock), 0, s, a_, delta, rs);
         OPT_HIP_CHECK(hipGetLastError());
@@ -717,6 +871,8 @@ private:
     int idx_X_, idx_D_, idx_Im_, idx_mR_, idx_mC_, idx_p_[16];
     sfs::Args<T> a_{};
     int strip_rows_ = env_int("OPT_AMD_SFS_ROWS", 16);
+    int cost_rows_ = env_int("OPT_AMD_SFS_COST_ROWS", 32);
+    bool cost_strip_ = env_int("OPT_AMD_SFS_COST_STRIP", 1) != 0;   // 0: the per-pixel sfs_cost
     T *BI_ = nullptr, *G00_ = nullptr, *Gm0_ = nullptr, *G0m_ = nullptr;
     uint8_t* valid_ = nullptr;
     T* userX_ = nullptr;

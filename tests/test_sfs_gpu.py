@@ -229,3 +229,22 @@ def test_fp32_trajectory_within_the_fp32_noise_floor(case):
                                   w, "X", n_pert=3)
     drift = np.abs(costs - c64) / c64
     assert np.all(drift <= 2 * floor + 1e-7), (drift, floor)
+
+
+@pytest.mark.parametrize("W,H", [(97, 61), (130, 9), (300, 257)])
+def test_cost_strip_equals_per_pixel_cost(monkeypatch, W, H):
+    """sfs_cost_strip (register strip, DPP neighbours) against the per-pixel sfs_cost:
+    the cost, and the model cost through whole LM trajectories."""
+    w = synthetic(W, H, seed=W)
+    out = {}
+    for strip in ("1", "0"):
+        monkeypatch.setenv("OPT_AMD_SFS_COST_STRIP", strip)
+        s = OptSolver([W, H], ENERGY, "LMGPU")
+        prm = params(w)
+        c0 = s.eval_cost(prm)
+        s.set_solver_params({"nIterations": 5, "lIterations": 10})
+        out[strip] = (c0, s.profiled_solve(prm))
+        s.close()
+    assert out["1"][0] == pytest.approx(out["0"][0], rel=1e-6)
+    assert out["1"][0] == pytest.approx(oracle.sfs_cost(w), rel=2e-5)
+    np.testing.assert_allclose(out["1"][1], out["0"][1], rtol=1e-5)
