@@ -43,6 +43,12 @@ void KernelTimer::begin(hipStream_t s, const char* name) {
     open_ev_ = get_event();
     OPT_HIP_CHECK(hipEventRecord(open_ev_, s));
 }
+bool KernelTimer::ext_pair(const char* name, hipEvent_t* a, hipEvent_t* b) {
+    if (mode == 0 || (mode == 2 && apply_name != name)) return false;
+    *a = get_event();
+    *b = get_event();
+    return true;
+}
 void KernelTimer::end(hipStream_t s) {
     if (!open_) return;
     hipEvent_t b = get_event();

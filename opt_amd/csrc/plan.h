@@ -51,6 +51,11 @@ public:
     std::string apply_name;
     void begin(hipStream_t s, const char* name);
     void end(hipStream_t s);
+    // Event pair to attach to the launch itself (hipExtLaunchKernel): the timestamps come
+    // from the kernel's own dispatch, with no marker packets between kernels.
+    // Returns false when `name` is not timed; else record() after the launch.
+    bool ext_pair(const char* name, hipEvent_t* a, hipEvent_t* b);
+    void ext_record(const char* name, hipEvent_t a, hipEvent_t b) { pending_.push_back({name, a, b}); }
     void flush();  // resolve recorded pairs (synchronises)
     void reset();
     bool stat(const std::string& name, long long* n, double* ms);
