@@ -16,6 +16,18 @@
 //   (J^T J p)_A,j(v) = -w sum_out (dR_j(v) d_e) . J_e p
 // K is computed once per vertex per apply by a first pass (arap_kdir, 36 B/vertex) so
 // the in-edge terms read the neighbour's K instead of rebuilding its rotation derivatives.
+// The apply reads its adjacency as sliced ELL (64-vertex slices, one slot row per wave
+// load) built from the CSR lists once per bind.
+//
+// Measured at 1 M vertices (profiles/r02_arap_*): kdir + apply ~60 us. Counters (r02q):
+// HBM traffic = the compulsory 176 B/vertex of the apply (132 B/vertex algorithmic + the
+// K gather 36 + CSR offsets 8) and 60 B/vertex of kdir; the apply is bound by the
+// texture/load path (TA busy 59 %, TD 67 % averaged over the dispatch incl. ramp and
+// tail; ~650 B/vertex requested through it by the 12 neighbour gathers) with 54 % of wave
+// time parked on loads. Variants measured within +-5 % or slower: edge batches 2-6 out x
+// 2-6 in, waves/EU forced to 5, branch-free tails, sin/cos stored per step (slower:
+// 6 loads beat 3 sincos), K recomputed per in-edge from the neighbour's angles (no kdir:
+// 63 us), an edge-parallel apply (100-143 us).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <algorithm>
@@ -38,15 +50,31 @@ struct Args {
     const int* out_nbr;
     const int* in_off;
     const int* in_nbr;
+    // the same lists as sliced ELL for the apply: slice s = vertices [64 s, 64 s + 64),
+    // its slot b of lane l at ell[eoff[s] + 64 b + l] (-1 past the vertex's degree), slot
+    // count ew[s] (a multiple of the apply's batch size)
+    const int *out_ell, *out_eoff, *out_ew;
+    const int *in_ell, *in_eoff, *in_ew;
     uint8_t* flags;
     T wf, wr;
 };
 
 template <typename T> struct V3 { T x, y, z; };
-constexpr int kEB = 4;   // edges gathered per batch
 template <typename T, typename S>
 __device__ __forceinline__ V3<T> ld3(const S* a, long long v) {
     return V3<T>{(T)a[3 * v], (T)a[3 * v + 1], (T)a[3 * v + 2]};
+}
+// Gathers address a neighbour as uniform base + 32-bit byte offset (the global_load
+// saddr form: one full-rate multiply per address instead of a 64-bit multiply-add;
+// make_arap_plan bounds N so 24 N fits in 32 bits)
+template <typename T, typename S>
+__device__ __forceinline__ V3<T> gld3(const S* a, int u) {
+    const S* q = (const S*)((const char*)a + (unsigned)u * (unsigned)(3 * sizeof(S)));
+    return V3<T>{(T)q[0], (T)q[1], (T)q[2]};
+}
+template <typename S>
+__device__ __forceinline__ S gld(const S* a, int u) {
+    return *(const S*)((const char*)a + (unsigned)u * (unsigned)sizeof(S));
 }
 template <typename T>
 __device__ __forceinline__ V3<T> mv(const T* M, const V3<T>& v) {
@@ -158,7 +186,8 @@ __global__ __launch_bounds__(kBlock) void arap_kdir(Args<T> a, const T* __restri
     for (int i = 0; i < 9; ++i) Kout[i * N + v] = K[i];   // SoA: a wave's gathers of K_u hit 2 lines per entry
 }
 
-template <typename T, int EBO = kEB, int EBI = kEB>
+constexpr int kEBO = 6, kEBI = 3;   // apply edge batches (out, in); ELL widths are padded to them
+template <typename T, int EBO = kEBO, int EBI = kEBI>
 __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
                                                      const T* __restrict__ Kall, const T* __restrict__ dadd,
                                                      const int* stop, ReduceSlot rs) {
@@ -183,28 +212,39 @@ __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restr
         T M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         V3<T> aO = {0, 0, 0}, aA = {0, 0, 0};
         if (fit_valid(a, v)) aO = {wf * (wf * pO.x), wf * (wf * pO.y), wf * (wf * pO.z)};
-        // Edges in batches (EBO / EBI; 4 / 4, 8 / 4, 4 / 2 and 8 / 2 measured within 4 %): all neighbour indices, then all neighbour data, are
-        // issued before any is used (memory-level parallelism for the dependent gathers).
-        const int ob = a.out_off[v], oe = a.out_off[v + 1], ib = a.in_off[v], ie = a.in_off[v + 1];
-        for (int i0 = ob; i0 < oe; i0 += EBO) {
+        // Edges in batches of EBO / EBI from the sliced-ELL lists: a wave's indices for one
+        // slot are 256 contiguous bytes, and a batch's indices, then all of its neighbour
+        // data, are loaded before any is used (memory-level parallelism for the dependent
+        // gathers). Padding slots (-1) gather the vertex itself and contribute exact zeros
+        // through a select; slots run in the CSR's (edge) order.
+        const int lane = v & 63;
+        const int* oel = a.out_ell + a.out_eoff[v >> 6] + lane;
+        const int ow = a.out_ew[v >> 6];
+        for (int i0 = 0; i0 < ow; i0 += EBO) {
             int u[EBO];
+            bool okb[EBO];
 #pragma unroll
-            for (int b = 0; b < EBO; ++b) u[b] = (i0 + b < oe) ? a.out_nbr[i0 + b] : v;
+            for (int b = 0; b < EBO; ++b) {
+                const int x = oel[64 * (i0 + b)];
+                okb[b] = x >= 0;
+                u[b] = okb[b] ? x : v;
+            }
             V3<T> pu[EBO];
             V3<float> Uu[EBO];
 #pragma unroll
-            for (int b = 0; b < EBO; ++b) { pu[b] = ld3<T>(p, u[b]); Uu[b] = ld3<float>(a.U, u[b]); }
+            for (int b = 0; b < EBO; ++b) { pu[b] = gld3<T>(p, u[b]); Uu[b] = gld3<float>(a.U, u[b]); }
 #pragma unroll
             for (int b = 0; b < EBO; ++b) {
-                if (i0 + b >= oe) break;
-                const V3<T> d = {(T)(Uv.x - Uu[b].x), (T)(Uv.y - Uu[b].y), (T)(Uv.z - Uu[b].z)};
+                const bool ok = okb[b];
+        const V3<T> d = {(T)(Uv.x - Uu[b].x), (T)(Uv.y - Uu[b].y), (T)(Uv.z - Uu[b].z)};
                 const V3<T> Kd = mv(K, d);
-                const V3<T> jp = {wr * (pO.x - pu[b].x - Kd.x), wr * (pO.y - pu[b].y - Kd.y),
-                                  wr * (pO.z - pu[b].z - Kd.z)};
+                const V3<T> jp = {ok ? wr * (pO.x - pu[b].x - Kd.x) : (T)0, ok ? wr * (pO.y - pu[b].y - Kd.y) : (T)0,
+                                  ok ? wr * (pO.z - pu[b].z - Kd.z) : (T)0};
+                const V3<T> dd = {ok ? d.x : (T)0, ok ? d.y : (T)0, ok ? d.z : (T)0};
                 aO.x += wr * jp.x; aO.y += wr * jp.y; aO.z += wr * jp.z;
-                M[0] += jp.x * d.x; M[1] += jp.x * d.y; M[2] += jp.x * d.z;
-                M[3] += jp.y * d.x; M[4] += jp.y * d.y; M[5] += jp.y * d.z;
-                M[6] += jp.z * d.x; M[7] += jp.z * d.y; M[8] += jp.z * d.z;
+                M[0] += jp.x * dd.x; M[1] += jp.x * dd.y; M[2] += jp.x * dd.z;
+                M[3] += jp.y * dd.x; M[4] += jp.y * dd.y; M[5] += jp.y * dd.z;
+                M[6] += jp.z * dd.x; M[7] += jp.z * dd.y; M[8] += jp.z * dd.z;
             }
         }
         {
@@ -215,27 +255,34 @@ __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restr
             for (int q = 0; q < 9; ++q) { s0 += dR[0][q] * M[q]; s1 += dR[1][q] * M[q]; s2 += dR[2][q] * M[q]; }
             aA = {-wr * s0, -wr * s1, -wr * s2};
         }
-        for (int i0 = ib; i0 < ie; i0 += EBI) {
+        const int* iel = a.in_ell + a.in_eoff[v >> 6] + lane;
+        const int iw = a.in_ew[v >> 6];
+        for (int i0 = 0; i0 < iw; i0 += EBI) {
             int u[EBI];
+            bool okb[EBI];
 #pragma unroll
-            for (int b = 0; b < EBI; ++b) u[b] = (i0 + b < ie) ? a.in_nbr[i0 + b] : v;
+            for (int b = 0; b < EBI; ++b) {
+                const int x = iel[64 * (i0 + b)];
+                okb[b] = x >= 0;
+                u[b] = okb[b] ? x : v;
+            }
             V3<T> pu[EBI];
             V3<float> Uu[EBI];
             T Ku[EBI][9];
 #pragma unroll
             for (int b = 0; b < EBI; ++b) {
-                pu[b] = ld3<T>(p, u[b]);
-                Uu[b] = ld3<float>(a.U, u[b]);
+                pu[b] = gld3<T>(p, u[b]);
+                Uu[b] = gld3<float>(a.U, u[b]);
 #pragma unroll
-                for (int q = 0; q < 9; ++q) Ku[b][q] = Kall[q * N + u[b]];
+                for (int q = 0; q < 9; ++q) Ku[b][q] = gld(Kall + q * N, u[b]);
             }
 #pragma unroll
             for (int b = 0; b < EBI; ++b) {
-                if (i0 + b >= ie) break;
+                const bool ok = okb[b];
                 const V3<T> d = {(T)(Uu[b].x - Uv.x), (T)(Uu[b].y - Uv.y), (T)(Uu[b].z - Uv.z)};
                 const V3<T> Kd = mv(Ku[b], d);
-                const V3<T> jp = {wr * (pu[b].x - pO.x - Kd.x), wr * (pu[b].y - pO.y - Kd.y),
-                                  wr * (pu[b].z - pO.z - Kd.z)};
+                const V3<T> jp = {ok ? wr * (pu[b].x - pO.x - Kd.x) : (T)0, ok ? wr * (pu[b].y - pO.y - Kd.y) : (T)0,
+                                  ok ? wr * (pu[b].z - pO.z - Kd.z) : (T)0};
                 aO.x -= wr * jp.x; aO.y -= wr * jp.y; aO.z -= wr * jp.z;
             }
         }
@@ -296,6 +343,23 @@ __global__ __launch_bounds__(kBlock) void arap_cost(Args<T> a, const T* __restri
     }
     double vv[1] = {(double)acc};
     block_reduce_publish<1>(vv, rs, blockIdx.x);
+}
+
+// Sliced ELL of a CSR (one wave per 64-vertex slice): slot counts, then the slots.
+__global__ void ell_width(const int* off, int N, int nslices, int pad, int* ew) {
+    const int s = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64, l = threadIdx.x & 63;
+    if (s >= nslices) return;
+    const int v = 64 * s + l;
+    int d = v < N ? off[v + 1] - off[v] : 0;
+    for (int m = 32; m >= 1; m >>= 1) d = max(d, __shfl_xor(d, m));
+    if (l == 0) ew[s] = (d + pad - 1) / pad * pad;
+}
+__global__ void ell_fill(const int* off, const int* nbr, int N, const int* eoff, const int* ew, int* ell) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x, s = v >> 6;
+    if (64 * s >= N) return;
+    const int b0 = v < N ? off[v] : 0, d = v < N ? off[v + 1] - b0 : 0;
+    int* e = ell + eoff[s] + (v & 63);
+    for (int b = 0; b < ew[s]; ++b) e[64 * b] = b < d ? nbr[b0 + b] : -1;
 }
 
 // vertex indices of the graph must lie in [0, N): checked once per CSR build
@@ -374,7 +438,12 @@ __global__ __launch_bounds__(kBlock) void arap_dump_edges(Args<T> a, const int* 
 struct GraphCSR {
     int* off = nullptr;   // N + 1
     int* nbr = nullptr;   // E
-    void release() { dfree(off); dfree(nbr); off = nbr = nullptr; }
+    int* ell = nullptr;   // sliced ELL of the same lists (arap::Args)
+    int* eoff = nullptr;  // per slice: first slot entry (nslices + 1, exclusive scan of 64 ew)
+    int* ew = nullptr;    // per slice: slot count
+    void release() {
+        for (int** q : {&off, &nbr, &ell, &eoff, &ew}) { dfree(*q); *q = nullptr; }
+    }
 };
 
 template <typename TT>
@@ -460,6 +529,8 @@ public:
         a_.N = N_;
         a_.out_off = out_.off; a_.out_nbr = out_.nbr;
         a_.in_off = in_.off; a_.in_nbr = in_.nbr;
+        a_.out_ell = out_.ell; a_.out_eoff = out_.eoff; a_.out_ew = out_.ew;
+        a_.in_ell = in_.ell; a_.in_eoff = in_.eoff; a_.in_ew = in_.ew;
     }
     void unbind(hipStream_t s) {
         if (!opts_.host_buffers) return;
@@ -528,6 +599,38 @@ private:
         size_t n2 = scratch_bytes_;
         OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(scratch_, n2, g.off, g.off, N_ + 1, s));
     }
+    // sliced ELL of g's lists, slot counts padded to multiples of `pad`
+    void ell(GraphCSR& g, int pad, hipStream_t s) {
+        const int ns = (N_ + 63) / 64;
+        g.ew = (int*)dmalloc(sizeof(int) * (ns + 1));
+        g.eoff = (int*)dmalloc(sizeof(int) * (ns + 1));
+        OPT_HIP_CHECK(hipMemsetAsync(g.ew, 0, sizeof(int) * (ns + 1), s));
+        hipLaunchKernelGGL(arap::ell_width, dim3((ns + 3) / 4), dim3(256), 0, s, g.off, N_, ns, pad, g.ew);
+        // eoff = 64 x exclusive scan of ew: scan the widths, then scale on the host copy
+        size_t need = 0;
+        OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, need, g.ew, g.eoff, ns + 1, s));
+        if (need > scratch_bytes_) {
+            dfree(scratch_);
+            scratch_ = dmalloc(need);
+            scratch_bytes_ = need;
+        }
+        OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(scratch_, need, g.ew, g.eoff, ns + 1, s));
+        std::vector<int> h(ns + 1);
+        OPT_HIP_CHECK(hipMemcpyAsync(h.data(), g.eoff, sizeof(int) * (ns + 1), hipMemcpyDeviceToHost, s));
+        OPT_HIP_CHECK(hipStreamSynchronize(s));
+        const long long total = 64LL * h[ns];
+        if (total >= (1LL << 31)) {
+            fprintf(stderr, "[opt_amd] arap_mesh_deformation: adjacency too large (%lld ELL slots)\n", total);
+            exit(1);
+        }
+        for (auto& x : h) x *= 64;
+        OPT_HIP_CHECK(hipMemcpyAsync(g.eoff, h.data(), sizeof(int) * (ns + 1), hipMemcpyHostToDevice, s));
+        g.ell = (int*)dmalloc(sizeof(int) * std::max(total, 1LL));
+        hipLaunchKernelGGL(arap::ell_fill, dim3((64LL * ns + 255) / 256), dim3(256), 0, s, g.off, g.nbr, N_, g.eoff,
+                           g.ew, g.ell);
+        OPT_HIP_CHECK(hipGetLastError());
+        OPT_HIP_CHECK(hipStreamSynchronize(s));   // h is a host temporary
+    }
     void build_csr(const int* v0, const int* v1, hipStream_t s) {
         if (E_ > 0) {
             int* bad = (int*)dmalloc(sizeof(int));
@@ -547,6 +650,8 @@ private:
         }
         csr(v0, v1, out_, s);
         csr(v1, v0, in_, s);
+        ell(out_, arap::kEBO, s);
+        ell(in_, arap::kEBI, s);
         graph_v0_ = v0;
         graph_v1_ = v1;
     }
@@ -581,7 +686,8 @@ std::unique_ptr<Plan> make_arap_plan(const ProblemSpec& spec, const StateOptions
         if (d.name == spec.graphs[0].dims[0]) E = dims[d.index];
     }
     if (N == 0) { *err = "arap_mesh_deformation: zero vertices"; return nullptr; }
-    if (N > (1u << 30) || E > (1u << 30)) { *err = "arap_mesh_deformation: graph too large"; return nullptr; }
+    // 24 N bytes must fit the gathers' 32-bit offsets (arap::gld3)
+    if (N > (1u << 27) || E > (1u << 30)) { *err = "arap_mesh_deformation: graph too large"; return nullptr; }
     Domain dom{(int)N, 1, 0, 1, 0, 1};
     dom.edges = (int)E;
     if (opts.double_precision) return make_stencil_plan<ArapOp<double>>(spec, opts, dom, err);
