@@ -56,6 +56,10 @@ struct Args {
     T wf, wr;
     int use_pre;
     int nstrips, nrowblocks, rows;   // rows per wavefront
+    // tiles (strip, row block) of this launch: local tile t < tn0 -> tb0 + t, else
+    // tb1 + t - tn0 (whole domain: 0, nstrips * nrowblocks, 0; the slab plans launch the
+    // interior row blocks and the two boundary row blocks separately to overlap the halo)
+    int tb0, tn0, tb1;
     // Jacobi preconditioner of the two Offset channels: diag(J^T J) there is
     // 2 wr^2 (#valid edges) + wf^2 [fit], so pre = 1/(1+sqrt(diag))^2 takes one of ten
     // values (host-computed once per step; 0.25 everywhere for UsePreconditioner(false)).
@@ -85,14 +89,15 @@ __device__ __forceinline__ void sc_of(float t, float* c, float* s) { sincosf(t, 
 __device__ __forceinline__ void sc_of(double t, double* c, double* s) { sincos(t, s, c); }
 
 struct WaveGeom {
-    int x, ex, lane, y0, y1;
+    int x, ex, lane, y0, y1, tile;
     bool out_lane, edge_lane;
 };
 template <typename T>
 __device__ __forceinline__ WaveGeom geom(const Args<T>& a) {
     WaveGeom g;
-    const int nb = a.nstrips * a.nrowblocks;
-    const int t = xcd_remap(blockIdx.x, nb);
+    const int lt = xcd_remap(blockIdx.x, gridDim.x);
+    const int t = lt < a.tn0 ? a.tb0 + lt : a.tb1 + (lt - a.tn0);
+    g.tile = t;
     const int strip = t % a.nstrips, rb = t / a.nstrips;
     g.lane = threadIdx.x & (kWave - 1);
     const int w = threadIdx.x / kWave;
@@ -363,7 +368,7 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
         }
     }
     double v[1] = {(double)dot};
-    block_reduce_publish<1>(v, rs, blockIdx.x);
+    block_reduce_publish<1>(v, rs, g.tile);   // partials by tile: split launches share the slot
 }
 
 // ------------------------------------------------------------- value rows
@@ -950,10 +955,25 @@ public:
         // (a hipGraph of this loop was measured: 4.38-4.41 ms/step against 4.38 with
         // plain launches — the 4-6 us gaps at the apply/residual boundaries are not
         // launch overhead, so the loop stays as plain stream launches)
+        // row slabs with >= 3 row blocks: the halo refresh of r and p_{i-1} runs beside the
+        // interior row blocks of the next apply (halo_mark / halo_begin / halo_join)
+        const bool split = distributed() && overlap_ && nrowblocks_ >= 3;
         for (int i = 0; i < L; ++i) {
             std::swap(pcur, pprev);   // pcur <- new p, pprev <- old p
             const bool last = i + 1 == L;   // timed by events on the launch (launch_apply)
             if (i == 0) launch_apply<1, 0>(nullptr, pcur, pap(i), 0, 0, 0, 0, nullptr, last);
+            else if (split) {
+                halo_mark();
+                if (i == 1) launch_apply<2, 1>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1), nullptr, last, 1);
+                else launch_apply<2, 2>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1), nullptr, last, 1);
+                std::vector<HaloPlane> pl;
+                add_vec_planes(pl, r_);
+                add_vec_planes(pl, pprev);
+                halo_begin(comm_, pl, dom_, 1);
+                halo_join();
+                if (i == 1) launch_apply<2, 1>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1), nullptr, last, 2);
+                else launch_apply<2, 2>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1), nullptr, last, 2);
+            }
             else if (i == 1) launch_apply<2, 1>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1), nullptr, last);
             else launch_apply<2, 2>(pprev, pcur, pap(i), rz(i), rz(i - 1), rz(i - 1), pap(i - 1), nullptr, last);
             allreduce(pap(i));
@@ -964,7 +984,7 @@ public:
             launch_residual(rz(i), pap(i), rz(i + 1));
             tend();
             allreduce(rz(i + 1));
-            if (distributed() && i + 1 < L) {   // the next apply reads r and p_i in the halo rows
+            if (distributed() && !split && i + 1 < L) {   // the next apply reads r and p_i in the halo rows
                 std::vector<HaloPlane> pl;
                 add_vec_planes(pl, r_);
                 add_vec_planes(pl, pcur);
@@ -1135,6 +1155,7 @@ private:
         a.wf = (T)wf_; a.wr = (T)wr_;
         a.use_pre = spec_.use_preconditioner ? 1 : 0;
         a.nstrips = nstrips_; a.nrowblocks = nrowblocks_; a.rows = rows_;
+        a.tb0 = 0; a.tn0 = nstrips_ * nrowblocks_; a.tb1 = 0;
         // same float expression the reference's evalJTF + guardedInvert evaluate
         const T wr2 = (T)wr_ * (T)wr_, wf2 = (T)wf_ * (T)wf_;
         for (int fit = 0; fit < 2; ++fit)
@@ -1199,15 +1220,32 @@ private:
                            red_.slot(nb, sc_out));
         OPT_HIP_CHECK(hipGetLastError());
     }
+    // part 0: every row block; 1: the interior row blocks [1, nrb - 1); 2: the first and
+    // last row blocks (the only ones whose stencil reads halo rows)
     template <int MODE, int DM>
     void launch_apply(const T* pin, T* pout, int sc_out, int ib_num, int ib_den, int ia_num, int ia_den,
-                      T* Ap = nullptr, bool no_ap = false) {
+                      T* Ap = nullptr, bool no_ap = false, int part = 0) {
         const int nb = stencil_blocks();
         Ap = no_ap ? nullptr : (Ap ? Ap : Ap_);
+        iw::Args<T> a = args();
+        int grid = nb;
+        if (part == 1) {
+            a.tb0 = nstrips_; a.tn0 = nstrips_ * (nrowblocks_ - 2);
+            grid = a.tn0;
+        } else if (part == 2) {
+            a.tb0 = 0; a.tn0 = nstrips_; a.tb1 = nstrips_ * (nrowblocks_ - 1);
+            grid = 2 * nstrips_;
+        }
+        launch_apply_grid<MODE, DM>(a, grid, pin, pout, sc_out, ib_num, ib_den, ia_num, ia_den, Ap);
+    }
+    template <int MODE, int DM>
+    void launch_apply_grid(const iw::Args<T>& a, int grid, const T* pin, T* pout, int sc_out, int ib_num,
+                           int ib_den, int ia_num, int ia_den, T* Ap) {
+        const int nb = stencil_blocks();   // the reduction slot spans every tile
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (nt_ == 6 && depth_ == 1 && timer_.ext_pair("iw_apply", &e0, &e1)) {   // the default variant
-            hipExtLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 2>), dim3(nb), dim3(kBlock), 0, stream_, e0,
-                                  e1, 0, args(), pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
+            hipExtLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 2>), dim3(grid), dim3(kBlock), 0, stream_, e0,
+                                  e1, 0, a, pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
                                   ib_num, ib_den, ia_num, ia_den, red_.slot(nb, sc_out), (const T*)nullptr,
                                   (const int*)nullptr);
             OPT_HIP_CHECK(hipGetLastError());
@@ -1215,23 +1253,23 @@ private:
             return;
         }
         if (depth_ == 2)
-            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 2>), dim3(nb), dim3(kBlock), 0, stream_, args(), pin,
+            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 2>), dim3(grid), dim3(kBlock), 0, stream_, a, pin,
                                (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars, ib_num,
                                ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
         else if ((nt_ & 3) == 1)
-            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 1>), dim3(nb), dim3(kBlock), 0, stream_,
-                               args(), pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
+            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 1>), dim3(grid), dim3(kBlock), 0, stream_,
+                               a, pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
                                ib_num, ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
         else if ((nt_ & 3) == 2)
-            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 2>), dim3(nb), dim3(kBlock), 0, stream_,
-                               args(), pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
+            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 2>), dim3(grid), dim3(kBlock), 0, stream_,
+                               a, pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
                                ib_num, ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
         else if ((nt_ & 3) == 3)
-            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 3>), dim3(nb), dim3(kBlock), 0, stream_,
-                               args(), pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
+            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 3>), dim3(grid), dim3(kBlock), 0, stream_,
+                               a, pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
                                ib_num, ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
         else
-            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1>), dim3(nb), dim3(kBlock), 0, stream_, args(), pin,
+            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1>), dim3(grid), dim3(kBlock), 0, stream_, a, pin,
                                (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars, ib_num,
                                ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
         OPT_HIP_CHECK(hipGetLastError());
@@ -1269,6 +1307,7 @@ private:
     int rows_ = 16, depth_ = 1, nstrips_ = 0, nrowblocks_ = 0;
     int nt_ = 6;   // streaming PCG-vector access: bit 0 iw_apply loads, bit 1 iw_apply stores, bit 2 iw_residual
     Comm* comm_ = nullptr;
+    const bool overlap_ = env_int("OPT_AMD_HALO_OVERLAP", 1) != 0;   // 0: blocking halo before each apply
     float wf_ = 0, wr_ = 0;
     T *user_O_ = nullptr, *user_A_ = nullptr;
     T *cur_O_ = nullptr, *cur_A_ = nullptr;
@@ -1354,6 +1393,7 @@ public:
         a_.dom = dom_;
         a_.use_pre = use_pre_ ? 1 : 0;
         a_.nstrips = nstrips_; a_.nrowblocks = nrowblocks_; a_.rows = rows_;
+        a_.tb0 = 0; a_.tn0 = nstrips_ * nrowblocks_; a_.tb1 = 0;
         for (int f = 0; f < 2; ++f)
             for (int v = 0; v < 5; ++v) a_.preO[f][v] = 0;   // MODE 0 never reads them
     }

@@ -132,6 +132,29 @@ Plan::Plan(const ProblemSpec& spec, const StateOptions& opts) : spec_(spec), opt
     timer_.mode = opts.kernel_timing ? 1 : 0;
 }
 
+Plan::~Plan() {
+    if (halo_stream_) {
+        OPT_HIP_CHECK(hipStreamSynchronize(halo_stream_));
+        OPT_HIP_CHECK(hipStreamDestroy(halo_stream_));
+    }
+    for (hipEvent_t e : halo_ev_)
+        if (e) OPT_HIP_CHECK(hipEventDestroy(e));
+}
+
+void Plan::halo_mark() {
+    if (!halo_stream_) {
+        OPT_HIP_CHECK(hipStreamCreateWithFlags(&halo_stream_, hipStreamNonBlocking));
+        for (hipEvent_t& e : halo_ev_) OPT_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    OPT_HIP_CHECK(hipEventRecord(halo_ev_[0], stream_));
+}
+void Plan::halo_begin(Comm* comm, const std::vector<HaloPlane>& planes, const Domain& dom, int halo) {
+    OPT_HIP_CHECK(hipStreamWaitEvent(halo_stream_, halo_ev_[0], 0));
+    comm->halo_exchange(planes, dom, halo, halo_stream_);
+    OPT_HIP_CHECK(hipEventRecord(halo_ev_[1], halo_stream_));
+}
+void Plan::halo_join() { OPT_HIP_CHECK(hipStreamWaitEvent(stream_, halo_ev_[1], 0)); }
+
 void Plan::set_solver_param(const char* name, const void* value) {
     if (!sp_.set(name, value))
         fprintf(stderr, "Warning: tried to set nonexistent solver parameter %s\n", name);

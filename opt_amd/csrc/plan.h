@@ -87,7 +87,7 @@ struct ReduceScratch {
 
 class Plan {
 public:
-    virtual ~Plan() {}
+    virtual ~Plan();
     virtual void init(void** params) = 0;
     virtual int step(void** params) = 0;
     virtual double cost() const { return prev_cost_; }
@@ -138,6 +138,16 @@ protected:
     void cleanup_log();
     // logSolver: printf to stdout when verbosityLevel > 0 (o.t:95-104)
     void log_solver(const char* fmt, ...);
+    // Halo refresh overlapped with interior work (row slabs): halo_mark() marks stream_'s
+    // work so far; the interior launches follow on stream_ (they read no halo row and
+    // write none of the exchanged rows); halo_begin() runs the exchange on a second
+    // stream ordered after the mark only (RCCL: queued; LocalGroup: host copies while the
+    // interior kernels run); halo_join() makes stream_ wait for it before the boundary
+    // launches. The plan's collectives keep one total order (each is ordered after the
+    // previous through stream_ and these events), as RCCL requires.
+    void halo_mark();
+    void halo_begin(Comm* comm, const std::vector<HaloPlane>& planes, const Domain& dom, int halo);
+    void halo_join();
     void tbegin(const char* name) { if (timer_.mode) timer_.begin(stream_, name); }
     void tend() { if (timer_.mode) timer_.end(stream_); }
 
@@ -145,6 +155,8 @@ protected:
     StateOptions opts_;
     SolverParams sp_;
     hipStream_t stream_ = nullptr;
+    hipStream_t halo_stream_ = nullptr;           // created on first halo_begin
+    hipEvent_t halo_ev_[2] = {nullptr, nullptr};  // stream_ -> halo stream, halo stream -> stream_
     KernelTimer timer_;
     ReduceScratch red_;
     double prev_cost_ = 0.0;

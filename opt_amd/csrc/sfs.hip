@@ -458,11 +458,15 @@ __device__ __forceinline__ SRow<T> strip_row(const Args<T>& a, const T* __restri
 template <typename T>
 __global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
                                                     const T* __restrict__ dadd, const int* stop, ReduceSlot rs,
-                                                    int nstrips, int rows) {
+                                                    int nstrips, int rows, int bb0 = 0, int bn0 = 1 << 30,
+                                                    int bb1 = 0) {
     if (stop && *stop) return;
     const Domain& d = a.dom;
     const int lane = threadIdx.x & (kWave - 1);
-    const int wave = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    // this launch's blocks: local b < bn0 -> bb0 + b, else bb1 + b - bn0 (whole slab: the
+    // identity; the slab plans launch interior and boundary block ranges separately)
+    const int gb = (int)blockIdx.x < bn0 ? bb0 + (int)blockIdx.x : bb1 + (int)blockIdx.x - bn0;
+    const int wave = gb * (kBlock / kWave) + (threadIdx.x >> 6);
     const int strip = wave % nstrips, rb = wave / nstrips;
     const int gx = strip * kStripOut - 2 + lane;
     const int y0 = d.y_lo + rb * rows, y1 = min(y0 + rows, d.y_hi);
@@ -535,7 +539,7 @@ __global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restri
         }
     }
     double v[1] = {(double)dot};
-    block_reduce_publish<1>(v, rs, blockIdx.x);
+    block_reduce_publish<1>(v, rs, gb);
 }
 
 // ------------------------------------------------------- cost / model cost
@@ -824,12 +828,39 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
     void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
+        apply_split(0, p, Ap, dadd, stop, rs, s);
+    }
+    // Row slabs: part 1 launches the blocks whose waves read no halo row (strip rows
+    // [y0 - 2, y1 + 1] inside the owned rows), part 2 the rest; together they are the
+    // whole launch block for block (same partial per block: bitwise the same sums).
+    bool split_ranges(int* i0, int* i1, int* blocks) const {
         const int nstrips = (dom_.W + sfs::kStripOut - 1) / sfs::kStripOut;
-        const int nrb = (dom_.y_hi - dom_.y_lo + strip_rows_ - 1) / strip_rows_;
-        const int blocks = (nstrips * nrb + kBlock / kWave - 1) / (kBlock / kWave);
-        rs.nblocks = blocks;   // the reduction's arrival count is this launch's grid
-        hipLaunchKernelGGL((sfs::sfs_strip<T>), dim3(blocks), dim3(kBlock), 0, s, a_, p, Ap, dadd, stop, rs, nstrips,
-                           strip_rows_);
+        const int rows = strip_rows_;
+        const int nrb = (dom_.y_hi - dom_.y_lo + rows - 1) / rows;
+        *blocks = (nstrips * nrb + kBlock / kWave - 1) / (kBlock / kWave);
+        int rb_a = 0, rb_b = nrb;   // interior row blocks [rb_a, rb_b)
+        while (rb_a < nrb && dom_.y_lo + rb_a * rows - 2 < dom_.y_lo) ++rb_a;
+        while (rb_b > rb_a && std::min(dom_.y_lo + rb_b * rows, dom_.y_hi) + 1 >= dom_.y_hi) --rb_b;
+        const int w4 = kBlock / kWave;
+        *i0 = (nstrips * rb_a + w4 - 1) / w4;   // first block with only interior waves
+        *i1 = (nstrips * rb_b) / w4;            // one past the last
+        return *i1 > *i0;
+    }
+    bool can_split() const {
+        int i0, i1, b;
+        return split_ranges(&i0, &i1, &b);
+    }
+    void apply_split(int part, const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
+        const int nstrips = (dom_.W + sfs::kStripOut - 1) / sfs::kStripOut;
+        int i0 = 0, i1 = 0, blocks = 0;
+        split_ranges(&i0, &i1, &blocks);
+        rs.nblocks = blocks;   // the reduction spans every block of the slab
+        int grid = blocks, bb0 = 0, bn0 = 1 << 30, bb1 = 0;
+        if (part == 1) { grid = i1 - i0; bb0 = i0; }
+        if (part == 2) { grid = i0 + (blocks - i1); bb0 = 0; bn0 = i0; bb1 = i1; }
+        if (grid <= 0) return;
+        hipLaunchKernelGGL((sfs::sfs_strip<T>), dim3(grid), dim3(kBlock), 0, s, a_, p, Ap, dadd, stop, rs, nstrips,
+                           strip_rows_, bb0, bn0, bb1);
         OPT_HIP_CHECK(hipGetLastError());
     }
     void cost(ReduceSlot rs, hipStream_t s) {

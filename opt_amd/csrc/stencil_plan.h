@@ -91,6 +91,14 @@ struct HasDumpJ<Op, std::void_t<decltype(std::declval<Op&>().dump_j((int*)nullpt
                                                                      (typename Op::T*)nullptr, hipStream_t{}))>>
     : std::true_type {};
 
+// Ops whose apply can run as interior + boundary launches (row slabs: the halo refresh
+// of p overlaps the interior part): bool can_split() const; void apply_split(int part,
+// ... apply's arguments) with part 1 = no halo reads, 2 = the rest, 0 = everything.
+template <class Op, class = void>
+struct HasApplySplit : std::false_type {};
+template <class Op>
+struct HasApplySplit<Op, std::void_t<decltype(std::declval<const Op&>().can_split())>> : std::true_type {};
+
 template <class Op, class = void>
 struct HasSlabRefusal : std::false_type {};
 template <class Op>
@@ -230,8 +238,23 @@ public:
         for (int i = 0; i < Lit; ++i) {
             // the zeta test rides in the kernel that reduces q (one GPU), else its own launch
             const ZetaArgs z{red_.scalars + kScQ0, stop_, i, sp_.q_tolerance, (lm_ && !distributed()) ? 1 : 0};
-            exchange_vec(p_);
-            if (mat_) {
+            bool split = false;
+            if constexpr (HasApplySplit<Op>::value)
+                split = distributed() && overlap_ && !mat_ && op_->can_split();
+            if (!split) exchange_vec(p_);
+            if (split) {
+                if constexpr (HasApplySplit<Op>::value) {
+                    // halo refresh of p beside the interior blocks (Plan::halo_mark/begin/join)
+                    tbegin(Op::kApplyName);
+                    halo_mark();
+                    const ReduceSlot rs = red_.slot(nb(), pap(i));
+                    op_->apply_split(1, p_, Ap_, lm_ ? CtC_ : nullptr, stop, rs, stream_);
+                    halo_begin(comm_, vec_planes(p_), dom_, op_->halo());
+                    halo_join();
+                    op_->apply_split(2, p_, Ap_, lm_ ? CtC_ : nullptr, stop, rs, stream_);
+                    tend();
+                }
+            } else if (mat_) {
                 // cusparseInner + PCGStep1_Finish (:2101-2118): the SpMV replaces PCGStep1;
                 // as in the reference, the LM CtC term is not part of this product
                 mat_apply(p_, Ap_, stop, pap(i));
@@ -543,11 +566,14 @@ private:
         comm_->halo_exchange(planes, dom_, op_->halo(), stream_);
         tend();
     }
-    void exchange_vec(T* v) {
-        if (!distributed()) return;
+    std::vector<HaloPlane> vec_planes(T* v) const {
         std::vector<HaloPlane> pl;
         for (int k = 0; k < L_.nimg; ++k) pl.push_back({(void*)(v + L_.off[k]), sizeof(T) * L_.ch[k] * dom_.W});
-        exchange(pl);
+        return pl;
+    }
+    void exchange_vec(T* v) {
+        if (!distributed()) return;
+        exchange(vec_planes(v));
     }
     void exchange_unknowns() {
         if (!distributed()) return;
@@ -638,6 +664,7 @@ private:
     std::vector<unsigned long long> graph_key_;
     bool capturing_ = false;
     const bool graph_off_ = getenv("OPT_AMD_NO_GRAPH") && atoi(getenv("OPT_AMD_NO_GRAPH"));
+    const bool overlap_ = env_int("OPT_AMD_HALO_OVERLAP", 1) != 0;   // 0: blocking halo before each apply
     std::unique_ptr<MaterializedJacobian<T>> mat_;
     float radius_ = 1e4f, decrease_ = 2.0f;
 };

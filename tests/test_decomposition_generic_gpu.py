@@ -206,3 +206,18 @@ def test_generated_kernels_refuse_slabs_where_reads_are_data_dependent(monkeypat
         with pytest.raises(Exception):
             sv.set_decomposition(lib.OptAMD_LocalGroupRank(group, 0), 0, 8)
     lib.OptAMD_LocalGroupDestroy(group)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sfs_halo_overlap_is_bitwise_the_blocking_exchange(monkeypatch, world):
+    """shape_from_shading slabs: the halo refresh of p runs on a second stream beside
+    the apply's interior blocks (sfs.hip apply_split, stencil_plan.h pcg_loop), the
+    boundary blocks after it; bitwise the blocking exchange before a whole-slab apply."""
+    W, H = 256, 240
+    w = SFS.make(W, H)
+    monkeypatch.setenv("OPT_AMD_HALO_OVERLAP", "0")
+    c0, X0 = run(SFS, w, world, 3, 10)
+    monkeypatch.setenv("OPT_AMD_HALO_OVERLAP", "1")
+    c1, X1 = run(SFS, w, world, 3, 10)
+    assert c1[0] == c0[0]
+    assert np.array_equal(X1, X0)

@@ -111,3 +111,21 @@ def test_rccl_transport_single_rank_is_exact():
     lib.OptAMD_CommDestroy(comm)
     assert got == ref
     assert np.array_equal(to_np(p0[0]), to_np(p1[0])) and np.array_equal(to_np(p0[1]), to_np(p1[1]))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_overlap_is_bitwise_the_blocking_exchange(monkeypatch, world):
+    """The halo refresh of r and p runs on a second stream beside the interior row blocks
+    of the next apply (image_warping.hip: split launches over tile ranges, one reduction
+    slot); the result must be bitwise that of the blocking exchange before a whole-slab
+    apply."""
+    monkeypatch.setenv("OPT_AMD_IW_SPEC", "0")
+    monkeypatch.setenv("OPT_AMD_ROWS", "4")      # 16-row blocks: >= 3 row blocks per slab
+    W, H = 130, 150
+    w = perturbed(W, H, seed=9)
+    monkeypatch.setenv("OPT_AMD_HALO_OVERLAP", "0")
+    c0, O0, A0 = run_decomposed(w, world, 3, 10)
+    monkeypatch.setenv("OPT_AMD_HALO_OVERLAP", "1")
+    c1, O1, A1 = run_decomposed(w, world, 3, 10)
+    assert c1 == c0
+    assert np.array_equal(O1, O0) and np.array_equal(A1, A0)
