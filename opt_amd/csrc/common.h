@@ -47,10 +47,28 @@ struct VecLayout {
     int ch[4];
     long long off[5];
     long long N;       // pixels in memory
-    __host__ __device__ long long pix(long long e) const {
+    // local element index -> pixel: channel counts 1..4 by shifts / a constant divide
+    // (no 64-bit integer division in the flat PCG kernels)
+    __host__ __device__ static long long div_ch(long long l, int c) {
+        switch (c) {
+            case 1: return l;
+            case 2: return l >> 1;
+            case 3: return l < (1LL << 32) ? (long long)((unsigned)l / 3u) : l / 3;
+            case 4: return l >> 2;
+            default: return l / c;
+        }
+    }
+    __host__ __device__ long long locate(long long e, int* img, long long* local) const {
         int k = 0;
         while (k + 1 < nimg && e >= off[k + 1]) ++k;
-        return (e - off[k]) / ch[k];
+        *img = k;
+        *local = e - off[k];
+        return div_ch(*local, ch[k]);
+    }
+    __host__ __device__ long long pix(long long e) const {
+        int k;
+        long long l;
+        return locate(e, &k, &l);
     }
 };
 

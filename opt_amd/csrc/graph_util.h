@@ -5,7 +5,7 @@
 // (problemparams are re-read on every Step, solverGPUGaussNewton.t:2001), so a caller may
 // pass different edges at any Step — possibly at the address of a freed earlier array
 // (allocators reuse addresses). A pointer comparison is therefore not enough: every bind
-// hashes the arrays' contents on the device (one streaming pass, ~10 µs per 6 M edges)
+// hashes the arrays' contents on the device (one streaming pass per array)
 // and the incidence lists are rebuilt when the hash changes.
 #pragma once
 #include <algorithm>
@@ -13,16 +13,29 @@
 
 namespace optamd {
 
-static __global__ void graph_fingerprint_kernel(const int* __restrict__ v, int E, unsigned long long salt,
-                                         unsigned long long* out) {
+__device__ __forceinline__ unsigned fp_mix(unsigned v, unsigned e, unsigned salt) {
+    unsigned x = v ^ (e * 0x9E3779B9u + salt);   // murmur3 fmix32 of (value, position)
+    x ^= x >> 16; x *= 0x85EBCA6Bu;
+    x ^= x >> 13; x *= 0xC2B2AE35u;
+    return x ^ (x >> 16);
+}
+// Position-keyed sum of 32-bit mixes (order-independent, so the block sums can meet in
+// one atomic): 16-byte loads, 32-bit arithmetic only — a streaming pass at HBM rate.
+// VEC = false: an array that is not 16-byte aligned, read as four 4-byte loads.
+template <bool VEC>
+static __global__ void graph_fingerprint_kernel(const int* __restrict__ v, int E, unsigned salt,
+                                                unsigned long long* out) {
     unsigned long long h = 0;
-    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x) {
-        unsigned long long x = ((unsigned long long)(unsigned)e << 32 | (unsigned)v[e]) ^ salt;
-        x += 0x9E3779B97F4A7C15ull;   // splitmix64 finaliser
-        x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-        x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-        h += x ^ (x >> 31);
+    const int n4 = E / 4;
+    const int4* v4 = reinterpret_cast<const int4*>(v);
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += gridDim.x * blockDim.x) {
+        const int4 w = VEC ? v4[q] : int4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+        const unsigned e = 4u * (unsigned)q;
+        h += fp_mix((unsigned)w.x, e, salt) + (unsigned long long)fp_mix((unsigned)w.y, e + 1, salt) +
+             fp_mix((unsigned)w.z, e + 2, salt) + (unsigned long long)fp_mix((unsigned)w.w, e + 3, salt);
     }
+    if (blockIdx.x == 0 && (int)threadIdx.x < E - 4 * n4)   // the tail
+        h += fp_mix((unsigned)v[4 * n4 + threadIdx.x], 4u * n4 + threadIdx.x, salt);
     for (int off = 32; off > 0; off >>= 1) h += __shfl_down(h, off, 64);
     __shared__ unsigned long long part[4];
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = h;
@@ -35,11 +48,15 @@ static __global__ void graph_fingerprint_kernel(const int* __restrict__ v, int E
 inline unsigned long long graph_fingerprint(const int* const* arrays, int n, int E, hipStream_t s,
                                             unsigned long long* d) {
     OPT_HIP_CHECK(hipMemsetAsync(d, 0, sizeof(unsigned long long), s));
-    const int grid = std::max(1, std::min((E + 255) / 256, 1024));   // one atomic per block
+    const int grid = std::max(1, std::min((E / 4 + 255) / 256, 4096));   // one atomic per block
     for (int k = 0; k < n; ++k)
-        if (E > 0)
-            hipLaunchKernelGGL(graph_fingerprint_kernel, dim3(grid), dim3(256), 0, s, arrays[k], E,
-                               0x5851F42D4C957F2Dull * (unsigned long long)(k + 1), d);
+        if (E > 0) {
+            const unsigned salt = 0x4C957F2Du * (unsigned)(k + 1);
+            if ((reinterpret_cast<uintptr_t>(arrays[k]) & 15) == 0)
+                hipLaunchKernelGGL(graph_fingerprint_kernel<true>, dim3(grid), dim3(256), 0, s, arrays[k], E, salt, d);
+            else
+                hipLaunchKernelGGL(graph_fingerprint_kernel<false>, dim3(grid), dim3(256), 0, s, arrays[k], E, salt, d);
+        }
     unsigned long long h = 0;
     OPT_HIP_CHECK(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, s));
     OPT_HIP_CHECK(hipStreamSynchronize(s));

@@ -430,10 +430,11 @@ __global__ __launch_bounds__(kBlock) void sfs_tiles(Args<T> a, const T* __restri
 constexpr int kStripOut = 60;
 template <typename T>
 struct SRow {   // raw loads of row r (+ flags / LM diagonal of the output row r-2)
-    T p, g0, g1, g2, dg;
+    T p, g0, g1, g2, dg, bi;
     int mr, mc, v, f;
 };
-template <typename T>
+// JTF: p is X, bi = B_I(r), dg = D_i and f = [D_i > 0] of the output row r-2.
+template <typename T, bool JTF = false>
 __device__ __forceinline__ SRow<T> strip_row(const Args<T>& a, const T* __restrict__ p, const T* __restrict__ dadd,
                                              int gx, int r) {
     const Domain& d = a.dom;
@@ -444,6 +445,7 @@ __device__ __forceinline__ SRow<T> strip_row(const Args<T>& a, const T* __restri
     s.g0 = in ? a.G00[o] : (T)0;
     s.g1 = in ? a.Gm0[o] : (T)0;
     s.g2 = in ? a.G0m[o] : (T)0;
+    s.bi = (JTF && in) ? a.BI[o] : (T)0;
     const bool ib = inbe(d, gx, r);
     s.mr = ib ? a.mR[o] : 0;
     s.mc = ib ? a.mC[o] : 0;
@@ -451,11 +453,19 @@ __device__ __forceinline__ SRow<T> strip_row(const Args<T>& a, const T* __restri
     const int rk = r - 2;
     const bool own = gx >= 0 && gx < d.W && rk >= d.y_lo && rk < d.y_hi;
     const long long ok = own ? d.off(gx, rk) : 0;
-    s.f = own ? a.flags[ok] : 0;
-    s.dg = (own && dadd) ? dadd[ok] : (T)0;
+    if (JTF) {
+        s.dg = own ? (T)a.D[ok] : (T)0;
+        s.f = own && a.D[ok] > 0.f;
+    } else {
+        s.f = own ? a.flags[ok] : 0;
+        s.dg = (own && dadd) ? dadd[ok] : (T)0;
+    }
     return s;
 }
-template <typename T>
+// JTF = true: r = -J^T F, diag(J^T J) and the flag byte (evalJTF, o.t:2870-2913) by the
+// same chain with D replaced by B_I, p by X and the fit term by w_p (X - D_i), as
+// sfs_tiles<T, true> does (same operations in the same order); Ap is r, dadd is diag.
+template <typename T, bool JTF = false>
 __global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
                                                     const T* __restrict__ dadd, const int* stop, ReduceSlot rs,
                                                     int nstrips, int rows, int bb0 = 0, int bn0 = 1 << 30,
@@ -479,13 +489,15 @@ __global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restri
         T g0_m2 = 0, g1_m2 = 0, g0_m1 = 0, g1_m1 = 0, g2_m1 = 0, qy_m1 = 0, qy_m2 = 0;
         T us_k[3] = {0, 0, 0}, us_km1[3] = {0, 0, 0};
         int mc_m1 = 0, v_m1 = 0;
-        SRow<T> nx = strip_row(a, p, dadd, gx, y0 - 2);
+        // JTF's diagonal: masks / valid of rows k-1 (m3), k (m2), k+1 (m1)
+        int mr_m2 = 0, mc_m2 = 0, mc_m3 = 0, v_m2 = 0, v_m3 = 0, mr_m1 = 0;
+        SRow<T> nx = strip_row<T, JTF>(a, p, dadd, gx, y0 - 2);
         for (int r = y0 - 2; r <= y1 + 1; ++r) {
             const SRow<T> cur = nx;
-            if (r + 1 <= y1 + 1) nx = strip_row(a, p, dadd, gx, r + 1);
+            if (r + 1 <= y1 + 1) nx = strip_row<T, JTF>(a, p, dadd, gx, r + 1);
             const T qy = ((T)r - a.uy) / a.fy;
-            // row r: D, V_h
-            const T D = cur.g0 * cur.p + cur.g1 * from_left(cur.p, (T)0) + cur.g2 * p_m1;
+            // row r: D (J^T F: the shading residual values B_I), V_h
+            const T D = JTF ? cur.bi : cur.g0 * cur.p + cur.g1 * from_left(cur.p, (T)0) + cur.g2 * p_m1;
             const T mh = (T)cur.mr;
             const T Vh = wg * mh * (wg * mh * (D - from_right(D, (T)0)));
             // row r-1: V_v, W, u_s
@@ -516,17 +528,43 @@ __global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restri
 #pragma unroll
             for (int c = 0; c < 3; ++c)
                 l[c] = (T)4 * us_k[c] - (from_left(us_k[c], (T)0) + us_km1[c] + from_right(us_k[c], (T)0) + us[c]);
+            // J^T F's diagonal operands of row k: masks of rows k-1..k+1 and their lane
+            // neighbours (evaluated by every lane: the DPP shifts need the whole wave)
+            T dgk = 0;
+            if constexpr (JTF) {
+                auto sq = [](T v) { return v * v; };
+                const T Gm0r = from_right(g1_m2, (T)0);   // Gm0(k + x)
+                const T mh0 = wg * (T)mr_m2, mv0 = wg * (T)mc_m2;
+                dgk = a.wp * a.wp;
+                dgk += sq(mh0 * (g0_m2 - Gm0r)) + sq(wg * (T)from_right_i(mr_m2, 0) * Gm0r) +
+                       sq(wg * (T)mr_m1 * g2_m1) + sq(wg * (T)from_left_i(mr_m2, 0) * g0_m2) +
+                       sq(wg * (T)from_left_i(mr_m1, 0) * g2_m1);
+                dgk += sq(mv0 * (g0_m2 - g2_m1)) + sq(wg * (T)from_right_i(mc_m2, 0) * Gm0r) +
+                       sq(wg * (T)mc_m1 * g2_m1) + sq(wg * (T)mc_m3 * g0_m2) +
+                       sq(wg * (T)from_right_i(mc_m3, 0) * Gm0r);
+                const T nv = (T)16 * (T)(v_m2 == 1) + (T)(from_left_i(v_m2, 0) == 1) + (T)(v_m3 == 1) +
+                             (T)(from_right_i(v_m2, 0) == 1) + (T)(v_m1 == 1);
+                dgk += ws * ws * (qxc * qxc + qy_m2 * qy_m2 + (T)1) * nv;
+            }
             if (k >= y0 && out_lane) {
                 const long long i = d.off(gx, k);
                 T acc = 0;
                 if (cur.f & 1) {
                     const T pk = p_m2;
-                    const T fit = a.wp * (a.wp * pk);
+                    const T fit = JTF ? a.wp * (a.wp * (pk - cur.dg)) : a.wp * (a.wp * pk);
                     acc = fit + shade + ws * (qxc * l[0] + qy_m2 * l[1] + l[2]);
-                    if (dadd) acc += cur.dg * pk;
-                    dot += pk * acc;
+                    if (!JTF) {
+                        if (dadd) acc += cur.dg * pk;
+                        dot += pk * acc;
+                    }
                 }
-                Ap[i] = acc;
+                if constexpr (JTF) {
+                    Ap[i] = -acc;   // r
+                    ((T*)dadd)[i] = (cur.f & 1) ? dgk : (T)0;
+                    a.flags[i] = (uint8_t)(cur.f & 1);
+                } else {
+                    Ap[i] = acc;
+                }
             }
             // roll the window
             p_m2 = p_m1; p_m1 = cur.p;
@@ -535,9 +573,11 @@ __global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restri
             qy_m2 = qy_m1; qy_m1 = qy;
 #pragma unroll
             for (int c = 0; c < 3; ++c) { us_km1[c] = us_k[c]; us_k[c] = us[c]; }
-            mc_m1 = cur.mc; v_m1 = cur.v;
+            mc_m3 = mc_m2; mc_m2 = mc_m1; v_m3 = v_m2; v_m2 = v_m1; mr_m2 = mr_m1;
+            mc_m1 = cur.mc; v_m1 = cur.v; mr_m1 = cur.mr;
         }
     }
+    if (JTF) return;
     double v[1] = {(double)dot};
     block_reduce_publish<1>(v, rs, gb);
 }
@@ -823,8 +863,16 @@ public:
     }
     void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {
         a_.flags = flags;
-        hipLaunchKernelGGL((sfs::sfs_tiles<T, true>), tile_grid(), dim3(kBlock), 0, s, a_, (const T*)a_.X, r, diag,
-                           (const T*)nullptr, (const int*)nullptr, ReduceSlot{});
+        if (jtf_strip_) {   // register strips (the apply's chain on B_I and X)
+            const int nstrips = (dom_.W + sfs::kStripOut - 1) / sfs::kStripOut;
+            const int nrb = (dom_.y_hi - dom_.y_lo + strip_rows_ - 1) / strip_rows_;
+            const int blocks = (nstrips * nrb + kBlock / kWave - 1) / (kBlock / kWave);
+            hipLaunchKernelGGL((sfs::sfs_strip<T, true>), dim3(blocks), dim3(kBlock), 0, s, a_, (const T*)a_.X, r,
+                               (const T*)diag, (const int*)nullptr, ReduceSlot{}, nstrips, strip_rows_, 0, 1 << 30, 0);
+        } else {
+            hipLaunchKernelGGL((sfs::sfs_tiles<T, true>), tile_grid(), dim3(kBlock), 0, s, a_, (const T*)a_.X, r, diag,
+                               (const T*)nullptr, (const int*)nullptr, ReduceSlot{});
+        }
         OPT_HIP_CHECK(hipGetLastError());
     }
     void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
@@ -904,6 +952,7 @@ private:
     int strip_rows_ = env_int("OPT_AMD_SFS_ROWS", 16);
     int cost_rows_ = env_int("OPT_AMD_SFS_COST_ROWS", 32);
     bool cost_strip_ = env_int("OPT_AMD_SFS_COST_STRIP", 1) != 0;   // 0: the per-pixel sfs_cost
+    bool jtf_strip_ = env_int("OPT_AMD_SFS_JTF_STRIP", 1) != 0;     // 0: the LDS-tile J^T F
     T *BI_ = nullptr, *G00_ = nullptr, *Gm0_ = nullptr, *G0m_ = nullptr;
     uint8_t* valid_ = nullptr;
     T* userX_ = nullptr;

@@ -29,10 +29,9 @@ __global__ __launch_bounds__(kBlock) void update_images_kernel(VecLayout L, cons
     const long long n = L.off[L.nimg];
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
-        int k = 0;
-        while (k + 1 < L.nimg && e >= L.off[k + 1]) ++k;
-        const long long local = e - L.off[k];
-        const long long px = local / L.ch[k];
+        int k;
+        long long local;
+        const long long px = L.locate(e, &k, &local);
         if (px < pix_lo || px >= pix_hi || !(flags[px] & 1)) continue;
         T* x = X.x[k];
         const T v = x[local];
@@ -47,10 +46,9 @@ __global__ __launch_bounds__(kBlock) void revert_images_kernel(VecLayout L, cons
     const long long n = L.off[L.nimg];
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
-        int k = 0;
-        while (k + 1 < L.nimg && e >= L.off[k + 1]) ++k;
-        const long long local = e - L.off[k];
-        const long long px = local / L.ch[k];
+        int k;
+        long long local;
+        const long long px = L.locate(e, &k, &local);
         if (px < pix_lo || px >= pix_hi || !(flags[px] & 1)) continue;
         X.x[k][local] = prev[e];
     }

@@ -248,3 +248,36 @@ def test_cost_strip_equals_per_pixel_cost(monkeypatch, W, H):
     assert out["1"][0] == pytest.approx(out["0"][0], rel=1e-6)
     assert out["1"][0] == pytest.approx(oracle.sfs_cost(w), rel=2e-5)
     np.testing.assert_allclose(out["1"][1], out["0"][1], rtol=1e-5)
+
+
+@pytest.mark.parametrize("W,H", [(97, 61), (130, 9), (300, 257)])
+@pytest.mark.parametrize("double", [False, True])
+def test_jtf_strip_equals_tile_jtf(monkeypatch, W, H, double):
+    """J^T F + diag(J^T J) + flags by the register strip (sfs_strip<T, true>) against the
+    LDS-tile kernel (sfs_tiles<T, true>): the same expressions in the same order; the two
+    kernels may contract different multiply-adds into FMAs, so r and the preconditioner
+    agree to a few ulps, and whole LM trajectories to the fp32 noise floor."""
+    import torch
+
+    w = synthetic(W, H, seed=W + 7)
+    out = {}
+    for strip in ("1", "0"):
+        monkeypatch.setenv("OPT_AMD_SFS_JTF_STRIP", strip)
+        s = OptSolver([W, H], ENERGY, "LMGPU", double_precision=double)
+        mk = params64 if double else params
+        prm = mk(w)
+        n = s.unknown_count()
+        dt = torch.float64 if double else torch.float32
+        r = torch.zeros(n, dtype=dt, device="cuda")
+        pre = torch.zeros_like(r)
+        s.eval_jtf(prm, r, pre)
+        s.set_solver_params({"nIterations": 4, "lIterations": 10})
+        out[strip] = (to_np(r), to_np(pre), s.profiled_solve(mk(w)))
+        s.close()
+    tol = 1e-13 if double else 2e-6
+    assert rel_err(out["1"][0], out["0"][0]) < tol
+    assert rel_err(out["1"][1], out["0"][1]) < tol
+    np.testing.assert_array_equal(out["1"][1] == 0, out["0"][1] == 0)   # flags (pre = 0 off them)
+    # fp32: ulp-level J^T F differences grow along an LM trajectory like any 1-ulp input
+    # change (test_fp32_trajectory_within_the_fp32_noise_floor measures that floor)
+    np.testing.assert_allclose(out["1"][2], out["0"][2], rtol=1e-12 if double else 5e-5)
