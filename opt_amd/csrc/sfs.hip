@@ -74,6 +74,45 @@ template <typename T>
 __device__ __forceinline__ bool DV(const Args<T>& a, int x, int y) { return get(a.D, a.dom, x, y) > 0.f; }
 
 // ---------------------------------------------------------------- precompute
+// B_I and its three gradient images at (x, y) from X(0,0) = d, X(-1,0) = A, X(0,-1) = B
+// and Im at (0,0), (-1,0), (0,-1) (shape_from_shading.t:26-52; o.t:1686-1716).
+template <typename T>
+__device__ __forceinline__ void shade_px(const Args<T>& a, int x, int y, T d, T A, T B, float Im0, float Iml,
+                                         float Imu, T* bi, T* g0, T* g1, T* g2) {
+    const T fx = a.fx, fy = a.fy, ux = a.ux, uy = a.uy;
+    const T i = (T)x, j = (T)y;
+    const T nx = B * (d - A) / fy;
+    const T ny = A * (d - B) / fx;
+    const T nz = (nx * (ux - i) / fx) + (ny * (uy - j) / fy) - (A * B / (fx * fy));
+    const T sq = nx * nx + ny * ny + nz * nz;
+    const T inv = sq > (T)0 ? (T)1 / sqrt(sq) : (T)1;
+    const T Nx = inv * nx, Ny = inv * ny, Nz = inv * nz;
+    const T* L = a.L;
+    const T Bv = L[0] + L[1] * Ny + L[2] * Nz + L[3] * Nx + L[4] * Nx * Ny + L[5] * Ny * Nz +
+                 L[6] * (-Nx * Nx - Ny * Ny + (T)2 * Nz * Nz) + L[7] * Nz * Nx + L[8] * (Nx * Nx - Ny * Ny);
+    const T I = (T)Im0 * (T)0.5 + (T)0.25 * ((T)Iml + (T)Imu);
+    *bi = Bv - I;
+    const T dBx = L[3] + L[4] * Ny + L[7] * Nz + (T)2 * Nx * (L[8] - L[6]);
+    const T dBy = L[1] + L[4] * Nx + L[5] * Nz - (T)2 * Ny * (L[6] + L[8]);
+    const T dBz = L[2] + L[5] * Ny + (T)4 * L[6] * Nz + L[7] * Nx;
+    // partials of the normal (divisions by the constants done once as reciprocals:
+    // these feed the gradient images only, never the energy value)
+    const T rfx = (T)1 / fx, rfy = (T)1 / fy, rfxy = (T)1 / (fx * fy);
+    const T cx_ = (ux - i) * rfx, cy_ = (uy - j) * rfy;
+    const T dnx[3] = {B * rfy, -B * rfy, (d - A) * rfy};
+    const T dny[3] = {A * rfx, (d - B) * rfx, -A * rfx};
+    const T dab[3] = {(T)0, B, A};
+    T gv[3];
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+        const T dnz = dnx[v] * cx_ + dny[v] * cy_ - dab[v] * rfxy;
+        const T dinv = sq > (T)0 ? -(inv * inv * inv) * (nx * dnx[v] + ny * dny[v] + nz * dnz) : (T)0;
+        const T dNx = dinv * nx + inv * dnx[v], dNy = dinv * ny + inv * dny[v], dNz = dinv * nz + inv * dnz;
+        gv[v] = dBx * dNx + dBy * dNy + dBz * dNz;
+    }
+    *g0 = gv[0]; *g1 = gv[1]; *g2 = gv[2];
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void sfs_precompute(Args<T> a) {
     const PixGeom g = pix(a.dom);
@@ -84,41 +123,9 @@ __global__ __launch_bounds__(kBlock) void sfs_precompute(Args<T> a) {
     const bool ib = inbe(a.dom, x, y);
     const float* D = a.D;
     T bi = 0, g0 = 0, g1 = 0, g2 = 0;
-    if (ib && D[i0 - 1] > 0.f && D[i0] > 0.f && D[i0 - W] > 0.f) {
-        const T d = a.X[i0], A = a.X[i0 - 1], B = a.X[i0 - W];
-        const T fx = a.fx, fy = a.fy, ux = a.ux, uy = a.uy;
-        const T i = (T)x, j = (T)y;
-        const T nx = B * (d - A) / fy;
-        const T ny = A * (d - B) / fx;
-        const T nz = (nx * (ux - i) / fx) + (ny * (uy - j) / fy) - (A * B / (fx * fy));
-        const T sq = nx * nx + ny * ny + nz * nz;
-        const T inv = sq > (T)0 ? (T)1 / sqrt(sq) : (T)1;
-        const T Nx = inv * nx, Ny = inv * ny, Nz = inv * nz;
-        const T* L = a.L;
-        const T Bv = L[0] + L[1] * Ny + L[2] * Nz + L[3] * Nx + L[4] * Nx * Ny + L[5] * Ny * Nz +
-                     L[6] * (-Nx * Nx - Ny * Ny + (T)2 * Nz * Nz) + L[7] * Nz * Nx + L[8] * (Nx * Nx - Ny * Ny);
-        const T I = (T)a.Im[i0] * (T)0.5 + (T)0.25 * ((T)a.Im[i0 - 1] + (T)a.Im[i0 - W]);
-        bi = Bv - I;
-        const T dBx = L[3] + L[4] * Ny + L[7] * Nz + (T)2 * Nx * (L[8] - L[6]);
-        const T dBy = L[1] + L[4] * Nx + L[5] * Nz - (T)2 * Ny * (L[6] + L[8]);
-        const T dBz = L[2] + L[5] * Ny + (T)4 * L[6] * Nz + L[7] * Nx;
-        // partials of the normal (divisions by the constants done once as reciprocals:
-        // these feed the gradient images only, never the energy value)
-        const T rfx = (T)1 / fx, rfy = (T)1 / fy, rfxy = (T)1 / (fx * fy);
-        const T cx_ = (ux - i) * rfx, cy_ = (uy - j) * rfy;
-        const T dnx[3] = {B * rfy, -B * rfy, (d - A) * rfy};
-        const T dny[3] = {A * rfx, (d - B) * rfx, -A * rfx};
-        const T dab[3] = {(T)0, B, A};
-        T gv[3];
-#pragma unroll
-        for (int v = 0; v < 3; ++v) {
-            const T dnz = dnx[v] * cx_ + dny[v] * cy_ - dab[v] * rfxy;
-            const T dinv = sq > (T)0 ? -(inv * inv * inv) * (nx * dnx[v] + ny * dny[v] + nz * dnz) : (T)0;
-            const T dNx = dinv * nx + inv * dnx[v], dNy = dinv * ny + inv * dny[v], dNz = dinv * nz + inv * dnz;
-            gv[v] = dBx * dNx + dBy * dNy + dBz * dNz;
-        }
-        g0 = gv[0]; g1 = gv[1]; g2 = gv[2];
-    }
+    if (ib && D[i0 - 1] > 0.f && D[i0] > 0.f && D[i0 - W] > 0.f)
+        shade_px(a, x, y, a.X[i0], a.X[i0 - 1], a.X[i0 - W], a.Im[i0], a.Im[i0 - 1], a.Im[i0 - W], &bi, &g0, &g1,
+                 &g2);
     a.BI[g.i] = bi; a.G00[g.i] = g0; a.Gm0[g.i] = g1; a.G0m[g.i] = g2;
     bool v = ib && D[i0] > 0.f && D[i0 - W] > 0.f && D[i0 + W] > 0.f && D[i0 - 1] > 0.f && D[i0 + 1] > 0.f;
     if (v) {
@@ -127,6 +134,47 @@ __global__ __launch_bounds__(kBlock) void sfs_precompute(Args<T> a) {
             fabs(xc - a.X[i0 - 1]) < (T)0.01 && fabs(xc - a.X[i0 + 1]) < (T)0.01;
     }
     a.valid[g.i] = v;
+}
+
+// The same per-pixel values from register strips: a wave owns 62 output columns (lanes
+// 1..62 of a 64-column window; lane 0 / 63 only feed their neighbours through DPP) and
+// walks `rows` rows with X and D of rows y-1, y, y+1 and Im of rows y-1, y in
+// registers: three loads per pixel instead of thirteen.
+constexpr int kPreOut = 62;
+template <typename T>
+__global__ __launch_bounds__(kBlock) void sfs_precompute_strip(Args<T> a, int nstrips, int rows) {
+    const Domain& d = a.dom;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    const int strip = wave % nstrips, rb = wave / nstrips;
+    const int x = strip * kPreOut - 1 + lane;
+    const int y0 = d.y_lo + rb * rows, y1 = min(y0 + rows, d.y_hi);
+    if (y0 >= y1) return;
+    const bool out_lane = lane >= 1 && lane <= kPreOut && x < d.W;
+    auto ldX = [&](int y) { return inside(d, x, y) ? a.X[d.off(x, y)] : (T)0; };
+    auto ldD = [&](int y) { return inside(d, x, y) ? a.D[d.off(x, y)] : 0.f; };
+    auto ldI = [&](int y) { return inside(d, x, y) ? a.Im[d.off(x, y)] : 0.f; };
+    T Xu = ldX(y0 - 1), Xc = ldX(y0);
+    float Du = ldD(y0 - 1), Dc = ldD(y0), Iu = ldI(y0 - 1), Ic = ldI(y0);
+    for (int y = y0; y < y1; ++y) {
+        const T Xd = ldX(y + 1);
+        const float Dd = ldD(y + 1), Id = ldI(y + 1);
+        const T Xl = from_left(Xc, (T)0), Xr = from_right(Xc, (T)0);
+        const float Dl = from_left(Dc, 0.f), Dr = from_right(Dc, 0.f), Il = from_left(Ic, 0.f);
+        if (out_lane) {
+            const bool ib = inbe(d, x, y);
+            T bi = 0, g0 = 0, g1 = 0, g2 = 0;
+            if (ib && Dl > 0.f && Dc > 0.f && Du > 0.f) shade_px(a, x, y, Xc, Xl, Xu, Ic, Il, Iu, &bi, &g0, &g1, &g2);
+            const long long i = d.off(x, y);
+            a.BI[i] = bi; a.G00[i] = g0; a.Gm0[i] = g1; a.G0m[i] = g2;
+            bool v = ib && Dc > 0.f && Du > 0.f && Dd > 0.f && Dl > 0.f && Dr > 0.f;
+            if (v)
+                v = fabs(Xc - Xu) < (T)0.01 && fabs(Xc - Xd) < (T)0.01 && fabs(Xc - Xl) < (T)0.01 &&
+                    fabs(Xc - Xr) < (T)0.01;
+            a.valid[i] = v;
+        }
+        Xu = Xc; Xc = Xd; Du = Dc; Dc = Dd; Iu = Ic; Ic = Id;
+    }
 }
 
 // ------------------------------------------------------- residual instances
@@ -854,7 +902,15 @@ public:
     }
     T* unknown(int k) { return k == 0 ? a_.X : nullptr; }
     void precompute(hipStream_t s) {
-        hipLaunchKernelGGL((sfs::sfs_precompute<T>), grid(), dim3(kBlock), 0, s, a_);
+        if (pre_strip_) {
+            const int nstrips = (dom_.W + sfs::kPreOut - 1) / sfs::kPreOut;
+            const int rows = pre_rows_;
+            const int nrb = (dom_.y_hi - dom_.y_lo + rows - 1) / rows;
+            const int blocks = (nstrips * nrb + kBlock / kWave - 1) / (kBlock / kWave);
+            hipLaunchKernelGGL((sfs::sfs_precompute_strip<T>), dim3(blocks), dim3(kBlock), 0, s, a_, nstrips, rows);
+        } else {
+            hipLaunchKernelGGL((sfs::sfs_precompute<T>), grid(), dim3(kBlock), 0, s, a_);
+        }
         OPT_HIP_CHECK(hipGetLastError());
     }
     void computed_planes(std::vector<HaloPlane>& v) const {
@@ -953,6 +1009,8 @@ private:
     int cost_rows_ = env_int("OPT_AMD_SFS_COST_ROWS", 32);
     bool cost_strip_ = env_int("OPT_AMD_SFS_COST_STRIP", 1) != 0;   // 0: the per-pixel sfs_cost
     bool jtf_strip_ = env_int("OPT_AMD_SFS_JTF_STRIP", 1) != 0;     // 0: the LDS-tile J^T F
+    bool pre_strip_ = env_int("OPT_AMD_SFS_PRE_STRIP", 1) != 0;     // 0: the per-pixel precompute
+    int pre_rows_ = std::max(1, env_int("OPT_AMD_SFS_PRE_ROWS", 32));
     T *BI_ = nullptr, *G00_ = nullptr, *Gm0_ = nullptr, *G0m_ = nullptr;
     uint8_t* valid_ = nullptr;
     T* userX_ = nullptr;

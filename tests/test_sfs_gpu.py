@@ -281,3 +281,23 @@ def test_jtf_strip_equals_tile_jtf(monkeypatch, W, H, double):
     # fp32: ulp-level J^T F differences grow along an LM trajectory like any 1-ulp input
     # change (test_fp32_trajectory_within_the_fp32_noise_floor measures that floor)
     np.testing.assert_allclose(out["1"][2], out["0"][2], rtol=1e-12 if double else 5e-5)
+
+
+@pytest.mark.parametrize("W,H", [(97, 61), (130, 9), (300, 257)])
+@pytest.mark.parametrize("double", [False, True])
+def test_precompute_strip_equals_per_pixel(monkeypatch, W, H, double):
+    """sfs_precompute_strip (register strips, DPP neighbours) against the per-pixel
+    sfs_precompute: B_I, its gradient images and valid feed every later kernel, so the
+    cost after init and whole LM trajectories agree."""
+    w = synthetic(W, H, seed=W + 11)
+    mk = params64 if double else params
+    out = {}
+    for strip in ("1", "0"):
+        monkeypatch.setenv("OPT_AMD_SFS_PRE_STRIP", strip)
+        s = OptSolver([W, H], ENERGY, "LMGPU", double_precision=double)
+        c0 = s.eval_cost(mk(w))
+        s.set_solver_params({"nIterations": 4, "lIterations": 10})
+        out[strip] = (c0, s.profiled_solve(mk(w)))
+        s.close()
+    assert out["1"][0] == pytest.approx(out["0"][0], rel=1e-12 if double else 1e-6)
+    np.testing.assert_allclose(out["1"][1], out["0"][1], rtol=1e-12 if double else 5e-5)
