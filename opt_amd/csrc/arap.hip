@@ -172,16 +172,37 @@ __global__ __launch_bounds__(kBlock) void arap_jtf(Args<T> a, T* __restrict__ r,
 // stored structure-of-arrays),
 // so the in-edge terms of the gather read a neighbour's K instead of rebuilding its
 // rotation derivatives (three sincos and ~80 FMA per in-edge).
-template <typename T>
-__global__ __launch_bounds__(kBlock) void arap_kdir(Args<T> a, const T* __restrict__ p, T* __restrict__ Kout,
-                                                    const int* stop) {
+// STEP3: PCGStep3 of the generic driver folded in (stencil_plan.h HasFusedStep3): the
+// vertex's six p entries become z + beta p first (step3_kernel's expression), then K is
+// formed from the new angle part.
+template <typename T, bool STEP3 = false>
+__global__ __launch_bounds__(kBlock) void arap_kdir(Args<T> a, const T* __restrict__ pin, T* __restrict__ Kout,
+                                                    const int* stop, const T* __restrict__ pre = nullptr,
+                                                    const T* __restrict__ r = nullptr, const double* sc = nullptr,
+                                                    int i_num = 0, int i_den = 0, int use_pre = 0) {
     if (stop && *stop) return;
     const int v = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;   // contiguous vertex ranges per XCD
     if (v >= a.N) return;
     const long long N = a.N;
+    T* p = const_cast<T*>(pin);
+    V3<T> pA;
+    if constexpr (STEP3) {
+        const T beta = (T)(sc[i_num] / sc[i_den]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const long long e = 3 * N * h + 3 * v + c;
+                const T z = use_pre ? pre[e] * r[e] : r[e];
+                p[e] = z + beta * p[e];
+                if (h == 1) (c == 0 ? pA.x : c == 1 ? pA.y : pA.z) = p[e];
+            }
+    } else {
+        pA = ld3<T>(p + 3 * N, v);
+    }
     T R[9], dR[3][9], K[9];
     rotation(ld3<T>(a.A, v), R, dR);
-    directional(dR, ld3<T>(p + 3 * N, v), K);
+    directional(dR, pA, K);
 #pragma unroll
     for (int i = 0; i < 9; ++i) Kout[i * N + v] = K[i];   // SoA: a wave's gathers of K_u hit 2 lines per entry
 }
@@ -546,7 +567,18 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
     void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
-        hipLaunchKernelGGL((arap::arap_kdir<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, K_, stop);
+        hipLaunchKernelGGL((arap::arap_kdir<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, K_, stop,
+                           (const T*)nullptr, (const T*)nullptr, (const double*)nullptr, 0, 0, 0);
+        apply_prepared(p, Ap, dadd, stop, rs, s);
+    }
+    // PCGStep3 + the apply's K pass in one kernel; the next apply is apply_prepared
+    void step3_fused(const T* pre, const T* r, T* p, const double* sc, int i_num, int i_den, int use_pre,
+                     const int* stop, hipStream_t s) {
+        hipLaunchKernelGGL((arap::arap_kdir<T, true>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, (const T*)p,
+                           K_, stop, pre, r, sc, i_num, i_den, use_pre);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    void apply_prepared(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
         hipLaunchKernelGGL((arap::arap_apply<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap,
                            (const T*)K_, dadd, stop, rs);
         OPT_HIP_CHECK(hipGetLastError());

@@ -97,6 +97,17 @@ struct HasApplySplit : std::false_type {};
 template <class Op>
 struct HasApplySplit<Op, std::void_t<decltype(std::declval<const Op&>().can_split())>> : std::true_type {};
 
+// Ops that fold PCGStep3 into the first pass of their next apply (ARAP: p = z + beta p
+// per vertex, then K of the new p): step3_fused(pre, r, p, sc, i_num, i_den, use_pre,
+// stop, s) replaces step3_kernel; apply_prepared(...apply's arguments) is the apply
+// without that first pass.
+template <class Op, class = void>
+struct HasFusedStep3 : std::false_type {};
+template <class Op>
+struct HasFusedStep3<Op, std::void_t<decltype(std::declval<Op&>().step3_fused(
+                             (const typename Op::T*)nullptr, (const typename Op::T*)nullptr, (typename Op::T*)nullptr,
+                             (const double*)nullptr, 0, 0, 0, (const int*)nullptr, hipStream_t{}))>> : std::true_type {};
+
 template <class Op, class = void>
 struct HasSlabRefusal : std::false_type {};
 template <class Op>
@@ -233,6 +244,7 @@ public:
 
     // PCG inner loop (PCGStep1-3, :607-845) of one step; launches only, no host sync.
     void pcg_loop(int Lit, int use_pre, const int* stop) {
+        const bool fuse3 = !distributed() && !mat_ && fuse3_on_;
         for (int i = 0; i < Lit; ++i) {
             // the zeta test rides in the kernel that reduces q (one GPU), else its own launch
             const ZetaArgs z{red_.scalars + kScQ0, stop_, i, sp_.q_tolerance, (lm_ && !distributed()) ? 1 : 0};
@@ -258,7 +270,13 @@ public:
                 mat_apply(p_, Ap_, stop, pap(i));
             } else {
                 tbegin(Op::kApplyName);
-                op_->apply(p_, Ap_, lm_ ? CtC_ : nullptr, stop, red_.slot(nb(), pap(i)), stream_);
+                bool done = false;
+                if constexpr (HasFusedStep3<Op>::value)
+                    if (i > 0 && fuse3) {   // step3 of i-1 already ran the apply's first pass
+                        op_->apply_prepared(p_, Ap_, lm_ ? CtC_ : nullptr, stop, red_.slot(nb(), pap(i)), stream_);
+                        done = true;
+                    }
+                if (!done) op_->apply(p_, Ap_, lm_ ? CtC_ : nullptr, stop, red_.slot(nb(), pap(i)), stream_);
                 tend();
             }
             allreduce(pap(i), 1);
@@ -278,8 +296,15 @@ public:
             }
             allreduce(rz(i + 1), lm_ ? 2 : 1);   // rz and q sit side by side
             tbegin("step3");
-            hipLaunchKernelGGL((step3_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)pre_,
-                               (const T*)r_, p_, red_.scalars, rz(i + 1), rz(i), use_pre, stop);
+            bool fused = false;
+            if constexpr (HasFusedStep3<Op>::value)
+                if (fuse3) {
+                    op_->step3_fused(pre_, r_, p_, red_.scalars, rz(i + 1), rz(i), use_pre, stop, stream_);
+                    fused = true;
+                }
+            if (!fused)
+                hipLaunchKernelGGL((step3_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)pre_,
+                                   (const T*)r_, p_, red_.scalars, rz(i + 1), rz(i), use_pre, stop);
             tend();
             if (lm_ && !z.on)
                 hipLaunchKernelGGL((zeta_kernel<T>), dim3(1), dim3(1), 0, stream_, red_.scalars, q(i + 1),
@@ -663,6 +688,7 @@ private:
     bool capturing_ = false;
     const bool graph_off_ = getenv("OPT_AMD_NO_GRAPH") && atoi(getenv("OPT_AMD_NO_GRAPH"));
     const bool overlap_ = env_int("OPT_AMD_HALO_OVERLAP", 1) != 0;   // 0: blocking halo before each apply
+    const bool fuse3_on_ = env_int("OPT_AMD_FUSE_STEP3", 1) != 0;    // 0: step3_kernel + the whole apply
     std::unique_ptr<MaterializedJacobian<T>> mat_;
     float radius_ = 1e4f, decrease_ = 2.0f;
 };

@@ -227,3 +227,22 @@ def test_apply_on_irregular_graphs(double):
     s.eval_jtf(prm, r, pre)
     r_ref, _ = oracle.arap_jtf(w, double=double)
     assert rel_err(to_np(r), r_ref) < (1e-10 if double else 5e-5)
+
+
+@pytest.mark.parametrize("kind", ["gaussNewtonGPU", "LMGPU"])
+@pytest.mark.parametrize("double", [False, True])
+def test_fused_step3_is_bitwise_the_separate_passes(monkeypatch, kind, double):
+    """PCGStep3 folded into the K pass of the next apply (arap_kdir<T, true>, the generic
+    driver's HasFusedStep3 hook): the same expressions per element, so whole solves
+    are bitwise those of step3_kernel + the whole apply."""
+    w = perturbed(23, 17, seed=4)
+    out = {}
+    for f in ("1", "0"):
+        monkeypatch.setenv("OPT_AMD_FUSE_STEP3", f)
+        s = solver(w, kind, double_precision=double)
+        prm = params(w, double=double)
+        s.set_solver_params({"nIterations": 4, "lIterations": 10})
+        out[f] = (s.profiled_solve(prm), to_np(prm[2]), to_np(prm[3]))
+        s.close()
+    assert out["1"][0] == out["0"][0]
+    assert np.array_equal(out["1"][1], out["0"][1]) and np.array_equal(out["1"][2], out["0"][2])
