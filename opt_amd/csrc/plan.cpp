@@ -113,8 +113,14 @@ void ReduceScratch::ensure(int mb, int kmax, int ns) {
         OPT_HIP_CHECK(hipMemset(ticket, 0, sizeof(unsigned) * kTicketWords));
     }
     if (ns > n_scalars) {
+        // grown (lIterations raised between Steps): the old values move along — the
+        // image_warping step's speculative rz[0] for the next step lives here
         double* s = (double*)dmalloc(sizeof(double) * ns);
         OPT_HIP_CHECK(hipMemset(s, 0, sizeof(double) * ns));
+        if (scalars) {
+            OPT_HIP_CHECK(hipDeviceSynchronize());
+            OPT_HIP_CHECK(hipMemcpy(s, scalars, sizeof(double) * n_scalars, hipMemcpyDeviceToDevice));
+        }
         dfree(scalars);
         scalars = s;
         n_scalars = ns;

@@ -214,6 +214,8 @@ def _stepwise(monkeypatch, spec, change):
             prm[-1] = float(w["w_regSqrt"]) * 1.7
         if change == "rebind" and k == 3:
             prm = [p.clone() if isinstance(p, torch.Tensor) else p for p in prm]
+        if change == "liter" and k == 2:   # more scalar slots: the reduction scratch grows
+            s.set_solver_params({"lIterations": 40})
         if change == "constraints" and k == 2:
             C = prm[3].clone()
             C[C >= 0] += 3.0
@@ -224,7 +226,7 @@ def _stepwise(monkeypatch, spec, change):
     return costs, prm[0].cpu().numpy(), prm[1].cpu().numpy()
 
 
-@pytest.mark.parametrize("change", ["none", "weight", "rebind", "constraints"])
+@pytest.mark.parametrize("change", ["none", "weight", "rebind", "constraints", "liter"])
 def test_fused_step_end_equals_separate_passes(monkeypatch, change):
     c0, o0, a0 = _stepwise(monkeypatch, False, change)
     c1, o1, a1 = _stepwise(monkeypatch, True, change)
