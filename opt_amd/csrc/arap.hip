@@ -696,7 +696,7 @@ private:
     const int* graph_v0_ = nullptr;
     const int* graph_v1_ = nullptr;
     unsigned long long fingerprint_ = 0;
-    unsigned long long* fp_scratch_ = (unsigned long long*)dmalloc(sizeof(unsigned long long));
+    unsigned long long* fp_scratch_ = (unsigned long long*)dmalloc(sizeof(unsigned long long) * (1 + kFingerprintGrid));
     void* scratch_ = nullptr;
     size_t scratch_bytes_ = 0;
     int* keys_tmp_ = nullptr;

@@ -483,7 +483,8 @@ private:
     }
     // vertex indices must lie in [0, N) (fail-stop, as the reference does on bad input)
     void check_graphs(hipStream_t s) {
-        if (!fp_scratch_) fp_scratch_ = (unsigned long long*)dmalloc(sizeof(unsigned long long));
+        if (!fp_scratch_)
+            fp_scratch_ = (unsigned long long*)dmalloc(sizeof(unsigned long long) * (1 + kFingerprintGrid));
         int sb = 0;
         for (size_t g = 0; g < m_.graphs.size(); ++g) {
             const int ns = (int)m_.graphs[g].slot_names.size();

@@ -24,7 +24,7 @@ __device__ __forceinline__ unsigned fp_mix(unsigned v, unsigned e, unsigned salt
 // VEC = false: an array that is not 16-byte aligned, read as four 4-byte loads.
 template <bool VEC>
 static __global__ void graph_fingerprint_kernel(const int* __restrict__ v, int E, unsigned salt,
-                                                unsigned long long* out) {
+                                                unsigned long long* parts) {
     unsigned long long h = 0;
     const int n4 = E / 4;
     const int4* v4 = reinterpret_cast<const int4*>(v);
@@ -40,22 +40,39 @@ static __global__ void graph_fingerprint_kernel(const int* __restrict__ v, int E
     __shared__ unsigned long long part[4];
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = h;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(out, part[0] + part[1] + part[2] + part[3]);   // a sum: order-independent
+    // one partial per block (a single hot atomic costs ~12 ns per add: 4096 blocks would
+    // serialise ~50 us on it); graph_fingerprint_sum adds them up
+    if (threadIdx.x == 0) parts[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+static __global__ void graph_fingerprint_sum(const unsigned long long* __restrict__ parts, int n,
+                                             unsigned long long* out) {
+    unsigned long long h = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) h += parts[i];
+    for (int off = 32; off > 0; off >>= 1) h += __shfl_down(h, off, 64);
+    __shared__ unsigned long long part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = h;
+    __syncthreads();
+    if (threadIdx.x == 0) *out += part[0] + part[1] + part[2] + part[3];   // integer sum: order-free
 }
 
-// Fingerprint of n vertex arrays of E entries each; `d` is 8 bytes of device scratch
-// (synchronises `s`).
+constexpr int kFingerprintGrid = 2048;   // blocks per array (one partial each)
+// Fingerprint of n vertex arrays of E entries each; `d` is device scratch of
+// 1 + kFingerprintGrid words (synchronises `s`).
 inline unsigned long long graph_fingerprint(const int* const* arrays, int n, int E, hipStream_t s,
                                             unsigned long long* d) {
+    const int grid = std::max(1, std::min((E / 4 + 255) / 256, kFingerprintGrid));
     OPT_HIP_CHECK(hipMemsetAsync(d, 0, sizeof(unsigned long long), s));
-    const int grid = std::max(1, std::min((E / 4 + 255) / 256, 4096));   // one atomic per block
     for (int k = 0; k < n; ++k)
         if (E > 0) {
             const unsigned salt = 0x4C957F2Du * (unsigned)(k + 1);
             if ((reinterpret_cast<uintptr_t>(arrays[k]) & 15) == 0)
-                hipLaunchKernelGGL(graph_fingerprint_kernel<true>, dim3(grid), dim3(256), 0, s, arrays[k], E, salt, d);
+                hipLaunchKernelGGL(graph_fingerprint_kernel<true>, dim3(grid), dim3(256), 0, s, arrays[k], E, salt,
+                                   d + 1);
             else
-                hipLaunchKernelGGL(graph_fingerprint_kernel<false>, dim3(grid), dim3(256), 0, s, arrays[k], E, salt, d);
+                hipLaunchKernelGGL(graph_fingerprint_kernel<false>, dim3(grid), dim3(256), 0, s, arrays[k], E, salt,
+                                   d + 1);
+            hipLaunchKernelGGL(graph_fingerprint_sum, dim3(1), dim3(256), 0, s, (const unsigned long long*)(d + 1),
+                               grid, d);
         }
     unsigned long long h = 0;
     OPT_HIP_CHECK(hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, s));
