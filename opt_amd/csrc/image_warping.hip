@@ -1252,6 +1252,7 @@ private:
             timer_.ext_record("iw_apply", e0, e1);
             return;
         }
+        tbegin("iw_apply");   // the other variants: event records around the launch
         if (depth_ == 2)
             hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 2>), dim3(grid), dim3(kBlock), 0, stream_, a, pin,
                                (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars, ib_num,
@@ -1272,6 +1273,7 @@ private:
             hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1>), dim3(grid), dim3(kBlock), 0, stream_, a, pin,
                                (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars, ib_num,
                                ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
+        tend();
         OPT_HIP_CHECK(hipGetLastError());
     }
     void launch_residual(int i_num, int i_den, int sc_out) {
