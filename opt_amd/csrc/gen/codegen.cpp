@@ -72,6 +72,29 @@ public:
     Body(GModel& m, std::ostringstream& o, int ndims, const std::vector<int>& unk_slot)
         : M_(m), P_(m.pool), o_(o), nd_(ndims), uslot_(unk_slot) {}
 
+    // Graph gathers: nodes that read only the gathering vertex's own slot (`self`), params
+    // and constants are the same for every incident edge; they go to `pre`, emitted before
+    // the edge loop (the vertex's own sin/cos, unknowns and knowns once per vertex instead
+    // of once per edge).
+    void hoist_to(std::ostringstream* pre, int self, int graph) { pre_ = pre; self_ = self; graph_ = graph; }
+    bool invariant(int id) {
+        if (!pre_) return false;
+        auto it = inv_.find(id);
+        if (it != inv_.end()) return it->second;
+        const Node n = P_.at(id);
+        bool r = true;
+        switch (n.op) {
+            case Op::Const: case Op::Param: r = true; break;
+            case Op::Read: r = n.slot == self_ && (n.g < 0 || n.g == graph_); break;
+            case Op::InBox: case Op::Coord: case Op::Sample: r = false; break;
+            default:
+                r = (n.a < 0 || invariant(n.a)) && (n.b < 0 || invariant(n.b)) && (n.d < 0 || invariant(n.d));
+        }
+        inv_[id] = r;
+        return r;
+    }
+    std::ostream& out(int id) { return invariant(id) ? static_cast<std::ostream&>(*pre_) : o_; }
+
     std::string v(int id) {
         auto it = done_.find(id);
         if (it != done_.end()) return it->second;
@@ -106,7 +129,7 @@ public:
             case Op::Cos: {   // one sincos per angle: both halves share the range reduction
                 const std::string x = v(n.a), sn = "s" + std::to_string(n.a), cn = "c" + std::to_string(n.a);
                 if (!sincos_.count(n.a)) {
-                    o_ << "        T " << sn << ", " << cn << "; opt_sincos(" << x << ", &" << sn << ", &" << cn << ");\n";
+                    out(n.a) << "        T " << sn << ", " << cn << "; opt_sincos(" << x << ", &" << sn << ", &" << cn << ");\n";
                     sincos_.insert(n.a);
                 }
                 done_[id] = n.op == Op::Sin ? sn : cn;
@@ -132,7 +155,7 @@ public:
             case Op::Not: e = "(T)(" + v(n.a) + " == (T)0)"; break;
         }
         const std::string name = "t" + std::to_string(id);
-        o_ << "        const T " << name << " = " << e << ";\n";
+        out(id) << "        const T " << name << " = " << e << ";\n";
         done_[id] = name;
         return name;
     }
@@ -143,7 +166,7 @@ public:
         if (it != vdone_.end()) return it->second;
         const Node n = P_.at(u);
         const std::string name = std::string(vname) + "_" + std::to_string(u);
-        o_ << "        const T " << name << " = " << read(n, vname) << ";\n";
+        out(u) << "        const T " << name << " = " << read(n, vname) << ";\n";
         vdone_[key] = name;
         return name;
     }
@@ -210,6 +233,9 @@ private:
     std::map<int, std::string> done_;
     std::set<int> sincos_;
     std::map<std::string, std::string> vdone_;
+    std::ostringstream* pre_ = nullptr;
+    int self_ = -1, graph_ = -1;
+    std::map<int, bool> inv_;
 };
 
 struct Instance {   // a centred residual shifted so that it contains unknown (image, ch) at 0
@@ -252,10 +278,14 @@ GenSource generate(GModel& m, bool dbl) {
          "    return ((T)1 - yn) * u + yn * b;\n}\n";
     // memory pixel index -> coordinates; 2-D energies may hold a row slab whose memory row 0
     // is global row a.ymem0 (coordinates, bounds and Index(1) are global)
+    // (32-bit unsigned divisions: the pixel index fits an int, as `li` assumes; a 64-bit
+    // division is a ~100-instruction sequence per pixel)
     const char* coords = nd == 2
-        ? "        const int x = (int)(lin % W); const int y = (int)(lin / W) + a.ymem0; const int z = 0;\n"
+        ? "        const unsigned ul = (unsigned)lin, uq = ul / (unsigned)W;\n"
+          "        const int x = (int)(ul - uq * (unsigned)W); const int y = (int)uq + a.ymem0; const int z = 0;\n"
           "        const int li = (int)lin; (void)x; (void)y; (void)z; (void)li;\n"
-        : "        const int x = (int)(lin % W); const int y = (int)((lin / W) % H); const int z = (int)(lin / ((long long)W * H));\n"
+        : "        const unsigned ul = (unsigned)lin, uq = ul / (unsigned)W, uz = uq / (unsigned)H;\n"
+          "        const int x = (int)(ul - uq * (unsigned)W); const int y = (int)(uq - uz * (unsigned)H); const int z = (int)uz;\n"
           "        const int li = (int)lin; (void)x; (void)y; (void)z; (void)li;\n";
 
     // centred instances per output (unknown image, channel)
@@ -755,13 +785,9 @@ GenSource generate(GModel& m, bool dbl) {
                         for (int u : r.unknowns) any |= P.at(u).slot == (int)k;
                 if (!any) continue;
                 const int sbk = gs.slot_base[g] + (int)k;
-                o << "        for (int q = a.goff[" << sbk << "][vtx]; q < a.goff[" << sbk << "][vtx + 1]; ++q) {\n"
-                  << "        const int e = a.geid[" << sbk << "][q];\n";
-                for (size_t s2 = 0; s2 < nslots; ++s2)
-                    o << "        const int v" << s2 << " = " << (s2 == k ? std::string("(int)vtx") :
-                                                              "a.slot[" + std::to_string(gs.slot_base[g] + s2) + "][e]")
-                      << ";\n";
-                Body b(m, o, nd, uslot);
+                std::ostringstream pre, body;
+                Body b(m, body, nd, uslot);
+                b.hoist_to(&pre, (int)k, (int)g);
                 int idx = 0;
                 for (auto& r : m.residuals) {
                     if (r.graph != (int)g) continue;
@@ -794,7 +820,14 @@ GenSource generate(GModel& m, bool dbl) {
                         b.line(a_ + " += " + gn + " * " + R + ";" + (apply ? "" : " " + d_ + " += " + gn + " * " + gn + ";"));
                     }
                 }
-                o << "        }\n";
+                // { own-vertex values; for each incident edge { the other slots; the rest } }
+                o << "        {\n        const int v" << k << " = (int)vtx;\n" << pre.str()
+                  << "        for (int q = a.goff[" << sbk << "][vtx]; q < a.goff[" << sbk << "][vtx + 1]; ++q) {\n"
+                  << "        const int e = a.geid[" << sbk << "][q];\n";
+                for (size_t s2 = 0; s2 < nslots; ++s2)
+                    if (s2 != k)
+                        o << "        const int v" << s2 << " = a.slot[" << gs.slot_base[g] + (int)s2 << "][e];\n";
+                o << body.str() << "        }\n        }\n";
             }
         }
     };
