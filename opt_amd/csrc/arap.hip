@@ -19,7 +19,11 @@
 // The apply reads its adjacency as sliced ELL (64-vertex slices, one slot row per wave
 // load) built from the CSR lists once per bind.
 //
-// Measured at 1 M vertices (profiles/r02_arap_*): kdir + apply ~60 us. Counters (r02q):
+// The apply walks one merged neighbour list (arap_apply_merged): on a mesh whose edges go
+// both ways every neighbour's p and UrShape are gathered once for its out- and its
+// in-edge term (kdir + apply 61 -> 53 us at 1 M vertices; OPT_AMD_ARAP_MERGED=0 keeps
+// the two lists).
+// Measured at 1 M vertices with the two lists (profiles/r02_arap_*): kdir + apply ~60 us. Counters (r02q):
 // HBM traffic = the compulsory 176 B/vertex of the apply (132 B/vertex algorithmic + the
 // K gather 36 + CSR offsets 8) and 60 B/vertex of kdir; the apply is bound by the
 // texture/load path (TA busy 59 %, TD 67 % averaged over the dispatch incl. ramp and
@@ -55,6 +59,11 @@ struct Args {
     // count ew[s] (a multiple of the apply's batch size)
     const int *out_ell, *out_eoff, *out_ew;
     const int *in_ell, *in_eoff, *in_ew;
+    // merged neighbour list (sliced ELL as above): every out-neighbour in out-list order,
+    // flagged when the same neighbour also sends an edge here (its in-edge is then taken
+    // in the same slot), then the unmatched in-neighbours; slot = u | kind << 28
+    // (kind 1 out, 2 in, 3 both), -1 padding
+    const int *nb_ell, *nb_eoff, *nb_ew;
     uint8_t* flags;
     T wf, wr;
 };
@@ -320,6 +329,142 @@ __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restr
     block_reduce_publish<1>(vv, rs, blockIdx.x);
 }
 
+// The same J^T J p over the merged neighbour list: a neighbour that is both an out- and
+// an in-neighbour (every neighbour of a mesh whose edges go both ways) has its p and
+// UrShape gathered once for both terms. The in-terms are summed in merged-list order
+// (the out-terms, and so the angle rows, keep the out-list order).
+constexpr int kEBM = 3;   // merged slots per batch (1, 2, 3 measured within 2 %); widths are padded to it
+template <typename T, int EB = kEBM>
+__global__ __launch_bounds__(kBlock) void arap_apply_merged(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
+                                                            const T* __restrict__ Kall, const T* __restrict__ dadd,
+                                                            const int* stop, ReduceSlot rs) {
+    if (stop && *stop) return;
+    const int v = xcd_remap(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;   // contiguous vertex ranges per XCD
+    T dot = 0;
+    if (v < a.N) {
+        const long long N = a.N;
+        const T wr = a.wr, wf = a.wf;
+        const V3<T> pO = ld3<T>(p, v), pA = ld3<T>(p + 3 * N, v);
+        const V3<T> Av = ld3<T>(a.A, v);
+        const V3<float> Uv = ld3<float>(a.U, v);
+        T K[9];
+        {
+            T R[9], dR[3][9];
+            rotation(Av, R, dR);
+            directional(dR, pA, K);
+        }
+        T M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        V3<T> aO = {0, 0, 0}, aA = {0, 0, 0};
+        if (fit_valid(a, v)) aO = {wf * (wf * pO.x), wf * (wf * pO.y), wf * (wf * pO.z)};
+        const int lane = v & 63;
+        const int* nel = a.nb_ell + a.nb_eoff[v >> 6] + lane;
+        const int nw = a.nb_ew[v >> 6];
+        for (int i0 = 0; i0 < nw; i0 += EB) {
+            int u[EB], kind[EB];
+#pragma unroll
+            for (int b = 0; b < EB; ++b) {
+                const int x = nel[64 * (i0 + b)];
+                kind[b] = x < 0 ? 0 : (x >> 28);
+                u[b] = x < 0 ? v : (x & 0x0FFFFFFF);
+            }
+            V3<T> pu[EB];
+            V3<float> Uu[EB];
+            T Ku[EB][9];
+#pragma unroll
+            for (int b = 0; b < EB; ++b) {
+                pu[b] = gld3<T>(p, u[b]);
+                Uu[b] = gld3<float>(a.U, u[b]);
+#pragma unroll
+                for (int q = 0; q < 9; ++q) Ku[b][q] = gld(Kall + q * N, u[b]);
+            }
+#pragma unroll
+            for (int b = 0; b < EB; ++b) {
+                const bool out = kind[b] & 1, in = kind[b] & 2;
+                const V3<T> d = {(T)(Uv.x - Uu[b].x), (T)(Uv.y - Uu[b].y), (T)(Uv.z - Uu[b].z)};
+                {   // out-edge v -> u
+                    const V3<T> Kd = mv(K, d);
+                    const V3<T> jp = {out ? wr * (pO.x - pu[b].x - Kd.x) : (T)0, out ? wr * (pO.y - pu[b].y - Kd.y) : (T)0,
+                                      out ? wr * (pO.z - pu[b].z - Kd.z) : (T)0};
+                    const V3<T> dd = {out ? d.x : (T)0, out ? d.y : (T)0, out ? d.z : (T)0};
+                    aO.x += wr * jp.x; aO.y += wr * jp.y; aO.z += wr * jp.z;
+                    M[0] += jp.x * dd.x; M[1] += jp.x * dd.y; M[2] += jp.x * dd.z;
+                    M[3] += jp.y * dd.x; M[4] += jp.y * dd.y; M[5] += jp.y * dd.z;
+                    M[6] += jp.z * dd.x; M[7] += jp.z * dd.y; M[8] += jp.z * dd.z;
+                }
+                {   // in-edge u -> v
+                    const V3<T> di = {(T)(Uu[b].x - Uv.x), (T)(Uu[b].y - Uv.y), (T)(Uu[b].z - Uv.z)};
+                    const V3<T> Kd = mv(Ku[b], di);
+                    const V3<T> jp = {in ? wr * (pu[b].x - pO.x - Kd.x) : (T)0, in ? wr * (pu[b].y - pO.y - Kd.y) : (T)0,
+                                      in ? wr * (pu[b].z - pO.z - Kd.z) : (T)0};
+                    aO.x -= wr * jp.x; aO.y -= wr * jp.y; aO.z -= wr * jp.z;
+                }
+            }
+        }
+        {
+            T R[9], dR[3][9];
+            rotation(Av, R, dR);
+            T s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll
+            for (int q = 0; q < 9; ++q) { s0 += dR[0][q] * M[q]; s1 += dR[1][q] * M[q]; s2 += dR[2][q] * M[q]; }
+            aA = {-wr * s0, -wr * s1, -wr * s2};
+        }
+        if (dadd) {
+            aO.x += dadd[3 * v] * pO.x; aO.y += dadd[3 * v + 1] * pO.y; aO.z += dadd[3 * v + 2] * pO.z;
+            aA.x += dadd[3 * N + 3 * v] * pA.x; aA.y += dadd[3 * N + 3 * v + 1] * pA.y;
+            aA.z += dadd[3 * N + 3 * v + 2] * pA.z;
+        }
+        Ap[3 * v] = aO.x; Ap[3 * v + 1] = aO.y; Ap[3 * v + 2] = aO.z;
+        Ap[3 * N + 3 * v] = aA.x; Ap[3 * N + 3 * v + 1] = aA.y; Ap[3 * N + 3 * v + 2] = aA.z;
+        dot = pO.x * aO.x + pO.y * aO.y + pO.z * aO.z + pA.x * aA.x + pA.y * aA.y + pA.z * aA.z;
+    }
+    double vv[1] = {(double)dot};
+    block_reduce_publish<1>(vv, rs, blockIdx.x);
+}
+
+// Merged list of one vertex (one thread per vertex): count (fill = false) or write
+// (fill = true) the entries as described at Args::nb_ell.
+__device__ __forceinline__ int merge_vertex(const int* oo, const int* on, const int* io, const int* in_, int v,
+                                            int* out, int stride) {
+    const int ob = oo[v], oe = oo[v + 1], ib = io[v], ie = io[v + 1];
+    unsigned long long used = 0;   // in-entries matched so far (a vertex with > 64 in-edges: see below)
+    int k = 0;
+    for (int i = ob; i < oe; ++i) {
+        const int u = on[i];
+        int kind = 1;
+        for (int j = ib; j < ie && j - ib < 64; ++j)
+            if (!(used >> (j - ib) & 1ull) && in_[j] == u) {
+                used |= 1ull << (j - ib);
+                kind = 3;
+                break;
+            }
+        if (out) out[(long long)k * stride] = u | (kind << 28);
+        ++k;
+    }
+    for (int j = ib; j < ie; ++j)
+        if (j - ib >= 64 || !(used >> (j - ib) & 1ull)) {
+            if (out) out[(long long)k * stride] = in_[j] | (2 << 28);
+            ++k;
+        }
+    return k;
+}
+__global__ void merged_width(const int* oo, const int* on, const int* io, const int* in_, int N, int nslices,
+                             int pad, int* ew) {
+    const int s = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64, l = threadIdx.x & 63;
+    if (s >= nslices) return;
+    const int v = 64 * s + l;
+    int d = v < N ? merge_vertex(oo, on, io, in_, v, nullptr, 0) : 0;
+    for (int m = 32; m >= 1; m >>= 1) d = max(d, __shfl_xor(d, m));
+    if (l == 0) ew[s] = (d + pad - 1) / pad * pad;
+}
+__global__ void merged_fill(const int* oo, const int* on, const int* io, const int* in_, int N, const int* eoff,
+                            const int* ew, int* ell) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x, s = v >> 6;
+    if (64 * s >= N) return;
+    int* e = ell + eoff[s] + (v & 63);
+    const int k = v < N ? merge_vertex(oo, on, io, in_, v, e, 64) : 0;
+    for (int b = k; b < ew[s]; ++b) e[64 * b] = -1;
+}
+
 // ------------------------------------------------------- cost / model cost
 // Each edge residual is summed by its head vertex (the edge's out-list owner).
 template <typename T>
@@ -502,7 +647,7 @@ public:
         }
     }
     ~ArapOp() {
-        out_.release(); in_.release();
+        out_.release(); in_.release(); nb_.release();
         dfree(dO_); dfree(dA_); dfree(dU_); dfree(dC_); dfree(dv0_); dfree(dv1_);
         dfree(scratch_); dfree(keys_tmp_); dfree(K_); dfree(fp_scratch_);
     }
@@ -552,6 +697,7 @@ public:
         a_.in_off = in_.off; a_.in_nbr = in_.nbr;
         a_.out_ell = out_.ell; a_.out_eoff = out_.eoff; a_.out_ew = out_.ew;
         a_.in_ell = in_.ell; a_.in_eoff = in_.eoff; a_.in_ew = in_.ew;
+        a_.nb_ell = nb_.ell; a_.nb_eoff = nb_.eoff; a_.nb_ew = nb_.ew;
     }
     void unbind(hipStream_t s) {
         if (!opts_.host_buffers) return;
@@ -579,8 +725,12 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
     void apply_prepared(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
-        hipLaunchKernelGGL((arap::arap_apply<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap,
-                           (const T*)K_, dadd, stop, rs);
+        if (merged_on_)
+            hipLaunchKernelGGL((arap::arap_apply_merged<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap,
+                               (const T*)K_, dadd, stop, rs);
+        else
+            hipLaunchKernelGGL((arap::arap_apply<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap,
+                               (const T*)K_, dadd, stop, rs);
         OPT_HIP_CHECK(hipGetLastError());
     }
     void cost(ReduceSlot rs, hipStream_t s) {
@@ -663,6 +813,40 @@ private:
         OPT_HIP_CHECK(hipGetLastError());
         OPT_HIP_CHECK(hipStreamSynchronize(s));   // h is a host temporary
     }
+    // the merged neighbour list (arap::Args nb_*) from the two CSRs, as sliced ELL
+    void merged_ell(hipStream_t s) {
+        nb_.release();
+        const int ns = (N_ + 63) / 64;
+        nb_.ew = (int*)dmalloc(sizeof(int) * (ns + 1));
+        nb_.eoff = (int*)dmalloc(sizeof(int) * (ns + 1));
+        OPT_HIP_CHECK(hipMemsetAsync(nb_.ew, 0, sizeof(int) * (ns + 1), s));
+        hipLaunchKernelGGL(arap::merged_width, dim3((ns + 3) / 4), dim3(256), 0, s, (const int*)out_.off,
+                           (const int*)out_.nbr, (const int*)in_.off, (const int*)in_.nbr, N_, ns, arap::kEBM, nb_.ew);
+        size_t need = 0;
+        OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, need, nb_.ew, nb_.eoff, ns + 1, s));
+        if (need > scratch_bytes_) {
+            dfree(scratch_);
+            scratch_ = dmalloc(need);
+            scratch_bytes_ = need;
+        }
+        OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(scratch_, need, nb_.ew, nb_.eoff, ns + 1, s));
+        std::vector<int> h(ns + 1);
+        OPT_HIP_CHECK(hipMemcpyAsync(h.data(), nb_.eoff, sizeof(int) * (ns + 1), hipMemcpyDeviceToHost, s));
+        OPT_HIP_CHECK(hipStreamSynchronize(s));
+        const long long total = 64LL * h[ns];
+        if (total >= (1LL << 31)) {
+            fprintf(stderr, "[opt_amd] arap_mesh_deformation: adjacency too large (%lld merged slots)\n", total);
+            exit(1);
+        }
+        for (auto& x : h) x *= 64;
+        OPT_HIP_CHECK(hipMemcpyAsync(nb_.eoff, h.data(), sizeof(int) * (ns + 1), hipMemcpyHostToDevice, s));
+        nb_.ell = (int*)dmalloc(sizeof(int) * std::max(total, 1LL));
+        hipLaunchKernelGGL(arap::merged_fill, dim3((64LL * ns + 255) / 256), dim3(256), 0, s, (const int*)out_.off,
+                           (const int*)out_.nbr, (const int*)in_.off, (const int*)in_.nbr, N_, (const int*)nb_.eoff,
+                           (const int*)nb_.ew, nb_.ell);
+        OPT_HIP_CHECK(hipGetLastError());
+        OPT_HIP_CHECK(hipStreamSynchronize(s));   // h is a host temporary
+    }
     void build_csr(const int* v0, const int* v1, hipStream_t s) {
         if (E_ > 0) {
             int* bad = (int*)dmalloc(sizeof(int));
@@ -684,6 +868,7 @@ private:
         csr(v1, v0, in_, s);
         ell(out_, arap::kEBO, s);
         ell(in_, arap::kEBI, s);
+        merged_ell(s);
         graph_v0_ = v0;
         graph_v1_ = v1;
     }
@@ -692,7 +877,7 @@ private:
     int N_ = 0, E_ = 0;
     int idx_O_, idx_A_, idx_U_, idx_C_, idx_v0_, idx_v1_, idx_wf_, idx_wr_;
     arap::Args<T> a_{};
-    GraphCSR out_, in_;
+    GraphCSR out_, in_, nb_;   // nb_: the merged list (ell / eoff / ew only)
     const int* graph_v0_ = nullptr;
     const int* graph_v1_ = nullptr;
     unsigned long long fingerprint_ = 0;
@@ -701,6 +886,7 @@ private:
     size_t scratch_bytes_ = 0;
     int* keys_tmp_ = nullptr;
     T* K_ = nullptr;   // per-vertex directional rotation derivative of the current p
+    const bool merged_on_ = env_int("OPT_AMD_ARAP_MERGED", 1) != 0;   // 0: separate out / in lists
     T *userO_ = nullptr, *userA_ = nullptr, *dO_ = nullptr, *dA_ = nullptr;
     float *dU_ = nullptr, *dC_ = nullptr;
     int *dv0_ = nullptr, *dv1_ = nullptr;

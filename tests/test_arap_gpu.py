@@ -246,3 +246,31 @@ def test_fused_step3_is_bitwise_the_separate_passes(monkeypatch, kind, double):
         s.close()
     assert out["1"][0] == out["0"][0]
     assert np.array_equal(out["1"][1], out["0"][1]) and np.array_equal(out["1"][2], out["0"][2])
+
+
+@pytest.mark.parametrize("double", [False, True])
+def test_merged_neighbour_list_matches_the_two_lists(monkeypatch, double):
+    """arap_apply_merged (one list: out-neighbours flagged when they also send an edge
+    here, then the unmatched in-neighbours) against the separate out / in lists, on the
+    grid mesh (every neighbour both ways) and on irregular hub graphs (one-way edges,
+    duplicates): the same terms in another in-edge order, so J^T J p agrees to rounding
+    and the solves to the fp32 noise floor (fp64: 1e-12)."""
+    import torch
+
+    for w in (perturbed(31, 19, seed=6), irregular(seed=21)):
+        out = {}
+        for m in ("1", "0"):
+            monkeypatch.setenv("OPT_AMD_ARAP_MERGED", m)
+            s = solver(w, double_precision=double)
+            prm = params(w, double=double)
+            n = s.unknown_count()
+            dt = torch.float64 if double else torch.float32
+            p = torch.from_numpy(np.random.default_rng(5).normal(size=n)).to(dt).cuda()
+            Ap = torch.zeros_like(p)
+            pAp = s.apply_jtj(prm, p, Ap)
+            s.set_solver_params({"nIterations": 3, "lIterations": 10})
+            out[m] = (to_np(Ap), pAp, s.profiled_solve(params(w, double=double)))
+            s.close()
+        assert rel_err(out["1"][0], out["0"][0]) < (1e-13 if double else 1e-5)
+        assert out["1"][1] == pytest.approx(out["0"][1], rel=1e-12 if double else 1e-5)
+        np.testing.assert_allclose(out["1"][2], out["0"][2], rtol=1e-12 if double else 1e-4)
