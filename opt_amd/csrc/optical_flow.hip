@@ -37,6 +37,7 @@ struct Args {
     const float* Ihx;  // I_hat_dx
     const float* Ihy;  // I_hat_dy
     T* G;              // cached sampled gradient (2 per pixel)
+    T* Ef;             // cached fit residual wf (I - S(I_hat)) at the step's X (the model cost)
     uint8_t* flags;
     T wf, wr;
 };
@@ -124,6 +125,7 @@ __global__ __launch_bounds__(kBlock) void of_jtf(Args<T> a, T* __restrict__ r, T
     st2(r, g.i, -Fx, -Fy);
     st2(diag, g.i, Dx, Dy);
     st2(a.G, g.i, gx, gy);
+    a.Ef[g.i] = ef;
     a.flags[g.i] = 1;
 }
 
@@ -184,14 +186,18 @@ __global__ __launch_bounds__(kBlock) void of_cost(Args<T> a, const T* __restrict
     const PixGeom g = tile_pix(a.dom, tile);
     if (g.ok) {
         const V2<T> xk = ld2((const T*)a.X, g.i);
-        T xn, yn;
-        const Taps t = taps_of((T)g.x + xk.x, (T)g.y + xk.y, xn, yn);
-        T ef = a.wf * ((T)a.I[g.i] - sample<T>(a.Ih, a.dom, t, xn, yn));
+        T ef;
         V2<T> dk = {0, 0};
         if (delta) {
+            // the model cost is taken at the step's X, where of_jtf sampled the fit residual
+            // and its gradient with these same expressions: no gathers
             dk = ld2(delta, g.i);
-            const T gx = sample<T>(a.Ihx, a.dom, t, xn, yn), gy = sample<T>(a.Ihy, a.dom, t, xn, yn);
-            ef = ef + ((-a.wf * gx) * dk.x + (-a.wf * gy) * dk.y);
+            const V2<T> gk = ld2((const T*)a.G, g.i);
+            ef = a.Ef[g.i] + ((-a.wf * gk.x) * dk.x + (-a.wf * gk.y) * dk.y);
+        } else {
+            T xn, yn;
+            const Taps t = taps_of((T)g.x + xk.x, (T)g.y + xk.y, xn, yn);
+            ef = a.wf * ((T)a.I[g.i] - sample<T>(a.Ih, a.dom, t, xn, yn));
         }
         T s2 = ef * ef;
         for (int d = 0; d < 4; ++d) {
@@ -275,6 +281,7 @@ public:
         idx_wr_ = ps[1].index;
         const long long N = dom_.npix_mem();
         G_ = (T*)dmalloc(sizeof(T) * 2 * N);
+        Ef_ = (T*)dmalloc(sizeof(T) * N);
         OPT_HIP_CHECK(hipMemset(G_, 0, sizeof(T) * 2 * N));
         if (opts.host_buffers) {
             dX_ = (T*)dmalloc(sizeof(T) * 2 * N);
@@ -283,6 +290,7 @@ public:
     }
     ~OpticalFlowOp() {
         dfree(G_);
+        dfree(Ef_);
         dfree(dX_);
         for (float* v : {dI_, dIh_, dIhx_, dIhy_}) dfree(v);
     }
@@ -317,6 +325,7 @@ public:
             a_.X = dX_; a_.I = dI_; a_.Ih = dIh_; a_.Ihx = dIhx_; a_.Ihy = dIhy_;
         }
         a_.G = G_;
+        a_.Ef = Ef_;
         a_.dom = dom_;
     }
     void unbind(hipStream_t s) {
@@ -364,6 +373,7 @@ private:
     int idx_X_, idx_I_, idx_Ih_, idx_Ihx_, idx_Ihy_, idx_wf_, idx_wr_;
     of::Args<T> a_{};
     T* G_ = nullptr;
+    T* Ef_ = nullptr;   // fit residual at the step's X (of_jtf -> model cost)
     T* userX_ = nullptr;
     T* dX_ = nullptr;
     float *dI_ = nullptr, *dIh_ = nullptr, *dIhx_ = nullptr, *dIhy_ = nullptr;
