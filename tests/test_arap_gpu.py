@@ -274,3 +274,42 @@ def test_merged_neighbour_list_matches_the_two_lists(monkeypatch, double):
         assert rel_err(out["1"][0], out["0"][0]) < (1e-13 if double else 1e-5)
         assert out["1"][1] == pytest.approx(out["0"][1], rel=1e-12 if double else 1e-5)
         np.testing.assert_allclose(out["1"][2], out["0"][2], rtol=1e-12 if double else 1e-4)
+
+
+def test_graph_without_edges_and_isolated_vertices():
+    """Edge cases of the adjacency build (CSR, sliced ELL, merged list): a graph with no
+    edges at all (only the fit term: J^T J p = w_fit^2 p on constrained vertices), and a
+    vertex count that is not a multiple of the 64-vertex slice with isolated vertices;
+    the apply against the oracle, whole solves against the oracle's trajectory."""
+    import torch
+
+    w = perturbed(9, 7, seed=3)          # 63 vertices
+    N = w["N"]
+    for keep in (0, len(w["v0"]) // 3):
+        w2 = dict(w)
+        w2["v0"] = np.ascontiguousarray(w["v0"][:keep])
+        w2["v1"] = np.ascontiguousarray(w["v1"][:keep])
+        w2["E"] = keep
+        s = solver(w2)
+        prm = params(w2)
+        p = torch.from_numpy(np.random.default_rng(1).normal(size=6 * N).astype(np.float32)).cuda()
+        Ap = torch.zeros_like(p)
+        pAp = s.apply_jtj(prm, p, Ap)
+        Ap_ref, pAp_ref = oracle.arap_apply(w2, to_np(p))
+        assert rel_err(to_np(Ap), Ap_ref) < 2e-5
+        assert pAp == pytest.approx(pAp_ref, rel=1e-5, abs=1e-12)
+        if keep == 0:
+            fit = np.repeat(w["Constraints"].reshape(-1, 3)[:, 0] >= -999999.9, 3)
+            expect = np.concatenate([np.where(fit, w["w_fitSqrt"] ** 2 * to_np(p)[:3 * N], 0.0), np.zeros(3 * N)])
+            np.testing.assert_allclose(to_np(Ap), expect, rtol=1e-6, atol=1e-7)
+        # with no edges the system is diagonal: one PCG iteration solves it, after which the
+        # reference's unguarded alpha = rz / pAp (solverGPUGaussNewton.t:696) is 0/0 or
+        # rounding noise depending on whether r came out exactly 0 — so that case takes one
+        # GN step of one PCG iteration
+        nit, lit = (1, 1) if keep == 0 else (2, 5)
+        s.set_solver_params({"nIterations": nit, "lIterations": lit})
+        costs = s.profiled_solve(params(w2))
+        ref = oracle.arap_solve(w2, nit, lit)[2]
+        assert len(costs) == len(ref)
+        np.testing.assert_allclose(costs, ref, rtol=1e-4, atol=1e-8 * ref[0])
+        s.close()
