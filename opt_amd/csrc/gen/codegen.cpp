@@ -171,6 +171,9 @@ public:
         return name;
     }
     void line(const std::string& s) { o_ << "        " << s << "\n"; }
+    // register-strip emission (gen_apply_strip): centred reads come from the caller's
+    // row windows instead of memory
+    void centred_reads(std::function<std::string(const Node&, const char*)> f) { centred_ = std::move(f); }
 
 private:
     std::string coord(int k, int off) const {
@@ -221,7 +224,8 @@ private:
             idx = "(long long)v" + std::to_string(n.slot) + " * " + ch + " + " + c;
             return "(T)(" + base + ")[" + idx + "]";
         }
-        idx = "(li + " + rel(n.off) + ") * " + ch + " + " + c;
+        if (centred_) return centred_(n, vname);
+        idx ="(li + " + rel(n.off) + ") * " + ch + " + " + c;
         return "((" + inb(n.off) + ") ? (T)(" + base + ")[" + idx + "] : (T)0)";
     }
 
@@ -236,6 +240,7 @@ private:
     std::ostringstream* pre_ = nullptr;
     int self_ = -1, graph_ = -1;
     std::map<int, bool> inv_;
+    std::function<std::string(const Node&, const char*)> centred_;
 };
 
 struct Instance {   // a centred residual shifted so that it contains unknown (image, ch) at 0
@@ -267,6 +272,18 @@ GenSource generate(GModel& m, bool dbl) {
     o << "#define OPT_COORDS const int W = a.dims[0], H = a.dims[1], D = a.dims[2]; (void)D;\n";
     o << "__device__ __forceinline__ void opt_sincos(float x, float* s, float* c) { sincosf(x, s, c); }\n"
          "__device__ __forceinline__ void opt_sincos(double x, double* s, double* c) { sincos(x, s, c); }\n";
+    // whole-wave DPP lane shifts (wave_shl:1 / wave_shr:1): opt_sh(v, d) is v of lane l + d
+    // (0 past the wave's ends); d is a literal at every use, so the loops unroll away
+    o << "__device__ __forceinline__ float opt_lr(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false)); }\n"
+         "__device__ __forceinline__ float opt_ll(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false)); }\n"
+         "__device__ __forceinline__ double opt_dd(double v, bool r) {\n"
+         "    const long long b = __double_as_longlong(v);\n"
+         "    const int lo = r ? __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xf, 0xf, false) : __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xf, 0xf, false);\n"
+         "    const int hi = r ? __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, false) : __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, false);\n"
+         "    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);\n}\n"
+         "__device__ __forceinline__ double opt_lr(double v) { return opt_dd(v, true); }\n"
+         "__device__ __forceinline__ double opt_ll(double v) { return opt_dd(v, false); }\n"
+         "__device__ __forceinline__ T opt_sh(T v, int d) { for (; d > 0; --d) v = opt_lr(v); for (; d < 0; ++d) v = opt_ll(v); return v; }\n";
     // Image:get / Image:sample (o.t:856-876): floor / ceil taps, zero outside, lerps in T
     o << "template <typename E> __device__ __forceinline__ T opt_tap(const E* im, int nch, int c, int x, int y, int W, int H) {\n"
          "    return (x >= 0 && x < W && y >= 0 && y < H) ? (T)im[((long long)y * W + x) * nch + c] : (T)0;\n}\n"
@@ -605,6 +622,153 @@ GenSource generate(GModel& m, bool dbl) {
                  "    if (finish) { double v[1] = {(double)dot}; block_reduce_publish<1>(v, rs, blockIdx.x); }\n}\n";
         }
 
+    // ------------------------------------------------------------ gen_apply_strip
+    // J^T J p in registers: each wave owns a column strip (one pixel per lane, halo lanes
+    // at both ends) and walks down a block of rows. Every centred residual is evaluated
+    // ONCE per centre (as the tiled form), its reads served from per-array row windows
+    // (the rows centre + dy the residuals touch; a column offset dx is a DPP lane shift);
+    // each centre's contributions d(r, u) Jp_r are summed per output offset (u's offset),
+    // lane-shifted to the output column and added to rolling per-row accumulators; an
+    // output row is finished once the last centre row that reaches it has been evaluated.
+    // No LDS and no barriers: the hand-written image_warping / SFS applies work this way.
+    // Same instance set as createjtjcentered (o.t:2770-2830): centres outside the image
+    // contribute nothing (gen_apply_tiled's rule).
+    if (tiled) {
+        bool ok = true;
+        for (int ci : cres)
+            P.visit(m.residuals[ci].expr, [&](int, const Node& n) { ok &= n.op != Op::Sample; });
+        // rows each (p?, image, channel) window must hold, lane reach of the reads
+        std::map<std::tuple<int, int, int>, std::pair<int, int>> win;
+        int rxlo = 0, rxhi = 0;
+        auto wname = [](const std::tuple<int, int, int>& k, int dy) {
+            return std::string(std::get<0>(k) ? "wp" : "wi") + std::to_string(std::get<1>(k)) + "c" +
+                   std::to_string(std::get<2>(k)) + (dy < 0 ? "m" : "p") + std::to_string(std::abs(dy));
+        };
+        std::ostringstream body;
+        const CacheMap* saved = g_cache;
+        g_cache = nullptr;   // sin / cos of a window value: no cache images
+        {
+            Body b(m, body, nd, uslot);
+            b.centred_reads([&](const Node& n, const char* vname) {
+                const auto key = std::make_tuple(vname ? 1 : 0, n.i, n.ch);
+                auto it = win.find(key);
+                if (it == win.end()) win[key] = {n.off[1], n.off[1]};
+                else it->second = {std::min(it->second.first, n.off[1]), std::max(it->second.second, n.off[1])};
+                rxlo = std::min(rxlo, n.off[0]);
+                rxhi = std::max(rxhi, n.off[0]);
+                const std::string w = wname(key, n.off[1]);
+                return n.off[0] == 0 ? w : "opt_sh(" + w + ", " + std::to_string(n.off[0]) + ")";
+            });
+            std::vector<std::string> dname(ents.size());
+            for (size_t ci = 0; ci < cres.size(); ++ci) {
+                std::string sum = "(T)0";
+                for (size_t ei = 0; ei < ents.size(); ++ei) {
+                    if (ents[ei].r != (int)ci) continue;
+                    const std::string dn = b.v(ents[ei].dnode);
+                    if (ents[ei].slot >= 0) {
+                        dname[ei] = "d" + std::to_string(ei);
+                        b.line("const T " + dname[ei] + " = qin ? " + dn + " : (T)0;");
+                    } else {
+                        double cv;
+                        P.is_const(ents[ei].dnode, &cv);
+                        dname[ei] = lit(cv);
+                    }
+                    sum += " + " + dn + " * " + b.vec(ents[ei].u, "p");
+                }
+                b.line("const T jp" + std::to_string(ci) + " = qin ? " + sum + " : (T)0;");
+            }
+            // contributions per output (image, channel, offset): one lane shift each
+            std::map<std::tuple<int, int, int, int>, std::string> grp;
+            for (size_t ei = 0; ei < ents.size(); ++ei) {
+                const Node n = P.at(ents[ei].u);
+                std::string& s = grp[std::make_tuple(n.i, n.ch, ents[ei].oy, ents[ei].ox)];
+                s += (s.empty() ? "" : " + ") + dname[ei] + " * jp" + std::to_string(ents[ei].r);
+            }
+            for (auto& g : grp) {
+                const int k = std::get<0>(g.first), c = std::get<1>(g.first), oy = std::get<2>(g.first),
+                          ox = std::get<3>(g.first);
+                const std::string acc = "ac" + std::to_string(uslot[k]) + "_" + std::to_string(c) + "_" +
+                                        std::to_string(oy - miny);
+                b.line(acc + " += " + (ox == 0 ? "(" + g.second + ")" : "opt_sh(" + g.second + ", " + std::to_string(-ox) + ")") + ";");
+            }
+        }
+        g_cache = saved;
+        int regs = 0;
+        for (auto& w : win) regs += w.second.second - w.second.first + 1;
+        int nacc = 0;
+        for (int k : unk) nacc += m.images[k].channels;
+        regs += nacc * (maxy - miny + 1);
+        const int loff = -rxlo + maxx, nout = 64 + rxlo - rxhi - (maxx - minx);
+        ok = ok && nout >= 16 && regs <= 96 * (dbl ? 1 : 2) / 2;
+        if (ok) {
+            gs.has_strip = true;
+            gs.strip_cols = nout;
+            o << "extern \"C\" __global__ __launch_bounds__(256) void gen_apply_strip(GenArgs a, const T* __restrict__ p, T* __restrict__ Ap,\n"
+                 "        const T* __restrict__ dadd, const int* stop, ReduceSlot rs, int finish) {\n"
+                 "    if (stop && *stop) return;\n"
+                 "    OPT_COORDS\n"
+                 "    T dot = 0;\n"
+                 "    const int lane = threadIdx.x & 63, z = 0; (void)z;\n"
+                 "    const int nsx = (W + " << nout - 1 << ") / " << nout << ", G = gridDim.x * 4;\n"
+                 "    const int RB = max(8, (int)(((long long)H * nsx + G - 1) / G)), nby = (H + RB - 1) / RB;\n"
+                 "    for (int wid = blockIdx.x * 4 + (threadIdx.x >> 6); wid < nsx * nby; wid += G) {\n"
+                 "        const int x = (wid % nsx) * " << nout << " + lane - " << loff << ";\n"
+                 "        const int y0 = (wid / nsx) * RB, y1 = min(H, y0 + RB);\n"
+                 "        const bool xin = x >= 0 && x < W, xout = xin && lane >= " << loff << " && lane < " << loff + nout << ";\n";
+            auto load = [&](const std::tuple<int, int, int>& k, const std::string& yy) {
+                const int i = std::get<1>(k), c = std::get<2>(k), ch = m.images[i].channels;
+                const std::string base = std::get<0>(k)
+                    ? "(p + a.uoff[" + std::to_string(uslot[i]) + "])"
+                    : "((const " + std::string(elem_type(m.images[i].elem, m.images[i].tvalued)) + "*)a.img[" +
+                          std::to_string(i) + "])";
+                return "((xin && " + yy + " >= 0 && " + yy + " < H) ? (T)" + base + "[(long long)(" + yy + " * W + x) * " +
+                       std::to_string(ch) + " + " + std::to_string(c) + "] : (T)0)";
+            };
+            const std::string qy0 = "(y0 - " + std::to_string(maxy) + ")";
+            for (auto& w : win) {
+                o << "        T " << wname(w.first, w.second.first) << " = 0";
+                for (int dy = w.second.first + 1; dy <= w.second.second; ++dy)
+                    o << ", " << wname(w.first, dy) << " = " << load(w.first, "(" + qy0 + " - 1 + " + std::to_string(dy) + ")");
+                o << ";\n";
+            }
+            for (int k : unk)
+                for (int c = 0; c < m.images[k].channels; ++c)
+                    for (int j = 0; j <= maxy - miny; ++j)
+                        o << "        T ac" << uslot[k] << "_" << c << "_" << j << " = 0;\n";
+            o << "        for (int y = " << qy0 << "; y < y1 - " << miny << "; ++y) {\n";
+            for (auto& w : win) {
+                for (int dy = w.second.first; dy < w.second.second; ++dy)
+                    o << "        " << wname(w.first, dy) << " = " << wname(w.first, dy + 1) << ";\n";
+                o << "        " << wname(w.first, w.second.second) << " = "
+                  << load(w.first, "(y + " + std::to_string(w.second.second) + ")") << ";\n";
+            }
+            o << "        const bool qin = xin && y >= 0 && y < H;\n" << body.str();
+            // output row y + miny has all its centres
+            o << "        const int yo = y + " << miny << ";\n"
+                 "        if (xout && yo >= y0 && yo < y1) {\n"
+                 "        const long long lin = (long long)yo * W + x;\n"
+                 "        const bool act = (a.flags[lin] & 1) != 0;\n";
+            for (int k : unk)
+                for (int c = 0; c < m.images[k].channels; ++c) {
+                    const std::string el = "a.uoff[" + std::to_string(uslot[k]) + "] + lin * " + std::to_string(m.images[k].channels) +
+                                           " + " + std::to_string(c);
+                    o << "        { const long long e = " << el << "; const T acc = ac" << uslot[k] << "_" << c << "_0;\n"
+                         "          if (finish) { const T pe = p[e]; const T o = act ? acc + (dadd ? dadd[e] * pe : (T)0) : (T)0; Ap[e] = o; dot += pe * o; }\n"
+                         "          else Ap[e] = acc; }\n";
+                }
+            o << "        }\n";
+            for (int k : unk)
+                for (int c = 0; c < m.images[k].channels; ++c) {
+                    const std::string a0 = "ac" + std::to_string(uslot[k]) + "_" + std::to_string(c) + "_";
+                    for (int j = 0; j < maxy - miny; ++j) o << "        " << a0 << j << " = " << a0 << j + 1 << ";\n";
+                    o << "        " << a0 << maxy - miny << " = 0;\n";
+                }
+            o << "        }\n"
+                 "    }\n"
+                 "    if (finish) { double v[1] = {(double)dot}; block_reduce_publish<1>(v, rs, blockIdx.x); }\n}\n";
+        }
+    }
+
     // ------------------------------------------------------------ gen_dump_j_<i>
     // saveJToCRS / saveJToCRS_Graph (solverGPUGaussNewton.t:1004-1022, 1287-1305) with
     // generateDumpJ (:385-442): the residuals grouped into energy specs by domain in order
@@ -871,7 +1035,8 @@ GenSource generate(GModel& m, bool dbl) {
     g_cache = nullptr;
     char note[128];
     snprintf(note, sizeof(note), "// apply: %s (%.2f residual instances per centred residual)\n",
-             gs.prefer_tiled ? "gen_apply_tiled" : "gen_apply", gs.instances_per_residual);
+             gs.has_strip ? "gen_apply_strip" : gs.prefer_tiled ? "gen_apply_tiled" : "gen_apply",
+             gs.instances_per_residual);
     gs.code = note + o.str();
     return gs;
 }

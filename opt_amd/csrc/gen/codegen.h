@@ -39,6 +39,8 @@ struct GenSource {
     size_t tiled_lds = 0;              // its LDS bytes
     double instances_per_residual = 0; // distinct (residual, shift) instances / centred residuals
     bool prefer_tiled = false;         // the plan's default apply (static rule, codegen.cpp)
+    bool has_strip = false;            // gen_apply_strip emitted (2-D centred, no sampled reads)
+    int strip_cols = 64;               // its output columns per wave
     // materialized J (saveJToCRS): one kernel gen_dump_j_<i> per energy spec, in order;
     // spec i: domain (-1 centred, else graph id), residual rows and nonzeros per element
     struct DumpSpec { int graph; int rows; int nnz; };

@@ -460,14 +460,24 @@ private:
                         std::make_pair(&k_cost_, "gen_cost"), std::make_pair(&k_jtf_graph_, "gen_jtf_graph"),
                         std::make_pair(&k_apply_graph_, "gen_apply_graph")})
             OPT_HIP_CHECK(hipModuleGetFunction(kv.first, mod_, kv.second));
-        // the two-phase LDS-tiled apply where the front end emitted one and prefers it
-        // (prefer_tiled: many residual instances per pixel); OPT_AMD_GEN_TILED=0/1 forces
-        // (row slabs use the gather: its reads stay within row_halo() of the owned rows)
+        // Centred apply: the register strip where the front end emitted one, else the
+        // two-phase LDS tiles where it prefers them (prefer_tiled: many residual instances
+        // per pixel), else the gather. OPT_AMD_GEN_APPLY=gather|tiled|strip forces one.
+        // (Row slabs use the gather: its reads stay within row_halo() of the owned rows.)
         const bool slab = dom_.mem_rows != dom_.H || dom_.y_lo != 0;
+        const char* want = getenv("OPT_AMD_GEN_APPLY");
+        const std::string force = want ? want : "";
         if (src_.has_tiled && !slab) {
             OPT_HIP_CHECK(hipModuleGetFunction(&k_apply_tiled_, mod_, "gen_apply_tiled"));
-            const int force = env_int("OPT_AMD_GEN_TILED", -1);
-            if (force == 1 || (force < 0 && src_.prefer_tiled)) k_apply_ = k_apply_tiled_;
+            if (force == "tiled" || (force.empty() && src_.prefer_tiled)) k_apply_ = k_apply_tiled_;
+        }
+        if (src_.has_strip && !slab) {
+            // one wave per (column strip, >= 8-row block): a small image leaves most SIMDs
+            // idle (poisson 512^2: 576 waves, 13.7 -> 20.4 us), so below ~2 waves per SIMD
+            // the other forms run
+            OPT_HIP_CHECK(hipModuleGetFunction(&k_apply_strip_, mod_, "gen_apply_strip"));
+            const long long waves = (long long)((dims_[0] + src_.strip_cols - 1) / src_.strip_cols) * ((dims_[1] + 7) / 8);
+            if (force == "strip" || (force.empty() && waves >= 2048)) k_apply_ = k_apply_strip_;
         }
         k_dump_.resize(src_.dump.size());
         for (size_t k = 0; k < src_.dump.size(); ++k)
@@ -565,7 +575,7 @@ private:
     int* geid_[16] = {};
     hipModule_t mod_ = nullptr;
     std::vector<hipFunction_t> k_pre_, k_dump_;
-    hipFunction_t k_apply_tiled_{};
+    hipFunction_t k_apply_tiled_{}, k_apply_strip_{};
     hipFunction_t k_jtf_{}, k_apply_{}, k_cost_{}, k_jtf_graph_{}, k_apply_graph_{};
 };
 

@@ -225,10 +225,13 @@ def test_our_energy_files_lower_exactly_as_the_reference_files(name):
     assert api.generic_describe(E(name)) == api.generic_describe(ref)
 
 
-@pytest.mark.parametrize("name,tiled", [("image_warping", False), ("poisson_image_editing", False),
-                                        ("optical_flow", False), ("shape_from_shading", True)])
-def test_apply_variant_rule(name, tiled):
-    """Static choice between the gather and the LDS-tiled apply (codegen.cpp): tiles when
-    the energy has many residual instances per centred residual (measured crossover)."""
+@pytest.mark.parametrize("name,kernel", [("image_warping", "gen_apply_strip"), ("poisson_image_editing", "gen_apply_strip"),
+                                         ("shape_from_shading", "gen_apply_strip"),
+                                         ("intrinsic_image_decomposition", "gen_apply_strip"),
+                                         ("optical_flow", "gen_apply ")])
+def test_apply_variant_rule(name, kernel):
+    """Static choice of the centred apply (codegen.cpp): the register strips for 2-D
+    energies without sampled reads (data-dependent addresses: optical_flow keeps the
+    gather), else tiles when the energy has many residual instances per centred residual."""
     head = api.generic_source(E(name)).splitlines()[0]
-    assert head.startswith("// apply: " + ("gen_apply_tiled" if tiled else "gen_apply "))
+    assert head.startswith("// apply: " + kernel)
