@@ -656,6 +656,10 @@ __global__ __launch_bounds__(kBlock) void iw_model_cost(Args<T> a, const T* __re
 //   r -= alpha Ap;  rz[i+1] = sum r.(pre r)  (pre = r's preconditioner; 1 when
 //   UsePreconditioner(false), :705-708). Two pixels per lane: Offset parts as one
 //   16-B access, angle parts and the angle preconditioner as 8-B, flags as 2 bytes.
+//   Walking each XCD's eighth backwards (so the first reads fall on the Ap lines the
+//   apply wrote last, in the 256 MB infinity cache) was measured: 4.41 -> 4.43 ms per
+//   GN step with streaming loads, 4.57 -> 4.47 without (gpurun_out sweep, tools/sweep_env.py)
+//   — the streaming form stays, in grid-stride order.
 template <typename T, bool NT = false>
 __global__ __launch_bounds__(kBlock) void iw_residual(Args<T> a, const T* __restrict__ Ap,
                                                       const T* __restrict__ pre, T* __restrict__ r,
