@@ -694,7 +694,7 @@ GenSource generate(GModel& m, bool dbl) {
         }
         g_cache = saved;
         int regs = 0;
-        for (auto& w : win) regs += w.second.second - w.second.first + 1;
+        for (auto& w : win) regs += w.second.second - w.second.first + 2;   // + the prefetched row
         int nacc = 0;
         for (int k : unk) nacc += m.images[k].channels;
         regs += nacc * (maxy - miny + 1);
@@ -725,11 +725,14 @@ GenSource generate(GModel& m, bool dbl) {
                        std::to_string(ch) + " + " + std::to_string(c) + "] : (T)0)";
             };
             const std::string qy0 = "(y0 - " + std::to_string(maxy) + ")";
+            // each window's next top row is loaded one row ahead (<window>_n): its loads are
+            // in flight during a whole row of residual arithmetic before they are consumed
             for (auto& w : win) {
                 o << "        T " << wname(w.first, w.second.first) << " = 0";
                 for (int dy = w.second.first + 1; dy <= w.second.second; ++dy)
                     o << ", " << wname(w.first, dy) << " = " << load(w.first, "(" + qy0 + " - 1 + " + std::to_string(dy) + ")");
-                o << ";\n";
+                o << ", " << wname(w.first, w.second.second) << "_n = "
+                  << load(w.first, "(" + qy0 + " + " + std::to_string(w.second.second) + ")") << ";\n";
             }
             for (int k : unk)
                 for (int c = 0; c < m.images[k].channels; ++c)
@@ -739,8 +742,9 @@ GenSource generate(GModel& m, bool dbl) {
             for (auto& w : win) {
                 for (int dy = w.second.first; dy < w.second.second; ++dy)
                     o << "        " << wname(w.first, dy) << " = " << wname(w.first, dy + 1) << ";\n";
-                o << "        " << wname(w.first, w.second.second) << " = "
-                  << load(w.first, "(y + " + std::to_string(w.second.second) + ")") << ";\n";
+                o << "        " << wname(w.first, w.second.second) << " = " << wname(w.first, w.second.second) << "_n;\n"
+                  << "        " << wname(w.first, w.second.second) << "_n = "
+                  << load(w.first, "(y + " + std::to_string(w.second.second + 1) + ")") << ";\n";
             }
             o << "        const bool qin = xin && y >= 0 && y < H;\n" << body.str();
             // output row y + miny has all its centres
@@ -752,8 +756,13 @@ GenSource generate(GModel& m, bool dbl) {
                 for (int c = 0; c < m.images[k].channels; ++c) {
                     const std::string el = "a.uoff[" + std::to_string(uslot[k]) + "] + lin * " + std::to_string(m.images[k].channels) +
                                            " + " + std::to_string(c);
+                    // p at the output pixel: its row window when one holds row yo (same load)
+                    std::string pe = "p[e]";
+                    auto wi = win.find(std::make_tuple(1, k, c));
+                    if (wi != win.end() && wi->second.first <= miny && miny <= wi->second.second)
+                        pe = wname(wi->first, miny);
                     o << "        { const long long e = " << el << "; const T acc = ac" << uslot[k] << "_" << c << "_0;\n"
-                         "          if (finish) { const T pe = p[e]; const T o = act ? acc + (dadd ? dadd[e] * pe : (T)0) : (T)0; Ap[e] = o; dot += pe * o; }\n"
+                         "          if (finish) { const T pe = " << pe << "; const T o = act ? acc + (dadd ? dadd[e] * pe : (T)0) : (T)0; Ap[e] = o; dot += pe * o; }\n"
                          "          else Ap[e] = acc; }\n";
                 }
             o << "        }\n";
