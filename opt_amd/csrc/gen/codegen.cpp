@@ -226,7 +226,7 @@ private:
         }
         if (centred_) return centred_(n, vname);
         idx ="(li + " + rel(n.off) + ") * " + ch + " + " + c;
-        return "((" + inb(n.off) + ") ? (T)(" + base + ")[" + idx + "] : (T)0)";
+        return "opt_ldm(" + base + ", " + idx + ", " + inb(n.off) + ")";
     }
 
     GModel& M_;
@@ -284,6 +284,10 @@ GenSource generate(GModel& m, bool dbl) {
          "__device__ __forceinline__ double opt_lr(double v) { return opt_dd(v, true); }\n"
          "__device__ __forceinline__ double opt_ll(double v) { return opt_dd(v, false); }\n"
          "__device__ __forceinline__ T opt_sh(T v, int d) { for (; d > 0; --d) v = opt_lr(v); for (; d < 0; ++d) v = opt_ll(v); return v; }\n";
+    // masked read without a branch: the load always issues (at element 0 of the array when
+    // the access is outside), the value is selected afterwards
+    o << "template <typename E> __device__ __forceinline__ T opt_ldm(const E* b, long long i, bool c) {\n"
+         "    const E v = b[c ? i : 0]; return c ? (T)v : (T)0;\n}\n";
     // Image:get / Image:sample (o.t:856-876): floor / ceil taps, zero outside, lerps in T
     o << "template <typename E> __device__ __forceinline__ T opt_tap(const E* im, int nch, int c, int x, int y, int W, int H) {\n"
          "    return (x >= 0 && x < W && y >= 0 && y < H) ? (T)im[((long long)y * W + x) * nch + c] : (T)0;\n}\n"
@@ -721,8 +725,8 @@ GenSource generate(GModel& m, bool dbl) {
                     ? "(p + a.uoff[" + std::to_string(uslot[i]) + "])"
                     : "((const " + std::string(elem_type(m.images[i].elem, m.images[i].tvalued)) + "*)a.img[" +
                           std::to_string(i) + "])";
-                return "((xin && " + yy + " >= 0 && " + yy + " < H) ? (T)" + base + "[(long long)(" + yy + " * W + x) * " +
-                       std::to_string(ch) + " + " + std::to_string(c) + "] : (T)0)";
+                return "opt_ldm(" + base + ", (long long)(" + yy + " * W + x) * " + std::to_string(ch) + " + " +
+                       std::to_string(c) + ", xin && " + yy + " >= 0 && " + yy + " < H)";
             };
             const std::string qy0 = "(y0 - " + std::to_string(maxy) + ")";
             // each window's next top row is loaded one row ahead (<window>_n): its loads are
