@@ -287,7 +287,17 @@ GenSource generate(GModel& m, bool dbl) {
     // masked read without a branch: the load always issues (at element 0 of the array when
     // the access is outside), the value is selected afterwards
     o << "template <typename E> __device__ __forceinline__ T opt_ldm(const E* b, long long i, bool c) {\n"
-         "    const E v = b[c ? i : 0]; return c ? (T)v : (T)0;\n}\n";
+         "    const E v = b[c ? i : 0]; return c ? (T)v : (T)0;\n}\n"
+         // both channels of a 2-channel element (i = its first channel) in one access when
+         // the array is aligned for it (a uniform branch), else two
+         "template <typename E> __device__ __forceinline__ void opt_ldm2(const E* b, long long i, bool c, T& v0, T& v1) {\n"
+         "    const long long j = c ? i : 0;\n"
+         "    E x, y;\n"
+         "    if ((((unsigned long long)b) & (2 * sizeof(E) - 1)) == 0) {\n"
+         "        struct alignas(2 * sizeof(E)) P2 { E x, y; };\n"
+         "        const P2 v = *reinterpret_cast<const P2*>(b + j); x = v.x; y = v.y;\n"
+         "    } else { x = b[j]; y = b[j + 1]; }\n"
+         "    v0 = c ? (T)x : (T)0; v1 = c ? (T)y : (T)0;\n}\n";
     // Image:get / Image:sample (o.t:856-876): floor / ceil taps, zero outside, lerps in T
     o << "template <typename E> __device__ __forceinline__ T opt_tap(const E* im, int nch, int c, int x, int y, int W, int H) {\n"
          "    return (x >= 0 && x < W && y >= 0 && y < H) ? (T)im[((long long)y * W + x) * nch + c] : (T)0;\n}\n"
@@ -719,24 +729,52 @@ GenSource generate(GModel& m, bool dbl) {
                  "        const int x = (wid % nsx) * " << nout << " + lane - " << loff << ";\n"
                  "        const int y0 = (wid / nsx) * RB, y1 = min(H, y0 + RB);\n"
                  "        const bool xin = x >= 0 && x < W, xout = xin && lane >= " << loff << " && lane < " << loff + nout << ";\n";
-            auto load = [&](const std::tuple<int, int, int>& k, const std::string& yy) {
+            auto base_of = [&](const std::tuple<int, int, int>& k) {
+                const int i = std::get<1>(k);
+                return std::get<0>(k) ? "(p + a.uoff[" + std::to_string(uslot[i]) + "])"
+                                      : "((const " + std::string(elem_type(m.images[i].elem, m.images[i].tvalued)) +
+                                            "*)a.img[" + std::to_string(i) + "])";
+            };
+            // the two channels of a 2-channel array whose windows span the same rows are
+            // read as one 8 / 16-byte access (opt_ldm2)
+            auto partner = [&](const std::tuple<int, int, int>& k) -> const std::pair<int, int>* {
+                const int i = std::get<1>(k);
+                if (m.images[i].channels != 2) return nullptr;
+                auto a0 = win.find(std::make_tuple(std::get<0>(k), i, 0));
+                auto a1 = win.find(std::make_tuple(std::get<0>(k), i, 1));
+                if (a0 == win.end() || a1 == win.end() || a0->second != a1->second) return nullptr;
+                return &a1->second;
+            };
+            // statement loading row yy of window k into `dst` (and of its partner channel)
+            auto load = [&](const std::tuple<int, int, int>& k, const std::string& yy, int dy, const char* sfx) {
                 const int i = std::get<1>(k), c = std::get<2>(k), ch = m.images[i].channels;
-                const std::string base = std::get<0>(k)
-                    ? "(p + a.uoff[" + std::to_string(uslot[i]) + "])"
-                    : "((const " + std::string(elem_type(m.images[i].elem, m.images[i].tvalued)) + "*)a.img[" +
-                          std::to_string(i) + "])";
-                return "opt_ldm(" + base + ", (long long)(" + yy + " * W + x) * " + std::to_string(ch) + " + " +
-                       std::to_string(c) + ", xin && " + yy + " >= 0 && " + yy + " < H)";
+                const std::string cond = "xin && " + yy + " >= 0 && " + yy + " < H";
+                const std::string pix = "(long long)(" + yy + " * W + x) * " + std::to_string(ch);
+                if (partner(k)) {
+                    if (c == 1) return std::string();
+                    const auto k1 = std::make_tuple(std::get<0>(k), i, 1);
+                    return "opt_ldm2(" + base_of(k) + ", " + pix + ", " + cond + ", " + wname(k, dy) + sfx + ", " +
+                           wname(k1, dy) + sfx + ");";
+                }
+                return wname(k, dy) + sfx + " = opt_ldm(" + base_of(k) + ", " + pix + " + " + std::to_string(c) +
+                       ", " + cond + ");";
             };
             const std::string qy0 = "(y0 - " + std::to_string(maxy) + ")";
             // each window's next top row is loaded one row ahead (<window>_n): its loads are
             // in flight during a whole row of residual arithmetic before they are consumed
             for (auto& w : win) {
-                o << "        T " << wname(w.first, w.second.first) << " = 0";
-                for (int dy = w.second.first + 1; dy <= w.second.second; ++dy)
-                    o << ", " << wname(w.first, dy) << " = " << load(w.first, "(" + qy0 + " - 1 + " + std::to_string(dy) + ")");
-                o << ", " << wname(w.first, w.second.second) << "_n = "
-                  << load(w.first, "(" + qy0 + " + " + std::to_string(w.second.second) + ")") << ";\n";
+                o << "        T " << wname(w.first, w.second.second) << "_n = 0";
+                for (int dy = w.second.first; dy <= w.second.second; ++dy) o << ", " << wname(w.first, dy) << " = 0";
+                o << ";\n";
+            }
+            for (auto& w : win) {
+                for (int dy = w.second.first + 1; dy <= w.second.second; ++dy) {
+                    const std::string st = load(w.first, "(" + qy0 + " - 1 + " + std::to_string(dy) + ")", dy, "");
+                    if (!st.empty()) o << "        " << st << "\n";
+                }
+                const std::string st = load(w.first, "(" + qy0 + " + " + std::to_string(w.second.second) + ")",
+                                            w.second.second, "_n");
+                if (!st.empty()) o << "        " << st << "\n";
             }
             for (int k : unk)
                 for (int c = 0; c < m.images[k].channels; ++c)
@@ -746,9 +784,11 @@ GenSource generate(GModel& m, bool dbl) {
             for (auto& w : win) {
                 for (int dy = w.second.first; dy < w.second.second; ++dy)
                     o << "        " << wname(w.first, dy) << " = " << wname(w.first, dy + 1) << ";\n";
-                o << "        " << wname(w.first, w.second.second) << " = " << wname(w.first, w.second.second) << "_n;\n"
-                  << "        " << wname(w.first, w.second.second) << "_n = "
-                  << load(w.first, "(y + " + std::to_string(w.second.second + 1) + ")") << ";\n";
+                o << "        " << wname(w.first, w.second.second) << " = " << wname(w.first, w.second.second) << "_n;\n";
+            }
+            for (auto& w : win) {
+                const std::string st = load(w.first, "(y + " + std::to_string(w.second.second + 1) + ")", w.second.second, "_n");
+                if (!st.empty()) o << "        " << st << "\n";
             }
             o << "        const bool qin = xin && y >= 0 && y < H;\n" << body.str();
             // output row y + miny has all its centres
