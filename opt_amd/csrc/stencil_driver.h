@@ -124,6 +124,8 @@ __device__ __forceinline__ void zeta_test(const ZetaArgs& z, double q1) {
 // PCGStep2 (:665-731): alpha = sc[i_num]/sc[i_den]; delta (+)= alpha p; r -= alpha Ap;
 // z = pre r (r when UsePreconditioner(false)); out[0] = sum z.r; LM: out[1] = q =
 // sum 1/2 delta.(r + b).
+// (16-byte vector accesses per thread were measured: shape_from_shading LM 3.46 -> 3.41 ms,
+// optical_flow fp64 LM 5.02 -> 5.05, generated image_warping GN 7.98 -> 8.27 — kept scalar.)
 template <typename T, bool FIRST, bool LM>
 __global__ __launch_bounds__(kBlock) void step2_kernel(long long n, const T* __restrict__ p,
                                                        const T* __restrict__ Ap, const T* __restrict__ pre,
