@@ -126,7 +126,8 @@ __device__ __forceinline__ void zeta_test(const ZetaArgs& z, double q1) {
 // sum 1/2 delta.(r + b).
 // (16-byte vector accesses per thread were measured: shape_from_shading LM 3.46 -> 3.41 ms,
 // optical_flow fp64 LM 5.02 -> 5.05, generated image_warping GN 7.98 -> 8.27 — kept scalar.)
-template <typename T, bool FIRST, bool LM>
+// DELTA false (GN): the delta update is left to step3_kernel, which reads p_old anyway.
+template <typename T, bool FIRST, bool LM, bool DELTA = true>
 __global__ __launch_bounds__(kBlock) void step2_kernel(long long n, const T* __restrict__ p,
                                                        const T* __restrict__ Ap, const T* __restrict__ pre,
                                                        const T* __restrict__ b, T* __restrict__ r,
@@ -138,9 +139,12 @@ __global__ __launch_bounds__(kBlock) void step2_kernel(long long n, const T* __r
     T acc = 0, accq = 0;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
-        const T d = FIRST ? alpha * p[e] : delta[e] + alpha * p[e];
         const T rr = r[e] - alpha * Ap[e];
-        delta[e] = d;
+        T d = 0;
+        if (DELTA) {
+            d = FIRST ? alpha * p[e] : delta[e] + alpha * p[e];
+            delta[e] = d;
+        }
         r[e] = rr;
         const T z = use_pre ? pre[e] * rr : rr;
         acc += z * rr;
@@ -157,17 +161,24 @@ __global__ __launch_bounds__(kBlock) void step2_kernel(long long n, const T* __r
 }
 
 // PCGStep3 (:814-845): beta = sc[i_num]/sc[i_den]; p = z + beta p.
-template <typename T>
+// DM (GN, PCGStep2's delta update moved here, where p_old is read anyway; same
+// expression): 1 delta = alpha p_old, 2 delta += alpha p_old, alpha = sc[ia_num]/sc[ia_den].
+template <typename T, int DM = 0>
 __global__ __launch_bounds__(kBlock) void step3_kernel(long long n, const T* __restrict__ pre,
                                                        const T* __restrict__ r, T* __restrict__ p,
                                                        const double* __restrict__ sc, int i_num, int i_den,
-                                                       int use_pre, const int* stop) {
+                                                       int use_pre, const int* stop, T* __restrict__ delta = nullptr,
+                                                       int ia_num = 0, int ia_den = 0) {
     if (stopped(stop)) return;
     const T beta = (T)(sc[i_num] / sc[i_den]);
+    const T alpha = DM ? (T)(sc[ia_num] / sc[ia_den]) : (T)0;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
         const T z = use_pre ? pre[e] * r[e] : r[e];
-        p[e] = z + beta * p[e];
+        const T po = p[e];
+        if (DM == 1) delta[e] = alpha * po;
+        if (DM == 2) delta[e] = delta[e] + alpha * po;
+        p[e] = z + beta * po;
     }
 }
 

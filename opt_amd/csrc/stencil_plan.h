@@ -245,6 +245,9 @@ public:
     // PCG inner loop (PCGStep1-3, :607-845) of one step; launches only, no host sync.
     void pcg_loop(int Lit, int use_pre, const int* stop) {
         const bool fuse3 = !distributed() && !mat_ && fuse3_on_;
+        // GN with step3_kernel: the delta update rides in PCGStep3 (reads p_old anyway)
+        bool d3 = !lm_ && delta3_on_;
+        if constexpr (HasFusedStep3<Op>::value) d3 = d3 && !fuse3;
         for (int i = 0; i < Lit; ++i) {
             // the zeta test rides in the kernel that reduces q (one GPU), else its own launch
             const ZetaArgs z{red_.scalars + kScQ0, stop_, i, sp_.q_tolerance, (lm_ && !distributed()) ? 1 : 0};
@@ -291,7 +294,7 @@ public:
                                    red_.slot(fg(), rz(i + 1)), z);
             } else {
                 tbegin("step2");
-                launch_step2(i == 0, rz(i), pap(i), rz(i + 1), stop, z);
+                launch_step2(i == 0, rz(i), pap(i), rz(i + 1), stop, z, !d3);
                 tend();
             }
             allreduce(rz(i + 1), lm_ ? 2 : 1);   // rz and q sit side by side
@@ -302,7 +305,13 @@ public:
                     op_->step3_fused(pre_, r_, p_, red_.scalars, rz(i + 1), rz(i), use_pre, stop, stream_);
                     fused = true;
                 }
-            if (!fused)
+            if (!fused && d3 && i == 0)
+                hipLaunchKernelGGL((step3_kernel<T, 1>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)pre_,
+                                   (const T*)r_, p_, red_.scalars, rz(i + 1), rz(i), use_pre, stop, delta_, rz(i), pap(i));
+            else if (!fused && d3)
+                hipLaunchKernelGGL((step3_kernel<T, 2>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)pre_,
+                                   (const T*)r_, p_, red_.scalars, rz(i + 1), rz(i), use_pre, stop, delta_, rz(i), pap(i));
+            else if (!fused)
                 hipLaunchKernelGGL((step3_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)pre_,
                                    (const T*)r_, p_, red_.scalars, rz(i + 1), rz(i), use_pre, stop);
             tend();
@@ -611,18 +620,20 @@ private:
         exchange(pl);
     }
 
-    void launch_step2(bool first, int i_num, int i_den, int out, const int* stop, ZetaArgs z = {}) {
+    void launch_step2(bool first, int i_num, int i_den, int out, const int* stop, ZetaArgs z = {},
+                      bool delta = true) {
         const int g = fg();
         const int use_pre = spec_.use_preconditioner ? 1 : 0;
         auto slot = red_.slot(g, out);
-#define S2(F, LMV)                                                                                     \
-    hipLaunchKernelGGL((step2_kernel<T, F, LMV>), dim3(g), dim3(kBlock), 0, stream_, n_, (const T*)p_,   \
+#define S2(F, LMV, D)                                                                                  \
+    hipLaunchKernelGGL((step2_kernel<T, F, LMV, D>), dim3(g), dim3(kBlock), 0, stream_, n_, (const T*)p_, \
                        (const T*)Ap_, (const T*)pre_, (const T*)b_, r_, delta_, red_.scalars, i_num,    \
                        i_den, use_pre, stop, slot, z)
-        if (first && lm_) S2(true, true);
-        else if (first) S2(true, false);
-        else if (lm_) S2(false, true);
-        else S2(false, false);
+        if (first && lm_) S2(true, true, true);
+        else if (lm_) S2(false, true, true);
+        else if (!delta) S2(false, false, false);
+        else if (first) S2(true, false, true);
+        else S2(false, false, true);
 #undef S2
     }
     UnknownPtrs<T> unknowns() {
@@ -688,7 +699,8 @@ private:
     bool capturing_ = false;
     const bool graph_off_ = getenv("OPT_AMD_NO_GRAPH") && atoi(getenv("OPT_AMD_NO_GRAPH"));
     const bool overlap_ = env_int("OPT_AMD_HALO_OVERLAP", 1) != 0;   // 0: blocking halo before each apply
-    const bool fuse3_on_ = env_int("OPT_AMD_FUSE_STEP3", 1) != 0;    // 0: step3_kernel + the whole apply
+    const bool fuse3_on_ = env_int("OPT_AMD_FUSE_STEP3", 1) != 0;
+    const bool delta3_on_ = env_int("OPT_AMD_DELTA_IN_STEP3", 1) != 0;   // 0: delta updated by step2    // 0: step3_kernel + the whole apply
     std::unique_ptr<MaterializedJacobian<T>> mat_;
     float radius_ = 1e4f, decrease_ = 2.0f;
 };
