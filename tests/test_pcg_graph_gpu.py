@@ -119,3 +119,28 @@ def test_graph_energy_rebinding_edges_matches_eager(monkeypatch):
     assert len(c_eager) >= 3
     assert c_graph == c_eager
     np.testing.assert_array_equal(o_graph, o_eager)
+
+
+def _gn_delta(monkeypatch, d3, generic):
+    """A GN solve with PCGStep2's delta update in PCGStep3 (d3) or in PCGStep2."""
+    monkeypatch.setenv("OPT_AMD_DELTA_IN_STEP3", "1" if d3 else "0")
+    if generic:
+        monkeypatch.setenv("OPT_AMD_GENERIC", "1")
+        w = perturbed(61, 43, seed=12)
+        s = solver(61, 43, kind="gaussNewtonGPU")
+        assert s.family() == "generic"
+        prm = device_params(w)
+        s.set_solver_params({"nIterations": 4, "lIterations": 10})
+        return s.profiled_solve(prm), prm[0].cpu().numpy()
+    return _poisson(monkeypatch, True, "gaussNewtonGPU")
+
+
+@pytest.mark.parametrize("generic", [False, True])
+def test_delta_in_step3_is_bitwise_step2(monkeypatch, generic):
+    """The generic GN driver forms delta += alpha p_old in PCGStep3 (stencil_driver.h
+    step3_kernel DM) instead of PCGStep2: the same expression on the same operands, so
+    whole solves are bitwise those with the reference's placement (:665-731)."""
+    c1, x1 = _gn_delta(monkeypatch, True, generic)
+    c0, x0 = _gn_delta(monkeypatch, False, generic)
+    assert c1 == c0
+    np.testing.assert_array_equal(x1, x0)
