@@ -1038,12 +1038,21 @@ GenSource generate(GModel& m, bool dbl) {
                     }
                 }
                 // { own-vertex values; for each incident edge { the other slots; the rest } }
+                // the other slots' vertices come from per-incidence-order copies (one load
+                // each instead of the edge id, then the slot array)
                 o << "        {\n        const int v" << k << " = (int)vtx;\n" << pre.str()
-                  << "        for (int q = a.goff[" << sbk << "][vtx]; q < a.goff[" << sbk << "][vtx + 1]; ++q) {\n"
-                  << "        const int e = a.geid[" << sbk << "][q];\n";
+                  << "        for (int q = a.goff[" << sbk << "][vtx]; q < a.goff[" << sbk << "][vtx + 1]; ++q) {\n";
                 for (size_t s2 = 0; s2 < nslots; ++s2)
-                    if (s2 != k)
-                        o << "        const int v" << s2 << " = a.slot[" << gs.slot_base[g] + (int)s2 << "][e];\n";
+                    if (s2 != k) {
+                        const std::pair<int, int> key(sbk, gs.slot_base[g] + (int)s2);
+                        auto it = std::find(gs.nb_pairs.begin(), gs.nb_pairs.end(), key);
+                        int idx = (int)(it - gs.nb_pairs.begin());
+                        if (it == gs.nb_pairs.end()) gs.nb_pairs.push_back(key);
+                        if (idx < 32)   // GenArgs::gnb capacity; past it, through the edge id
+                            o << "        const int v" << s2 << " = a.gnb[" << idx << "][q];\n";
+                        else
+                            o << "        const int v" << s2 << " = a.slot[" << key.second << "][a.geid[" << sbk << "][q]];\n";
+                    }
                 o << body.str() << "        }\n        }\n";
             }
         }

@@ -17,6 +17,7 @@
         const int* slot[16];        /* graph vertex arrays, graph-major */                  \
         const int* goff[16];        /* per slot: incidence offsets by vertex (N+1) */       \
         const int* geid[16];        /* per slot: incident edge ids, ascending */            \
+        const int* gnb[32];         /* per (slot k, other slot): its vertex per incident edge */ \
         int nedge[4];               /* edges per graph */                                   \
         unsigned char* flags;       /* bit0: active (not excluded) */                       \
         long long uoff[4];          /* offset of each unknown image in the vector */        \
@@ -45,6 +46,9 @@ struct GenSource {
     // spec i: domain (-1 centred, else graph id), residual rows and nonzeros per element
     struct DumpSpec { int graph; int rows; int nnz; };
     std::vector<DumpSpec> dump;
+    // GenArgs::gnb[i] = slot nb_pairs[i].second's vertex of each edge in slot
+    // nb_pairs[i].first's incidence order (the graph gathers read neighbours through it)
+    std::vector<std::pair<int, int>> nb_pairs;
 };
 
 // Generate the kernels for `m` in float (dbl = false) or double.

@@ -68,6 +68,10 @@ __global__ void incidence_count(const int* keys, int E, int* counts) {
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < E; e += gridDim.x * blockDim.x)
         atomicAdd(&counts[keys[e]], 1);
 }
+// out[q] = slot[geid[q]]: one slot's vertex of each edge of an incidence list, in its order
+__global__ void incidence_gather(const int* slot, const int* geid, int E, int* out) {
+    for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < E; q += gridDim.x * blockDim.x) out[q] = slot[geid[q]];
+}
 __global__ void iota_kernel(int* v, int n) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) v[i] = i;
 }
@@ -255,6 +259,7 @@ public:
         for (void* p : dimg_) dfree(p);
         for (int* p : dslot_) dfree(p);
         for (int k = 0; k < 16; ++k) { dfree(goff_[k]); dfree(geid_[k]); }
+        for (int k = 0; k < 32; ++k) dfree(gnb_[k]);
         dfree(fp_scratch_);
         if (mod_) (void)hipModuleUnload(mod_);
     }
@@ -516,12 +521,28 @@ private:
                     }
                     build_incidence(sb + k, nedge_[g], s);
                 }
+                for (int k = 0; k < ns; ++k) build_neighbours(sb + k, nedge_[g], s);
             }
             sb += ns;
         }
         for (int k = 0; k < sb; ++k) {
             a_.goff[k] = goff_[k];
             a_.geid[k] = geid_[k];
+        }
+        for (size_t i = 0; i < src_.nb_pairs.size() && i < 32; ++i) a_.gnb[i] = gnb_[i];
+    }
+    // GenArgs::gnb of every (slot k, other slot) pair whose incidence list was rebuilt:
+    // the other slot's vertex of each incident edge, in the incidence order
+    void build_neighbours(int sb, int E, hipStream_t s) {
+        for (size_t i = 0; i < src_.nb_pairs.size() && i < 32; ++i) {
+            if (src_.nb_pairs[i].first != sb) continue;
+            dfree(gnb_[i]);
+            gnb_[i] = (int*)dmalloc(sizeof(int) * std::max(E, 1));
+            if (E == 0) continue;
+            const int grid = std::min((E + 255) / 256, 4096);
+            hipLaunchKernelGGL(incidence_gather, dim3(grid), dim3(256), 0, s, a_.slot[src_.nb_pairs[i].second],
+                               (const int*)geid_[sb], E, gnb_[i]);
+            OPT_HIP_CHECK(hipGetLastError());
         }
     }
     // Edges by vertex for slot array sb: a stable radix sort of (vertex, edge id) pairs and
@@ -573,6 +594,7 @@ private:
     unsigned long long* fp_scratch_ = nullptr;
     int* goff_[16] = {};
     int* geid_[16] = {};
+    int* gnb_[32] = {};
     hipModule_t mod_ = nullptr;
     std::vector<hipFunction_t> k_pre_, k_dump_;
     hipFunction_t k_apply_tiled_{}, k_apply_strip_{};
