@@ -275,6 +275,9 @@ __device__ __forceinline__ PRow<T> finish_prow(const Args<T>& a, const PRaw<T>& 
 //         iteration's delta update (PCGStep2's delta += alpha p, :680), alpha =
 //         sc[ia_num]/sc[ia_den]: DM 1 delta = alpha p_old, DM 2 delta += alpha p_old.
 // Always: sc[rs.out] = sum p.Ap over active pixels (the alpha denominator).
+// (Measured: even waves walking bottom-up so both waves at a shared row-block boundary
+// read its halo rows at the same moment — 4.43 ms per GN step either way, the in-loop
+// apply 296-298 us either way; every wave walks top-down.)
 // LMX (MODE 0 only, the generic LM driver): Ap += dadd p (the CtC term of
 // PCGStep1's LM variant, :617-622) and the whole grid returns at entry once the
 // device-side zeta test has set *stop.
