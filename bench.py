@@ -78,6 +78,23 @@ def pmc_traffic(liter: int):
     return total / liter
 
 
+PMC_FILE_SFS = os.path.join(ROOT, "profiles", "r02_pmc_sfs.json")
+
+
+def pmc_traffic_sfs():
+    """The same for the shape_from_shading leg: the in-loop J^T J p strip (sfs_strip<float,
+    false>) from the committed PMC summary of that workload (tools/measure_r02.sh)."""
+    try:
+        with open(PMC_FILE_SFS) as f:
+            ks = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    hit = [v for k, v in ks.items() if "sfs_strip<float, false>" in k]
+    if not hit or "FETCH_SIZE" not in hit[0] or "WRITE_SIZE" not in hit[0]:
+        return None
+    return (2.0 * hit[0]["FETCH_SIZE"] + hit[0]["WRITE_SIZE"]) * 1024.0
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -279,8 +296,10 @@ def main():
             "peak": PEAK_HBM_GBS,
             "unit": "GB/s",
             "frac": achieved / PEAK_HBM_GBS,
-            "traffic": (pmc_traffic(args.liter) if world == 1 and args.size == 4096 and not sfs else None),
-            "traffic_unit": f"bytes per launch (2 FETCH_SIZE + WRITE_SIZE, {os.path.relpath(PMC_FILE, ROOT)})",
+            "traffic": (None if world != 1 or args.size != 4096 else
+                        pmc_traffic_sfs() if sfs else pmc_traffic(args.liter)),
+            "traffic_unit": "bytes per launch (2 FETCH_SIZE + WRITE_SIZE, "
+                            f"{os.path.relpath(PMC_FILE_SFS if sfs else PMC_FILE, ROOT)})",
             "avg_us": avg_apply_s * 1e6,
             "launches": n_apply,
             "bytes_per_px": bpp,

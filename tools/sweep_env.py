@@ -33,7 +33,7 @@ def main():
         s.set_solver_params({"nIterations": 2 + rounds * steps + steps + 2, "lIterations": 10})
         s.init(prm)
         s.step()
-        solvers.append((c or "default", s))
+        solvers.append((f"{len(solvers)}:{c or 'default'}", s))
         for kv in filter(None, c.split(",")):
             os.environ.pop(kv.split("=")[0])
     times = {c: [] for c, _ in solvers}
