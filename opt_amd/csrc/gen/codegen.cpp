@@ -647,10 +647,15 @@ GenSource generate(GModel& m, bool dbl) {
     // No LDS and no barriers: the hand-written image_warping / SFS applies work this way.
     // Same instance set as createjtjcentered (o.t:2770-2830): centres outside the image
     // contribute nothing (gen_apply_tiled's rule).
-    if (tiled) {
+    // gen_jtf_strip: the same walk for J^T F + diag(J^T J) + flags: each centre's residual
+    // values R_r and partials d(r, u) once, d R and d^2 accumulated per output offset; the
+    // output's Exclude is evaluated at the output row (shifted by miny). Same instance set.
+    auto strip_kernel = [&](bool jtf) {
         bool ok = true;
         for (int ci : cres)
             P.visit(m.residuals[ci].expr, [&](int, const Node& n) { ok &= n.op != Op::Sample; });
+        if (jtf && m.exclude >= 0)
+            P.visit(m.exclude, [&](int, const Node& n) { ok &= n.op != Op::Sample && !(n.op == Op::Read && n.slot >= 0); });
         // rows each (p?, image, channel) window must hold, lane reach of the reads
         std::map<std::tuple<int, int, int>, std::pair<int, int>> win;
         int rxlo = 0, rxhi = 0;
@@ -658,7 +663,7 @@ GenSource generate(GModel& m, bool dbl) {
             return std::string(std::get<0>(k) ? "wp" : "wi") + std::to_string(std::get<1>(k)) + "c" +
                    std::to_string(std::get<2>(k)) + (dy < 0 ? "m" : "p") + std::to_string(std::abs(dy));
         };
-        std::ostringstream body;
+        std::ostringstream body, fin;
         const CacheMap* saved = g_cache;
         g_cache = nullptr;   // sin / cos of a window value: no cache images
         {
@@ -687,23 +692,50 @@ GenSource generate(GModel& m, bool dbl) {
                         P.is_const(ents[ei].dnode, &cv);
                         dname[ei] = lit(cv);
                     }
-                    sum += " + " + dn + " * " + b.vec(ents[ei].u, "p");
+                    if (!jtf) sum += " + " + dn + " * " + b.vec(ents[ei].u, "p");
                 }
-                b.line("const T jp" + std::to_string(ci) + " = qin ? " + sum + " : (T)0;");
+                if (jtf) b.line("const T jp" + std::to_string(ci) + " = qin ? " + b.v(m.residuals[cres[ci]].expr) + " : (T)0;");
+                else b.line("const T jp" + std::to_string(ci) + " = qin ? " + sum + " : (T)0;");
             }
             // contributions per output (image, channel, offset): one lane shift each
-            std::map<std::tuple<int, int, int, int>, std::string> grp;
+            // (jtf: jp holds the residual value; dg the squared partials)
+            std::map<std::tuple<int, int, int, int>, std::pair<std::string, std::string>> grp;
             for (size_t ei = 0; ei < ents.size(); ++ei) {
                 const Node n = P.at(ents[ei].u);
-                std::string& s = grp[std::make_tuple(n.i, n.ch, ents[ei].oy, ents[ei].ox)];
-                s += (s.empty() ? "" : " + ") + dname[ei] + " * jp" + std::to_string(ents[ei].r);
+                auto& s = grp[std::make_tuple(n.i, n.ch, ents[ei].oy, ents[ei].ox)];
+                s.first += (s.first.empty() ? "" : " + ") + dname[ei] + " * jp" + std::to_string(ents[ei].r);
+                if (jtf) {
+                    // a constant partial still only counts where its centre is inside
+                    const std::string d = ents[ei].slot >= 0 ? dname[ei] : "(qin ? " + dname[ei] + " : (T)0)";
+                    s.second += (s.second.empty() ? "" : " + ") + d + " * " + d;
+                }
             }
             for (auto& g : grp) {
                 const int k = std::get<0>(g.first), c = std::get<1>(g.first), oy = std::get<2>(g.first),
                           ox = std::get<3>(g.first);
-                const std::string acc = "ac" + std::to_string(uslot[k]) + "_" + std::to_string(c) + "_" +
-                                        std::to_string(oy - miny);
-                b.line(acc + " += " + (ox == 0 ? "(" + g.second + ")" : "opt_sh(" + g.second + ", " + std::to_string(-ox) + ")") + ";");
+                const std::string sfx = std::to_string(uslot[k]) + "_" + std::to_string(c) + "_" + std::to_string(oy - miny);
+                auto add = [&](const std::string& acc, const std::string& e) {
+                    b.line(acc + " += " + (ox == 0 ? "(" + e + ")" : "opt_sh(" + e + ", " + std::to_string(-ox) + ")") + ";");
+                };
+                add("ac" + sfx, g.second.first);
+                if (jtf) add("dq" + sfx, g.second.second);
+            }
+            if (jtf) {
+                // the output row's Exclude, read from the same windows
+                Body bf(m, fin, nd, uslot);
+                bf.centred_reads([&](const Node& n, const char* vname) {
+                    const auto key = std::make_tuple(vname ? 1 : 0, n.i, n.ch);
+                    auto it = win.find(key);
+                    if (it == win.end()) win[key] = {n.off[1], n.off[1]};
+                    else it->second = {std::min(it->second.first, n.off[1]), std::max(it->second.second, n.off[1])};
+                    rxlo = std::min(rxlo, n.off[0]);
+                    rxhi = std::max(rxhi, n.off[0]);
+                    const std::string w = wname(key, n.off[1]);
+                    return n.off[0] == 0 ? w : "opt_sh(" + w + ", " + std::to_string(n.off[0]) + ")";
+                });
+                const int sh[3] = {0, miny, 0};
+                const std::string act = m.exclude >= 0 ? "(" + bf.v(shifted(m.exclude, sh)) + " == (T)0)" : "true";
+                bf.line("const bool act = " + act + ";");
             }
         }
         g_cache = saved;
@@ -711,115 +743,136 @@ GenSource generate(GModel& m, bool dbl) {
         for (auto& w : win) regs += w.second.second - w.second.first + 2;   // + the prefetched row
         int nacc = 0;
         for (int k : unk) nacc += m.images[k].channels;
-        regs += nacc * (maxy - miny + 1);
+        regs += nacc * (maxy - miny + 1) * (jtf ? 2 : 1);
         const int loff = -rxlo + maxx, nout = 64 + rxlo - rxhi - (maxx - minx);
         ok = ok && nout >= 16 && regs <= 96 * (dbl ? 1 : 2) / 2;
-        if (ok) {
+        if (!ok) return;
+        if (jtf) {
+            gs.has_jtf_strip = true;
+            gs.jtf_strip_cols = nout;
+            o << "extern \"C\" __global__ __launch_bounds__(256) void gen_jtf_strip(GenArgs a, T* __restrict__ r, T* __restrict__ diag) {\n"
+                 "    OPT_COORDS\n";
+        } else {
             gs.has_strip = true;
             gs.strip_cols = nout;
             o << "extern \"C\" __global__ __launch_bounds__(256) void gen_apply_strip(GenArgs a, const T* __restrict__ p, T* __restrict__ Ap,\n"
                  "        const T* __restrict__ dadd, const int* stop, ReduceSlot rs, int finish) {\n"
                  "    if (stop && *stop) return;\n"
                  "    OPT_COORDS\n"
-                 "    T dot = 0;\n"
-                 "    const int lane = threadIdx.x & 63, z = 0; (void)z;\n"
-                 "    const int nsx = (W + " << nout - 1 << ") / " << nout << ", G = gridDim.x * 4;\n"
-                 "    const int RB = max(8, (int)(((long long)H * nsx + G - 1) / G)), nby = (H + RB - 1) / RB;\n"
-                 "    for (int wid = blockIdx.x * 4 + (threadIdx.x >> 6); wid < nsx * nby; wid += G) {\n"
-                 "        const int x = (wid % nsx) * " << nout << " + lane - " << loff << ";\n"
-                 "        const int y0 = (wid / nsx) * RB, y1 = min(H, y0 + RB);\n"
-                 "        const bool xin = x >= 0 && x < W, xout = xin && lane >= " << loff << " && lane < " << loff + nout << ";\n";
-            auto base_of = [&](const std::tuple<int, int, int>& k) {
-                const int i = std::get<1>(k);
-                return std::get<0>(k) ? "(p + a.uoff[" + std::to_string(uslot[i]) + "])"
-                                      : "((const " + std::string(elem_type(m.images[i].elem, m.images[i].tvalued)) +
-                                            "*)a.img[" + std::to_string(i) + "])";
-            };
-            // the two channels of a 2-channel array whose windows span the same rows are
-            // read as one 8 / 16-byte access (opt_ldm2)
-            auto partner = [&](const std::tuple<int, int, int>& k) -> const std::pair<int, int>* {
-                const int i = std::get<1>(k);
-                if (m.images[i].channels != 2) return nullptr;
-                auto a0 = win.find(std::make_tuple(std::get<0>(k), i, 0));
-                auto a1 = win.find(std::make_tuple(std::get<0>(k), i, 1));
-                if (a0 == win.end() || a1 == win.end() || a0->second != a1->second) return nullptr;
-                return &a1->second;
-            };
-            // statement loading row yy of window k into `dst` (and of its partner channel)
-            auto load = [&](const std::tuple<int, int, int>& k, const std::string& yy, int dy, const char* sfx) {
-                const int i = std::get<1>(k), c = std::get<2>(k), ch = m.images[i].channels;
-                const std::string cond = "xin && " + yy + " >= 0 && " + yy + " < H";
-                const std::string pix = "(long long)(" + yy + " * W + x) * " + std::to_string(ch);
-                if (partner(k)) {
-                    if (c == 1) return std::string();
-                    const auto k1 = std::make_tuple(std::get<0>(k), i, 1);
-                    return "opt_ldm2(" + base_of(k) + ", " + pix + ", " + cond + ", " + wname(k, dy) + sfx + ", " +
-                           wname(k1, dy) + sfx + ");";
-                }
-                return wname(k, dy) + sfx + " = opt_ldm(" + base_of(k) + ", " + pix + " + " + std::to_string(c) +
-                       ", " + cond + ");";
-            };
-            const std::string qy0 = "(y0 - " + std::to_string(maxy) + ")";
-            // each window's next top row is loaded one row ahead (<window>_n): its loads are
-            // in flight during a whole row of residual arithmetic before they are consumed
-            for (auto& w : win) {
-                o << "        T " << wname(w.first, w.second.second) << "_n = 0";
-                for (int dy = w.second.first; dy <= w.second.second; ++dy) o << ", " << wname(w.first, dy) << " = 0";
-                o << ";\n";
+                 "    T dot = 0;\n";
+        }
+        o << "    const int lane = threadIdx.x & 63, z = 0; (void)z;\n"
+             "    const int nsx = (W + " << nout - 1 << ") / " << nout << ", G = gridDim.x * 4;\n"
+             "    const int RB = max(8, (int)(((long long)H * nsx + G - 1) / G)), nby = (H + RB - 1) / RB;\n"
+             "    for (int wid = blockIdx.x * 4 + (threadIdx.x >> 6); wid < nsx * nby; wid += G) {\n"
+             "        const int x = (wid % nsx) * " << nout << " + lane - " << loff << ";\n"
+             "        const int y0 = (wid / nsx) * RB, y1 = min(H, y0 + RB);\n"
+             "        const bool xin = x >= 0 && x < W, xout = xin && lane >= " << loff << " && lane < " << loff + nout << ";\n";
+        auto base_of = [&](const std::tuple<int, int, int>& k) {
+            const int i = std::get<1>(k);
+            return std::get<0>(k) ? "(p + a.uoff[" + std::to_string(uslot[i]) + "])"
+                                  : "((const " + std::string(elem_type(m.images[i].elem, m.images[i].tvalued)) +
+                                        "*)a.img[" + std::to_string(i) + "])";
+        };
+        // the two channels of a 2-channel array whose windows span the same rows are
+        // read as one 8 / 16-byte access (opt_ldm2)
+        auto partner = [&](const std::tuple<int, int, int>& k) -> const std::pair<int, int>* {
+            const int i = std::get<1>(k);
+            if (m.images[i].channels != 2) return nullptr;
+            auto a0 = win.find(std::make_tuple(std::get<0>(k), i, 0));
+            auto a1 = win.find(std::make_tuple(std::get<0>(k), i, 1));
+            if (a0 == win.end() || a1 == win.end() || a0->second != a1->second) return nullptr;
+            return &a1->second;
+        };
+        // statement loading row yy of window k into `dst` (and of its partner channel)
+        auto load = [&](const std::tuple<int, int, int>& k, const std::string& yy, int dy, const char* sfx) {
+            const int i = std::get<1>(k), c = std::get<2>(k), ch = m.images[i].channels;
+            const std::string cond = "xin && " + yy + " >= 0 && " + yy + " < H";
+            const std::string pix = "(long long)(" + yy + " * W + x) * " + std::to_string(ch);
+            if (partner(k)) {
+                if (c == 1) return std::string();
+                const auto k1 = std::make_tuple(std::get<0>(k), i, 1);
+                return "opt_ldm2(" + base_of(k) + ", " + pix + ", " + cond + ", " + wname(k, dy) + sfx + ", " +
+                       wname(k1, dy) + sfx + ");";
             }
-            for (auto& w : win) {
-                for (int dy = w.second.first + 1; dy <= w.second.second; ++dy) {
-                    const std::string st = load(w.first, "(" + qy0 + " - 1 + " + std::to_string(dy) + ")", dy, "");
-                    if (!st.empty()) o << "        " << st << "\n";
-                }
-                const std::string st = load(w.first, "(" + qy0 + " + " + std::to_string(w.second.second) + ")",
-                                            w.second.second, "_n");
+            return wname(k, dy) + sfx + " = opt_ldm(" + base_of(k) + ", " + pix + " + " + std::to_string(c) +
+                   ", " + cond + ");";
+        };
+        const std::string qy0 = "(y0 - " + std::to_string(maxy) + ")";
+        // each window's next top row is loaded one row ahead (<window>_n): its loads are
+        // in flight during a whole row of residual arithmetic before they are consumed
+        for (auto& w : win) {
+            o << "        T " << wname(w.first, w.second.second) << "_n = 0";
+            for (int dy = w.second.first; dy <= w.second.second; ++dy) o << ", " << wname(w.first, dy) << " = 0";
+            o << ";\n";
+        }
+        for (auto& w : win) {
+            for (int dy = w.second.first + 1; dy <= w.second.second; ++dy) {
+                const std::string st = load(w.first, "(" + qy0 + " - 1 + " + std::to_string(dy) + ")", dy, "");
                 if (!st.empty()) o << "        " << st << "\n";
             }
-            for (int k : unk)
-                for (int c = 0; c < m.images[k].channels; ++c)
-                    for (int j = 0; j <= maxy - miny; ++j)
-                        o << "        T ac" << uslot[k] << "_" << c << "_" << j << " = 0;\n";
-            o << "        for (int y = " << qy0 << "; y < y1 - " << miny << "; ++y) {\n";
-            for (auto& w : win) {
-                for (int dy = w.second.first; dy < w.second.second; ++dy)
-                    o << "        " << wname(w.first, dy) << " = " << wname(w.first, dy + 1) << ";\n";
-                o << "        " << wname(w.first, w.second.second) << " = " << wname(w.first, w.second.second) << "_n;\n";
-            }
-            for (auto& w : win) {
-                const std::string st = load(w.first, "(y + " + std::to_string(w.second.second + 1) + ")", w.second.second, "_n");
-                if (!st.empty()) o << "        " << st << "\n";
-            }
-            o << "        const bool qin = xin && y >= 0 && y < H;\n" << body.str();
-            // output row y + miny has all its centres
-            o << "        const int yo = y + " << miny << ";\n"
-                 "        if (xout && yo >= y0 && yo < y1) {\n"
-                 "        const long long lin = (long long)yo * W + x;\n"
-                 "        const bool act = (a.flags[lin] & 1) != 0;\n";
-            for (int k : unk)
-                for (int c = 0; c < m.images[k].channels; ++c) {
-                    const std::string el = "a.uoff[" + std::to_string(uslot[k]) + "] + lin * " + std::to_string(m.images[k].channels) +
-                                           " + " + std::to_string(c);
-                    // p at the output pixel: its row window when one holds row yo (same load)
-                    std::string pe = "p[e]";
-                    auto wi = win.find(std::make_tuple(1, k, c));
-                    if (wi != win.end() && wi->second.first <= miny && miny <= wi->second.second)
-                        pe = wname(wi->first, miny);
-                    o << "        { const long long e = " << el << "; const T acc = ac" << uslot[k] << "_" << c << "_0;\n"
-                         "          if (finish) { const T pe = " << pe << "; const T o = act ? acc + (dadd ? dadd[e] * pe : (T)0) : (T)0; Ap[e] = o; dot += pe * o; }\n"
-                         "          else Ap[e] = acc; }\n";
+            const std::string st = load(w.first, "(" + qy0 + " + " + std::to_string(w.second.second) + ")",
+                                        w.second.second, "_n");
+            if (!st.empty()) o << "        " << st << "\n";
+        }
+        for (int k : unk)
+            for (int c = 0; c < m.images[k].channels; ++c)
+                for (int j = 0; j <= maxy - miny; ++j) {
+                    o << "        T ac" << uslot[k] << "_" << c << "_" << j << " = 0;\n";
+                    if (jtf) o << "        T dq" << uslot[k] << "_" << c << "_" << j << " = 0;\n";
                 }
-            o << "        }\n";
-            for (int k : unk)
-                for (int c = 0; c < m.images[k].channels; ++c) {
-                    const std::string a0 = "ac" + std::to_string(uslot[k]) + "_" + std::to_string(c) + "_";
+        o << "        for (int y = " << qy0 << "; y < y1 - " << miny << "; ++y) {\n";
+        for (auto& w : win) {
+            for (int dy = w.second.first; dy < w.second.second; ++dy)
+                o << "        " << wname(w.first, dy) << " = " << wname(w.first, dy + 1) << ";\n";
+            o << "        " << wname(w.first, w.second.second) << " = " << wname(w.first, w.second.second) << "_n;\n";
+        }
+        for (auto& w : win) {
+            const std::string st = load(w.first, "(y + " + std::to_string(w.second.second + 1) + ")", w.second.second, "_n");
+            if (!st.empty()) o << "        " << st << "\n";
+        }
+        o << "        const bool qin = xin && y >= 0 && y < H;\n" << body.str();
+        // output row y + miny has all its centres
+        o << "        const int yo = y + " << miny << ";\n"
+             "        if (xout && yo >= y0 && yo < y1) {\n"
+             "        const long long lin = (long long)yo * W + x;\n";
+        if (jtf) o << fin.str() << "        a.flags[lin] = act ? 1 : 0;\n";
+        else o << "        const bool act = (a.flags[lin] & 1) != 0;\n";
+        for (int k : unk)
+            for (int c = 0; c < m.images[k].channels; ++c) {
+                const std::string el = "a.uoff[" + std::to_string(uslot[k]) + "] + lin * " + std::to_string(m.images[k].channels) +
+                                       " + " + std::to_string(c);
+                const std::string sfx = std::to_string(uslot[k]) + "_" + std::to_string(c) + "_0";
+                if (jtf) {
+                    o << "        { const long long e = " << el << "; r[e] = act ? -ac" << sfx << " : (T)0; diag[e] = dq" << sfx << "; }\n";
+                    continue;
+                }
+                // p at the output pixel: its row window when one holds row yo (same load)
+                std::string pe = "p[e]";
+                auto wi = win.find(std::make_tuple(1, k, c));
+                if (wi != win.end() && wi->second.first <= miny && miny <= wi->second.second)
+                    pe = wname(wi->first, miny);
+                o << "        { const long long e = " << el << "; const T acc = ac" << sfx << ";\n"
+                     "          if (finish) { const T pe = " << pe << "; const T o = act ? acc + (dadd ? dadd[e] * pe : (T)0) : (T)0; Ap[e] = o; dot += pe * o; }\n"
+                     "          else Ap[e] = acc; }\n";
+            }
+        o << "        }\n";
+        for (int k : unk)
+            for (int c = 0; c < m.images[k].channels; ++c)
+                for (const char* an : {"ac", "dq"}) {
+                    if (!jtf && an[0] == 'd') continue;
+                    const std::string a0 = an + std::to_string(uslot[k]) + "_" + std::to_string(c) + "_";
                     for (int j = 0; j < maxy - miny; ++j) o << "        " << a0 << j << " = " << a0 << j + 1 << ";\n";
                     o << "        " << a0 << maxy - miny << " = 0;\n";
                 }
-            o << "        }\n"
-                 "    }\n"
-                 "    if (finish) { double v[1] = {(double)dot}; block_reduce_publish<1>(v, rs, blockIdx.x); }\n}\n";
-        }
+        o << "        }\n"
+             "    }\n";
+        if (jtf) o << "}\n";
+        else o << "    if (finish) { double v[1] = {(double)dot}; block_reduce_publish<1>(v, rs, blockIdx.x); }\n}\n";
+    };
+    if (tiled) {
+        strip_kernel(false);
+        strip_kernel(true);
     }
 
     // ------------------------------------------------------------ gen_dump_j_<i>

@@ -42,6 +42,8 @@ struct GenSource {
     bool prefer_tiled = false;         // the plan's default apply (static rule, codegen.cpp)
     bool has_strip = false;            // gen_apply_strip emitted (2-D centred, no sampled reads)
     int strip_cols = 64;               // its output columns per wave
+    bool has_jtf_strip = false;        // gen_jtf_strip emitted (the same walk for J^T F)
+    int jtf_strip_cols = 64;
     // materialized J (saveJToCRS): one kernel gen_dump_j_<i> per energy spec, in order;
     // spec i: domain (-1 centred, else graph id), residual rows and nonzeros per element
     struct DumpSpec { int graph; int rows; int nnz; };

@@ -484,6 +484,14 @@ private:
             const long long waves = (long long)((dims_[0] + src_.strip_cols - 1) / src_.strip_cols) * ((dims_[1] + 7) / 8);
             if (force == "strip" || (force.empty() && waves >= 2048)) k_apply_ = k_apply_strip_;
         }
+        // J^T F: the register strip under the same rule (OPT_AMD_GEN_JTF=gather|strip forces)
+        if (src_.has_jtf_strip && !slab) {
+            const char* wj = getenv("OPT_AMD_GEN_JTF");
+            const std::string fj = wj ? wj : "";
+            const long long waves = (long long)((dims_[0] + src_.jtf_strip_cols - 1) / src_.jtf_strip_cols) * ((dims_[1] + 7) / 8);
+            if (fj == "strip" || (fj.empty() && waves >= 2048))
+                OPT_HIP_CHECK(hipModuleGetFunction(&k_jtf_, mod_, "gen_jtf_strip"));
+        }
         k_dump_.resize(src_.dump.size());
         for (size_t k = 0; k < src_.dump.size(); ++k)
             OPT_HIP_CHECK(hipModuleGetFunction(&k_dump_[k], mod_, ("gen_dump_j_" + std::to_string(k)).c_str()));
