@@ -870,9 +870,142 @@ GenSource generate(GModel& m, bool dbl) {
         if (jtf) o << "}\n";
         else o << "    if (finish) { double v[1] = {(double)dot}; block_reduce_publish<1>(v, rs, blockIdx.x); }\n}\n";
     };
+    // gen_cost_strip: cost / model cost (gen_cost's per-centre expression: excluded centres
+    // skipped, 1/2 sum r^2, or with delta the linearised residuals r + sum_u dr/du delta_u)
+    // with every read served from row windows (unknowns, knowns, delta) walked down a
+    // column strip, one pixel per lane and centre; no scatter, so no row lag.
+    auto cost_strip = [&]() {
+        bool ok = !cres.empty();
+        for (int ci : cres)
+            P.visit(m.residuals[ci].expr, [&](int, const Node& n) { ok &= n.op != Op::Sample; });
+        if (m.exclude >= 0)
+            P.visit(m.exclude, [&](int, const Node& n) { ok &= n.op != Op::Sample && !(n.op == Op::Read && n.slot >= 0); });
+        for (auto& r : m.residuals) ok &= r.graph < 0;   // graph terms: gen_cost
+        if (!ok) return;
+        // window key: (0 known / unknown image, 2 delta; image; channel)
+        std::map<std::tuple<int, int, int>, std::pair<int, int>> win;
+        int rxlo = 0, rxhi = 0;
+        auto wname = [](const std::tuple<int, int, int>& k, int dy) {
+            return std::string(std::get<0>(k) ? "wd" : "wi") + std::to_string(std::get<1>(k)) + "c" +
+                   std::to_string(std::get<2>(k)) + (dy < 0 ? "m" : "p") + std::to_string(std::abs(dy));
+        };
+        std::ostringstream body;
+        const CacheMap* saved = g_cache;
+        g_cache = nullptr;
+        {
+            Body b(m, body, nd, uslot);
+            b.centred_reads([&](const Node& n, const char* vname) {
+                const auto key = std::make_tuple(vname ? 2 : 0, n.i, n.ch);
+                auto it = win.find(key);
+                if (it == win.end()) win[key] = {n.off[1], n.off[1]};
+                else it->second = {std::min(it->second.first, n.off[1]), std::max(it->second.second, n.off[1])};
+                rxlo = std::min(rxlo, n.off[0]);
+                rxhi = std::max(rxhi, n.off[0]);
+                const std::string w = wname(key, n.off[1]);
+                return n.off[0] == 0 ? w : "opt_sh(" + w + ", " + std::to_string(n.off[0]) + ")";
+            });
+            b.line("bool on = xout && y >= y0 && y < y1;");
+            if (m.exclude >= 0) b.line("on = on && " + b.v(m.exclude) + " == (T)0;");
+            std::string sum = "(T)0";
+            for (int ci : cres) {
+                const std::string R = b.v(m.residuals[ci].expr);
+                sum += " + " + R + " * " + R;
+            }
+            b.line("T s = " + sum + ";");
+            b.line("if (delta) {");
+            std::string ms = "(T)0";
+            int idx = 0;
+            for (int ci : cres) {
+                const GResidual& r = m.residuals[ci];
+                std::string e = b.v(r.expr);
+                for (int u : r.unknowns) {
+                    const int gu = P.diff(r.expr, u);
+                    double gv;
+                    if (P.is_const(gu, &gv) && gv == 0.0) continue;
+                    e += " + " + b.v(gu) + " * " + b.vec(u, "delta");
+                }
+                b.line("  const T m" + std::to_string(idx) + " = " + e + ";");
+                ms += " + m" + std::to_string(idx) + " * m" + std::to_string(idx);
+                ++idx;
+            }
+            b.line("  s = " + ms + ";");
+            b.line("}");
+            b.line("if (on) acc += (T)0.5 * s;");
+        }
+        g_cache = saved;
+        int regs = 0;
+        for (auto& w : win) regs += w.second.second - w.second.first + 2;
+        const int loff = -rxlo, nout = 64 + rxlo - rxhi;
+        if (nout < 16 || regs > 96 * (dbl ? 1 : 2) / 2) return;
+        gs.has_cost_strip = true;
+        gs.cost_strip_cols = nout;
+        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_cost_strip(GenArgs a, const T* __restrict__ delta, ReduceSlot rs) {\n"
+             "    OPT_COORDS\n"
+             "    T acc = 0;\n"
+             "    const int lane = threadIdx.x & 63, z = 0; (void)z;\n"
+             "    const int nsx = (W + " << nout - 1 << ") / " << nout << ", G = gridDim.x * 4;\n"
+             "    const int RB = max(8, (int)(((long long)H * nsx + G - 1) / G)), nby = (H + RB - 1) / RB;\n"
+             "    for (int wid = blockIdx.x * 4 + (threadIdx.x >> 6); wid < nsx * nby; wid += G) {\n"
+             "        const int x = (wid % nsx) * " << nout << " + lane - " << loff << ";\n"
+             "        const int y0 = (wid / nsx) * RB, y1 = min(H, y0 + RB);\n"
+             "        const bool xin = x >= 0 && x < W, xout = xin && lane >= " << loff << " && lane < " << loff + nout << ";\n";
+        auto base_of = [&](const std::tuple<int, int, int>& k) {
+            const int i = std::get<1>(k);
+            const std::string own = "((const " + std::string(elem_type(m.images[i].elem, m.images[i].tvalued)) +
+                                    "*)a.img[" + std::to_string(i) + "])";
+            // delta may be null (the cost): the image itself stands in as a valid address
+            return std::get<0>(k) ? "(delta ? delta + a.uoff[" + std::to_string(uslot[i]) + "] : " + own + ")" : own;
+        };
+        auto partner = [&](const std::tuple<int, int, int>& k) {
+            const int i = std::get<1>(k);
+            if (m.images[i].channels != 2) return false;
+            auto a0 = win.find(std::make_tuple(std::get<0>(k), i, 0));
+            auto a1 = win.find(std::make_tuple(std::get<0>(k), i, 1));
+            return a0 != win.end() && a1 != win.end() && a0->second == a1->second;
+        };
+        auto load = [&](const std::tuple<int, int, int>& k, const std::string& yy, int dy, const char* sfx) {
+            const int i = std::get<1>(k), c = std::get<2>(k), ch = m.images[i].channels;
+            const std::string cond = "xin && " + yy + " >= 0 && " + yy + " < H" + (std::get<0>(k) ? " && delta" : "");
+            const std::string pix = "(long long)(" + yy + " * W + x) * " + std::to_string(ch);
+            if (partner(k)) {
+                if (c == 1) return std::string();
+                const auto k1 = std::make_tuple(std::get<0>(k), i, 1);
+                return "opt_ldm2(" + base_of(k) + ", " + pix + ", " + cond + ", " + wname(k, dy) + sfx + ", " +
+                       wname(k1, dy) + sfx + ");";
+            }
+            return wname(k, dy) + sfx + " = opt_ldm(" + base_of(k) + ", " + pix + " + " + std::to_string(c) +
+                   ", " + cond + ");";
+        };
+        for (auto& w : win) {
+            o << "        T " << wname(w.first, w.second.second) << "_n = 0";
+            for (int dy = w.second.first; dy <= w.second.second; ++dy) o << ", " << wname(w.first, dy) << " = 0";
+            o << ";\n";
+        }
+        for (auto& w : win) {
+            for (int dy = w.second.first + 1; dy <= w.second.second; ++dy) {
+                const std::string st = load(w.first, "(y0 - 1 + " + std::to_string(dy) + ")", dy, "");
+                if (!st.empty()) o << "        " << st << "\n";
+            }
+            const std::string st = load(w.first, "(y0 + " + std::to_string(w.second.second) + ")", w.second.second, "_n");
+            if (!st.empty()) o << "        " << st << "\n";
+        }
+        o << "        for (int y = y0; y < y1; ++y) {\n";
+        for (auto& w : win) {
+            for (int dy = w.second.first; dy < w.second.second; ++dy)
+                o << "        " << wname(w.first, dy) << " = " << wname(w.first, dy + 1) << ";\n";
+            o << "        " << wname(w.first, w.second.second) << " = " << wname(w.first, w.second.second) << "_n;\n";
+        }
+        for (auto& w : win) {
+            const std::string st = load(w.first, "(y + " + std::to_string(w.second.second + 1) + ")", w.second.second, "_n");
+            if (!st.empty()) o << "        " << st << "\n";
+        }
+        o << "        const bool qin = xin; (void)qin;\n" << body.str() << "        }\n    }\n"
+             "    double v[1] = {(double)acc}; block_reduce_publish<1>(v, rs, blockIdx.x);\n}\n";
+    };
     if (tiled) {
         strip_kernel(false);
         strip_kernel(true);
+        cost_strip();
     }
 
     // ------------------------------------------------------------ gen_dump_j_<i>

@@ -44,6 +44,8 @@ struct GenSource {
     int strip_cols = 64;               // its output columns per wave
     bool has_jtf_strip = false;        // gen_jtf_strip emitted (the same walk for J^T F)
     int jtf_strip_cols = 64;
+    bool has_cost_strip = false;       // gen_cost_strip emitted (centred-only 2-D energies)
+    int cost_strip_cols = 64;
     // materialized J (saveJToCRS): one kernel gen_dump_j_<i> per energy spec, in order;
     // spec i: domain (-1 centred, else graph id), residual rows and nonzeros per element
     struct DumpSpec { int graph; int rows; int nnz; };

@@ -492,6 +492,14 @@ private:
             if (fj == "strip" || (fj.empty() && waves >= 2048))
                 OPT_HIP_CHECK(hipModuleGetFunction(&k_jtf_, mod_, "gen_jtf_strip"));
         }
+        // cost / model cost: the register strip under the same rule (OPT_AMD_GEN_COST forces)
+        if (src_.has_cost_strip && !slab) {
+            const char* wc = getenv("OPT_AMD_GEN_COST");
+            const std::string fc = wc ? wc : "";
+            const long long waves = (long long)((dims_[0] + src_.cost_strip_cols - 1) / src_.cost_strip_cols) * ((dims_[1] + 7) / 8);
+            if (fc == "strip" || (fc.empty() && waves >= 2048))
+                OPT_HIP_CHECK(hipModuleGetFunction(&k_cost_, mod_, "gen_cost_strip"));
+        }
         k_dump_.resize(src_.dump.size());
         for (size_t k = 0; k < src_.dump.size(); ++k)
             OPT_HIP_CHECK(hipModuleGetFunction(&k_dump_[k], mod_, ("gen_dump_j_" + std::to_string(k)).c_str()));
