@@ -34,25 +34,47 @@ __device__ __forceinline__ T guarded_invert(T d) {   // CERES form, :480-487
 // pre = guardedInvert(diag) (guardedInvert(1) = 1/4 for UsePreconditioner(false)),
 // p = pre r, rz[0] = sum r.p. Excluded unknowns get pre = p = 0; so do the halo rows of
 // a decomposed slab (pixels outside [pix_lo, pix_hi)), whose r is zeroed too.
+// The per-element init / update kernels find each element's pixel flag first (a load that
+// the element's own loads wait on); each thread keeps kIlp elements of its grid-stride
+// sequence in flight (their loads issued together, then the arithmetic in element order),
+// as one element per iteration left too few loads outstanding to stream at HBM speed.
+constexpr int kIlp = 4;
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void gn_init_kernel(VecLayout L, const uint8_t* __restrict__ flags,
                                                          T* __restrict__ r, const T* __restrict__ diag,
                                                          T* __restrict__ pre, T* __restrict__ p, int use_pre,
                                                          long long pix_lo, long long pix_hi, ReduceSlot rs) {
     const long long n = L.off[L.nimg];
+    const long long stride = (long long)gridDim.x * blockDim.x;
     T acc = 0;
-    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
-         e += (long long)gridDim.x * blockDim.x) {
-        const long long px = L.pix(e);
-        const bool own = px >= pix_lo && px < pix_hi;
-        const bool act = own && (flags[px] & 1);
-        const T w = act ? guarded_invert(use_pre ? diag[e] : (T)1) : (T)0;
-        const T re = own ? r[e] : (T)0;
-        const T pp = w * re;
-        if (!own) r[e] = 0;
-        pre[e] = w;
-        p[e] = pp;
-        acc += re * pp;
+    for (long long e0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; e0 < n; e0 += kIlp * stride) {
+        bool in[kIlp], own[kIlp];
+        uint8_t f[kIlp];
+        T dv[kIlp], rv[kIlp];
+#pragma unroll
+        for (int u = 0; u < kIlp; ++u) {
+            const long long e = e0 + u * stride;
+            in[u] = e < n;
+            const long long px = in[u] ? L.pix(e) : 0;
+            own[u] = in[u] && px >= pix_lo && px < pix_hi;
+            f[u] = flags[px];
+            rv[u] = r[in[u] ? e : 0];
+            dv[u] = use_pre ? diag[in[u] ? e : 0] : (T)1;
+        }
+#pragma unroll
+        for (int u = 0; u < kIlp; ++u) {
+            if (!in[u]) continue;
+            const long long e = e0 + u * stride;
+            const bool act = own[u] && (f[u] & 1);
+            const T w = act ? guarded_invert(use_pre ? dv[u] : (T)1) : (T)0;
+            const T re = own[u] ? rv[u] : (T)0;
+            const T pp = w * re;
+            if (!own[u]) r[e] = 0;
+            pre[e] = w;
+            p[e] = pp;
+            acc += re * pp;
+        }
     }
     double v[1] = {(double)acc};
     block_reduce_publish<1>(v, rs, blockIdx.x);
@@ -70,33 +92,51 @@ __global__ __launch_bounds__(kBlock) void lm_init_kernel(VecLayout L, const uint
                                                          int use_pre, LMScalars lm, long long pix_lo,
                                                          long long pix_hi, ReduceSlot rs) {
     const long long n = L.off[L.nimg];
+    const long long stride = (long long)gridDim.x * blockDim.x;
     const T radius = (T)lm.radius;
     const T inv_radius = (T)1 / radius;
     T acc = 0;
-    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
-         e += (long long)gridDim.x * blockDim.x) {
-        const long long px = L.pix(e);
-        const bool own = px >= pix_lo && px < pix_hi;
-        if (!own || !(flags[px] & 1)) {
-            if (FIRST) SSq[e] = 0;
-            CtC[e] = 0; pre[e] = 0; b[e] = 0; p[e] = 0;
-            if (!own) r[e] = 0;
-            continue;
+    for (long long e0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; e0 < n; e0 += kIlp * stride) {
+        bool in[kIlp], own[kIlp];
+        uint8_t f[kIlp];
+        T dv[kIlp], rv[kIlp], sv[kIlp];
+#pragma unroll
+        for (int u = 0; u < kIlp; ++u) {
+            const long long e = e0 + u * stride;
+            in[u] = e < n;
+            const long long ec = in[u] ? e : 0;
+            const long long px = in[u] ? L.pix(e) : 0;
+            own[u] = in[u] && px >= pix_lo && px < pix_hi;
+            f[u] = flags[px];
+            rv[u] = r[ec];
+            dv[u] = diag[ec];
+            if (!FIRST) sv[u] = SSq[ec];
         }
-        T ssq;
-        if (FIRST) { ssq = guarded_invert(use_pre ? diag[e] : (T)1); SSq[e] = ssq; }
-        else ssq = SSq[e];
-        const T unclamped = diag[e] * inv_radius;
-        const T clampm = ((T)1 / ssq) / radius;
-        const T lo = (T)lm.min_diag * clampm, hi = (T)lm.max_diag * clampm;
-        const T c = std::min(std::max(unclamped, lo), hi);
-        const T w = (T)1 / (c + radius * unclamped);
-        const T re = r[e];
-        CtC[e] = c;
-        pre[e] = w;
-        b[e] = re;
-        p[e] = w * re;
-        acc += re * (w * re);
+#pragma unroll
+        for (int u = 0; u < kIlp; ++u) {
+            if (!in[u]) continue;
+            const long long e = e0 + u * stride;
+            if (!own[u] || !(f[u] & 1)) {
+                if (FIRST) SSq[e] = 0;
+                CtC[e] = 0; pre[e] = 0; b[e] = 0; p[e] = 0;
+                if (!own[u]) r[e] = 0;
+                continue;
+            }
+            T ssq;
+            if (FIRST) { ssq = guarded_invert(use_pre ? dv[u] : (T)1); SSq[e] = ssq; }
+            else ssq = sv[u];
+            const T unclamped = dv[u] * inv_radius;
+            const T clampm = ((T)1 / ssq) / radius;
+            const T lo = (T)lm.min_diag * clampm, hi = (T)lm.max_diag * clampm;
+            const T c = std::min(std::max(unclamped, lo), hi);
+            const T w = (T)1 / (c + radius * unclamped);
+            const T re = rv[u];
+            CtC[e] = c;
+            pre[e] = w;
+            b[e] = re;
+            p[e] = w * re;
+            acc += re * (w * re);
+        }
     }
     double v[1] = {(double)acc};
     block_reduce_publish<1>(v, rs, blockIdx.x);

@@ -27,16 +27,29 @@ __global__ __launch_bounds__(kBlock) void update_images_kernel(VecLayout L, cons
                                                                T* __restrict__ prev, long long pix_lo,
                                                                long long pix_hi) {
     const long long n = L.off[L.nimg];
-    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
-         e += (long long)gridDim.x * blockDim.x) {
-        int k;
-        long long local;
-        const long long px = L.locate(e, &k, &local);
-        if (px < pix_lo || px >= pix_hi || !(flags[px] & 1)) continue;
-        T* x = X.x[k];
-        const T v = x[local];
-        if (SAVE) prev[e] = v;
-        x[local] = v + delta[e];
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long e0 = (long long)blockIdx.x * blockDim.x + threadIdx.x; e0 < n; e0 += kIlp * stride) {
+        bool on[kIlp];
+        T* xp[kIlp];
+        T xv[kIlp], dv[kIlp];
+#pragma unroll
+        for (int u = 0; u < kIlp; ++u) {   // kIlp elements' loads in flight together
+            const long long e = e0 + u * stride;
+            const bool in = e < n;
+            int k = 0;
+            long long local = 0;
+            const long long px = in ? L.locate(e, &k, &local) : 0;
+            on[u] = in && px >= pix_lo && px < pix_hi && (flags[px] & 1);
+            xp[u] = X.x[k] + local;
+            xv[u] = *xp[u];
+            dv[u] = delta[in ? e : 0];
+        }
+#pragma unroll
+        for (int u = 0; u < kIlp; ++u) {
+            if (!on[u]) continue;
+            if (SAVE) prev[e0 + u * stride] = xv[u];
+            *xp[u] = xv[u] + dv[u];
+        }
     }
 }
 template <typename T>
