@@ -1005,7 +1005,11 @@ private:
     StateOptions opts_;
     int idx_X_, idx_D_, idx_Im_, idx_mR_, idx_mC_, idx_p_[16];
     sfs::Args<T> a_{};
-    int strip_rows_ = env_int("OPT_AMD_SFS_ROWS", 16);
+    // rows per strip wave (apply and J^T F strips). Measured at 4096^2 (sfs_strip, LM step):
+    // 12 rows 113.9 us / 3.44 ms, 16: 110-111 / 3.42, 20: 105 / 3.41, 24: 108 / 3.45,
+    // 36: 118 / 3.51 — 20 rows make the 69 x 205 strip waves ~2 full resident rounds at
+    // 7 waves per SIMD (16 rows: 2.46 rounds, a partly idle last one)
+    int strip_rows_ = env_int("OPT_AMD_SFS_ROWS", 20);
     int cost_rows_ = env_int("OPT_AMD_SFS_COST_ROWS", 32);
     bool cost_strip_ = env_int("OPT_AMD_SFS_COST_STRIP", 1) != 0;   // 0: the per-pixel sfs_cost
     bool jtf_strip_ = env_int("OPT_AMD_SFS_JTF_STRIP", 1) != 0;     // 0: the LDS-tile J^T F
