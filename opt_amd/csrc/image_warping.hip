@@ -43,6 +43,19 @@ namespace iw {
 
 constexpr int kStrip = 64;   // columns per wavefront strip (aligned: x = 64*strip + lane)
 
+// Rows per wave of the stencil kernels: 32 while that still gives >= 2048 tiles of
+// 4 waves (4096^2: 64 strips x 32 row blocks, two resident rounds at 4 waves per SIMD);
+// a row slab of the multi-GPU split (4096 x 512 at 8 ranks) would otherwise fill a
+// quarter of the chip, so shorter waves down to 8 rows keep the tile count up.
+// Measured on one GPU at each rank's slab shape (GN step, rows 32 / 16 / 8 / 4):
+// 4096 x 512 0.89 / 0.73 / 0.70 / 0.76 ms, 4096 x 1024 1.33 / 1.17 / 1.21 / 1.40,
+// 4096 x 2048 2.33 / 2.21 / 2.31 / 2.78 (this rule: 8, 8, 16).
+inline int rows_for(int nstrips, int nrows) {
+    int rows = 32;
+    while (rows > 8 && (long long)nstrips * ((nrows + 4 * rows - 1) / (4 * rows)) < 2048) rows /= 2;
+    return rows;
+}
+
 template <typename T>
 struct Args {
     Domain dom;
@@ -880,7 +893,7 @@ public:
             if (p.name == "w_fitSqrt") idx_wf_ = p.index;
             if (p.name == "w_regSqrt") idx_wr_ = p.index;
         }
-        rows_ = env_int("OPT_AMD_ROWS", 32);
+        rows_ = env_int("OPT_AMD_ROWS", 0);   // 0: iw::rows_for (per domain)
         depth_ = env_int("OPT_AMD_DEPTH", 1);
         nt_ = env_int("OPT_AMD_IW_NT", 6);
         spec_on_ = env_int("OPT_AMD_IW_SPEC", 1) != 0;
@@ -1105,6 +1118,7 @@ private:
         flags_ = (uint8_t*)dmalloc(N);
         OPT_HIP_CHECK(hipMemset(flags_, 0, N));
         nstrips_ = (dom_.W + iw::kStrip - 1) / iw::kStrip;
+        if (rows_ <= 0 || rows_auto_) { rows_auto_ = true; rows_ = iw::rows_for(nstrips_, dom_.y_hi - dom_.y_lo); }
         nrowblocks_ = (dom_.y_hi - dom_.y_lo + rows_ * 4 - 1) / (rows_ * 4);
         red_.ensure(std::max(stencil_blocks(), 2048), 1, 64);
         if (opts_.host_buffers) {
@@ -1314,6 +1328,7 @@ private:
     bool spec_on_ = true;               // OPT_AMD_IW_SPEC=0: separate cost and J^T F passes
     std::vector<double> spec_key_;
     int rows_ = 16, depth_ = 1, nstrips_ = 0, nrowblocks_ = 0;
+    bool rows_auto_ = false;
     int nt_ = 6;   // streaming PCG-vector access: bit 0 iw_apply loads, bit 1 iw_apply stores, bit 2 iw_residual
     Comm* comm_ = nullptr;
     const bool overlap_ = env_int("OPT_AMD_HALO_OVERLAP", 1) != 0;   // 0: blocking halo before each apply
@@ -1353,8 +1368,9 @@ public:
             if (p.name == "w_regSqrt") idx_wr_ = p.index;
         }
         use_pre_ = spec.use_preconditioner;
-        rows_ = env_int("OPT_AMD_ROWS", 32);
+        rows_ = env_int("OPT_AMD_ROWS", 0);   // 0: iw::rows_for (per domain)
         nstrips_ = (dom_.W + iw::kStrip - 1) / iw::kStrip;
+        if (rows_ <= 0 || rows_auto_) { rows_auto_ = true; rows_ = iw::rows_for(nstrips_, dom_.y_hi - dom_.y_lo); }
         nrowblocks_ = (dom_.y_hi - dom_.y_lo + rows_ * 4 - 1) / (rows_ * 4);
         const long long N = dom_.npix_mem();
         if (opts.host_buffers) {
@@ -1450,6 +1466,7 @@ private:
     int idx_O_, idx_A_, idx_U_, idx_C_, idx_M_, idx_wf_, idx_wr_;
     bool use_pre_ = true;
     int rows_ = 32, nstrips_ = 0, nrowblocks_ = 0;
+    bool rows_auto_ = false;
     iw::Args<T> a_{};
     T *user_O_ = nullptr, *user_A_ = nullptr, *dO_ = nullptr, *dA_ = nullptr;
     float *dU_ = nullptr, *dC_ = nullptr, *dM_ = nullptr;

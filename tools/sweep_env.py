@@ -17,6 +17,7 @@ from opt_amd import OptSolver, workloads  # noqa: E402
 
 def main():
     W = H = int(os.environ.get("SWEEP_SIZE", "4096"))
+    H = int(os.environ.get("SWEEP_H", H))   # e.g. 512: one rank's slab of the 8-GPU split
     steps = int(os.environ.get("SWEEP_STEPS", "10"))
     rounds = int(os.environ.get("SWEEP_ROUNDS", "3"))
     configs = [c for c in os.environ.get("SWEEP_CONFIGS", "").split(";")]
