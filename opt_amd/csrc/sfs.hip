@@ -1009,7 +1009,12 @@ private:
     // 12 rows 113.9 us / 3.44 ms, 16: 110-111 / 3.42, 20: 105 / 3.41, 24: 108 / 3.45,
     // 36: 118 / 3.51 — 20 rows make the 69 x 205 strip waves ~2 full resident rounds at
     // 7 waves per SIMD (16 rows: 2.46 rounds, a partly idle last one)
-    int strip_rows_ = env_int("OPT_AMD_SFS_ROWS", 20);
+    // A row slab of the multi-GPU split fills less of the chip: below 4096 strip waves at 20
+    // rows, 12-row waves (LM step at 4096 x 512: 20 rows 0.748 ms, 16 0.736, 12 0.704,
+    // 8 0.712; 4096 x 1024: 1.033 / 1.028 / 1.016 / 1.091; 4096 x 2048: 20 rows best,
+    // 1.711 ms; tools/sweep_sfs_rows.py)
+    int strip_rows_ = env_int("OPT_AMD_SFS_ROWS", 0) > 0 ? env_int("OPT_AMD_SFS_ROWS", 0)
+        : ((long long)((dom_.W + sfs::kStripOut - 1) / sfs::kStripOut) * ((dom_.y_hi - dom_.y_lo + 19) / 20) < 4096 ? 12 : 20);
     int cost_rows_ = env_int("OPT_AMD_SFS_COST_ROWS", 32);
     bool cost_strip_ = env_int("OPT_AMD_SFS_COST_STRIP", 1) != 0;   // 0: the per-pixel sfs_cost
     bool jtf_strip_ = env_int("OPT_AMD_SFS_JTF_STRIP", 1) != 0;     // 0: the LDS-tile J^T F
