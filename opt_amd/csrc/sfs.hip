@@ -21,6 +21,7 @@
 // w_s c (px(q), py(q), 1) with px, py functions of q alone, so it is formed in registers.
 // One thread per unknown, 64 x 4 pixel blocks; the 5x5 neighbourhood reads are L1/L2 hits.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -933,6 +934,17 @@ public:
     }
     void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
         apply_split(0, p, Ap, dadd, stop, rs, s);
+    }
+    // the same launch with the timer's events attached (StencilPlan's HasApplyExt)
+    void apply_ext(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s,
+                   hipEvent_t e0, hipEvent_t e1) {
+        const int nstrips = (dom_.W + sfs::kStripOut - 1) / sfs::kStripOut;
+        int i0 = 0, i1 = 0, blocks = 0;
+        split_ranges(&i0, &i1, &blocks);
+        rs.nblocks = blocks;
+        hipExtLaunchKernelGGL((sfs::sfs_strip<T>), dim3(blocks), dim3(kBlock), 0, s, e0, e1, 0, a_, p, Ap, dadd,
+                              stop, rs, nstrips, strip_rows_, 0, 1 << 30, 0);
+        OPT_HIP_CHECK(hipGetLastError());
     }
     // Row slabs: part 1 launches the blocks whose waves read no halo row (strip rows
     // [y0 - 2, y1 + 1] inside the owned rows), part 2 the rest; together they are the

@@ -121,6 +121,16 @@ struct HasFusedStep3<Op, std::void_t<decltype(std::declval<Op&>().step3_fused(
                              (const typename Op::T*)nullptr, (const typename Op::T*)nullptr, (typename Op::T*)nullptr,
                              (const double*)nullptr, 0, 0, 0, (const int*)nullptr, hipStream_t{}))>> : std::true_type {};
 
+// Optional Op::apply_ext(p, Ap, dadd, stop, rs, stream, e0, e1): the apply with HIP
+// events attached to its launch (hipExtLaunchKernelGGL), so the per-kernel timer measures
+// the kernel itself instead of event records around the launch.
+template <class Op, class = void>
+struct HasApplyExt : std::false_type {};
+template <class Op>
+struct HasApplyExt<Op, std::void_t<decltype(std::declval<Op&>().apply_ext(
+                           (const typename Op::T*)nullptr, (typename Op::T*)nullptr, (const typename Op::T*)nullptr,
+                           (const int*)nullptr, ReduceSlot{}, hipStream_t{}, hipEvent_t{}, hipEvent_t{}))>> : std::true_type {};
+
 template <class Op, class = void>
 struct HasSlabRefusal : std::false_type {};
 template <class Op>
@@ -285,15 +295,27 @@ public:
                 // as in the reference, the LM CtC term is not part of this product
                 mat_apply(p_, Ap_, stop, pap(i));
             } else {
-                tbegin(Op::kApplyName);
                 bool done = false;
                 if constexpr (HasFusedStep3<Op>::value)
                     if (i > 0 && fuse3) {   // step3 of i-1 already ran the apply's first pass
+                        tbegin(Op::kApplyName);
                         op_->apply_prepared(p_, Ap_, lm_ ? CtC_ : nullptr, stop, red_.slot(nb(), pap(i)), stream_);
+                        tend();
                         done = true;
                     }
-                if (!done) op_->apply(p_, Ap_, lm_ ? CtC_ : nullptr, stop, red_.slot(nb(), pap(i)), stream_);
-                tend();
+                if constexpr (HasApplyExt<Op>::value) {
+                    hipEvent_t e0 = nullptr, e1 = nullptr;
+                    if (!done && timer_.mode && timer_.ext_pair(Op::kApplyName, &e0, &e1)) {
+                        op_->apply_ext(p_, Ap_, lm_ ? CtC_ : nullptr, stop, red_.slot(nb(), pap(i)), stream_, e0, e1);
+                        timer_.ext_record(Op::kApplyName, e0, e1);
+                        done = true;
+                    }
+                }
+                if (!done) {
+                    tbegin(Op::kApplyName);
+                    op_->apply(p_, Ap_, lm_ ? CtC_ : nullptr, stop, red_.slot(nb(), pap(i)), stream_);
+                    tend();
+                }
             }
             allreduce(pap(i), 1);
             const bool reset = lm_ && ((i + 1) % std::max(1, sp_.residual_reset_period)) == 0;
