@@ -62,20 +62,26 @@ PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc.json")
 APPLY_VARIANT = {0: "iw_apply<float, 1, 0,", 1: "iw_apply<float, 2, 1,", 2: "iw_apply<float, 2, 2,"}
 
 
-def pmc_traffic(liter: int):
+# PCGInit1 fused with the first apply (iw_jtf_apply, one strip pass): Offset 8 + Angle 4 +
+# UrShape 8 + Constraints 8 + Mask 4 read; r 12 + angle pre 4 + flag 1 + p 12 + Ap 12 written.
+INIT_KERNEL = "iw_jtf_apply"
+INIT_BYTES_PER_PX = 8 + 4 + 8 + 8 + 4 + 12 + 4 + 1 + 12 + 12
+
+
+def pmc_traffic(liter: int, first: int = 0):
     try:
         with open(PMC_FILE) as f:
             ks = json.load(f)["kernels"]
     except (OSError, ValueError, KeyError):
         return None
     total = 0.0
-    for i in range(liter):
+    for i in range(first, liter):
         key = APPLY_VARIANT[min(i, 2)]
         hit = [v for k, v in ks.items() if key in k]
         if not hit or "FETCH_SIZE" not in hit[0] or "WRITE_SIZE" not in hit[0]:
             return None
         total += (2.0 * hit[0]["FETCH_SIZE"] + hit[0]["WRITE_SIZE"]) * 1024.0
-    return total / liter
+    return total / (liter - first)
 
 
 PMC_FILE_SFS = os.path.join(ROOT, "profiles", "r02_pmc_sfs.json")
@@ -252,14 +258,18 @@ def main():
     torch.cuda.synchronize()
     kname = s.apply_kernel_name()
     n_apply, apply_ms = s.kernel_stat(kname)
+    n_init, init_ms = (0, 0.0) if sfs else s.kernel_stat(INIT_KERNEL)
     s.set_kernel_timing(0)
+    # the in-loop applies of one step: PCG iterations first..liter-1 (first = 1 when the
+    # first iteration's apply ran inside iw_jtf_apply)
+    first = 0 if sfs else args.liter - int(round(n_apply / max(1, args.steps)))
     avg_apply_s = (apply_ms / 1e3) / max(1, n_apply)
     npx = W * (sl.rows if sl else H)
     ch = 1 if sfs else 3          # unknowns per pixel
     if sfs:   # sfs_strip: SURVEY.md §8d's per-pixel apply bytes
         bpp = SFS_APPLY_BYTES_PER_PX
     else:
-        bpp = sum(apply_bytes_per_px(i, args.liter) for i in range(args.liter)) / args.liter
+        bpp = sum(apply_bytes_per_px(i, args.liter) for i in range(first, args.liter)) / (args.liter - first)
     achieved = bpp * npx / avg_apply_s / 1e9
     # the pure apply (reads p) timed separately for the kernel-only unknowns/s
     n_local = ch * W * (sl.mem_rows if sl else H)
@@ -297,7 +307,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / PEAK_HBM_GBS,
             "traffic": (None if world != 1 or args.size != 4096 else
-                        pmc_traffic_sfs() if sfs else pmc_traffic(args.liter)),
+                        pmc_traffic_sfs() if sfs else pmc_traffic(args.liter, first)),
             "traffic_unit": "bytes per launch (2 FETCH_SIZE + WRITE_SIZE, "
                             f"{os.path.relpath(PMC_FILE_SFS if sfs else PMC_FILE, ROOT)})",
             "avg_us": avg_apply_s * 1e6,
@@ -305,6 +315,12 @@ def main():
             "bytes_per_px": bpp,
         },
     }
+    if n_init:
+        init_s = (init_ms / 1e3) / n_init
+        ach = INIT_BYTES_PER_PX * npx / init_s / 1e9
+        result["init_kernel"] = {"kernel": INIT_KERNEL, "avg_us": init_s * 1e6, "launches": n_init,
+                                 "bytes_per_px": INIT_BYTES_PER_PX, "achieved": ach,
+                                 "frac": ach / PEAK_HBM_GBS}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not sfs:
         result["cpu_baseline"] = cpu_baseline(w, n_unknowns, args.liter)
     if rank == 0:

@@ -634,10 +634,9 @@ public:
         std::sort(ps.begin(), ps.end(), [](auto& x, auto& y) { return x.index < y.index; });
         idx_wf_ = ps[0].index;
         idx_wr_ = ps[1].index;
-        for (auto& p : ps) {
-            if (p.name == "w_fitSqrt") idx_wf_ = p.index;
-            if (p.name == "w_regSqrt") idx_wr_ = p.index;
-        }
+        // by declared index: the routing matched this file's structural signature, in which
+        // each parameter is identified by its problemparams index (generic.hip: generic_signature),
+        // against the canonical energy's (fit weight declared first), so names play no part
         K_ = (T*)dmalloc(sizeof(T) * 9 * std::max(N_, 1));
         if (opts.host_buffers) {
             dO_ = (T*)dmalloc(sizeof(T) * 3 * N_);

@@ -13,17 +13,20 @@
 
 namespace optamd {
 
-__device__ __forceinline__ unsigned fp_mix(unsigned v, unsigned e, unsigned salt) {
-    unsigned x = v ^ (e * 0x9E3779B9u + salt);   // murmur3 fmix32 of (value, position)
-    x ^= x >> 16; x *= 0x85EBCA6Bu;
-    x ^= x >> 13; x *= 0xC2B2AE35u;
-    return x ^ (x >> 16);
+// splitmix64's finaliser of (position, value, salt): a full 64-bit mix per entry, so two
+// different edge lists collide with probability ~2^-64 (a 32-bit mix per entry would leave
+// ~2^-32 once two or more entries change).
+__device__ __forceinline__ unsigned long long fp_mix(unsigned v, unsigned e, unsigned long long salt) {
+    unsigned long long x = (((unsigned long long)e << 32) | v) ^ salt;
+    x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+    x ^= x >> 27; x *= 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
 }
-// Position-keyed sum of 32-bit mixes (order-independent, so the block sums can meet in
-// one atomic): 16-byte loads, 32-bit arithmetic only — a streaming pass at HBM rate.
+// Position-keyed sum of 64-bit mixes (order-independent, so the block sums can meet in
+// one place): 16-byte loads, a streaming pass at HBM rate.
 // VEC = false: an array that is not 16-byte aligned, read as four 4-byte loads.
 template <bool VEC>
-static __global__ void graph_fingerprint_kernel(const int* __restrict__ v, int E, unsigned salt,
+static __global__ void graph_fingerprint_kernel(const int* __restrict__ v, int E, unsigned long long salt,
                                                 unsigned long long* parts) {
     unsigned long long h = 0;
     const int n4 = E / 4;
@@ -31,8 +34,8 @@ static __global__ void graph_fingerprint_kernel(const int* __restrict__ v, int E
     for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += gridDim.x * blockDim.x) {
         const int4 w = VEC ? v4[q] : int4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
         const unsigned e = 4u * (unsigned)q;
-        h += fp_mix((unsigned)w.x, e, salt) + (unsigned long long)fp_mix((unsigned)w.y, e + 1, salt) +
-             fp_mix((unsigned)w.z, e + 2, salt) + (unsigned long long)fp_mix((unsigned)w.w, e + 3, salt);
+        h += fp_mix((unsigned)w.x, e, salt) + fp_mix((unsigned)w.y, e + 1, salt) +
+             fp_mix((unsigned)w.z, e + 2, salt) + fp_mix((unsigned)w.w, e + 3, salt);
     }
     if (blockIdx.x == 0 && (int)threadIdx.x < E - 4 * n4)   // the tail
         h += fp_mix((unsigned)v[4 * n4 + threadIdx.x], 4u * n4 + threadIdx.x, salt);
@@ -64,7 +67,7 @@ inline unsigned long long graph_fingerprint(const int* const* arrays, int n, int
     OPT_HIP_CHECK(hipMemsetAsync(d, 0, sizeof(unsigned long long), s));
     for (int k = 0; k < n; ++k)
         if (E > 0) {
-            const unsigned salt = 0x4C957F2Du * (unsigned)(k + 1);
+            const unsigned long long salt = 0x9E3779B97F4A7C15ull * (unsigned long long)(k + 1);
             if ((reinterpret_cast<uintptr_t>(arrays[k]) & 15) == 0)
                 hipLaunchKernelGGL(graph_fingerprint_kernel<true>, dim3(grid), dim3(256), 0, s, arrays[k], E, salt,
                                    d + 1);

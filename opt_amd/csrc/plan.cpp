@@ -38,13 +38,13 @@ hipEvent_t KernelTimer::get_event() {
 }
 void KernelTimer::begin(hipStream_t s, const char* name) {
     if (mode == 0) return;
-    if (mode == 2 && apply_name != name) return;
+    if (mode == 2 && apply_name != name && aux_name != name) return;
     open_ = name;
     open_ev_ = get_event();
     OPT_HIP_CHECK(hipEventRecord(open_ev_, s));
 }
 bool KernelTimer::ext_pair(const char* name, hipEvent_t* a, hipEvent_t* b) {
-    if (mode == 0 || (mode == 2 && apply_name != name)) return false;
+    if (mode == 0 || (mode == 2 && apply_name != name && aux_name != name)) return false;
     *a = get_event();
     *b = get_event();
     return true;

@@ -47,8 +47,9 @@ struct StateOptions {
 // hipEvent-pair accounting per kernel name (reference Timer, backend_cuda.t:152-297).
 class KernelTimer {
 public:
-    int mode = 0;  // 0 off, 1 all kernels, 2 apply kernel only
+    int mode = 0;  // 0 off, 1 all kernels, 2 apply kernel (+ aux_name) only
     std::string apply_name;
+    std::string aux_name;   // a second kernel mode 2 times (the image_warping fused init + apply)
     void begin(hipStream_t s, const char* name);
     void end(hipStream_t s);
     // Event pair to attach to the launch itself (hipExtLaunchKernel): the timestamps come

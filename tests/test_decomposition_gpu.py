@@ -57,9 +57,9 @@ def run_decomposed(w, world, nit, lit):
 @pytest.mark.parametrize("world,W,H", [(1, 130, 90), (2, 130, 90), (3, 97, 61), (4, 256, 200)])
 def test_decomposed_solve_matches_single_domain(monkeypatch, world, W, H):
     # like for like: the single-domain reference runs the same kernel sequence as the
-    # slabs (separate cost and J^T F passes; the fused end-of-step pass is one-GPU only
-    # and is checked against separate passes in test_image_warping_gpu.py)
-    monkeypatch.setenv("OPT_AMD_IW_SPEC", "0")
+    # slabs (PCGInit1 and the first apply as separate passes; the fused iw_jtf_apply is
+    # one-domain only and is checked against them in test_image_warping_gpu.py)
+    monkeypatch.setenv("OPT_AMD_IW_FUSED_INIT", "0")
     w = perturbed(W, H, seed=21 + world)
     s = solver(W, H)
     prm = device_params(w)
@@ -81,9 +81,11 @@ def test_decomposed_solve_matches_single_domain(monkeypatch, world, W, H):
         # 1-ulp input change moves one GN step's energy by 1e-3..4e-2 (DESIGN.md §5,
         # test_fp32_noise_floor_of_the_gn_trajectory). 256x200 at 4 ranks lands at
         # 1.8e-4 of max|A| after 3 steps (tools/dbg_dec4.py: deterministic, independent of
-        # freed-memory contents), the energies at 5e-6.
+        # freed-memory contents), the energies at 5e-6; that case alone gets its measured
+        # floor plus margin, the smaller worlds keep 1e-4.
         ra = to_np(prm[1])
-        assert np.abs(A - ra).max() < 1e-3 * max(1.0, np.abs(ra).max())
+        bar = 3e-4 if world == 4 else 1e-4
+        assert np.abs(A - ra).max() < bar * max(1.0, np.abs(ra).max())
 
 
 def test_rccl_transport_single_rank_is_exact():
@@ -119,7 +121,6 @@ def test_halo_overlap_is_bitwise_the_blocking_exchange(monkeypatch, world):
     of the next apply (image_warping.hip: split launches over tile ranges, one reduction
     slot); the result must be bitwise that of the blocking exchange before a whole-slab
     apply."""
-    monkeypatch.setenv("OPT_AMD_IW_SPEC", "0")
     monkeypatch.setenv("OPT_AMD_ROWS", "4")      # 16-row blocks: >= 3 row blocks per slab
     W, H = 130, 150
     w = perturbed(W, H, seed=9)

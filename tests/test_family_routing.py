@@ -196,3 +196,24 @@ def test_perturbed_energy_solves_its_own_energy(tmp_path, family, vid):
     s.set_solver_params({"nIterations": 2, "lIterations": 10})
     costs = s.profiled_solve(prm)
     assert costs[-1] < costs[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("family", ["image_warping", "arap_mesh_deformation"])
+def test_swapped_weight_names_bind_by_index(tmp_path, family):
+    """A file whose two weight Params swap their declared NAMES (same indices, same roles
+    in the templates) has the family's structural signature, so it runs on the family;
+    the weights must bind by problemparams index as the templates use them,
+    giving the canonical file's cost."""
+    from opt_amd import OptSolver
+
+    text = open(E(family)).read()
+    text = text.replace('"w_fitSqrt"', '"TMP"').replace('"w_regSqrt"', '"w_fitSqrt"').replace('"TMP"', '"w_regSqrt"')
+    p = tmp_path / "swapped.t"
+    p.write_text(text)
+    assert api.problem_family(str(p)) == family
+    dims, prm, _ = _problem(family, np.random.default_rng(5))
+    a = OptSolver(dims, str(p), "gaussNewtonGPU", double_precision=True)
+    b = OptSolver(dims, E(family), "gaussNewtonGPU", double_precision=True)
+    assert a.family() == family
+    assert a.eval_cost(prm) == b.eval_cost(prm)
