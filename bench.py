@@ -1,13 +1,15 @@
 """Benchmark: image_warping 4096x4096 fp32 Gauss-Newton + PCG through the Opt C ABI.
 
-One step = one Opt_ProblemStep (one GN iteration: J^T F + Jacobi preconditioner,
-lIterations x {fused p-update + J^T J p apply + p.Ap, PCG vector update + r.z},
-X += delta, cost). Inputs are resident in HBM before the timed region starts.
+One step = one Opt_ProblemStep (one GN iteration: J^T F + Jacobi preconditioner from the
+arrays bound at that Step fused with the first PCG apply, then lIterations - 1 passes of
+{residual update, p-update, J^T J p apply, delta update, the four PCG sums}, X += delta,
+cost). Inputs are resident in HBM before the timed region starts.
 
   value       PCG unknowns processed per second over the whole job:
               n_unknowns * lIterations * steps / wall time of the timed steps
-  roofline    the dominant kernel (the J^T J p apply): its duration from HIP events on
-              its launches (plan stream) over K more steps after the timed ones
+  roofline    the dominant kernel (the in-loop J^T J p pass, iw_apply_res): its duration
+              from HIP events on its launches (plan stream) over K more steps after the
+              timed ones; init_kernel: the same for iw_jtf_apply
   cpu_baseline the oracle (C restatement of the reference's GN/PCG, pthreads over rows
               as backend_cpu_mt) timing one whole GN step on this host's cores, in the
               same unit, plus apply-only rates on all cores and on one; rank 0 at N=1
@@ -58,8 +60,25 @@ def apply_bytes_per_px(i: int, liter: int = 10) -> int:
 # bench). FETCH_SIZE reads exactly 1/2 of the bytes on gfx950 for 1/4/8/16-B-per-lane
 # streaming reads and WRITE_SIZE is exact (profiles/r01_fetchcal.json, 1 GiB arrays), so
 # traffic = 2 FETCH_SIZE + WRITE_SIZE, averaged over the lIterations in-loop launches.
-PMC_FILE = os.path.join(ROOT, "profiles", "r02_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r03_pmc.json")
 APPLY_VARIANT = {0: "iw_apply<float, 1, 0,", 1: "iw_apply<float, 2, 1,", 2: "iw_apply<float, 2, 2,"}
+
+
+# PCG iteration i >= 1 as ONE pass (iw_apply_res: the apply with the previous iteration's
+# residual update folded in): Angle 4 + UrShape 8 + flag 1 + angle pre 4 + r_{i-1} 12 +
+# Ap_{i-1} 12 + p_{i-1} 12 read, p_i 12 + delta 12 written; delta 12 read from i = 2 on;
+# r_i 12 + Ap_i 12 written except in the last iteration (nothing reads them).
+def res_bytes_per_px(i: int, liter: int = 10) -> int:
+    b = 4 + 8 + 1 + 4 + 12 + 12 + 12 + 12 + 12
+    if i >= 2:
+        b += 12
+    if i < liter - 1:
+        b += 24
+    return b
+
+
+RES_KERNEL = "iw_apply_res"
+RES_VARIANT = {1: "iw_apply_res<float, 1,", 2: "iw_apply_res<float, 2,"}
 
 
 # PCGInit1 fused with the first apply (iw_jtf_apply, one strip pass): Offset 8 + Angle 4 +
@@ -68,7 +87,7 @@ INIT_KERNEL = "iw_jtf_apply"
 INIT_BYTES_PER_PX = 8 + 4 + 8 + 8 + 4 + 12 + 4 + 1 + 12 + 12
 
 
-def pmc_traffic(liter: int, first: int = 0):
+def pmc_traffic(liter: int, first: int = 0, res: bool = False):
     try:
         with open(PMC_FILE) as f:
             ks = json.load(f)["kernels"]
@@ -76,7 +95,7 @@ def pmc_traffic(liter: int, first: int = 0):
         return None
     total = 0.0
     for i in range(first, liter):
-        key = APPLY_VARIANT[min(i, 2)]
+        key = RES_VARIANT[min(i, 2)] if res else APPLY_VARIANT[min(i, 2)]
         hit = [v for k, v in ks.items() if key in k]
         if not hit or "FETCH_SIZE" not in hit[0] or "WRITE_SIZE" not in hit[0]:
             return None
@@ -259,6 +278,11 @@ def main():
     kname = s.apply_kernel_name()
     n_apply, apply_ms = s.kernel_stat(kname)
     n_init, init_ms = (0, 0.0) if sfs else s.kernel_stat(INIT_KERNEL)
+    res = False
+    if not sfs:
+        n_res, res_ms = s.kernel_stat(RES_KERNEL)
+        if n_res:   # the loop ran as iw_apply_res passes: that is the dominant kernel
+            kname, n_apply, apply_ms, res = RES_KERNEL, n_res, res_ms, True
     s.set_kernel_timing(0)
     # the in-loop applies of one step: PCG iterations first..liter-1 (first = 1 when the
     # first iteration's apply ran inside iw_jtf_apply)
@@ -269,7 +293,8 @@ def main():
     if sfs:   # sfs_strip: SURVEY.md §8d's per-pixel apply bytes
         bpp = SFS_APPLY_BYTES_PER_PX
     else:
-        bpp = sum(apply_bytes_per_px(i, args.liter) for i in range(first, args.liter)) / (args.liter - first)
+        per = res_bytes_per_px if res else apply_bytes_per_px
+        bpp = sum(per(i, args.liter) for i in range(first, args.liter)) / (args.liter - first)
     achieved = bpp * npx / avg_apply_s / 1e9
     # the pure apply (reads p) timed separately for the kernel-only unknowns/s
     n_local = ch * W * (sl.mem_rows if sl else H)
@@ -307,7 +332,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / PEAK_HBM_GBS,
             "traffic": (None if world != 1 or args.size != 4096 else
-                        pmc_traffic_sfs() if sfs else pmc_traffic(args.liter, first)),
+                        pmc_traffic_sfs() if sfs else pmc_traffic(args.liter, first, res)),
             "traffic_unit": "bytes per launch (2 FETCH_SIZE + WRITE_SIZE, "
                             f"{os.path.relpath(PMC_FILE_SFS if sfs else PMC_FILE, ROOT)})",
             "avg_us": avg_apply_s * 1e6,

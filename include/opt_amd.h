@@ -85,6 +85,12 @@ void* OptAMD_PlanStream(Opt_Plan* plan);
 /* Outer iterations completed since the last Init. */
 int OptAMD_PlanIterations(Opt_Plan* plan);
 
+/* Copy up to n of the plan's device scalar slots (fp64: costs, the PCG rz / pAp sums of
+ * the last Step, ...) to `out` after synchronising; returns the number copied. The slot
+ * layout is the family's (image_warping: opt_amd/csrc/image_warping.hip, kScBase /
+ * kSlots); a parity/diagnostic hook with no reference counterpart. */
+int OptAMD_PlanScalars(Opt_Plan* plan, double* out, int n);
+
 /* ---- multi-GPU row-slab decomposition (no reference counterpart:
  * the reference is single-device, §2.3) ------------------------------------------ */
 typedef struct OptAMD_Comm OptAMD_Comm;

@@ -66,6 +66,7 @@ _SIGNATURES = [
     ("OptAMD_KernelReport", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int]),
     ("OptAMD_PlanStream", _VP, [_VP]),
     ("OptAMD_PlanIterations", ctypes.c_int, [_VP]),
+    ("OptAMD_PlanScalars", ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     ("OptAMD_RcclUniqueId", ctypes.c_int, [_VP]),
     ("OptAMD_CommCreateRccl", _VP, [_VP, ctypes.c_int, ctypes.c_int]),
     ("OptAMD_CommDestroy", None, [_VP]),
@@ -284,6 +285,12 @@ class OptSolver:
 
     def iterations(self) -> int:
         return self.lib.OptAMD_PlanIterations(self.plan)
+
+    def scalars(self, n: int = 256):
+        """The plan's device scalar slots after the last call (OptAMD_PlanScalars)."""
+        buf = (ctypes.c_double * n)()
+        k = self.lib.OptAMD_PlanScalars(self.plan, buf, n)
+        return list(buf)[: max(k, 0)]
 
     def halo(self) -> int:
         return self.lib.OptAMD_PlanHalo(self.plan)

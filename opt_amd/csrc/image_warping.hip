@@ -387,6 +387,300 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
     block_reduce_publish<1>(v, rs, g.tile);   // partials by tile: split launches share the slot
 }
 
+// ------------------------------------------ apply with the residual update fused
+// PCG iteration i >= 1 as ONE pass (iw_apply<2> + the previous iteration's iw_residual):
+//   r_i   = r_{i-1} - alpha_{i-1} Ap_{i-1}                       (PCGStep2's r update, :690)
+//   p_i   = z_i + beta_i p_{i-1},  z_i = pre r_i                  (PCGStep3, :814-845)
+//   delta = delta + alpha_{i-1} p_{i-1}                          (PCGStep2's delta update, :680)
+//   Ap_i  = J^T J p_i                                            (PCGStep1, :607-632)
+// r_i is formed wherever the stencil needs it (own pixel, vertical window, edge pixel)
+// from r_{i-1} and Ap_{i-1}, so the separate residual pass — which re-read r, Ap, pre and
+// the flags and wrote r — is gone. Its reduction rz_i = r_i.(pre r_i) is still summed
+// here, directly, for alpha_i and as the next expansion's base; what this pass cannot
+// have is rz_i before it forms p_i, so beta_i's numerator comes from the exact identity
+//   r_i.W r_i = r_{i-1}.W r_{i-1} - 2 alpha r_{i-1}.W Ap_{i-1} + alpha^2 Ap_{i-1}.W Ap_{i-1}
+// (W = pre, or 1 without a preconditioner: PCGStep2's weighting, :705-708), whose two
+// new sums the previous pass reduced beside p.Ap. All four sums accumulate in fp64 per
+// lane, so the identity's value agrees with the direct sum to ~1e-10 relative (stored in
+// slot `rzx_out`; the reference's own float-atomic sums move by ~1e-7 run to run).
+// Reductions: sc[rs.out + 0..3] = {rz_i, p_i.Ap_i, r_i.W Ap_i, Ap_i.W Ap_i}.
+// DM 1: delta = alpha p_{i-1} (i == 1), DM 2: delta += alpha p_{i-1}. rout / Apout null
+// in the last iteration (nothing reads r_L or Ap_L).
+// Scalar slots of iteration j (ImageWarpingPlan: kScBase + kSlots * j): rz, pAp, rAp, ApAp, rz by the identity
+constexpr int kSlots = 5;
+// Accumulation of the fused passes' sums: 0 fp32 products and lane sums, 1 fp32 products
+// summed in fp64, 2 fp64 products summed in fp64 (the identity's terms cancel: their
+// rounding is amplified by rz_{i-1} / rz_i).
+#ifndef OPTAMD_IW_ACC
+#define OPTAMD_IW_ACC 2
+#endif
+#if OPTAMD_IW_ACC == 0
+typedef float acc_t;
+#else
+typedef double acc_t;
+#endif
+// w0 a0 b0 + w1 a1 b1 + w2 a2 b2 at the accumulation precision
+template <typename T>
+__device__ __forceinline__ acc_t wdot3(T w0, T a0, T b0, T w1, T a1, T b1, T w2, T a2, T b2) {
+#if OPTAMD_IW_ACC == 2
+    return (double)w0 * (double)a0 * (double)b0 + (double)w1 * (double)a1 * (double)b1 +
+           (double)w2 * (double)a2 * (double)b2;
+#else
+    return (acc_t)(w0 * a0 * b0 + w1 * a1 * b1 + w2 * a2 * b2);
+#endif
+}
+// minimum waves per SIMD the fused passes are compiled for (0: the compiler's choice)
+#ifndef OPTAMD_IW_WPE
+#define OPTAMD_IW_WPE 0
+#endif
+#if OPTAMD_IW_WPE > 0
+#define IW_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(OPTAMD_IW_WPE)))
+#else
+#define IW_FUSED_ATTR
+#endif
+// 32-bit byte offsets from a uniform base: global_load / global_store with an SGPR base and
+// a VGPR offset, no 64-bit address arithmetic per access (the plan takes these kernels
+// only when 3 N sizeof(T) < 2^32). Vec2 = the two interleaved Offset channels of a pixel.
+template <typename T>
+using vec2_t = T __attribute__((ext_vector_type(2)));
+template <bool NT, typename V, typename T>
+__device__ __forceinline__ V ldb(const T* base, unsigned off) {
+    const V* p = reinterpret_cast<const V*>(reinterpret_cast<const char*>(base) + off);
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT, typename V, typename T>
+__device__ __forceinline__ void stb(T* base, unsigned off, V v) {
+    V* p = reinterpret_cast<V*>(reinterpret_cast<char*>(base) + off);
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+constexpr int kFStrip = 62;
+template <typename T>
+__device__ __forceinline__ WaveGeom geom_fused(const Args<T>& a) {
+    WaveGeom g;
+    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    g.tile = t;
+    const int strip = t % a.nstrips, rb = t / a.nstrips;
+    g.lane = threadIdx.x & (kWave - 1);
+    const int w = threadIdx.x / kWave;
+    g.x = strip * kFStrip - 1 + g.lane;
+    g.edge_lane = (g.lane == 0) || (g.lane == kWave - 1);
+    g.ex = g.lane == 0 ? g.x - 1 : g.x + 1;
+    g.y0 = a.dom.y_lo + (rb * (kBlock / kWave) + w) * a.rows;
+    g.y1 = min(g.y0 + a.rows, a.dom.y_hi);
+    g.out_lane = g.lane >= 1 && g.lane <= kFStrip && g.x < a.dom.W;
+    return g;
+}
+template <typename T>
+struct RRaw {
+    vec2_t<T> r, ap, q, d;     // r_{i-1}, Ap_{i-1}, p_{i-1}, delta (Offset channels)
+    T rt, at, qt, dt, w2, ang;  // the angle channels, its pre, the angle
+    float2 u;
+    int f, in;
+    vec2_t<T> er, eap, eq;      // edge pixel
+    T ert, eat, eqt, ew2, eang;
+    float2 eu;
+    int ef, ein;
+};
+template <typename T>
+struct RRow {
+    T px, py, pt, c, s;
+    float ux, uy;
+    int act, fit;
+    T rx, ry, rt;      // r_i (for r.W Ap)
+    T w0, w2;          // PCGStep2's weights of the Offset / angle channels
+    T epx, epy;        // edge pixel, as PRow
+    float eux, euy;
+    int eact;
+    T ejx, ejy;
+};
+// byte offsets of pixel i's Offset pair, angle channel (tb = 2 N sizeof(T)) and scalar
+template <typename T>
+struct POff {
+    unsigned xy, t, s;
+    __device__ __forceinline__ POff(unsigned i, unsigned tb) : xy(i * 2u * (unsigned)sizeof(T)),
+        t(tb + i * (unsigned)sizeof(T)), s(i * (unsigned)sizeof(T)) {}
+};
+template <typename T, int DM, bool NT>
+__device__ __forceinline__ RRaw<T> raw_rrow(const Args<T>& a, const WaveGeom& g, int y, unsigned tb,
+                                            const T* pin, const T* rin, const T* Apin, const T* pre,
+                                            const T* delta) {
+    RRaw<T> q;
+    q.in = present(a.dom, g.x, y);
+    const unsigned i = q.in ? (unsigned)a.dom.off(g.x, y) : 0u;
+    const POff<T> o(i, tb);
+    q.f = ldb<false, uint8_t>(a.flags, i);
+    q.u = ldb<false, float2>(a.U, 8u * i);
+    q.ang = ldb<false, T>(a.A, o.s);
+    q.r = ldb<NT, vec2_t<T>>(rin, o.xy); q.rt = ldb<NT, T>(rin, o.t);
+    q.ap = ldb<NT, vec2_t<T>>(Apin, o.xy); q.at = ldb<NT, T>(Apin, o.t);
+    q.w2 = ldb<NT, T>(pre, o.s);
+    q.q = ldb<NT, vec2_t<T>>(pin, o.xy); q.qt = ldb<NT, T>(pin, o.t);
+    if (DM == 2) { q.d = ldb<NT, vec2_t<T>>(delta, o.xy); q.dt = ldb<NT, T>(delta, o.t); }
+    q.ein = 0;
+    if (g.edge_lane) {
+        q.ein = present(a.dom, g.ex, y);
+        const unsigned e = q.ein ? (unsigned)a.dom.off(g.ex, y) : 0u;
+        const POff<T> oe(e, tb);
+        q.ef = ldb<false, uint8_t>(a.flags, e);
+        q.eu = ldb<false, float2>(a.U, 8u * e);
+        q.eang = ldb<false, T>(a.A, oe.s);
+        q.er = ldb<false, vec2_t<T>>(rin, oe.xy); q.ert = ldb<false, T>(rin, oe.t);
+        q.eap = ldb<false, vec2_t<T>>(Apin, oe.xy); q.eat = ldb<false, T>(Apin, oe.t);
+        q.ew2 = ldb<false, T>(pre, oe.s);
+        q.eq = ldb<false, vec2_t<T>>(pin, oe.xy); q.eqt = ldb<false, T>(pin, oe.t);
+    }
+    return q;
+}
+// r_i from r_{i-1}, Ap_{i-1} (iw_residual's expression), then z_i and p_i (make_p<2>)
+template <typename T>
+__device__ __forceinline__ void make_rp(const Args<T>& a, int f, T alpha, T beta, T r0, T r1, T r2, T a0, T a1,
+                                        T a2, T w2, T q0, T q1, T q2, T& rx, T& ry, T& rt, T& px, T& py,
+                                        T& pt) {
+    rx = r0 - alpha * a0; ry = r1 - alpha * a1; rt = r2 - alpha * a2;
+    make_p<T, 2>(a, f, beta, rx, ry, rt, w2, q0, q1, q2, px, py, pt);
+}
+// Finish a raw row: r_i, p_i, the edge pixel's p and residual; an owned row (own) also
+// stores r_i (unless rout is null) and the updated delta right here and adds its r_i.W r_i.
+template <typename T, int DM, bool NT>
+__device__ __forceinline__ RRow<T> finish_rrow(const Args<T>& a, const RRaw<T>& q, T beta, T alpha, bool own,
+                                               const WaveGeom& g, int y, unsigned tb, T* rout, T* delta,
+                                               acc_t& rzd) {
+    RRow<T> o;
+    const int f = q.in ? q.f : 0;
+    o.act = f & 1;
+    o.fit = (f >> 1) & 1;
+    o.ux = q.in ? q.u.x : 0.f;
+    o.uy = q.in ? q.u.y : 0.f;
+    sc_of(q.in ? q.ang : (T)0, &o.c, &o.s);
+    make_rp(a, f, alpha, beta, q.r.x, q.r.y, q.rt, q.ap.x, q.ap.y, q.at, q.w2, q.q.x, q.q.y, q.qt, o.rx, o.ry, o.rt,
+            o.px, o.py, o.pt);
+    o.w0 = a.use_pre ? pre_offset(a, f) : (T)1;
+    o.w2 = a.use_pre ? q.w2 : (T)1;
+    if (own && g.out_lane) {
+        const POff<T> off((unsigned)a.dom.off(g.x, y), tb);
+        vec2_t<T> d;
+        T dt;
+        if (DM == 1) { d.x = alpha * q.q.x; d.y = alpha * q.q.y; dt = alpha * q.qt; }
+        else { d.x = q.d.x + alpha * q.q.x; d.y = q.d.y + alpha * q.q.y; dt = q.dt + alpha * q.qt; }
+        if (!o.act) { d.x = 0; d.y = 0; dt = 0; }
+        stb<NT>(delta, off.xy, d); stb<NT>(delta, off.t, dt);
+        if (rout) {
+            vec2_t<T> r; r.x = o.rx; r.y = o.ry;
+            stb<NT>(rout, off.xy, r); stb<NT>(rout, off.t, o.rt);
+        }
+        rzd += wdot3(o.w0, o.rx, o.rx, o.w0, o.ry, o.ry, o.w2, o.rt, o.rt);
+    }
+    if (!o.act) { o.px = 0; o.py = 0; o.pt = 0; }
+    const int ef = q.ein ? q.ef : 0;
+    o.eact = ef & 1;
+    o.eux = q.ein ? q.eu.x : 0.f;
+    o.euy = q.ein ? q.eu.y : 0.f;
+    T ec, es, ept, erx, ery, ert, ax, ay;
+    sc_of(q.ein ? q.eang : (T)0, &ec, &es);
+    make_rp(a, ef, alpha, beta, q.er.x, q.er.y, q.ert, q.eap.x, q.eap.y, q.eat, q.ew2, q.eq.x, q.eq.y, q.eqt, erx,
+            ery, ert, o.epx, o.epy, ept);
+    if (!o.eact) { o.epx = 0; o.epy = 0; ept = 0; }
+    jedge(o.epx, o.epy, ept, ec, es, o.eux, o.euy, o.px, o.py, o.ux, o.uy, o.eact && o.act, a.wr,
+          o.ejx, o.ejy, ax, ay);
+    return o;
+}
+template <typename T, int DM, int NT = 2>
+__global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_apply_res(Args<T> a, const T* __restrict__ pin,
+                                                       const T* __restrict__ rin, const T* __restrict__ Apin,
+                                                       const T* __restrict__ pre, T* __restrict__ pout,
+                                                       T* __restrict__ rout, T* __restrict__ Apout,
+                                                       T* __restrict__ delta, double* __restrict__ sc,
+                                                       int prev, double base_scale, ReduceSlot rs) {
+    constexpr bool LNT = (NT & 1) != 0, SNT = (NT & 2) != 0;
+    // 64-column strips with the 2-lane edge record (iw_apply's geometry): every store is a
+    // whole aligned 256-B run per wave. (62-column strips without the edge record — 116
+    // instead of 154 VGPRs, 4 waves per SIMD — took 423-502 us against 406-441: their
+    // stores split cache lines between waves.)
+    const WaveGeom g = geom(a);
+    // iteration i-1's scalars: alpha_{i-1} = rz / pAp; beta_i from the identity over rz
+    const double rzp = sc[prev], papp = sc[prev + 1];
+    // the identity takes alpha as the pixels apply it (rounded to T): with the cancellation
+    // in it (rz_i << rz_{i-1}) the fp64 alpha would be off by ~1e-7 x rz_{i-1} / rz_i
+    const T alpha = (T)(rzp / papp);
+    const double alpha_d = (double)alpha;
+    const double rz_id = base_scale * rzp - 2.0 * alpha_d * sc[prev + 2] + alpha_d * alpha_d * sc[prev + 3];
+    const T beta = (T)(rz_id / rzp);
+    if (blockIdx.x == 0 && threadIdx.x == 0) sc[prev + kSlots + 4] = rz_id;
+    const T wr = a.wr, wf2 = a.wf * a.wf;
+    const unsigned tb = (unsigned)(2 * a.dom.npix_mem() * (long long)sizeof(T));
+    acc_t rzd = 0, papd = 0, rapd = 0, apapd = 0;
+    if (g.y0 < g.y1) {
+        auto raw = [&](int y) { return raw_rrow<T, DM, LNT>(a, g, y, tb, pin, rin, Apin, pre, delta); };
+        auto fin = [&](const RRaw<T>& q, int y) {
+            return finish_rrow<T, DM, SNT>(a, q, beta, alpha, y >= g.y0 && y < g.y1, g, y, tb, rout, delta, rzd);
+        };
+        const RRow<T> up = fin(raw(g.y0 - 1), g.y0 - 1);
+        RRow<T> A = fin(raw(g.y0), g.y0);
+        RRow<T> B = fin(raw(g.y0 + 1), g.y0 + 1);
+        T in_up_x, in_up_y, my_x, my_y, thm, ax, ay;
+        jedge(up.px, up.py, up.pt, up.c, up.s, up.ux, up.uy, A.px, A.py, A.ux, A.uy,
+              up.act && A.act, wr, in_up_x, in_up_y, ax, ay);
+        jedge(A.px, A.py, A.pt, A.c, A.s, A.ux, A.uy, up.px, up.py, up.ux, up.uy,
+              up.act && A.act, wr, my_x, my_y, ax, ay);
+        thm = -wr * (ax * my_x + ay * my_y);
+        // Ap of row y from (cur, dn) and the carries from the row above; rolls the carries
+        auto apply_row = [&](const RRow<T>& cur, const RRow<T>& dn, int y) {
+            const T lpx = from_left(cur.px, cur.epx), lpy = from_left(cur.py, cur.epy);
+            const T rpx = from_right(cur.px, cur.epx), rpy = from_right(cur.py, cur.epy);
+            const float lux = from_left(cur.ux, cur.eux), luy = from_left(cur.uy, cur.euy);
+            const float rux = from_right(cur.ux, cur.eux), ruy = from_right(cur.uy, cur.euy);
+            const int lact = from_left_i(cur.act, cur.eact), ract = from_right_i(cur.act, cur.eact);
+            T jpx_x, jpx_y, apx_x, apx_y, jmx_x, jmx_y, amx_x, amx_y;
+            T jpy_x, jpy_y, apy_x, apy_y, jdn_x, jdn_y, adn_x, adn_y;
+            jedge(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, rpx, rpy, rux, ruy,
+                  cur.act && ract, wr, jpx_x, jpx_y, apx_x, apx_y);
+            jedge(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, lpx, lpy, lux, luy,
+                  cur.act && lact, wr, jmx_x, jmx_y, amx_x, amx_y);
+            jedge(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, dn.px, dn.py, dn.ux, dn.uy,
+                  cur.act && dn.act, wr, jpy_x, jpy_y, apy_x, apy_y);
+            jedge(dn.px, dn.py, dn.pt, dn.c, dn.s, dn.ux, dn.uy, cur.px, cur.py, cur.ux, cur.uy,
+                  cur.act && dn.act, wr, jdn_x, jdn_y, adn_x, adn_y);
+            const T inpx_x = from_right(jmx_x, cur.ejx), inpx_y = from_right(jmx_y, cur.ejy);
+            const T inmx_x = from_left(jpx_x, cur.ejx), inmx_y = from_left(jpx_y, cur.ejy);
+            T aox = wr * ((jpx_x + jmx_x + jpy_x + my_x) - (inpx_x + inmx_x + jdn_x + in_up_x));
+            T aoy = wr * ((jpx_y + jmx_y + jpy_y + my_y) - (inpx_y + inmx_y + jdn_y + in_up_y));
+            if (cur.fit) { aox += wf2 * cur.px; aoy += wf2 * cur.py; }
+            T aot = thm - wr * ((apx_x * jpx_x + apx_y * jpx_y) + (amx_x * jmx_x + amx_y * jmx_y) +
+                                (apy_x * jpy_x + apy_y * jpy_y));
+            if (!cur.act) { aox = 0; aoy = 0; aot = 0; }
+            if (g.out_lane) {
+                const POff<T> off((unsigned)a.dom.off(g.x, y), tb);
+                if (Apout) {
+                    vec2_t<T> v; v.x = aox; v.y = aoy;
+                    stb<SNT>(Apout, off.xy, v); stb<SNT>(Apout, off.t, aot);
+                }
+                vec2_t<T> pv; pv.x = cur.px; pv.y = cur.py;
+                stb<SNT>(pout, off.xy, pv); stb<SNT>(pout, off.t, cur.pt);
+                papd += (acc_t)(cur.px * aox + cur.py * aoy + cur.pt * aot);
+                rapd += wdot3(cur.w0, cur.rx, aox, cur.w0, cur.ry, aoy, cur.w2, cur.rt, aot);
+                apapd += wdot3(cur.w0, aox, aox, cur.w0, aoy, aoy, cur.w2, aot, aot);
+            }
+            in_up_x = jpy_x; in_up_y = jpy_y;
+            my_x = jdn_x; my_y = jdn_y;
+            thm = -wr * (adn_x * jdn_x + adn_y * jdn_y);
+        };
+        // two rows per trip, the two row records swapping roles (no register copies)
+        for (int y = g.y0; y < g.y1; y += 2) {
+            const RRaw<T> n1 = raw(y + 2);
+            apply_row(A, B, y);
+            A = fin(n1, y + 2);
+            if (y + 1 >= g.y1) break;
+            const RRaw<T> n2 = raw(y + 3);
+            apply_row(B, A, y + 1);
+            B = fin(n2, y + 3);
+        }
+    }
+    double v[4] = {(double)rzd, (double)papd, (double)rapd, (double)apapd};
+    block_reduce_publish<4>(v, rs, g.tile);
+}
+
 // ------------------------------------------------------------- value rows
 template <typename T>
 struct VRaw {
@@ -615,38 +909,26 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
 // 1..62 finds every horizontal neighbour's p in a lane neighbour (DPP) and needs no
 // second edge ring. Rows: J^T F runs one row ahead of the apply (rows y0-1 .. y1,
 // the outer two for the apply's vertical neighbours only; unknown rows y0-2 .. y1+1).
-// One reduction of two scalars: sc[rs.out] = rz[0], sc[rs.out + 1] = pAp[0].
-constexpr int kFStrip = 62;
+// One reduction of four scalars (fp64 per lane): sc[rs.out + 0..3] = {rz[0], pAp[0],
+// r_0.W Ap_0, Ap_0.W Ap_0} — the last two for iw_apply_res's identity for rz[1] (W r_0
+// is summed from r_0, not taken as p_0: p_0 is rounded to T, and the identity cancels
+// rz[0] down to rz[1], 2e4 x smaller on the test problems).
 template <typename T>
 struct FRow {          // a finished row of the fused kernel's apply window
     T px, py, pt, c, s;
+    T rx, ry, rt;      // r_0
+    T w0, w2;          // PCGStep2's weights (pre, or 1 without a preconditioner)
     float ux, uy;
     int act, fit;
 };
-template <typename T>
-__device__ __forceinline__ WaveGeom geom_fused(const Args<T>& a) {
-    WaveGeom g;
-    const int t = xcd_remap(blockIdx.x, gridDim.x);
-    g.tile = t;
-    const int strip = t % a.nstrips, rb = t / a.nstrips;
-    g.lane = threadIdx.x & (kWave - 1);
-    const int w = threadIdx.x / kWave;
-    g.x = strip * kFStrip - 1 + g.lane;
-    g.edge_lane = (g.lane == 0) || (g.lane == kWave - 1);
-    g.ex = g.lane == 0 ? g.x - 1 : g.x + 1;
-    g.y0 = a.dom.y_lo + (rb * (kBlock / kWave) + w) * a.rows;
-    g.y1 = min(g.y0 + a.rows, a.dom.y_hi);
-    g.out_lane = g.lane >= 1 && g.lane <= kFStrip && g.x < a.dom.W;
-    return g;
-}
 template <typename T, int NT = 2>
-__global__ __launch_bounds__(kBlock) void iw_jtf_apply(Args<T> a, T* __restrict__ r, T* __restrict__ pre,
+__global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_jtf_apply(Args<T> a, T* __restrict__ r, T* __restrict__ pre,
                                                        T* __restrict__ pout, T* __restrict__ Ap,
                                                        ReduceSlot rs) {
     const WaveGeom g = geom_fused(a);
     const T wr = a.wr, wf2 = a.wf * a.wf;
     const long long N = a.dom.npix_mem();
-    T rzdot = 0, papdot = 0;
+    acc_t rzdot = 0, papdot = 0, rapd = 0, apapd = 0;
     // J^T F of row y from the window (cur = row y, dn = row y+1): stores r / pre / flags
     // when the row is this wave's, returns the apply's view of the row (p = pre r)
     auto jrow = [&](const VRow<T>& cur, const VRow<T>& dn, JCarry<T>& k, int y, bool own) {
@@ -658,13 +940,16 @@ __global__ __launch_bounds__(kBlock) void iw_jtf_apply(Args<T> a, T* __restrict_
             st_v<(NT & 2) != 0>(r + 2 * i, o.rx); st_v<(NT & 2) != 0>(r + 2 * i + 1, o.ry);
             st_v<(NT & 2) != 0>(r + 2 * N + i, o.rt);
             st_v<(NT & 2) != 0>(pre + i, o.wt);
-            if (cur.act) rzdot += o.rx * (o.wo * o.rx) + o.ry * (o.wo * o.ry) + o.rt * (o.wt * o.rt);
+            if (cur.act) rzdot += wdot3(o.wo, o.rx, o.rx, o.wo, o.ry, o.ry, o.wt, o.rt, o.rt);
         }
         FRow<T> p;
         // iw_apply<1>'s make_p: p = pre r per channel (zero on inactive pixels)
         p.px = o.wo * o.rx; p.py = o.wo * o.ry; p.pt = o.wt * o.rt;
         if (!cur.act) { p.px = 0; p.py = 0; p.pt = 0; }
         p.c = cur.c; p.s = cur.s; p.ux = cur.ux; p.uy = cur.uy; p.act = cur.act; p.fit = cur.fit;
+        p.w0 = a.use_pre ? o.wo : (T)1;
+        p.w2 = a.use_pre ? o.wt : (T)1;
+        p.rx = o.rx; p.ry = o.ry; p.rt = o.rt;
         return p;
     };
     if (g.y0 < g.y1) {
@@ -720,7 +1005,9 @@ __global__ __launch_bounds__(kBlock) void iw_jtf_apply(Args<T> a, T* __restrict_
                 }
                 st_v<(NT & 2) != 0>(pout + 2 * i, cur.px); st_v<(NT & 2) != 0>(pout + 2 * i + 1, cur.py);
                 st_v<(NT & 2) != 0>(pout + 2 * N + i, cur.pt);
-                papdot += cur.px * aox + cur.py * aoy + cur.pt * aot;
+                papdot += (acc_t)(cur.px * aox + cur.py * aoy + cur.pt * aot);
+                rapd += wdot3(cur.w0, cur.rx, aox, cur.w0, cur.ry, aoy, cur.w2, cur.rt, aot);
+                apapd += wdot3(cur.w0, aox, aox, cur.w0, aoy, aoy, cur.w2, aot, aot);
             }
             in_up_x = jpy_x; in_up_y = jpy_y;
             my_x = jdn_x; my_y = jdn_y;
@@ -730,8 +1017,8 @@ __global__ __launch_bounds__(kBlock) void iw_jtf_apply(Args<T> a, T* __restrict_
             vdn = finish_vrow<T, true>(nx);
         }
     }
-    double v[2] = {(double)rzdot, (double)papdot};
-    block_reduce_publish<2>(v, rs, g.tile);
+    double v[4] = {(double)rzdot, (double)papdot, (double)rapd, (double)apapd};
+    block_reduce_publish<4>(v, rs, g.tile);
 }
 
 // ----------------------------------------------------------------- cost kernel
@@ -1051,9 +1338,9 @@ public:
         rows_ = env_int("OPT_AMD_ROWS", 0);   // 0: iw::rows_for (per domain)
         depth_ = env_int("OPT_AMD_DEPTH", 1);
         nt_ = env_int("OPT_AMD_IW_NT", 6);
-        fused_init_ = env_int("OPT_AMD_IW_FUSED_INIT", 1) != 0;
+        read_knobs();
         timer_.apply_name = apply_kernel_name();
-        timer_.aux_name = "iw_jtf_apply";
+        timer_.aux_names = {"iw_jtf_apply", "iw_apply_res"};
         allocate();
     }
     ~ImageWarpingPlan() override {
@@ -1096,6 +1383,7 @@ public:
     }
 
     int step(void** params) override {
+        read_knobs();   // per Step: an A/B of the loop structure on one plan (same allocations)
         if (!initialised_) init(params);
         if (n_iter_ >= sp_.nIterations) {
             cleanup_log();
@@ -1105,7 +1393,14 @@ public:
         bind(params, false);
         exchange_unknowns();
         const int L = std::max(0, sp_.lIterations);
-        red_.ensure(std::max({stencil_blocks(), fused_blocks(), 2048}), 2, kScBase + 2 * (L + 2));
+        red_.ensure(std::max({stencil_blocks(), fused_blocks(), 2048}), 4, kScBase + iw::kSlots * (L + 2));
+        if (print_addr_) {   // OPT_AMD_PRINT_ADDR=1: placement of every stream (HBM channel study)
+            print_addr_ = false;
+            fprintf(stderr, "[opt_amd] addr r=%p r1=%p p0=%p p1=%p Ap=%p Ap1=%p delta=%p pre=%p flags=%p "
+                    "O=%p A=%p U=%p C=%p M=%p\n", (void*)r_, (void*)r1_, (void*)p0_, (void*)p1_, (void*)Ap_,
+                    (void*)Ap1_, (void*)delta_, (void*)pre_, (void*)flags_, (void*)cur_O_, (void*)cur_A_,
+                    (void*)cur_U_, (void*)cur_C_, (void*)cur_M_);
+        }
         T* pcur = p0_;
         T* pprev = p1_;
         // PCGInit1 (r, pre, flags, rz[0]) from the arrays bound at THIS Step, as the
@@ -1113,6 +1408,9 @@ public:
         // in place between Steps (Opt.h:64-65). On one domain it is fused with the first
         // PCG iteration's apply (iw_jtf_apply: the first p = pre r needs no global scalar).
         const bool fused = fused_init_ && !distributed() && L >= 1;
+        // iterations 1.. as iw_apply_res (the residual update folded into the next apply;
+        // needs iw_jtf_apply's two extra sums)
+        const bool res = fused && fused_res_;
         if (fused) {
             launch_jtf_apply(pcur, L == 1);
         } else {
@@ -1135,7 +1433,16 @@ public:
         for (int i = 0; i < L; ++i) {
             if (i > 0 || !fused) std::swap(pcur, pprev);   // pcur <- new p, pprev <- old p
             const bool last = i + 1 == L;   // timed by events on the launch (launch_apply)
-            if (i == 0 && fused) { /* iw_jtf_apply above */ }
+            if (i == 0 && fused) {   // iw_jtf_apply above
+                if (res) {   // r_1 is formed inside iteration 1's pass
+                    if (last) break;
+                    continue;
+                }
+            } else if (res) {
+                launch_apply_res(i, pprev, pcur, last);
+                if (last) break;
+                continue;
+            }
             else if (i == 0) launch_apply<1, 0>(nullptr, pcur, pap(i), 0, 0, 0, 0, nullptr, last);
             else if (split) {
                 halo_mark();
@@ -1249,17 +1556,51 @@ public:
     }
 
 private:
+    void read_knobs() {
+        const int rw = env_int("OPT_AMD_ROWS", 0);   // 0: iw::rows_for (per domain)
+        if (rw > 0 && rw != rows_) {
+            rows_ = rw;
+            rows_auto_ = false;
+            nrowblocks_ = (dom_.y_hi - dom_.y_lo + rows_ * 4 - 1) / (rows_ * 4);
+        }
+        const long long st = env_int("OPT_AMD_STAGGER", kStagger) & ~255LL;
+        if (st != stagger_) {
+            stagger_ = st;
+            OPT_HIP_CHECK(hipStreamSynchronize(stream_));
+            place();
+        }
+        fused_init_ = env_int("OPT_AMD_IW_FUSED_INIT", 1) != 0;
+        fused_res_ = env_int("OPT_AMD_IW_FUSED_RES", 1) != 0;
+    }
+    // A zeroed plan vector with kSlack spare bytes: place() may move each vector's base
+    // within them between Steps (every vector is rewritten before it is read in a Step).
+    static constexpr size_t kSlack = 1 << 20;
+    // default stagger: 9 pages. On one plan (same physical pages) staggers of 0 .. 128 KiB
+    // moved the 4096^2 GN step by 1-2.5 %, 0 the slowest and 36 KiB among the fastest on
+    // three plans (tools/ab_knobs.py)
+    static constexpr long long kStagger = 36864;
+    void* vec_alloc(size_t bytes) {
+        char* p = (char*)dmalloc(bytes + kSlack);
+        raw_.push_back(p);
+        OPT_HIP_CHECK(hipMemset(p, 0, bytes + kSlack));
+        return p;
+    }
+    // OPT_AMD_STAGGER=S: vector k starts (k S) mod kSlack bytes into its allocation (HBM
+    // placement study: the step time moves by up to ~8% with where the streams land)
+    void place() {
+        T** vs[] = {&r_, &p0_, &p1_, &Ap_, &delta_, &r1_, &Ap1_, &pre_};
+        if (raw_.size() < 9) return;
+        for (int k = 0; k < 8; ++k) *vs[k] = (T*)(raw_[k] + ((size_t)stagger_ * k) % kSlack);
+        flags_ = (uint8_t*)(raw_[8] + ((size_t)stagger_ * 8) % kSlack);
+    }
     void allocate() {
         const long long N = dom_.npix_mem();
         nvec_ = 3 * N;
-        for (T** v : {&r_, &p0_, &p1_, &Ap_, &delta_})
-            *v = (T*)dmalloc(sizeof(T) * nvec_);
-        for (T* v : {r_, p0_, p1_, Ap_, delta_})
-            OPT_HIP_CHECK(hipMemset(v, 0, sizeof(T) * nvec_));
-        pre_ = (T*)dmalloc(sizeof(T) * N);   // angle channel only (Args::preO)
-        OPT_HIP_CHECK(hipMemset(pre_, 0, sizeof(T) * N));
-        flags_ = (uint8_t*)dmalloc(N);
-        OPT_HIP_CHECK(hipMemset(flags_, 0, N));
+        for (T** v : {&r_, &p0_, &p1_, &Ap_, &delta_, &r1_, &Ap1_})
+            *v = (T*)vec_alloc(sizeof(T) * nvec_);
+        pre_ = (T*)vec_alloc(sizeof(T) * N);   // angle channel only (Args::preO)
+        flags_ = (uint8_t*)vec_alloc(N);
+        place();
         nstrips_ = (dom_.W + iw::kStrip - 1) / iw::kStrip;
         if (rows_ <= 0 || rows_auto_) { rows_auto_ = true; rows_ = iw::rows_for(nstrips_, dom_.y_hi - dom_.y_lo); }
         nrowblocks_ = (dom_.y_hi - dom_.y_lo + rows_ * 4 - 1) / (rows_ * 4);
@@ -1273,10 +1614,12 @@ private:
         }
     }
     void release() {
-        for (T** v : {&r_, &pre_, &p0_, &p1_, &Ap_, &delta_, &dO_, &dA_}) { dfree(*v); *v = nullptr; }
-        for (float** v : {&dU_, &dC_, &dM_}) { dfree(*v); *v = nullptr; }
-        dfree(flags_);
+        for (char* p : raw_) dfree(p);
+        raw_.clear();
+        for (T** v : {&r_, &pre_, &p0_, &p1_, &Ap_, &delta_, &r1_, &Ap1_}) *v = nullptr;
         flags_ = nullptr;
+        for (T** v : {&dO_, &dA_}) { dfree(*v); *v = nullptr; }
+        for (float** v : {&dU_, &dC_, &dM_}) { dfree(*v); *v = nullptr; }
     }
 
     bool distributed() const { return comm_ && comm_->size() > 1; }
@@ -1299,10 +1642,12 @@ private:
         exchange({{(void*)cur_O_, sizeof(T) * 2 * dom_.W}, {(void*)cur_A_, sizeof(T) * dom_.W}});
     }
 
-    // scalar slots in red_.scalars; rz(i), pap(i) adjacent (iw_jtf_apply reduces both at once)
+    // scalar slots in red_.scalars: iteration i owns kSlots adjacent slots from rz(i):
+    // rz, pAp, r.W Ap, Ap.W Ap, rz by the identity (iw_jtf_apply / iw_apply_res reduce the
+    // first four at once)
     static constexpr int kScCost = 0, kScTmp = 1, kScBase = 2;
-    int rz(int i) const { return kScBase + 2 * i; }
-    int pap(int i) const { return kScBase + 2 * i + 1; }
+    int rz(int i) const { return kScBase + iw::kSlots * i; }
+    int pap(int i) const { return rz(i) + 1; }
 
     int stencil_blocks() const { return nstrips_ * nrowblocks_; }
     // tiles of iw_jtf_apply: 62-column strips
@@ -1376,24 +1721,25 @@ private:
                                red_.slot(nb, sc_out));
         OPT_HIP_CHECK(hipGetLastError());
     }
+    // A launch with HIP events attached to it when the plan's timer asks for `name`.
+    template <typename X> struct same { typedef X type; };
+    template <typename... KA>
+    void launch_timed(const char* name, void (*k)(KA...), int grid, typename same<KA>::type... args) {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        const bool ev = timer_.ext_pair(name, &e0, &e1);
+        if (ev) hipExtLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, stream_, e0, e1, 0, args...);
+        else hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, stream_, args...);
+        OPT_HIP_CHECK(hipGetLastError());
+        if (ev) timer_.ext_record(name, e0, e1);
+    }
     // PCGInit1 + the first apply: r, pre, flags, p_0 = pre r (into pout), Ap_0 (unless
-    // lIterations == 1: nothing reads that Ap), sc[rz(0)] and sc[pap(0)]. Timed under the
-    // apply's name when only the apply is timed (the first of the step's L applies).
+    // lIterations == 1: nothing reads that Ap), the four sums from sc[rz(0)].
     void launch_jtf_apply(T* pout, bool no_ap) {
         iw::Args<T> a = args();
         a.nstrips = fused_strips();
         const int nb = fused_blocks();
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        const bool ev = timer_.ext_pair("iw_jtf_apply", &e0, &e1);   // events on the launch itself
-        T* Ap = no_ap ? nullptr : Ap_;
-        if (ev)
-            hipExtLaunchKernelGGL((iw::iw_jtf_apply<T>), dim3(nb), dim3(kBlock), 0, stream_, e0, e1, 0, a, r_, pre_,
-                                  pout, Ap, red_.slot(nb, rz(0)));
-        else
-            hipLaunchKernelGGL((iw::iw_jtf_apply<T>), dim3(nb), dim3(kBlock), 0, stream_, a, r_, pre_, pout, Ap,
-                               red_.slot(nb, rz(0)));
-        OPT_HIP_CHECK(hipGetLastError());
-        if (ev) timer_.ext_record("iw_jtf_apply", e0, e1);
+        launch_timed("iw_jtf_apply", iw::iw_jtf_apply<T>, nb, a, r_, pre_, pout, no_ap ? nullptr : Ap_,
+                     red_.slot(nb, rz(0)));
     }
     // part 0: every row block; 1: the interior row blocks [1, nrb - 1); 2: the first and
     // last row blocks (the only ones whose stencil reads halo rows)
@@ -1451,6 +1797,26 @@ private:
         tend();
         OPT_HIP_CHECK(hipGetLastError());
     }
+    // PCG iteration i >= 1 of the fused loop: r_{i-1} / Ap_{i-1} in buffer (i-1) & 1 (r_ / Ap_
+    // for even), r_i / Ap_i into the other one (none in the last iteration)
+    void launch_apply_res(int i, const T* pin, T* pout, bool last) {
+        T* rb[2] = {r_, r1_};
+        T* ab[2] = {Ap_, Ap1_};
+        const T* rin = rb[(i - 1) & 1];
+        const T* Apin = ab[(i - 1) & 1];
+        T* rout = last ? nullptr : rb[i & 1];
+        T* Apout = last ? nullptr : ab[i & 1];
+        const double base_scale = (i == 1 && !spec_.use_preconditioner) ? 4.0 : 1.0;
+        const iw::Args<T> a = args();
+        const int nb = stencil_blocks();
+        const ReduceSlot rs = red_.slot(nb, rz(i));
+        auto go = [&](auto kern) {
+            launch_timed("iw_apply_res", kern, nb, a, pin, rin, Apin, (const T*)pre_, pout, rout, Apout, delta_,
+                         red_.scalars, rz(i - 1), base_scale, rs);
+        };
+        if (i == 1) go(iw::iw_apply_res<T, 1>);
+        else go(iw::iw_apply_res<T, 2>);
+    }
     void launch_residual(int i_num, int i_den, int sc_out) {
         const int nb = flat_grid(dom_.npix_mem(), 2);
         if (nt_ & 4)
@@ -1476,8 +1842,13 @@ private:
     int idx_O_, idx_A_, idx_U_, idx_C_, idx_M_, idx_wf_, idx_wr_;
     long long nvec_ = 0;
     T *r_ = nullptr, *pre_ = nullptr, *p0_ = nullptr, *p1_ = nullptr, *Ap_ = nullptr, *delta_ = nullptr;
+    T *r1_ = nullptr, *Ap1_ = nullptr;   // iw_apply_res ping-pongs r and Ap (neighbours read the old ones)
+    std::vector<char*> raw_;             // the plan vectors' allocations (vec_alloc)
+    long long stagger_ = env_int("OPT_AMD_STAGGER", kStagger) & ~255LL;
+    bool print_addr_ = env_int("OPT_AMD_PRINT_ADDR", 0) != 0;
     uint8_t* flags_ = nullptr;
     bool fused_init_ = true;            // OPT_AMD_IW_FUSED_INIT=0: iw_jtf, then iw_apply<1,0>
+    bool fused_res_ = true;             // OPT_AMD_IW_FUSED_RES=0: iw_apply<2> + iw_residual per iteration
     int rows_ = 16, depth_ = 1, nstrips_ = 0, nrowblocks_ = 0;
     bool rows_auto_ = false;
     int nt_ = 6;   // streaming PCG-vector access: bit 0 iw_apply loads, bit 1 iw_apply stores, bit 2 iw_residual

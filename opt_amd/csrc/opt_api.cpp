@@ -256,6 +256,10 @@ int OptAMD_PlanIterations(Opt_Plan* plan) {
     return valid_plan(plan, "OptAMD_PlanIterations") ? plan->impl->iterations() : -1;
 }
 
+int OptAMD_PlanScalars(Opt_Plan* plan, double* out, int n) {
+    return valid_plan(plan, "OptAMD_PlanScalars") && out ? plan->impl->scalars(out, n) : -1;
+}
+
 struct OptAMD_Comm {
     optamd::Comm* impl;
     bool owned;

@@ -38,13 +38,13 @@ hipEvent_t KernelTimer::get_event() {
 }
 void KernelTimer::begin(hipStream_t s, const char* name) {
     if (mode == 0) return;
-    if (mode == 2 && apply_name != name && aux_name != name) return;
+    if (mode == 2 && !timed(name)) return;
     open_ = name;
     open_ev_ = get_event();
     OPT_HIP_CHECK(hipEventRecord(open_ev_, s));
 }
 bool KernelTimer::ext_pair(const char* name, hipEvent_t* a, hipEvent_t* b) {
-    if (mode == 0 || (mode == 2 && apply_name != name && aux_name != name)) return false;
+    if (mode == 0 || (mode == 2 && !timed(name))) return false;
     *a = get_event();
     *b = get_event();
     return true;
@@ -102,8 +102,16 @@ KernelTimer::~KernelTimer() {
 }
 
 // ------------------------------------------------------------- ReduceScratch
+int Plan::scalars(double* out, int n) {
+    const int k = std::min(n, red_.n_scalars);
+    OPT_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (k > 0) OPT_HIP_CHECK(hipMemcpy(out, red_.scalars, sizeof(double) * k, hipMemcpyDeviceToHost));
+    return std::max(k, 0);
+}
+
 void ReduceScratch::ensure(int mb, int kmax, int ns) {
-    if (mb * kmax > max_blocks * kMaxReduce || !partials) {
+    (void)kmax;   // partials hold kMaxReduce rows of max_blocks: any K <= kMaxReduce fits
+    if (mb > max_blocks || !partials) {
         dfree(partials);
         max_blocks = std::max(mb, max_blocks);
         partials = (double*)dmalloc(sizeof(double) * (size_t)max_blocks * kMaxReduce);
@@ -113,8 +121,7 @@ void ReduceScratch::ensure(int mb, int kmax, int ns) {
         OPT_HIP_CHECK(hipMemset(ticket, 0, sizeof(unsigned) * kTicketWords));
     }
     if (ns > n_scalars) {
-        // grown (lIterations raised between Steps): the old values move along — the
-        // image_warping step's speculative rz[0] for the next step lives here
+        // grown (lIterations raised between Steps): the old values move along
         double* s = (double*)dmalloc(sizeof(double) * ns);
         OPT_HIP_CHECK(hipMemset(s, 0, sizeof(double) * ns));
         if (scalars) {

@@ -47,9 +47,14 @@ struct StateOptions {
 // hipEvent-pair accounting per kernel name (reference Timer, backend_cuda.t:152-297).
 class KernelTimer {
 public:
-    int mode = 0;  // 0 off, 1 all kernels, 2 apply kernel (+ aux_name) only
+    int mode = 0;  // 0 off, 1 all kernels, 2 apply kernel (+ aux_names) only
     std::string apply_name;
-    std::string aux_name;   // a second kernel mode 2 times (the image_warping fused init + apply)
+    std::vector<std::string> aux_names;   // more kernels mode 2 times (image_warping: its fused passes)
+    bool timed(const char* name) const {
+        if (apply_name == name) return true;
+        for (auto& n : aux_names) if (n == name) return true;
+        return false;
+    }
     void begin(hipStream_t s, const char* name);
     void end(hipStream_t s);
     // Event pair to attach to the launch itself (hipExtLaunchKernel): the timestamps come
@@ -124,6 +129,8 @@ public:
     }
 
     void set_solver_param(const char* name, const void* value);
+    // the device scalar slots (red_.scalars) to the host, up to n; the count copied
+    int scalars(double* out, int n);
     int iterations() const { return n_iter_; }
     hipStream_t stream() const { return stream_; }
     KernelTimer& timer() { return timer_; }
