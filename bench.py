@@ -199,6 +199,32 @@ def cpu_baseline(w, n_unknowns, liter):
     }
 
 
+def cpu_baseline_sfs(W, liter, rows=256):
+    """Config 3's comparator: the oracle (oracle/sfs_impl.h, the reference's
+    shape_from_shading energy and LM/PCG loop restated in C, single-threaded) timing ONE
+    LM step (precompute, J^T F, `liter` PCG iterations, model cost, cost) of a W x `rows`
+    crop of the same seeded workload, in the headline's unit (unknowns x lIterations per
+    second). The reference's backend_cpu_mt splits the same loops over rows across
+    threads (backend_cpu_mt.t:716-737); this comparator uses one core."""
+    from oracle import oracle
+    from opt_amd import workloads
+
+    w = workloads.shape_from_shading(W, rows, seed=3)
+    t0 = time.perf_counter()
+    oracle.sfs_solve(w, 1, liter, lm=True)
+    dt = time.perf_counter() - t0
+    return {
+        "value": W * rows * liter / dt,
+        "unit": "unknowns/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"one LM step ({liter} PCG iterations, incl. precompute and both costs) of a {W}x{rows} crop "
+                  f"of the seeded workload, oracle/sfs_impl.h on 1 thread: {dt:.2f} s",
+        "lm_iters_per_s_at_crop": 1.0 / dt,
+        "cpu_model": cpu_model(),
+    }
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -346,8 +372,9 @@ def main():
         result["init_kernel"] = {"kernel": INIT_KERNEL, "avg_us": init_s * 1e6, "launches": n_init,
                                  "bytes_per_px": INIT_BYTES_PER_PX, "achieved": ach,
                                  "frac": ach / PEAK_HBM_GBS}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not sfs:
-        result["cpu_baseline"] = cpu_baseline(w, n_unknowns, args.liter)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = (cpu_baseline_sfs(W, args.liter) if sfs
+                                  else cpu_baseline(w, n_unknowns, args.liter))
     if rank == 0:
         print(json.dumps(result), flush=True)
     s.close()

@@ -167,29 +167,36 @@ def test_full_size_properties(W, H):
     assert costs[1] < costs[0]
 
 
-def test_bench_workload_trajectory_within_fp32_noise_floor():
-    """The bench generator's workload (seeded) at 1024^2, 2 GN steps x 10
-    PCG: the GPU energies must lie within the oracle's own sensitivity to a 1-ulp change
-    of the inputs (the fp32 noise floor of this energy, tests/test_oracle.py), and one
-    short-PCG step within 1e-5."""
+@pytest.mark.parametrize("N", [1024, 2048, 4096])
+def test_bench_workload_trajectory_within_fp32_noise_floor(N):
+    """The bench generator's workload (seeded) at 1024^2, config 2's
+    2048^2 and the headline's 4096^2, 2 GN steps x 10 PCG (solverGPUGaussNewton.t:
+    1913-2349): at every step the GPU energy must lie within the oracle's own spread under
+    1-ulp changes of the inputs (the fp32 noise floor of this energy; two
+    samples, twice their max) or 1e-5, with the same step count; and one short-PCG step
+    within 1e-5."""
     import numpy as np
     from opt_amd import workloads
 
-    W = H = 1024
+    W = H = N
     w = workloads.image_warping(W, H, seed=1234)
     s = solver(W, H)
     prm = device_params(w)
     s.set_solver_params({"nIterations": 2, "lIterations": 10})
     c = np.array(s.profiled_solve(prm))
     _, _, ref, _ = oracle.iw_solve(w, 2, 10, nthreads=16)
-    rng = np.random.default_rng(0)
-    w2 = dict(w)
-    w2["Offset"] = (w["Offset"] * (1 + 2.0 ** -24 * rng.standard_normal(w["Offset"].size))).astype(np.float32)
-    _, _, ref2, _ = oracle.iw_solve(w2, 2, 10, nthreads=16)
-    floor = np.abs(ref2 - ref) / ref
+    floor = np.zeros_like(ref)
+    for seed in (0, 1):
+        rng = np.random.default_rng(seed)
+        w2 = dict(w)
+        w2["Offset"] = (w["Offset"] * (1 + 2.0 ** -24 * rng.standard_normal(w["Offset"].size))).astype(np.float32)
+        _, _, ref2, _ = oracle.iw_solve(w2, 2, 10, nthreads=16)
+        floor = np.maximum(floor, np.abs(ref2 - ref) / ref)
     drift = np.abs(c - ref) / ref
+    print(f"N={N} drift {drift} floor {floor}")
+    assert len(c) == len(ref)
     assert drift[0] < 1e-6
-    assert np.all(drift[1:] <= np.maximum(floor[1:], 1e-5)), (drift, floor)
+    assert np.all(drift[1:] <= np.maximum(2 * floor[1:], 1e-5)), (drift, floor)
     s1 = solver(W, H)
     p1 = device_params(w)
     s1.set_solver_params({"nIterations": 1, "lIterations": 1})
