@@ -34,6 +34,8 @@ struct RcclApi {
     decltype(&ncclGroupStart) groupStart = nullptr;
     decltype(&ncclGroupEnd) groupEnd = nullptr;
     decltype(&ncclGetErrorString) errStr = nullptr;
+    // optional (RCCL >= 2.18): a second communicator for the halo traffic
+    ncclResult_t (*commSplit)(ncclComm_t, int, int, ncclComm_t*, void*) = nullptr;
     bool load(std::string* err) {
         if (h) return true;
         for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
@@ -48,6 +50,7 @@ struct RcclApi {
         SYM(recv, "ncclRecv") SYM(groupStart, "ncclGroupStart") SYM(groupEnd, "ncclGroupEnd")
         SYM(errStr, "ncclGetErrorString")
 #undef SYM
+        commSplit = (decltype(commSplit))dlsym(h, "ncclCommSplit");
         return true;
     }
 };
@@ -62,13 +65,21 @@ RcclApi g_rccl;
         }                                                                                    \
     } while (0)
 
+// Two communicators when RCCL can split one: c_ carries the scalar all-reduces (plan
+// stream), ch_ the halo send/recv (the plan's halo stream when it overlaps halos with the
+// interior apply). Each is then used from one stream, in the same order on every rank;
+// without a split both share c_ and the plans exchange halos on the plan stream.
 class RcclComm final : public Comm {
 public:
-    RcclComm(ncclComm_t c, int rank, int n) : c_(c), rank_(rank), n_(n) {}
-    ~RcclComm() override { if (c_) g_rccl.commDestroy(c_); }
+    RcclComm(ncclComm_t c, ncclComm_t ch, int rank, int n) : c_(c), ch_(ch), rank_(rank), n_(n) {}
+    ~RcclComm() override {
+        if (ch_ && ch_ != c_) g_rccl.commDestroy(ch_);
+        if (c_) g_rccl.commDestroy(c_);
+    }
     int rank() const override { return rank_; }
     int size() const override { return n_; }
     std::string kind() const override { return "rccl"; }
+    bool concurrent_halo() const override { return ch_ != c_; }
     void allreduce_sum(double* dev, int n, hipStream_t s) override {
         RCCL_CHECK(g_rccl.allReduce(dev, dev, (size_t)n, ncclFloat64, ncclSum, c_, s));
     }
@@ -79,19 +90,19 @@ public:
         for (const auto& p : planes) {
             const size_t bytes = (size_t)h * p.row_bytes;
             if (rank_ > 0) {
-                RCCL_CHECK(g_rccl.send(row_ptr(p, d, send_up(d, h).y0), bytes, ncclChar, rank_ - 1, c_, s));
-                RCCL_CHECK(g_rccl.recv(row_ptr(p, d, recv_up(d, h).y0), bytes, ncclChar, rank_ - 1, c_, s));
+                RCCL_CHECK(g_rccl.send(row_ptr(p, d, send_up(d, h).y0), bytes, ncclChar, rank_ - 1, ch_, s));
+                RCCL_CHECK(g_rccl.recv(row_ptr(p, d, recv_up(d, h).y0), bytes, ncclChar, rank_ - 1, ch_, s));
             }
             if (rank_ < n_ - 1) {
-                RCCL_CHECK(g_rccl.send(row_ptr(p, d, send_dn(d, h).y0), bytes, ncclChar, rank_ + 1, c_, s));
-                RCCL_CHECK(g_rccl.recv(row_ptr(p, d, recv_dn(d, h).y0), bytes, ncclChar, rank_ + 1, c_, s));
+                RCCL_CHECK(g_rccl.send(row_ptr(p, d, send_dn(d, h).y0), bytes, ncclChar, rank_ + 1, ch_, s));
+                RCCL_CHECK(g_rccl.recv(row_ptr(p, d, recv_dn(d, h).y0), bytes, ncclChar, rank_ + 1, ch_, s));
             }
         }
         RCCL_CHECK(g_rccl.groupEnd());
     }
 
 private:
-    ncclComm_t c_;
+    ncclComm_t c_, ch_;
     int rank_, n_;
 };
 }  // namespace
@@ -111,7 +122,9 @@ Comm* make_rccl_comm(const void* id128, int rank, int nranks, std::string* err) 
     ncclComm_t c;
     ncclResult_t r = g_rccl.commInitRank(&c, nranks, id, rank);
     if (r != ncclSuccess) { *err = std::string("ncclCommInitRank: ") + g_rccl.errStr(r); return nullptr; }
-    return new RcclComm(c, rank, nranks);
+    ncclComm_t ch = c;   // collective over all ranks: every rank takes the same branch
+    if (g_rccl.commSplit && nranks > 1 && g_rccl.commSplit(c, 0, rank, &ch, nullptr) != ncclSuccess) ch = c;
+    return new RcclComm(c, ch, rank, nranks);
 }
 
 // ================================================================ local group

@@ -37,6 +37,10 @@ public:
     virtual void halo_exchange(const std::vector<HaloPlane>& planes, const Domain& dom, int halo,
                                hipStream_t s) = 0;
     virtual std::string kind() const = 0;
+    // May a halo exchange on a second stream run concurrently with all-reduces on the
+    // plan stream? (RCCL: only when the halos have a communicator of their own, so each
+    // communicator is used from one stream in one order on every rank.)
+    virtual bool concurrent_halo() const { return true; }
 };
 
 // ------------------------------------------------------------------ RCCL

@@ -1429,7 +1429,7 @@ public:
         // launch overhead, so the loop stays as plain stream launches)
         // row slabs with >= 3 row blocks: the halo refresh of r and p_{i-1} runs beside the
         // interior row blocks of the next apply (halo_mark / halo_begin / halo_join)
-        const bool split = distributed() && overlap_ && nrowblocks_ >= 3;
+        const bool split = distributed() && overlap_ && comm_->concurrent_halo() && nrowblocks_ >= 3;
         for (int i = 0; i < L; ++i) {
             if (i > 0 || !fused) std::swap(pcur, pprev);   // pcur <- new p, pprev <- old p
             const bool last = i + 1 == L;   // timed by events on the launch (launch_apply)

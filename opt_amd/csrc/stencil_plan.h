@@ -276,7 +276,7 @@ public:
             const ZetaArgs z{red_.scalars + kScQ0, stop_, i, sp_.q_tolerance, (lm_ && !distributed()) ? 1 : 0};
             bool split = false;
             if constexpr (HasApplySplit<Op>::value)
-                split = distributed() && overlap_ && !mat_ && op_->can_split();
+                split = distributed() && overlap_ && comm_->concurrent_halo() && !mat_ && op_->can_split();
             if (!split) exchange_vec(p_);
             if (split) {
                 if constexpr (HasApplySplit<Op>::value) {
