@@ -66,19 +66,35 @@ APPLY_VARIANT = {0: "iw_apply<float, 1, 0,", 1: "iw_apply<float, 2, 1,", 2: "iw_
 
 # PCG iteration i >= 1 as ONE pass (iw_apply_res: the apply with the previous iteration's
 # residual update folded in): Angle 4 + UrShape 8 + flag 1 + angle pre 4 + r_{i-1} 12 +
-# Ap_{i-1} 12 + p_{i-1} 12 read, p_i 12 + delta 12 written; delta 12 read from i = 2 on;
-# r_i 12 + Ap_i 12 written except in the last iteration (nothing reads them).
-def res_bytes_per_px(i: int, liter: int = 10) -> int:
-    b = 4 + 8 + 1 + 4 + 12 + 12 + 12 + 12 + 12
-    if i >= 2:
-        b += 12
+# Ap_{i-1} 12 + p_{i-1} 12 read, p_i 12 written; r_i 12 + Ap_i 12 written except in the last
+# iteration (nothing reads them). The delta update, deferred (OPT_AMD_IW_DEFER, default on):
+# none in odd iterations; i = 2 reads p_0 12 and writes delta 12; even i >= 4 read delta 12 +
+# p_{i-2} 12 and write delta 12. Per iteration (OPT_AMD_IW_DEFER=0): delta 12 written, and
+# read from i = 2 on.
+IW_DEFER = os.environ.get("OPT_AMD_IW_DEFER", "1") != "0"
+
+
+def res_bytes_per_px(i: int, liter: int = 10, defer: bool = IW_DEFER) -> int:
+    b = 4 + 8 + 1 + 4 + 12 + 12 + 12 + 12
     if i < liter - 1:
         b += 24
+    if defer:
+        b += 0 if i % 2 == 1 else (24 if i == 2 else 36)
+    else:
+        b += 12 if i == 1 else 24
     return b
 
 
 RES_KERNEL = "iw_apply_res"
-RES_VARIANT = {1: "iw_apply_res<float, 1,", 2: "iw_apply_res<float, 2,"}
+
+
+def res_variant(i: int, defer: bool = IW_DEFER) -> str:
+    """The iw_apply_res instantiation PCG iteration i >= 1 runs (<T, DM, NT, E>)."""
+    if defer:
+        dm, e = (0, 0) if i % 2 == 1 else ((1, 1) if i == 2 else (2, 1))
+    else:
+        dm, e = (1 if i == 1 else 2), 0
+    return f"iw_apply_res<float, {dm}, 2, {e}>"
 
 
 # PCGInit1 fused with the first apply (iw_jtf_apply, one strip pass): Offset 8 + Angle 4 +
@@ -95,7 +111,7 @@ def pmc_traffic(liter: int, first: int = 0, res: bool = False):
         return None
     total = 0.0
     for i in range(first, liter):
-        key = RES_VARIANT[min(i, 2)] if res else APPLY_VARIANT[min(i, 2)]
+        key = res_variant(i) if res else APPLY_VARIANT[min(i, 2)]
         hit = [v for k, v in ks.items() if key in k]
         if not hit or "FETCH_SIZE" not in hit[0] or "WRITE_SIZE" not in hit[0]:
             return None

@@ -80,10 +80,29 @@ struct Args {
     T preO[2][5];
 };
 
+// In the kernels the same ten values live in LDS, entry fit | nv << 1 (IW_PRE_TABLE).
+__shared__ float iw_ptab_f[16];
+__shared__ double iw_ptab_d[16];
+template <typename T> __device__ __forceinline__ T* iw_ptab();
+template <> __device__ __forceinline__ float* iw_ptab<float>() { return iw_ptab_f; }
+template <> __device__ __forceinline__ double* iw_ptab<double>() { return iw_ptab_d; }
+
 template <typename T>
-__device__ __forceinline__ T pre_offset(const Args<T>& a, int f) {
-    return (f & 1) ? a.preO[(f >> 1) & 1][(f >> 2) & 7] : (T)0;
+__device__ __forceinline__ T pre_offset(const Args<T>&, int f) {
+    return (f & 1) ? iw_ptab<T>()[(f >> 1) & 15] : (T)0;
 }
+template <typename T>
+__device__ __forceinline__ T pre_entry(const Args<T>& a, int k) {
+    return k < 10 ? a.preO[k & 1][k >> 1] : (T)0;
+}
+// Every kernel that calls pre_offset starts with IW_PRE_TABLE(a). Indexed by a per-lane
+// value, a.preO itself compiles to a vector-memory load from the kernel arguments, and
+// vmcnt retires in order: the wait for that load drained every row prefetch issued before
+// it, once per row (4.45 -> 4.26 ms per GN step at 4096^2, in-loop pass 409 -> 390 us).
+// LDS reads wait on lgkmcnt instead.
+#define IW_PRE_TABLE(a)                                                           \
+    if (threadIdx.x < 16) iw_ptab<T>()[threadIdx.x] = pre_entry(a, threadIdx.x); \
+    __syncthreads();
 
 // ---------------------------------------------------------------- helpers
 // Element access of the once-touched PCG vectors; NT: streaming (nontemporal) form.
@@ -100,6 +119,11 @@ __device__ __forceinline__ void st_v(T* p, T v) {
 
 __device__ __forceinline__ void sc_of(float t, float* c, float* s) { sincosf(t, s, c); }
 __device__ __forceinline__ void sc_of(double t, double* c, double* s) { sincos(t, s, c); }
+// a b + c with one rounding: the delta accumulation delta += alpha p is written as an
+// explicit fma everywhere, so deferring some of its terms to a later pass (iw_apply_res
+// E, iw_update E2) keeps every delta bitwise
+__device__ __forceinline__ float fmad(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fmad(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
 struct WaveGeom {
     int x, ex, lane, y0, y1, tile;
@@ -263,7 +287,7 @@ __device__ __forceinline__ PRow<T> finish_prow(const Args<T>& a, const PRaw<T>& 
     make_p<T, MODE>(a, f, beta, q.v0, q.v1, q.v2, q.w2, q.q0, q.q1, q.q2, o.px, o.py, o.pt);
     if (MODE == 2 && DM == 1) { o.dx = alpha * q.q0; o.dy = alpha * q.q1; o.dt = alpha * q.q2; }
     if (MODE == 2 && DM == 2) {
-        o.dx = q.d0 + alpha * q.q0; o.dy = q.d1 + alpha * q.q1; o.dt = q.d2 + alpha * q.q2;
+        o.dx = fmad(alpha, q.q0, q.d0); o.dy = fmad(alpha, q.q1, q.d1); o.dt = fmad(alpha, q.q2, q.d2);
     }
     if (!o.act) { o.px = 0; o.py = 0; o.pt = 0; }
     // edge pixel: its p, and the residual it sends to this lane's pixel
@@ -305,6 +329,7 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
                                                    const T* __restrict__ dadd = nullptr,
                                                    const int* stop = nullptr) {
     if (LMX && stop && *stop) return;
+    IW_PRE_TABLE(a);
     const WaveGeom g = geom(a);
     const T beta = (MODE == 2) ? (T)(sc[ib_num] / sc[ib_den]) : (T)0;
     const T alpha = (MODE == 2 && DM != 0) ? (T)(sc[ia_num] / sc[ia_den]) : (T)0;
@@ -474,8 +499,8 @@ __device__ __forceinline__ WaveGeom geom_fused(const Args<T>& a) {
 }
 template <typename T>
 struct RRaw {
-    vec2_t<T> r, ap, q, d;     // r_{i-1}, Ap_{i-1}, p_{i-1}, delta (Offset channels)
-    T rt, at, qt, dt, w2, ang;  // the angle channels, its pre, the angle
+    vec2_t<T> r, ap, q, d, q2;  // r_{i-1}, Ap_{i-1}, p_{i-1}, delta, p_{i-2} (Offset channels)
+    T rt, at, qt, dt, q2t, w2, ang;  // the angle channels, its pre, the angle
     float2 u;
     int f, in;
     vec2_t<T> er, eap, eq;      // edge pixel
@@ -502,10 +527,10 @@ struct POff {
     __device__ __forceinline__ POff(unsigned i, unsigned tb) : xy(i * 2u * (unsigned)sizeof(T)),
         t(tb + i * (unsigned)sizeof(T)), s(i * (unsigned)sizeof(T)) {}
 };
-template <typename T, int DM, bool NT>
+template <typename T, int DM, bool NT, int E>
 __device__ __forceinline__ RRaw<T> raw_rrow(const Args<T>& a, const WaveGeom& g, int y, unsigned tb,
                                             const T* pin, const T* rin, const T* Apin, const T* pre,
-                                            const T* delta) {
+                                            const T* delta, const T* pin2) {
     RRaw<T> q;
     q.in = present(a.dom, g.x, y);
     const unsigned i = q.in ? (unsigned)a.dom.off(g.x, y) : 0u;
@@ -518,6 +543,7 @@ __device__ __forceinline__ RRaw<T> raw_rrow(const Args<T>& a, const WaveGeom& g,
     q.w2 = ldb<NT, T>(pre, o.s);
     q.q = ldb<NT, vec2_t<T>>(pin, o.xy); q.qt = ldb<NT, T>(pin, o.t);
     if (DM == 2) { q.d = ldb<NT, vec2_t<T>>(delta, o.xy); q.dt = ldb<NT, T>(delta, o.t); }
+    if (E) { q.q2 = ldb<NT, vec2_t<T>>(pin2, o.xy); q.q2t = ldb<NT, T>(pin2, o.t); }
     q.ein = 0;
     if (g.edge_lane) {
         q.ein = present(a.dom, g.ex, y);
@@ -543,8 +569,8 @@ __device__ __forceinline__ void make_rp(const Args<T>& a, int f, T alpha, T beta
 }
 // Finish a raw row: r_i, p_i, the edge pixel's p and residual; an owned row (own) also
 // stores r_i (unless rout is null) and the updated delta right here and adds its r_i.W r_i.
-template <typename T, int DM, bool NT>
-__device__ __forceinline__ RRow<T> finish_rrow(const Args<T>& a, const RRaw<T>& q, T beta, T alpha, bool own,
+template <typename T, int DM, bool NT, int E>
+__device__ __forceinline__ RRow<T> finish_rrow(const Args<T>& a, const RRaw<T>& q, T beta, T alpha, T alpha2, bool own,
                                                const WaveGeom& g, int y, unsigned tb, T* rout, T* delta,
                                                acc_t& rzd) {
     RRow<T> o;
@@ -560,12 +586,22 @@ __device__ __forceinline__ RRow<T> finish_rrow(const Args<T>& a, const RRaw<T>& 
     o.w2 = a.use_pre ? q.w2 : (T)1;
     if (own && g.out_lane) {
         const POff<T> off((unsigned)a.dom.off(g.x, y), tb);
-        vec2_t<T> d;
-        T dt;
-        if (DM == 1) { d.x = alpha * q.q.x; d.y = alpha * q.q.y; dt = alpha * q.qt; }
-        else { d.x = q.d.x + alpha * q.q.x; d.y = q.d.y + alpha * q.q.y; dt = q.dt + alpha * q.qt; }
-        if (!o.act) { d.x = 0; d.y = 0; dt = 0; }
-        stb<NT>(delta, off.xy, d); stb<NT>(delta, off.t, dt);
+        if (DM != 0) {
+            // delta (+)= [alpha_{i-2} p_{i-2} (E)] + alpha_{i-1} p_{i-1}, term by term
+            vec2_t<T> d;
+            T dt;
+            if (E) {
+                if (DM == 1) { d.x = alpha2 * q.q2.x; d.y = alpha2 * q.q2.y; dt = alpha2 * q.q2t; }
+                else { d.x = fmad(alpha2, q.q2.x, q.d.x); d.y = fmad(alpha2, q.q2.y, q.d.y); dt = fmad(alpha2, q.q2t, q.dt); }
+                d.x = fmad(alpha, q.q.x, d.x); d.y = fmad(alpha, q.q.y, d.y); dt = fmad(alpha, q.qt, dt);
+            } else if (DM == 1) {
+                d.x = alpha * q.q.x; d.y = alpha * q.q.y; dt = alpha * q.qt;
+            } else {
+                d.x = fmad(alpha, q.q.x, q.d.x); d.y = fmad(alpha, q.q.y, q.d.y); dt = fmad(alpha, q.qt, q.dt);
+            }
+            if (!o.act) { d.x = 0; d.y = 0; dt = 0; }
+            stb<NT>(delta, off.xy, d); stb<NT>(delta, off.t, dt);
+        }
         if (rout) {
             vec2_t<T> r; r.x = o.rx; r.y = o.ry;
             stb<NT>(rout, off.xy, r); stb<NT>(rout, off.t, o.rt);
@@ -586,14 +622,16 @@ __device__ __forceinline__ RRow<T> finish_rrow(const Args<T>& a, const RRaw<T>& 
           o.ejx, o.ejy, ax, ay);
     return o;
 }
-template <typename T, int DM, int NT = 2>
+template <typename T, int DM, int NT = 2, int E = 0>
 __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_apply_res(Args<T> a, const T* __restrict__ pin,
                                                        const T* __restrict__ rin, const T* __restrict__ Apin,
                                                        const T* __restrict__ pre, T* __restrict__ pout,
                                                        T* __restrict__ rout, T* __restrict__ Apout,
                                                        T* __restrict__ delta, double* __restrict__ sc,
-                                                       int prev, double base_scale, ReduceSlot rs) {
+                                                       int prev, double base_scale, ReduceSlot rs,
+                                                       const T* __restrict__ pin2 = nullptr) {
     constexpr bool LNT = (NT & 1) != 0, SNT = (NT & 2) != 0;
+    IW_PRE_TABLE(a);
     // 64-column strips with the 2-lane edge record (iw_apply's geometry): every store is a
     // whole aligned 256-B run per wave. (62-column strips without the edge record — 116
     // instead of 154 VGPRs, 4 waves per SIMD — took 423-502 us against 406-441: their
@@ -607,14 +645,17 @@ __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_apply_res(Args<T> a, 
     const double alpha_d = (double)alpha;
     const double rz_id = base_scale * rzp - 2.0 * alpha_d * sc[prev + 2] + alpha_d * alpha_d * sc[prev + 3];
     const T beta = (T)(rz_id / rzp);
+    // E: p_{i-2}'s delta term was deferred by the previous pass; alpha_{i-2} from its slots
+    const T alpha2 = E ? (T)(sc[prev - kSlots] / sc[prev - kSlots + 1]) : (T)0;
     if (blockIdx.x == 0 && threadIdx.x == 0) sc[prev + kSlots + 4] = rz_id;
     const T wr = a.wr, wf2 = a.wf * a.wf;
     const unsigned tb = (unsigned)(2 * a.dom.npix_mem() * (long long)sizeof(T));
     acc_t rzd = 0, papd = 0, rapd = 0, apapd = 0;
     if (g.y0 < g.y1) {
-        auto raw = [&](int y) { return raw_rrow<T, DM, LNT>(a, g, y, tb, pin, rin, Apin, pre, delta); };
+        auto raw = [&](int y) { return raw_rrow<T, DM, LNT, E>(a, g, y, tb, pin, rin, Apin, pre, delta, pin2); };
         auto fin = [&](const RRaw<T>& q, int y) {
-            return finish_rrow<T, DM, SNT>(a, q, beta, alpha, y >= g.y0 && y < g.y1, g, y, tb, rout, delta, rzd);
+            return finish_rrow<T, DM, SNT, E>(a, q, beta, alpha, alpha2, y >= g.y0 && y < g.y1, g, y, tb, rout,
+                                              delta, rzd);
         };
         const RRow<T> up = fin(raw(g.y0 - 1), g.y0 - 1);
         RRow<T> A = fin(raw(g.y0), g.y0);
@@ -858,6 +899,7 @@ __device__ __forceinline__ JOut<T> jtf_out(const Args<T>& a, const VRow<T>& cur,
 template <typename T, int OUT>
 __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T* __restrict__ pre,
                                                  ReduceSlot rs) {
+    IW_PRE_TABLE(a);
     const WaveGeom g = geom(a);
     const T wf = a.wf, wr2 = a.wr * a.wr;
     const long long N = a.dom.npix_mem();
@@ -925,6 +967,7 @@ template <typename T, int NT = 2>
 __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_jtf_apply(Args<T> a, T* __restrict__ r, T* __restrict__ pre,
                                                        T* __restrict__ pout, T* __restrict__ Ap,
                                                        ReduceSlot rs) {
+    IW_PRE_TABLE(a);
     const WaveGeom g = geom_fused(a);
     const T wr = a.wr, wf2 = a.wf * a.wf;
     const long long N = a.dom.npix_mem();
@@ -1124,6 +1167,7 @@ __global__ __launch_bounds__(kBlock) void iw_residual(Args<T> a, const T* __rest
                                                       const T* __restrict__ pre, T* __restrict__ r,
                                                       const double* __restrict__ sc, int i_num, int i_den,
                                                       ReduceSlot rs) {
+    IW_PRE_TABLE(a);
     const long long N = a.dom.npix_mem();
     const T alpha = (T)(sc[i_num] / sc[i_den]);
     const long long b0 = a.dom.off(0, a.dom.y_lo), e = a.dom.off(0, a.dom.y_hi);
@@ -1202,12 +1246,15 @@ __global__ __launch_bounds__(kBlock) void iw_flags(Args<T> a) {
 // X += delta_L on active pixels of the owned rows (PCGLinearUpdate, :854-859), where
 // delta_L = delta_{L-1} + alpha_{L-1} p_{L-1} is the last PCG iteration's delta update
 // (HAS_DELTA = false when lIterations == 1: delta_0 = 0).
-template <typename T, bool HAS_DELTA>
+template <typename T, bool HAS_DELTA, bool E2 = false>
 __global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O, T* __restrict__ A,
                                                     const T* __restrict__ delta, const T* __restrict__ p,
-                                                    const double* __restrict__ sc, int ia_num, int ia_den) {
+                                                    const double* __restrict__ sc, int ia_num, int ia_den,
+                                                    const T* __restrict__ p2 = nullptr, int ia2_num = 0,
+                                                    int ia2_den = 0) {
     const long long N = a.dom.npix_mem();
     const T alpha = (T)(sc[ia_num] / sc[ia_den]);
+    const T alpha2 = E2 ? (T)(sc[ia2_num] / sc[ia2_den]) : (T)0;
     const long long b = a.dom.off(0, a.dom.y_lo), e = a.dom.off(0, a.dom.y_hi);
     for (long long i = b + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < e;
          i += (long long)gridDim.x * blockDim.x) {
@@ -1220,7 +1267,15 @@ __global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O
         if (HAS_DELTA) {
             d = reinterpret_cast<const Vec2<T>*>(delta)[i];
             dt = delta[2 * N + i];
-            d.x = d.x + alpha * pp.x; d.y = d.y + alpha * pp.y; dt = dt + alpha * pt;
+        }
+        if (E2) {   // the deferred alpha_{L-2} p_{L-2} term first
+            const Vec2<T> q2 = reinterpret_cast<const Vec2<T>*>(p2)[i];
+            const T q2t = p2[2 * N + i];
+            if (HAS_DELTA) { d.x = fmad(alpha2, q2.x, d.x); d.y = fmad(alpha2, q2.y, d.y); dt = fmad(alpha2, q2t, dt); }
+            else { d.x = alpha2 * q2.x; d.y = alpha2 * q2.y; dt = alpha2 * q2t; }
+        }
+        if (HAS_DELTA || E2) {
+            d.x = fmad(alpha, pp.x, d.x); d.y = fmad(alpha, pp.y, d.y); dt = fmad(alpha, pt, dt);
         } else {
             d.x = alpha * pp.x; d.y = alpha * pp.y; dt = alpha * pt;
         }
@@ -1411,6 +1466,10 @@ public:
         // iterations 1.. as iw_apply_res (the residual update folded into the next apply;
         // needs iw_jtf_apply's two extra sums)
         const bool res = fused && fused_res_;
+        // res with defer_: p_i in pb[i % 3]; the delta terms of odd iterations are folded
+        // in pairs by the next even iteration (or the update), which reads p_{i-2} again
+        const bool defer = res && defer_;
+        T* pb[3] = {p0_, p1_, p2_};
         if (fused) {
             launch_jtf_apply(pcur, L == 1);
         } else {
@@ -1439,7 +1498,8 @@ public:
                     continue;
                 }
             } else if (res) {
-                launch_apply_res(i, pprev, pcur, last);
+                if (defer) launch_apply_res(i, pb[(i - 1) % 3], pb[i % 3], last, i >= 2 ? pb[(i - 2) % 3] : nullptr);
+                else launch_apply_res(i, pprev, pcur, last);
                 if (last) break;
                 continue;
             }
@@ -1474,15 +1534,43 @@ public:
             }
         }
         // PCGLinearUpdate (with the last delta += alpha p) + cost
-        if (L > 0) {
+        if (L > 0 && defer) {
+            // pending: p_{L-1}, and p_{L-2} too when L-1 is odd (the even iterations fold pairs)
+            const int ub = flat_grid(dom_.npix_mem(), 1);
+            const T* pl = pb[(L - 1) % 3];
+            const T* pl2 = L >= 2 ? pb[(L - 2) % 3] : nullptr;
+            const bool e2 = L % 2 == 0, has = L >= 3;
+            tbegin("iw_update");
+            if (e2 && has)
+                hipLaunchKernelGGL((iw::iw_update<T, true, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
+                                   cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1), pl2, rz(L - 2),
+                                   pap(L - 2));
+            else if (e2)
+                hipLaunchKernelGGL((iw::iw_update<T, false, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
+                                   cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1), pl2, rz(L - 2),
+                                   pap(L - 2));
+            else if (has)
+                hipLaunchKernelGGL((iw::iw_update<T, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
+                                   cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1),
+                                   (const T*)nullptr, 0, 0);
+            else
+                hipLaunchKernelGGL((iw::iw_update<T, false>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
+                                   cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1),
+                                   (const T*)nullptr, 0, 0);
+            OPT_HIP_CHECK(hipGetLastError());
+            tend();
+            exchange_unknowns();
+        } else if (L > 0) {
             const int ub = flat_grid(dom_.npix_mem(), 1);
             tbegin("iw_update");
             if (L >= 2)
                 hipLaunchKernelGGL((iw::iw_update<T, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
-                                   cur_A_, (const T*)delta_, (const T*)pcur, red_.scalars, rz(L - 1), pap(L - 1));
+                                   cur_A_, (const T*)delta_, (const T*)pcur, red_.scalars, rz(L - 1), pap(L - 1),
+                                   (const T*)nullptr, 0, 0);
             else
                 hipLaunchKernelGGL((iw::iw_update<T, false>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
-                                   cur_A_, (const T*)delta_, (const T*)pcur, red_.scalars, rz(L - 1), pap(L - 1));
+                                   cur_A_, (const T*)delta_, (const T*)pcur, red_.scalars, rz(L - 1), pap(L - 1),
+                                   (const T*)nullptr, 0, 0);
             OPT_HIP_CHECK(hipGetLastError());
             tend();
             exchange_unknowns();
@@ -1571,6 +1659,7 @@ private:
         }
         fused_init_ = env_int("OPT_AMD_IW_FUSED_INIT", 1) != 0;
         fused_res_ = env_int("OPT_AMD_IW_FUSED_RES", 1) != 0;
+        defer_ = env_int("OPT_AMD_IW_DEFER", 1) != 0;
     }
     // A zeroed plan vector with kSlack spare bytes: place() may move each vector's base
     // within them between Steps (every vector is rewritten before it is read in a Step).
@@ -1588,10 +1677,11 @@ private:
     // OPT_AMD_STAGGER=S: vector k starts (k S) mod kSlack bytes into its allocation (HBM
     // placement study: the step time moves by up to ~8% with where the streams land)
     void place() {
-        T** vs[] = {&r_, &p0_, &p1_, &Ap_, &delta_, &r1_, &Ap1_, &pre_};
-        if (raw_.size() < 9) return;
+        T** vs[] = {&r_, &p0_, &p1_, &Ap_, &delta_, &r1_, &Ap1_, &pre_, &p2_};
+        if (raw_.size() < 10) return;
         for (int k = 0; k < 8; ++k) *vs[k] = (T*)(raw_[k] + ((size_t)stagger_ * k) % kSlack);
         flags_ = (uint8_t*)(raw_[8] + ((size_t)stagger_ * 8) % kSlack);
+        p2_ = (T*)(raw_[9] + ((size_t)stagger_ * 9) % kSlack);
     }
     void allocate() {
         const long long N = dom_.npix_mem();
@@ -1600,6 +1690,7 @@ private:
             *v = (T*)vec_alloc(sizeof(T) * nvec_);
         pre_ = (T*)vec_alloc(sizeof(T) * N);   // angle channel only (Args::preO)
         flags_ = (uint8_t*)vec_alloc(N);
+        p2_ = (T*)vec_alloc(sizeof(T) * nvec_);   // third p buffer (deferred delta)
         place();
         nstrips_ = (dom_.W + iw::kStrip - 1) / iw::kStrip;
         if (rows_ <= 0 || rows_auto_) { rows_auto_ = true; rows_ = iw::rows_for(nstrips_, dom_.y_hi - dom_.y_lo); }
@@ -1616,7 +1707,7 @@ private:
     void release() {
         for (char* p : raw_) dfree(p);
         raw_.clear();
-        for (T** v : {&r_, &pre_, &p0_, &p1_, &Ap_, &delta_, &r1_, &Ap1_}) *v = nullptr;
+        for (T** v : {&r_, &pre_, &p0_, &p1_, &Ap_, &delta_, &r1_, &Ap1_, &p2_}) *v = nullptr;
         flags_ = nullptr;
         for (T** v : {&dO_, &dA_}) { dfree(*v); *v = nullptr; }
         for (float** v : {&dU_, &dC_, &dM_}) { dfree(*v); *v = nullptr; }
@@ -1799,7 +1890,7 @@ private:
     }
     // PCG iteration i >= 1 of the fused loop: r_{i-1} / Ap_{i-1} in buffer (i-1) & 1 (r_ / Ap_
     // for even), r_i / Ap_i into the other one (none in the last iteration)
-    void launch_apply_res(int i, const T* pin, T* pout, bool last) {
+    void launch_apply_res(int i, const T* pin, T* pout, bool last, const T* pin2 = nullptr) {
         T* rb[2] = {r_, r1_};
         T* ab[2] = {Ap_, Ap1_};
         const T* rin = rb[(i - 1) & 1];
@@ -1812,9 +1903,13 @@ private:
         const ReduceSlot rs = red_.slot(nb, rz(i));
         auto go = [&](auto kern) {
             launch_timed("iw_apply_res", kern, nb, a, pin, rin, Apin, (const T*)pre_, pout, rout, Apout, delta_,
-                         red_.scalars, rz(i - 1), base_scale, rs);
+                         red_.scalars, rz(i - 1), base_scale, rs, pin2);
         };
-        if (i == 1) go(iw::iw_apply_res<T, 1>);
+        if (pin2 || (defer_ && i == 1)) {   // deferred delta: odd i none, i = 2 starts it, even i > 2 folds a pair
+            if (i % 2 == 1) go(iw::iw_apply_res<T, 0, 2, 0>);
+            else if (i == 2) go(iw::iw_apply_res<T, 1, 2, 1>);
+            else go(iw::iw_apply_res<T, 2, 2, 1>);
+        } else if (i == 1) go(iw::iw_apply_res<T, 1>);
         else go(iw::iw_apply_res<T, 2>);
     }
     void launch_residual(int i_num, int i_den, int sc_out) {
@@ -1843,12 +1938,14 @@ private:
     long long nvec_ = 0;
     T *r_ = nullptr, *pre_ = nullptr, *p0_ = nullptr, *p1_ = nullptr, *Ap_ = nullptr, *delta_ = nullptr;
     T *r1_ = nullptr, *Ap1_ = nullptr;   // iw_apply_res ping-pongs r and Ap (neighbours read the old ones)
+    T* p2_ = nullptr;                    // p_i in {p0_, p1_, p2_}[i % 3] with the deferred delta
     std::vector<char*> raw_;             // the plan vectors' allocations (vec_alloc)
     long long stagger_ = env_int("OPT_AMD_STAGGER", kStagger) & ~255LL;
     bool print_addr_ = env_int("OPT_AMD_PRINT_ADDR", 0) != 0;
     uint8_t* flags_ = nullptr;
     bool fused_init_ = true;            // OPT_AMD_IW_FUSED_INIT=0: iw_jtf, then iw_apply<1,0>
     bool fused_res_ = true;             // OPT_AMD_IW_FUSED_RES=0: iw_apply<2> + iw_residual per iteration
+    bool defer_ = true;                 // OPT_AMD_IW_DEFER=0: iw_apply_res updates delta in every iteration
     int rows_ = 16, depth_ = 1, nstrips_ = 0, nrowblocks_ = 0;
     bool rows_auto_ = false;
     int nt_ = 6;   // streaming PCG-vector access: bit 0 iw_apply loads, bit 1 iw_apply stores, bit 2 iw_residual

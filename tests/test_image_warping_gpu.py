@@ -358,3 +358,23 @@ def test_fused_residual_equals_separate_passes(monkeypatch, tmp_path, W, H, lit,
     for i in range(1, lit):
         rz, rzx = sc[2 + 5 * i], sc[2 + 5 * i + 4]
         assert abs(rzx - rz) <= 1e-6 * abs(rz) + 1e-30, (i, rz, rzx)
+
+
+
+@pytest.mark.parametrize("W,H,lit", [(150, 110, 10), (37, 29, 1), (64, 64, 2), (5, 3, 3), (200, 1, 4), (700, 300, 7)])
+def test_deferred_delta_is_bitwise_the_per_iteration_update(monkeypatch, W, H, lit):
+    """iw_apply_res folding the delta terms of odd PCG iterations into the next even one
+    (p in three rotating buffers, p_{i-2} read again) and iw_update taking whatever is
+    still pending: every delta is the same chain of fmas, so the GN trajectory (energies,
+    Offset, Angle, PCG scalars) is bitwise that of the per-iteration update."""
+    out = []
+    for val in (0, 1):
+        monkeypatch.setenv("OPT_AMD_IW_DEFER", str(val))
+        w = perturbed(W, H, seed=5 * W + H)
+        s = OptSolver([W, H], ENERGY, "gaussNewtonGPU")
+        s.set_solver_params({"nIterations": 3, "lIterations": lit})
+        prm = device_params(w)
+        c = np.array(s.profiled_solve(prm))
+        out.append((c, to_np(prm[0]), to_np(prm[1]), np.array(s.scalars(2 + 5 * (lit + 2)))))
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)

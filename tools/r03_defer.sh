@@ -1,0 +1,10 @@
+#!/bin/bash
+# Deferred-delta A/B (through gpurun): the bitwise tests, then the headline bench with the
+# per-iteration delta update (OPT_AMD_IW_DEFER=0) and the deferred one (=1), interleaved.
+set -e
+O=gpurun_out/${1:-r03_defer}
+mkdir -p $O
+timeout -k 10 400 python3 -u -m pytest tests/test_image_warping_gpu.py -x -q \
+    --timeout 120 --timeout-method thread > $O/tests.txt 2>&1
+tail -2 $O/tests.txt
+bash tools/ab_run.sh ${1:-r03_defer} tree@OPT_AMD_IW_DEFER=0 tree@OPT_AMD_IW_DEFER=1
