@@ -527,10 +527,11 @@ struct POff {
     __device__ __forceinline__ POff(unsigned i, unsigned tb) : xy(i * 2u * (unsigned)sizeof(T)),
         t(tb + i * (unsigned)sizeof(T)), s(i * (unsigned)sizeof(T)) {}
 };
+// own: a row of this wave (the halo rows y0-1 and y1 feed the stencil only: no delta terms)
 template <typename T, int DM, bool NT, int E>
 __device__ __forceinline__ RRaw<T> raw_rrow(const Args<T>& a, const WaveGeom& g, int y, unsigned tb,
                                             const T* pin, const T* rin, const T* Apin, const T* pre,
-                                            const T* delta, const T* pin2) {
+                                            const T* delta, const T* pin2, bool own) {
     RRaw<T> q;
     q.in = present(a.dom, g.x, y);
     const unsigned i = q.in ? (unsigned)a.dom.off(g.x, y) : 0u;
@@ -542,8 +543,8 @@ __device__ __forceinline__ RRaw<T> raw_rrow(const Args<T>& a, const WaveGeom& g,
     q.ap = ldb<NT, vec2_t<T>>(Apin, o.xy); q.at = ldb<NT, T>(Apin, o.t);
     q.w2 = ldb<NT, T>(pre, o.s);
     q.q = ldb<NT, vec2_t<T>>(pin, o.xy); q.qt = ldb<NT, T>(pin, o.t);
-    if (DM == 2) { q.d = ldb<NT, vec2_t<T>>(delta, o.xy); q.dt = ldb<NT, T>(delta, o.t); }
-    if (E) { q.q2 = ldb<NT, vec2_t<T>>(pin2, o.xy); q.q2t = ldb<NT, T>(pin2, o.t); }
+    if (DM == 2 && own) { q.d = ldb<NT, vec2_t<T>>(delta, o.xy); q.dt = ldb<NT, T>(delta, o.t); }
+    if (E && own) { q.q2 = ldb<NT, vec2_t<T>>(pin2, o.xy); q.q2t = ldb<NT, T>(pin2, o.t); }
     q.ein = 0;
     if (g.edge_lane) {
         q.ein = present(a.dom, g.ex, y);
@@ -652,7 +653,9 @@ __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_apply_res(Args<T> a, 
     const unsigned tb = (unsigned)(2 * a.dom.npix_mem() * (long long)sizeof(T));
     acc_t rzd = 0, papd = 0, rapd = 0, apapd = 0;
     if (g.y0 < g.y1) {
-        auto raw = [&](int y) { return raw_rrow<T, DM, LNT, E>(a, g, y, tb, pin, rin, Apin, pre, delta, pin2); };
+        auto raw = [&](int y) {
+            return raw_rrow<T, DM, LNT, E>(a, g, y, tb, pin, rin, Apin, pre, delta, pin2, y >= g.y0 && y < g.y1);
+        };
         auto fin = [&](const RRaw<T>& q, int y) {
             return finish_rrow<T, DM, SNT, E>(a, q, beta, alpha, alpha2, y >= g.y0 && y < g.y1, g, y, tb, rout,
                                               delta, rzd);
@@ -1660,6 +1663,7 @@ private:
         fused_init_ = env_int("OPT_AMD_IW_FUSED_INIT", 1) != 0;
         fused_res_ = env_int("OPT_AMD_IW_FUSED_RES", 1) != 0;
         defer_ = env_int("OPT_AMD_IW_DEFER", 1) != 0;
+        res_nt_ = env_int("OPT_AMD_IW_RES_NT", 2);
     }
     // A zeroed plan vector with kSlack spare bytes: place() may move each vector's base
     // within them between Steps (every vector is rewritten before it is read in a Step).
@@ -1905,12 +1909,19 @@ private:
             launch_timed("iw_apply_res", kern, nb, a, pin, rin, Apin, (const T*)pre_, pout, rout, Apout, delta_,
                          red_.scalars, rz(i - 1), base_scale, rs, pin2);
         };
+        if (res_nt_ == 3) go_res<3>(go, i, pin2);
+        else if (res_nt_ == 0) go_res<0>(go, i, pin2);
+        else go_res<2>(go, i, pin2);
+    }
+    // OPT_AMD_IW_RES_NT: streaming (nontemporal) loads (bit 0) / stores (bit 1) of the PCG vectors
+    template <int NT, typename G>
+    void go_res(G&& go, int i, const T* pin2) {
         if (pin2 || (defer_ && i == 1)) {   // deferred delta: odd i none, i = 2 starts it, even i > 2 folds a pair
-            if (i % 2 == 1) go(iw::iw_apply_res<T, 0, 2, 0>);
-            else if (i == 2) go(iw::iw_apply_res<T, 1, 2, 1>);
-            else go(iw::iw_apply_res<T, 2, 2, 1>);
-        } else if (i == 1) go(iw::iw_apply_res<T, 1>);
-        else go(iw::iw_apply_res<T, 2>);
+            if (i % 2 == 1) go(iw::iw_apply_res<T, 0, NT, 0>);
+            else if (i == 2) go(iw::iw_apply_res<T, 1, NT, 1>);
+            else go(iw::iw_apply_res<T, 2, NT, 1>);
+        } else if (i == 1) go(iw::iw_apply_res<T, 1, NT>);
+        else go(iw::iw_apply_res<T, 2, NT>);
     }
     void launch_residual(int i_num, int i_den, int sc_out) {
         const int nb = flat_grid(dom_.npix_mem(), 2);
@@ -1946,6 +1957,7 @@ private:
     bool fused_init_ = true;            // OPT_AMD_IW_FUSED_INIT=0: iw_jtf, then iw_apply<1,0>
     bool fused_res_ = true;             // OPT_AMD_IW_FUSED_RES=0: iw_apply<2> + iw_residual per iteration
     bool defer_ = true;                 // OPT_AMD_IW_DEFER=0: iw_apply_res updates delta in every iteration
+    int res_nt_ = 2;                    // iw_apply_res NT template argument (0, 2, 3)
     int rows_ = 16, depth_ = 1, nstrips_ = 0, nrowblocks_ = 0;
     bool rows_auto_ = false;
     int nt_ = 6;   // streaming PCG-vector access: bit 0 iw_apply loads, bit 1 iw_apply stores, bit 2 iw_residual
