@@ -16,7 +16,8 @@ cost). Inputs are resident in HBM before the timed region starts.
 
 Multi-GPU (--gpus N under torch.distributed.run): the 4096² image is split into N
 row slabs, one per rank (OptAMD_PlanSetDecomposition over an RCCL communicator):
-per PCG iteration two scalar all-reduces (p.Ap, r.z) and one halo-row exchange.
+per PCG iteration one all-reduce of four fp64 scalars (r.z, p.Ap, r.W Ap, Ap.W Ap: the
+fused pass takes beta's numerator from their identity) and one halo-row exchange.
 Total work is fixed, so the scaling is strong.
 
 --workload shape_from_shading: BASELINE config 3 (4096² fp32 LM + PCG, the config
@@ -360,7 +361,8 @@ def main():
         "config": {
             "workload": f"{args.workload} {W}x{H} fp32 {kind}+PCG, lIterations={args.liter}",
             "unknowns": n_unknowns,
-            "parallelism": f"row-slabs x{world} (RCCL: 2 allreduce + 1 halo exchange per PCG iteration)" if world > 1 else "single",
+            "parallelism": (f"row-slabs x{world} (RCCL: {2 if sfs else 1} allreduce + 1 halo exchange per PCG iteration)"
+                            if world > 1 else "single"),
         },
         f"{kind.lower()}_iters_per_s": args.steps / dt,
         "apply_unknowns_per_s": ch * npx * world / avg_apply_s,

@@ -181,6 +181,28 @@ __device__ __forceinline__ void eedge(T ojx, T ojy, T cj, T sj, float ujx, float
     ey = v ? wr * (ojy - oty - ry) : (T)0;
 }
 
+// Accumulation of the fused passes' sums: 0 fp32 products and lane sums, 1 fp32 products
+// summed in fp64, 2 fp64 products summed in fp64 (the identity's terms cancel: their
+// rounding is amplified by rz_{i-1} / rz_i).
+#ifndef OPTAMD_IW_ACC
+#define OPTAMD_IW_ACC 2
+#endif
+#if OPTAMD_IW_ACC == 0
+typedef float acc_t;
+#else
+typedef double acc_t;
+#endif
+// w0 a0 b0 + w1 a1 b1 + w2 a2 b2 at the accumulation precision
+template <typename T>
+__device__ __forceinline__ acc_t wdot3(T w0, T a0, T b0, T w1, T a1, T b1, T w2, T a2, T b2) {
+#if OPTAMD_IW_ACC == 2
+    return (double)w0 * (double)a0 * (double)b0 + (double)w1 * (double)a1 * (double)b1 +
+           (double)w2 * (double)a2 * (double)b2;
+#else
+    return (acc_t)(w0 * a0 * b0 + w1 * a1 * b1 + w2 * a2 * b2);
+#endif
+}
+
 // ------------------------------------------------------------ row records
 // Every stencil kernel keeps rows y-1, y, y+1 finished in registers and has row y+2
 // (DEPTH 2: also y+3) in flight: a raw row is issued as pure loads (no arithmetic on
@@ -210,6 +232,7 @@ struct PRow {          // finished row
     float ux, uy;
     int act, fit;
     T dx, dy, dt;      // delta after this iteration's update (MODE 2 with delta)
+    T rx, ry, rt, ww0, ww2;   // MODE 1: r_0 and PCGStep2's weights (iw_apply<SUMS>)
     // edge pixel seen by this lane (lane 0: left of the strip, lane 63: right of it)
     T epx, epy;        // its p (x, y)
     float eux, euy;
@@ -285,6 +308,11 @@ __device__ __forceinline__ PRow<T> finish_prow(const Args<T>& a, const PRaw<T>& 
     o.uy = q.in ? q.u.y : 0.f;
     sc_of(q.in ? q.ang : (T)0, &o.c, &o.s);
     make_p<T, MODE>(a, f, beta, q.v0, q.v1, q.v2, q.w2, q.q0, q.q1, q.q2, o.px, o.py, o.pt);
+    if (MODE == 1) {
+        o.rx = q.v0; o.ry = q.v1; o.rt = q.v2;
+        o.ww0 = a.use_pre ? pre_offset(a, f) : (T)1;
+        o.ww2 = a.use_pre ? q.w2 : (T)1;
+    }
     if (MODE == 2 && DM == 1) { o.dx = alpha * q.q0; o.dy = alpha * q.q1; o.dt = alpha * q.q2; }
     if (MODE == 2 && DM == 2) {
         o.dx = fmad(alpha, q.q0, q.d0); o.dy = fmad(alpha, q.q1, q.d1); o.dt = fmad(alpha, q.q2, q.d2);
@@ -319,7 +347,9 @@ __device__ __forceinline__ PRow<T> finish_prow(const Args<T>& a, const PRaw<T>& 
 // PCGStep1's LM variant, :617-622) and the whole grid returns at entry once the
 // device-side zeta test has set *stop.
 // NT bit 0: streaming loads of the PCG vectors (raw_prow); bit 1: streaming stores.
-template <typename T, int MODE, int DM, int DEPTH, bool LMX = false, int NT = 0>
+// SUMS (MODE 1): iteration 0 of iw_apply_res's loop when PCGInit1 is not fused with it
+// (row slabs): sc[rs.out + 0..2] = {p.Ap, r.W Ap, Ap.W Ap} in fp64, as iw_jtf_apply sums them.
+template <typename T, int MODE, int DM, int DEPTH, bool LMX = false, int NT = 0, bool SUMS = false>
 __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restrict__ pin,
                                                    const T* __restrict__ r,
                                                    const T* __restrict__ pre, T* __restrict__ pout,
@@ -336,6 +366,7 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
     const T wr = a.wr, wf2 = a.wf * a.wf;
     const long long N = a.dom.npix_mem();
     T dot = 0;
+    acc_t papd = 0, rapd = 0, apapd = 0;
     if (g.y0 < g.y1) {
         PRow<T> up = finish_prow<T, MODE, DM>(a, raw_prow<T, MODE, DM, (NT & 1) != 0>(a, g, g.y0 - 1, pin, r, pre, delta), beta, alpha);
         PRow<T> cur = finish_prow<T, MODE, DM>(a, raw_prow<T, MODE, DM, (NT & 1) != 0>(a, g, g.y0, pin, r, pre, delta), beta, alpha);
@@ -397,7 +428,13 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
                     st_v<(NT & 2) != 0>(delta + 2 * i, on ? cur.dx : (T)0); st_v<(NT & 2) != 0>(delta + 2 * i + 1, on ? cur.dy : (T)0);
                     st_v<(NT & 2) != 0>(delta + 2 * N + i, on ? cur.dt : (T)0);
                 }
-                dot += cur.px * aox + cur.py * aoy + cur.pt * aot;
+                if (SUMS) {
+                    papd += (acc_t)(cur.px * aox + cur.py * aoy + cur.pt * aot);
+                    rapd += wdot3(cur.ww0, cur.rx, aox, cur.ww0, cur.ry, aoy, cur.ww2, cur.rt, aot);
+                    apapd += wdot3(cur.ww0, aox, aox, cur.ww0, aoy, aoy, cur.ww2, aot, aot);
+                } else {
+                    dot += cur.px * aox + cur.py * aoy + cur.pt * aot;
+                }
             }
             // roll the window; the raw row is finished only now
             in_up_x = jpy_x; in_up_y = jpy_y;
@@ -408,8 +445,13 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
             if (DEPTH == 2) nx = nn;
         }
     }
-    double v[1] = {(double)dot};
-    block_reduce_publish<1>(v, rs, g.tile);   // partials by tile: split launches share the slot
+    if constexpr (SUMS) {
+        double v[3] = {(double)papd, (double)rapd, (double)apapd};
+        block_reduce_publish<3>(v, rs, g.tile);
+    } else {
+        double v[1] = {(double)dot};
+        block_reduce_publish<1>(v, rs, g.tile);   // partials by tile: split launches share the slot
+    }
 }
 
 // ------------------------------------------ apply with the residual update fused
@@ -433,27 +475,6 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
 // in the last iteration (nothing reads r_L or Ap_L).
 // Scalar slots of iteration j (ImageWarpingPlan: kScBase + kSlots * j): rz, pAp, rAp, ApAp, rz by the identity
 constexpr int kSlots = 5;
-// Accumulation of the fused passes' sums: 0 fp32 products and lane sums, 1 fp32 products
-// summed in fp64, 2 fp64 products summed in fp64 (the identity's terms cancel: their
-// rounding is amplified by rz_{i-1} / rz_i).
-#ifndef OPTAMD_IW_ACC
-#define OPTAMD_IW_ACC 2
-#endif
-#if OPTAMD_IW_ACC == 0
-typedef float acc_t;
-#else
-typedef double acc_t;
-#endif
-// w0 a0 b0 + w1 a1 b1 + w2 a2 b2 at the accumulation precision
-template <typename T>
-__device__ __forceinline__ acc_t wdot3(T w0, T a0, T b0, T w1, T a1, T b1, T w2, T a2, T b2) {
-#if OPTAMD_IW_ACC == 2
-    return (double)w0 * (double)a0 * (double)b0 + (double)w1 * (double)a1 * (double)b1 +
-           (double)w2 * (double)a2 * (double)b2;
-#else
-    return (acc_t)(w0 * a0 * b0 + w1 * a1 * b1 + w2 * a2 * b2);
-#endif
-}
 // minimum waves per SIMD the fused passes are compiled for (0: the compiler's choice)
 #ifndef OPTAMD_IW_WPE
 #define OPTAMD_IW_WPE 0
@@ -899,7 +920,10 @@ __device__ __forceinline__ JOut<T> jtf_out(const Args<T>& a, const VRow<T>& cur,
 // OUT 1: all three preconditioner channels (OptAMD_EvalJTF layout);
 // OUT 2: diag(J^T J) in all three channels instead of pre, no reduction (the generic
 //        GN/LM driver, which forms pre / the LM diagonal itself).
-template <typename T, int OUT>
+// ACC: rz[0] summed as iw_jtf_apply sums it (fp64 products and sums, wdot3), the base of
+// iw_apply_res's identity on row slabs (an fp32 sum is off by ~1e-7 of rz[0], which the
+// identity's cancellation would amplify)
+template <typename T, int OUT, bool ACC = false>
 __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T* __restrict__ pre,
                                                  ReduceSlot rs) {
     IW_PRE_TABLE(a);
@@ -907,6 +931,7 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
     const T wf = a.wf, wr2 = a.wr * a.wr;
     const long long N = a.dom.npix_mem();
     T dot = 0;
+    acc_t dotd = 0;
     if (g.y0 < g.y1) {
         const VRow<T> up = finish_vrow<T, true>(raw_vrow<T, true>(a, g, g.y0 - 1));
         VRow<T> cur = finish_vrow<T, true>(raw_vrow<T, true>(a, g, g.y0)),
@@ -919,7 +944,11 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
                 const long long i = a.dom.off(g.x, y);
                 const JOut<T> o = jtf_out(a, cur, j);
                 a.flags[i] = (uint8_t)o.f;
-                if (cur.act) dot += o.rx * (o.wo * o.rx) + o.ry * (o.wo * o.ry) + o.rt * (o.wt * o.rt);
+                if (ACC) {
+                    if (cur.act) dotd += wdot3(o.wo, o.rx, o.rx, o.wo, o.ry, o.ry, o.wt, o.rt, o.rt);
+                } else if (cur.act) {
+                    dot += o.rx * (o.wo * o.rx) + o.ry * (o.wo * o.ry) + o.rt * (o.wt * o.rt);
+                }
                 r[2 * i] = o.rx; r[2 * i + 1] = o.ry; r[2 * N + i] = o.rt;
                 if (OUT == 2) {
                     // the reference sums (d e/d O)^2 = wr^2 once per valid residual, then wf^2
@@ -939,7 +968,7 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
         }
     }
     if (OUT == 2) return;
-    double v[1] = {(double)dot};
+    double v[1] = {ACC ? (double)dotd : (double)dot};
     block_reduce_publish<1>(v, rs, blockIdx.x);
 }
 
@@ -1467,8 +1496,9 @@ public:
         // PCG iteration's apply (iw_jtf_apply: the first p = pre r needs no global scalar).
         const bool fused = fused_init_ && !distributed() && L >= 1;
         // iterations 1.. as iw_apply_res (the residual update folded into the next apply;
-        // needs iw_jtf_apply's two extra sums)
-        const bool res = fused && fused_res_;
+        // needs the sums r_0.W Ap_0, Ap_0.W Ap_0 of iteration 0), on one domain and on row
+        // slabs: ONE all-reduce of four scalars per PCG iteration instead of two
+        const bool res = fused_res_ && L >= 1;
         // res with defer_: p_i in pb[i % 3]; the delta terms of odd iterations are folded
         // in pairs by the next even iteration (or the update), which reads p_{i-2} again
         const bool defer = res && defer_;
@@ -1476,7 +1506,7 @@ public:
         if (fused) {
             launch_jtf_apply(pcur, L == 1);
         } else {
-            tbegin("iw_jtf"); launch_jtf(r_, pre_, rz(0)); tend();
+            tbegin("iw_jtf"); launch_jtf(r_, pre_, rz(0), false, res); tend();
             allreduce(rz(0));
             if (distributed()) {
                 std::vector<HaloPlane> pl;
@@ -1492,19 +1522,44 @@ public:
         // row slabs with >= 3 row blocks: the halo refresh of r and p_{i-1} runs beside the
         // interior row blocks of the next apply (halo_mark / halo_begin / halo_join)
         const bool split = distributed() && overlap_ && comm_->concurrent_halo() && nrowblocks_ >= 3;
-        for (int i = 0; i < L; ++i) {
+        if (res) {
+            // p_i in pb[i % 3] (deferred delta) or pb[i % 2]
+            auto pbuf = [&](int i) { return pb[defer ? i % 3 : i % 2]; };
+            if (!fused) {   // iteration 0 with the two extra sums (PCGInit1 ran as iw_jtf)
+                launch_apply<1, 0>(nullptr, pbuf(0), pap(0), 0, 0, 0, 0, nullptr, L == 1, 0, true);
+                allreduce(pap(0), 3);
+            }
+            for (int i = 1; i < L; ++i) {
+                const bool last = i + 1 == L;
+                T* rb[2] = {r_, r1_};
+                T* ab[2] = {Ap_, Ap1_};
+                const T* pin2 = (defer && i >= 2) ? pbuf(i - 2) : nullptr;
+                if (distributed()) {   // the stencil reads r, Ap and p of iteration i-1 in the halo rows
+                    std::vector<HaloPlane> pl;
+                    add_vec_planes(pl, rb[(i - 1) & 1]);
+                    add_vec_planes(pl, ab[(i - 1) & 1]);
+                    add_vec_planes(pl, pbuf(i - 1));
+                    if (split) {   // beside the interior row blocks
+                        halo_mark();
+                        launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 1);
+                        halo_begin(comm_, pl, dom_, 1);
+                        halo_join();
+                        launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 2);
+                    } else {
+                        exchange(pl);
+                        launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2);
+                    }
+                } else {
+                    launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2);
+                }
+                allreduce(rz(i), 4);   // rz, pAp, r.W Ap, Ap.W Ap of iteration i
+            }
+            pcur = pbuf(L - 1);
+        }
+        for (int i = 0; i < L && !res; ++i) {
             if (i > 0 || !fused) std::swap(pcur, pprev);   // pcur <- new p, pprev <- old p
             const bool last = i + 1 == L;   // timed by events on the launch (launch_apply)
             if (i == 0 && fused) {   // iw_jtf_apply above
-                if (res) {   // r_1 is formed inside iteration 1's pass
-                    if (last) break;
-                    continue;
-                }
-            } else if (res) {
-                if (defer) launch_apply_res(i, pb[(i - 1) % 3], pb[i % 3], last, i >= 2 ? pb[(i - 2) % 3] : nullptr);
-                else launch_apply_res(i, pprev, pcur, last);
-                if (last) break;
-                continue;
             }
             else if (i == 0) launch_apply<1, 0>(nullptr, pcur, pap(i), 0, 0, 0, 0, nullptr, last);
             else if (split) {
@@ -1719,8 +1774,8 @@ private:
 
     bool distributed() const { return comm_ && comm_->size() > 1; }
     // sum a scalar slot over ranks (no-op on one rank)
-    void allreduce(int idx) {
-        if (distributed()) comm_->allreduce_sum(red_.scalars + idx, 1, stream_);
+    void allreduce(int idx, int n = 1) {
+        if (distributed()) comm_->allreduce_sum(red_.scalars + idx, n, stream_);
     }
     // halo planes of an unknown-layout vector [Offset.xy | Angle]
     void add_vec_planes(std::vector<HaloPlane>& v, const T* x) const {
@@ -1806,9 +1861,12 @@ private:
         return v;
     }
 
-    void launch_jtf(T* r, T* pre, int sc_out, bool full_pre = false) {
+    void launch_jtf(T* r, T* pre, int sc_out, bool full_pre = false, bool acc = false) {
         const int nb = stencil_blocks();
-        if (full_pre)
+        if (acc)
+            hipLaunchKernelGGL((iw::iw_jtf<T, 0, true>), dim3(nb), dim3(kBlock), 0, stream_, args(), r, pre,
+                               red_.slot(nb, sc_out));
+        else if (full_pre)
             hipLaunchKernelGGL((iw::iw_jtf<T, 1>), dim3(nb), dim3(kBlock), 0, stream_, args(), r, pre,
                                red_.slot(nb, sc_out));
         else
@@ -1840,7 +1898,7 @@ private:
     // last row blocks (the only ones whose stencil reads halo rows)
     template <int MODE, int DM>
     void launch_apply(const T* pin, T* pout, int sc_out, int ib_num, int ib_den, int ia_num, int ia_den,
-                      T* Ap = nullptr, bool no_ap = false, int part = 0) {
+                      T* Ap = nullptr, bool no_ap = false, int part = 0, bool sums = false) {
         const int nb = stencil_blocks();
         Ap = no_ap ? nullptr : (Ap ? Ap : Ap_);
         iw::Args<T> a = args();
@@ -1851,6 +1909,14 @@ private:
         } else if (part == 2) {
             a.tb0 = 0; a.tn0 = nstrips_; a.tb1 = nstrips_ * (nrowblocks_ - 1);
             grid = 2 * nstrips_;
+        }
+        if constexpr (MODE == 1) {
+            if (sums) {   // iteration 0 of the fused loop (iw_apply_res's identity needs its sums)
+                launch_timed("iw_apply", iw::iw_apply<T, 1, 0, 1, false, 2, true>, grid, a, pin, (const T*)r_,
+                             (const T*)pre_, pout, Ap, delta_, (const double*)red_.scalars, ib_num, ib_den, ia_num,
+                             ia_den, red_.slot(nb, sc_out), (const T*)nullptr, (const int*)nullptr);
+                return;
+            }
         }
         launch_apply_grid<MODE, DM>(a, grid, pin, pout, sc_out, ib_num, ib_den, ia_num, ia_den, Ap);
     }
@@ -1894,7 +1960,8 @@ private:
     }
     // PCG iteration i >= 1 of the fused loop: r_{i-1} / Ap_{i-1} in buffer (i-1) & 1 (r_ / Ap_
     // for even), r_i / Ap_i into the other one (none in the last iteration)
-    void launch_apply_res(int i, const T* pin, T* pout, bool last, const T* pin2 = nullptr) {
+    // part: 0 every row block, 1 the interior ones, 2 the first and last (launch_apply)
+    void launch_apply_res(int i, const T* pin, T* pout, bool last, const T* pin2 = nullptr, int part = 0) {
         T* rb[2] = {r_, r1_};
         T* ab[2] = {Ap_, Ap1_};
         const T* rin = rb[(i - 1) & 1];
@@ -1902,11 +1969,19 @@ private:
         T* rout = last ? nullptr : rb[i & 1];
         T* Apout = last ? nullptr : ab[i & 1];
         const double base_scale = (i == 1 && !spec_.use_preconditioner) ? 4.0 : 1.0;
-        const iw::Args<T> a = args();
-        const int nb = stencil_blocks();
+        iw::Args<T> a = args();
+        const int nb = stencil_blocks();   // the reduction slot spans every tile
+        int grid = nb;
+        if (part == 1) {
+            a.tb0 = nstrips_; a.tn0 = nstrips_ * (nrowblocks_ - 2);
+            grid = a.tn0;
+        } else if (part == 2) {
+            a.tb0 = 0; a.tn0 = nstrips_; a.tb1 = nstrips_ * (nrowblocks_ - 1);
+            grid = 2 * nstrips_;
+        }
         const ReduceSlot rs = red_.slot(nb, rz(i));
         auto go = [&](auto kern) {
-            launch_timed("iw_apply_res", kern, nb, a, pin, rin, Apin, (const T*)pre_, pout, rout, Apout, delta_,
+            launch_timed("iw_apply_res", kern, grid, a, pin, rin, Apin, (const T*)pre_, pout, rout, Apout, delta_,
                          red_.scalars, rz(i - 1), base_scale, rs, pin2);
         };
         if (res_nt_ == 3) go_res<3>(go, i, pin2);
