@@ -77,7 +77,7 @@ __device__ __forceinline__ V3<T> ld3(const S* a, long long v) {
 }
 // Gathers address a neighbour as uniform base + 32-bit byte offset (the global_load
 // saddr form: one full-rate multiply per address instead of a 64-bit multiply-add;
-// make_arap_plan bounds N so 24 N fits in 32 bits)
+// make_arap_plan bounds N so 24 N and 72 N fit in 32 bits)
 template <typename T, typename S>
 __device__ __forceinline__ V3<T> gld3(const S* a, int u) {
     const S* q = (const S*)((const char*)a + (unsigned)u * (unsigned)(3 * sizeof(S)));
@@ -86,6 +86,14 @@ __device__ __forceinline__ V3<T> gld3(const S* a, int u) {
 template <typename S>
 __device__ __forceinline__ S gld(const S* a, int u) {
     return *(const S*)((const char*)a + (unsigned)u * (unsigned)sizeof(S));
+}
+// Element u of plane q of an N-strided SoA array: one uniform base for every plane and a
+// 32-bit offset (q N + u) sizeof(S) (make_arap_plan bounds 9 N sizeof(S) below 2^32), so
+// the nine K gathers of a neighbour use the saddr form instead of nine 64-bit per-lane
+// addresses (27 VGPR pairs at three neighbours per batch)
+template <typename S>
+__device__ __forceinline__ S gldq(const S* a, unsigned qN, int u) {
+    return *(const S*)((const char*)a + (qN + (unsigned)u) * (unsigned)sizeof(S));
 }
 template <typename T>
 __device__ __forceinline__ V3<T> mv(const T* M, const V3<T>& v) {
@@ -306,7 +314,7 @@ __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restr
                 pu[b] = gld3<T>(p, u[b]);
                 Uu[b] = gld3<float>(a.U, u[b]);
 #pragma unroll
-                for (int q = 0; q < 9; ++q) Ku[b][q] = gld(Kall + q * N, u[b]);
+                for (int q = 0; q < 9; ++q) Ku[b][q] = gldq(Kall, (unsigned)q * (unsigned)N, u[b]);
             }
 #pragma unroll
             for (int b = 0; b < EBI; ++b) {
@@ -335,7 +343,10 @@ __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restr
 // an in-neighbour (every neighbour of a mesh whose edges go both ways) has its p and
 // UrShape gathered once for both terms. The in-terms are summed in merged-list order
 // (the out-terms, and so the angle rows, keep the out-list order).
-constexpr int kEBM = 3;   // merged slots per batch (1, 2, 3 measured within 2 %); widths are padded to it
+// merged slots per batch; widths are padded to it. Round 3: 2 slots (89 VGPRs, 5 waves
+// per SIMD) 50.6-50.9 us against 3 slots (110 VGPRs, 4 waves) 52.4-52.5 us for kdir +
+// apply at 1 M vertices (profiles/r03_arap_eb.txt); OPT_AMD_ARAP_EB=3 restores 3
+constexpr int kEBM = 2;
 template <typename T, int EB = kEBM>
 __global__ __launch_bounds__(kBlock) void arap_apply_merged(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
                                                             const T* __restrict__ Kall, const T* __restrict__ dadd,
@@ -377,7 +388,7 @@ __global__ __launch_bounds__(kBlock) void arap_apply_merged(Args<T> a, const T* 
                 pu[b] = gld3<T>(p, u[b]);
                 Uu[b] = gld3<float>(a.U, u[b]);
 #pragma unroll
-                for (int q = 0; q < 9; ++q) Ku[b][q] = gld(Kall + q * N, u[b]);
+                for (int q = 0; q < 9; ++q) Ku[b][q] = gldq(Kall, (unsigned)q * (unsigned)N, u[b]);
             }
 #pragma unroll
             for (int b = 0; b < EB; ++b) {
@@ -726,8 +737,11 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
     void apply_prepared(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
-        if (merged_on_)
-            hipLaunchKernelGGL((arap::arap_apply_merged<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap,
+        if (merged_on_ && eb_ == 3)
+            hipLaunchKernelGGL((arap::arap_apply_merged<T, 3>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap,
+                               (const T*)K_, dadd, stop, rs);
+        else if (merged_on_)
+            hipLaunchKernelGGL((arap::arap_apply_merged<T, 2>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap,
                                (const T*)K_, dadd, stop, rs);
         else
             hipLaunchKernelGGL((arap::arap_apply<T>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap,
@@ -822,7 +836,7 @@ private:
         nb_.eoff = (int*)dmalloc(sizeof(int) * (ns + 1));
         OPT_HIP_CHECK(hipMemsetAsync(nb_.ew, 0, sizeof(int) * (ns + 1), s));
         hipLaunchKernelGGL(arap::merged_width, dim3((ns + 3) / 4), dim3(256), 0, s, (const int*)out_.off,
-                           (const int*)out_.nbr, (const int*)in_.off, (const int*)in_.nbr, N_, ns, arap::kEBM, nb_.ew);
+                           (const int*)out_.nbr, (const int*)in_.off, (const int*)in_.nbr, N_, ns, eb_, nb_.ew);
         size_t need = 0;
         OPT_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, need, nb_.ew, nb_.eoff, ns + 1, s));
         if (need > scratch_bytes_) {
@@ -888,6 +902,8 @@ private:
     int* keys_tmp_ = nullptr;
     T* K_ = nullptr;   // per-vertex directional rotation derivative of the current p
     const bool merged_on_ = env_int("OPT_AMD_ARAP_MERGED", 1) != 0;   // 0: separate out / in lists
+    // merged slots per batch of arap_apply_merged (the merged ELL widths are padded to it)
+    const int eb_ = env_int("OPT_AMD_ARAP_EB", arap::kEBM) == 3 ? 3 : 2;
     T *userO_ = nullptr, *userA_ = nullptr, *dO_ = nullptr, *dA_ = nullptr;
     float *dU_ = nullptr, *dC_ = nullptr;
     int *dv0_ = nullptr, *dv1_ = nullptr;
@@ -905,8 +921,9 @@ std::unique_ptr<Plan> make_arap_plan(const ProblemSpec& spec, const StateOptions
         if (d.name == spec.graphs[0].dims[0]) E = dims[d.index];
     }
     if (N == 0) { *err = "arap_mesh_deformation: zero vertices"; return nullptr; }
-    // 24 N bytes must fit the gathers' 32-bit offsets (arap::gld3)
-    if (N > (1u << 27) || E > (1u << 30)) { *err = "arap_mesh_deformation: graph too large"; return nullptr; }
+    // 24 N bytes (arap::gld3) and 9 N sizeof(T) bytes (arap::gldq, the K planes) must fit the
+    // gathers' 32-bit offsets: at most 2^25 vertices
+    if (N > (1u << 25) || E > (1u << 30)) { *err = "arap_mesh_deformation: graph too large"; return nullptr; }
     Domain dom{(int)N, 1, 0, 1, 0, 1};
     dom.edges = (int)E;
     if (opts.double_precision) return make_stencil_plan<ArapOp<double>>(spec, opts, dom, err);

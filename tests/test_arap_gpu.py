@@ -313,3 +313,21 @@ def test_graph_without_edges_and_isolated_vertices():
         assert len(costs) == len(ref)
         np.testing.assert_allclose(costs, ref, rtol=1e-4, atol=1e-8 * ref[0])
         s.close()
+
+
+@pytest.mark.parametrize("double", [False, True])
+def test_merged_batch_size_is_bitwise(monkeypatch, double):
+    """arap_apply_merged with 2 or 3 merged slots per load batch (OPT_AMD_ARAP_EB; the ELL
+    widths padded to it): the slots are summed in the same order either way, padding slots
+    add exact zeros, so whole GN solves are bitwise equal."""
+    w = perturbed(23, 17, seed=6)
+    out = {}
+    for eb in ("2", "3"):
+        monkeypatch.setenv("OPT_AMD_ARAP_EB", eb)
+        s = solver(w, "gaussNewtonGPU", double_precision=double)
+        prm = params(w, double=double)
+        s.set_solver_params({"nIterations": 3, "lIterations": 10})
+        out[eb] = (s.profiled_solve(prm), to_np(prm[2]), to_np(prm[3]))
+        s.close()
+    assert out["2"][0] == out["3"][0]
+    assert np.array_equal(out["2"][1], out["3"][1]) and np.array_equal(out["2"][2], out["3"][2])
