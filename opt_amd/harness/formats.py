@@ -200,3 +200,29 @@ def read_off(path):
         fl.append([int(x) for x in toks[pos + 1:pos + 1 + c]])
         pos += 1 + c
     return v, np.array(fl, np.int32)
+
+
+def read_obj(path):
+    """(vertices (n, 3) float32, faces (m, 3) int32, 0-based) of a triangle OBJ file — the
+    'v' and 'f' records OpenMesh's OBJ reader turns into a TriMesh in file order
+    (examples/robust_nonrigid_alignment/src/main.cpp: createMesh); f entries may be
+    v, v/vt, v/vt/vn or v//vn."""
+    v, f = [], []
+    for line in open(path):
+        t = line.split()
+        if not t:
+            continue
+        if t[0] == "v":
+            v.append([float(x) for x in t[1:4]])
+        elif t[0] == "f":
+            f.append([int(x.split("/")[0]) - 1 for x in t[1:4]])
+    return np.array(v, np.float64).astype(np.float32), np.array(f, np.int32)
+
+
+def read_ele(path):
+    """Tetrahedra (n, 4) int32 of a TetGen .ele file (count, 4, attrs; then index + 4
+    vertex ids per line), as main.cpp: getSourceTetIndices reads them."""
+    tok = open(path).read().split()
+    n = int(tok[0])
+    a = np.array([int(x) for x in tok[3:3 + 5 * n]], np.int64).reshape(n, 5)
+    return a[:, 1:].astype(np.int32)

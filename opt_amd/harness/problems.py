@@ -530,3 +530,155 @@ UNKNOWN_INDEX = {"image_warping": 0, "poisson_image_editing": 0, "optical_flow":
                  "arap_mesh_deformation": 2, "shape_from_shading": 16, "cotangent_mesh_smoothing": 2,
                  "embedded_mesh_deformation": 3, "intrinsic_image_decomposition": 4,
                  "volumetric_mesh_deformation": 0}
+
+
+# ------------------------------------------------------- robust_nonrigid_alignment
+class StdMt19937:
+    """std::mt19937 (its init_genrand seeding = numpy's legacy MT19937 seeding)."""
+
+    def __init__(self, seed: int):
+        self.bg = np.random.MT19937(0)
+        self.bg._legacy_seeding(seed)
+
+    def __call__(self) -> int:
+        return int(self.bg.random_raw())
+
+
+def std_uniform_int(rng, a: int, b: int, lemire: bool = False) -> int:
+    """libstdc++ std::uniform_int_distribution<int>(a, b) over a 32-bit engine: the
+    downscaling loop of GCC < 11, or (lemire) GCC 11's nearly-divisionless method."""
+    r = b - a + 1
+    if lemire:
+        prod = rng() * r
+        low = prod & 0xFFFFFFFF
+        if low < r:
+            thr = ((1 << 32) - r) % r
+            while low < thr:
+                prod = rng() * r
+                low = prod & 0xFFFFFFFF
+        return (prod >> 32) + a
+    scaling = 0xFFFFFFFF // r
+    past = r * scaling
+    while True:
+        v = rng()
+        if v < past:
+            return v // scaling + a
+
+
+class StdNormal:
+    """libstdc++ std::normal_distribution<double>: Marsaglia's polar method (the second
+    value saved for the next call) over generate_canonical<double, 53> (two 32-bit draws)."""
+
+    def __init__(self, mean: float, stddev: float):
+        self.mean, self.stddev, self.saved = mean, stddev, None
+
+    def __call__(self, rng) -> float:
+        if self.saved is not None:
+            v, self.saved = self.saved, None
+        else:
+            def canon():
+                s = (rng() + rng() * 4294967296.0) / 18446744073709551616.0
+                return s if s < 1.0 else np.nextafter(1.0, 0.0)
+            while True:
+                x = 2.0 * canon() - 1.0
+                y = 2.0 * canon() - 1.0
+                r2 = x * x + y * y
+                if 0.0 < r2 <= 1.0:
+                    break
+            mult = np.sqrt(-2.0 * np.log(r2) / r2)
+            self.saved = x * mult
+            v = y * mult
+        return v * self.stddev + self.mean
+
+
+def mesh_vertex_normals(v: np.ndarray, f: np.ndarray) -> np.ndarray:
+    """OpenMesh update_normals(): per face the normalised (p2 - p1) x (p0 - p1), per vertex
+    the normalised sum of its faces' normals (float32 as the SimpleMesh's Vec3f)."""
+    p0, p1, p2 = v[f[:, 0]], v[f[:, 1]], v[f[:, 2]]
+    n = np.cross(p2 - p1, p0 - p1).astype(np.float32)
+    ln = np.sqrt((n * n).sum(1, dtype=np.float32))
+    n = np.where(ln[:, None] != 0, n / np.where(ln == 0, 1, ln)[:, None], 0).astype(np.float32)
+    vn = np.zeros_like(v, dtype=np.float32)
+    for k in range(3):
+        np.add.at(vn, f[:, k], n)
+    lv = np.sqrt((vn * vn).sum(1, dtype=np.float32))
+    return np.where(lv[:, None] != 0, vn / np.where(lv == 0, 1, lv)[:, None], 0).astype(np.float32)
+
+
+def tet_graph(tets: np.ndarray, nv: int):
+    """generateOptEdges with tetrahedra (CombinedSolver.h:381-404): every vertex's
+    neighbours in its tets as a std::set (ascending), then the directed edges v -> n in
+    that order (createGraphFromNeighborLists)."""
+    nb = [set() for _ in range(nv)]
+    for t in tets.tolist():
+        for i in range(4):
+            for j in range(1, 4):
+                nb[t[i]].add(t[(i + j) % 4])
+    v0 = np.array([i for i in range(nv) for _ in nb[i]], np.int32)
+    v1 = np.array([n for i in range(nv) for n in sorted(nb[i])], np.int32)
+    return v0, v1
+
+
+def robust_nonrigid_alignment(src_v, src_f, tets, tgt_v, tgt_f, arg_order: str = "rtl",
+                              lemire: bool = False, K: int = 20) -> dict:
+    """The FIRST solve of the robust_nonrigid_alignment example (the one
+    examples/test_final_cost.py's reference cost 66.784683 is taken from): CombinedSolver
+    construction (CombinedSolver.h:72-137: average edge length, the mt19937(230948) draws
+    of 5 % spurious target indices and their normal(0, 30 x edge length) offsets),
+    combinedSolveInit (w_fit = sqrt 10, w_reg = sqrt 64), and preNonlinearSolve(0) on the
+    first target (setConstraints, :266-352: per source vertex the K = 20 nearest target
+    vertices (nanoflann, exact), the first within 5 edge lengths whose normal is within
+    acos 0.7 of the source normal, else -inf; the spurious offsets added; every changed
+    constraint's robust weight 1). arg_order: the order C++ evaluated
+    make_float3(normal(), normal(), normal())'s arguments ("rtl" = GCC on x86-64)."""
+    src_v = np.asarray(src_v, np.float32)
+    tgt_v = np.asarray(tgt_v, np.float32)
+    N = len(src_v)
+    # average edge length (float edge lengths summed in double over the mesh's edges)
+    e = np.concatenate([src_f[:, [0, 1]], src_f[:, [1, 2]], src_f[:, [2, 0]]])
+    e = np.sort(e, axis=1)
+    _, first = np.unique(e[:, 0].astype(np.int64) * N + e[:, 1], return_index=True)
+    ue = e[np.sort(first)]
+    d = src_v[ue[:, 1]] - src_v[ue[:, 0]]
+    lens = np.sqrt((d * d).sum(1, dtype=np.float32)).astype(np.float32)
+    avg = float(np.sum(lens.astype(np.float64))) / len(ue)
+    # spurious correspondences
+    rng = StdMt19937(230948)
+    nd = StdNormal(0.0, avg * 30.0)
+    spurious, noisy = [], []
+    for _ in range(int(np.float32(N) * np.float32(0.05))):
+        spurious.append(std_uniform_int(rng, 0, len(tgt_v) - 1, lemire))
+        a, b, c = nd(rng), nd(rng), nd(rng)
+        noisy.append((c, b, a) if arg_order == "rtl" else (a, b, c))
+    noisy = np.array(noisy, np.float32)
+    # correspondences of the initial mesh against the first target
+    sn = mesh_vertex_normals(src_v, src_f)
+    tn = mesh_vertex_normals(tgt_v, tgt_f)
+    thr = np.float32(avg) * np.float32(5.0)
+    C = np.full((N, 3), -np.inf, np.float32)
+    CN = np.zeros((N, 3), np.float32)
+    for s0 in range(0, N, 512):
+        q = src_v[s0:s0 + 512]
+        dd = q[:, None, :] - tgt_v[None, :, :]
+        d2 = (dd[..., 0] * dd[..., 0] + dd[..., 1] * dd[..., 1]) + dd[..., 2] * dd[..., 2]
+        nn = np.argpartition(d2, K, axis=1)[:, :K]
+        for r in range(len(q)):
+            cand = nn[r][np.lexsort((nn[r], d2[r, nn[r]]))]
+            i = s0 + r
+            for t in cand:
+                dv = tgt_v[t] - src_v[i]
+                dist = np.sqrt(np.float32(dv[0] * dv[0] + dv[1] * dv[1] + dv[2] * dv[2]))
+                if dist > thr:
+                    break
+                if np.float32(tn[t, 0] * sn[i, 0] + tn[t, 1] * sn[i, 1] + tn[t, 2] * sn[i, 2]) > np.float32(0.7):
+                    C[i] = tgt_v[t]
+                    CN[i] = tn[t]
+                    break
+    for k, idx in enumerate(spurious):
+        if idx < N:
+            C[idx] += noisy[k]
+    v0, v1 = tet_graph(tets, N)
+    return dict(N=N, E=len(v0), w_fitSqrt=float(np.sqrt(np.float32(10.0))), w_regSqrt=float(np.float32(8.0)),
+                Offset=src_v.copy(), Angle=np.zeros((N, 3), np.float32), RobustWeights=np.ones(N, np.float32),
+                UrShape=src_v.copy(), Constraints=C, ConstraintNormals=CN, v0=v0, v1=v1,
+                average_edge_length=avg, spurious=np.array(spurious, np.int64))

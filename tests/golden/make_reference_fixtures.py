@@ -34,6 +34,10 @@ harness loads them:
   intrinsic_image_decomposition (main.cpp:19-40, stride 12 as test_final_cost.py:85
     sets): the RGB pixels of ye_high2.png at (12 x, 12 y).
 
+  robust_nonrigid_alignment (main.cpp, CombinedSolver.h): squat_source.obj (positions,
+    triangles), squat_tetmesh.ele (the tetrahedra the graph is built from) and the first
+    target of squat_target/ in directory order (the first solve).
+
 The problem construction of each (harness mirror, opt_amd/harness/problems.py) runs on
 these at test time.
 
@@ -103,6 +107,15 @@ def main(ref):
     out = os.path.join(here, "iid_ye_s12.npz")
     np.savez_compressed(out, rgb=a[: H * stride: stride, : W * stride: stride].copy(), stride=stride)
     print(out, (H, W))
+    # robust_nonrigid_alignment's first solve (the one test_final_cost.py's 66.784683 is
+    # taken from): the source mesh, its tetrahedra and the first target in directory order
+    sv, sf = formats.read_obj(os.path.join(data, "squat_source.obj"))
+    first = sorted(os.listdir(os.path.join(data, "squat_target")))[0]
+    tv, tf = formats.read_obj(os.path.join(data, "squat_target", first))
+    te = formats.read_ele(os.path.join(data, "squat_tetmesh.ele"))
+    out = os.path.join(here, "squat_first.npz")
+    np.savez_compressed(out, src_verts=sv, src_faces=sf, tets=te, tgt_verts=tv, tgt_faces=tf, target=first)
+    print(out, sv.shape, te.shape, first)
 
 
 if __name__ == "__main__":

@@ -108,3 +108,35 @@ def test_generated_example_known_answers_materialized(name, mode):
     s.set_solver_params({"nIterations": 1, "lIterations": 1})
     s.solve(problems.problem_params(name, w, dev))
     assert rel(s.cost(), REFERENCE_FINAL_COST[name]) < REFERENCE_RTOL, (s.cost(), REFERENCE_FINAL_COST[name])
+
+
+ROBUST_REFERENCE = 66.784683   # examples/test_final_cost.py:64 ("CUDA cost of first!!! solve"; broken, :41-43)
+
+
+def _robust_first(arg_order):
+    z = np.load(os.path.join(ROOT, "tests", "golden", "squat_first.npz"))
+    w = problems.robust_nonrigid_alignment(z["src_verts"], z["src_faces"], z["tets"], z["tgt_verts"], z["tgt_faces"],
+                                           arg_order=arg_order)
+    prm = [w["w_fitSqrt"], w["w_regSqrt"]] + [dev(w[k]) for k in ("Offset", "Angle", "RobustWeights", "UrShape",
+                                                                  "Constraints", "ConstraintNormals")] + \
+          [None, dev(w["v0"]), dev(w["v1"])]
+    s = OptSolver([w["N"], w["E"]], os.path.join(ROOT, "energies", "robust_nonrigid_alignment.t"), "LMGPU")
+    assert s.family() == "generic"
+    s.set_solver_params({"nIterations": 1, "lIterations": 1, "function_tolerance": 1e-7})
+    s.solve(prm)
+    return s.cost()
+
+
+def test_robust_nonrigid_alignment_first_solve_brackets_the_reference():
+    """robust_nonrigid_alignment, flagged broken by the reference's own test, is pinned only
+    loosely: its first solve's cost depends on harness details C++ leaves to the platform
+    — the order make_float3(normal(), normal(), normal()) evaluates its arguments in, and
+    libstdc++'s distribution algorithms — through the 5 % spurious correspondences, which
+    move it by several percent (tools/robust_first_solve.py on the first target in sorted
+    directory order: 69.23 evaluating right to left, as GCC does on x86-64, 65.71 left to
+    right; GCC 11's uniform_int 69.36 / 65.85; the other targets further off). The draws
+    themselves match this image's libstdc++ bit for bit (test_harness_rng.py). The
+    reference's 66.784683 lies between the two argument orders' costs, each within 4 %."""
+    ltr, rtl = _robust_first("ltr"), _robust_first("rtl")
+    assert ltr < ROBUST_REFERENCE < rtl, (ltr, rtl)
+    assert rel(ltr, ROBUST_REFERENCE) < 0.04 and rel(rtl, ROBUST_REFERENCE) < 0.04, (ltr, rtl)
