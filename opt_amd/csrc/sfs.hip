@@ -480,12 +480,14 @@ constexpr int kStripOut = 60;
 template <typename T>
 struct SRow {   // raw loads of row r (+ flags / LM diagonal of the output row r-2)
     T p, g0, g1, g2, dg, bi;
+    T rr, w;        // SUMS: r and the preconditioner of the output row r-2
     int mr, mc, v, f;
 };
 // JTF: p is X, bi = B_I(r), dg = D_i and f = [D_i > 0] of the output row r-2.
-template <typename T, bool JTF = false>
+template <typename T, bool JTF = false, bool SUMS = false>
 __device__ __forceinline__ SRow<T> strip_row(const Args<T>& a, const T* __restrict__ p, const T* __restrict__ dadd,
-                                             int gx, int r) {
+                                             int gx, int r, const T* __restrict__ rv = nullptr,
+                                             const T* __restrict__ wv = nullptr) {
     const Domain& d = a.dom;
     SRow<T> s;
     const bool in = inside(d, gx, r);
@@ -509,16 +511,24 @@ __device__ __forceinline__ SRow<T> strip_row(const Args<T>& a, const T* __restri
         s.f = own ? a.flags[ok] : 0;
         s.dg = (own && dadd) ? dadd[ok] : (T)0;
     }
+    if (SUMS) {
+        s.rr = own ? rv[ok] : (T)0;
+        s.w = (own && wv) ? wv[ok] : (T)1;
+    }
     return s;
 }
 // JTF = true: r = -J^T F, diag(J^T J) and the flag byte (evalJTF, o.t:2870-2913) by the
 // same chain with D replaced by B_I, p by X and the fit term by w_p (X - D_i), as
 // sfs_tiles<T, true> does (same operations in the same order); Ap is r, dadd is diag.
-template <typename T, bool JTF = false>
+// SUMS (the generic driver's fused PCGStep2+3, Op::apply_sums): instead of p.Ap alone,
+// sc[rs.out + 0..3] = {p.Ap, r.W Ap, Ap.W Ap, r.W r}, products in T summed in fp64 per
+// lane, W = the preconditioner wv (null: 1), r = rv of the output pixels.
+template <typename T, bool JTF = false, bool SUMS = false>
 __global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
                                                     const T* __restrict__ dadd, const int* stop, ReduceSlot rs,
                                                     int nstrips, int rows, int bb0 = 0, int bn0 = 1 << 30,
-                                                    int bb1 = 0) {
+                                                    int bb1 = 0, const T* __restrict__ rv = nullptr,
+                                                    const T* __restrict__ wv = nullptr) {
     if (stop && *stop) return;
     const Domain& d = a.dom;
     const int lane = threadIdx.x & (kWave - 1);
@@ -533,6 +543,7 @@ __global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restri
     const T wg = a.wg, ws = a.ws;
     const T qxc = ((T)gx - a.ux) / a.fx, qxl = ((T)(gx - 1) - a.ux) / a.fx, qxr = ((T)(gx + 1) - a.ux) / a.fx;
     T dot = 0;
+    double papd = 0, rapd = 0, apapd = 0, rwrd = 0;
     if (y0 < y1) {
         T p_m2 = 0, p_m1 = 0, D_m1 = 0, Vh_m1 = 0, Vv_m2 = 0, W_k = 0;
         T g0_m2 = 0, g1_m2 = 0, g0_m1 = 0, g1_m1 = 0, g2_m1 = 0, qy_m1 = 0, qy_m2 = 0;
@@ -540,10 +551,10 @@ __global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restri
         int mc_m1 = 0, v_m1 = 0;
         // JTF's diagonal: masks / valid of rows k-1 (m3), k (m2), k+1 (m1)
         int mr_m2 = 0, mc_m2 = 0, mc_m3 = 0, v_m2 = 0, v_m3 = 0, mr_m1 = 0;
-        SRow<T> nx = strip_row<T, JTF>(a, p, dadd, gx, y0 - 2);
+        SRow<T> nx = strip_row<T, JTF, SUMS>(a, p, dadd, gx, y0 - 2, rv, wv);
         for (int r = y0 - 2; r <= y1 + 1; ++r) {
             const SRow<T> cur = nx;
-            if (r + 1 <= y1 + 1) nx = strip_row<T, JTF>(a, p, dadd, gx, r + 1);
+            if (r + 1 <= y1 + 1) nx = strip_row<T, JTF, SUMS>(a, p, dadd, gx, r + 1, rv, wv);
             const T qy = ((T)r - a.uy) / a.fy;
             // row r: D (J^T F: the shading residual values B_I), V_h
             const T D = JTF ? cur.bi : cur.g0 * cur.p + cur.g1 * from_left(cur.p, (T)0) + cur.g2 * p_m1;
@@ -604,8 +615,15 @@ __global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restri
                     acc = fit + shade + ws * (qxc * l[0] + qy_m2 * l[1] + l[2]);
                     if (!JTF) {
                         if (dadd) acc += cur.dg * pk;
-                        dot += pk * acc;
+                        if (SUMS) papd += (double)(pk * acc);
+                        else dot += pk * acc;
                     }
+                }
+                if (SUMS) {   // inactive pixels: Ap = 0 (r is 0 there too); T products, fp64 sums
+                    const T wr_ = cur.w * cur.rr;
+                    rapd += (double)(wr_ * acc);
+                    apapd += (double)(cur.w * acc * acc);
+                    rwrd += (double)(wr_ * cur.rr);
                 }
                 if constexpr (JTF) {
                     Ap[i] = -acc;   // r
@@ -627,8 +645,13 @@ __global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restri
         }
     }
     if (JTF) return;
-    double v[1] = {(double)dot};
-    block_reduce_publish<1>(v, rs, gb);
+    if constexpr (SUMS) {
+        double v[4] = {papd, rapd, apapd, rwrd};
+        block_reduce_publish<4>(v, rs, gb);
+    } else {
+        double v[1] = {(double)dot};
+        block_reduce_publish<1>(v, rs, gb);
+    }
 }
 
 // ------------------------------------------------------- cost / model cost
@@ -925,7 +948,8 @@ public:
             const int nrb = (dom_.y_hi - dom_.y_lo + strip_rows_ - 1) / strip_rows_;
             const int blocks = (nstrips * nrb + kBlock / kWave - 1) / (kBlock / kWave);
             hipLaunchKernelGGL((sfs::sfs_strip<T, true>), dim3(blocks), dim3(kBlock), 0, s, a_, (const T*)a_.X, r,
-                               (const T*)diag, (const int*)nullptr, ReduceSlot{}, nstrips, strip_rows_, 0, 1 << 30, 0);
+                               (const T*)diag, (const int*)nullptr, ReduceSlot{}, nstrips, strip_rows_, 0, 1 << 30, 0,
+                               (const T*)nullptr, (const T*)nullptr);
         } else {
             hipLaunchKernelGGL((sfs::sfs_tiles<T, true>), tile_grid(), dim3(kBlock), 0, s, a_, (const T*)a_.X, r, diag,
                                (const T*)nullptr, (const int*)nullptr, ReduceSlot{});
@@ -943,7 +967,7 @@ public:
         split_ranges(&i0, &i1, &blocks);
         rs.nblocks = blocks;
         hipExtLaunchKernelGGL((sfs::sfs_strip<T>), dim3(blocks), dim3(kBlock), 0, s, e0, e1, 0, a_, p, Ap, dadd,
-                              stop, rs, nstrips, strip_rows_, 0, 1 << 30, 0);
+                              stop, rs, nstrips, strip_rows_, 0, 1 << 30, 0, (const T*)nullptr, (const T*)nullptr);
         OPT_HIP_CHECK(hipGetLastError());
     }
     // Row slabs: part 1 launches the blocks whose waves read no halo row (strip rows
@@ -976,7 +1000,28 @@ public:
         if (part == 2) { grid = i0 + (blocks - i1); bb0 = 0; bn0 = i0; bb1 = i1; }
         if (grid <= 0) return;
         hipLaunchKernelGGL((sfs::sfs_strip<T>), dim3(grid), dim3(kBlock), 0, s, a_, p, Ap, dadd, stop, rs, nstrips,
-                           strip_rows_, bb0, bn0, bb1);
+                           strip_rows_, bb0, bn0, bb1, (const T*)nullptr, (const T*)nullptr);
+        OPT_HIP_CHECK(hipGetLastError());
+    }
+    // The apply with the fused PCG step's four sums (StencilPlan's HasApplySums): part as
+    // apply_split; r and w (the preconditioner, null without one) of the output pixels;
+    // events attached to the launch when e0 is given.
+    void apply_sums(int part, const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, const T* r,
+                    const T* w, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+        const int nstrips = (dom_.W + sfs::kStripOut - 1) / sfs::kStripOut;
+        int i0 = 0, i1 = 0, blocks = 0;
+        split_ranges(&i0, &i1, &blocks);
+        rs.nblocks = blocks;
+        int grid = blocks, bb0 = 0, bn0 = 1 << 30, bb1 = 0;
+        if (part == 1) { grid = i1 - i0; bb0 = i0; }
+        if (part == 2) { grid = i0 + (blocks - i1); bb0 = 0; bn0 = i0; bb1 = i1; }
+        if (grid <= 0) return;
+        if (e0)
+            hipExtLaunchKernelGGL((sfs::sfs_strip<T, false, true>), dim3(grid), dim3(kBlock), 0, s, e0, e1, 0, a_, p,
+                                  Ap, dadd, stop, rs, nstrips, strip_rows_, bb0, bn0, bb1, r, w);
+        else
+            hipLaunchKernelGGL((sfs::sfs_strip<T, false, true>), dim3(grid), dim3(kBlock), 0, s, a_, p, Ap, dadd, stop,
+                               rs, nstrips, strip_rows_, bb0, bn0, bb1, r, w);
         OPT_HIP_CHECK(hipGetLastError());
     }
     void cost(ReduceSlot rs, hipStream_t s) {

@@ -222,6 +222,50 @@ __global__ __launch_bounds__(kBlock) void step3_kernel(long long n, const T* __r
     }
 }
 
+// PCGStep2 + PCGStep3 of iteration i in ONE pass: the family's apply also reduced
+// p.Ap_i, r_i.W Ap_i, Ap_i.W Ap_i and r_i.W r_i in fp64 (Op::apply_sums), so PCGStep3's
+// beta numerator comes from the exact identity
+//   r_{i+1}.W r_{i+1} = r_i.W r_i - 2 alpha r_i.W Ap_i + alpha^2 Ap_i.W Ap_i
+// (alpha = rz_i / pAp_i as the elements apply it, W = pre with UsePreconditioner, else 1:
+// PCGStep2's weighting, :705-708), and p_{i+1} = z_{i+1} + beta p_i is formed in the same
+// pass as r_{i+1}, z_{i+1} and delta += alpha p_i (PCGStep2's expressions; GN's delta too).
+// The denominator is rz_i as the classic step has it (PCGInit1's r.(pre r) at i = 0). The
+// direct rz_{i+1} (fp64 products w r r) is still reduced, for alpha_{i+1}, with LM's q
+// beside it (and the device-side zeta test on one GPU); the identity's value goes to
+// sc[id_out] for the tests. Slots: i_rz = rz_i, i_rz + 2 .. + 5 = the apply's four sums.
+template <typename T, bool FIRST, bool LM>
+__global__ __launch_bounds__(kBlock) void step23_kernel(long long n, T* __restrict__ p, const T* __restrict__ Ap,
+                                                        const T* __restrict__ pre, const T* __restrict__ b,
+                                                        T* __restrict__ r, T* __restrict__ delta,
+                                                        double* __restrict__ sc, int i_rz, int id_out, int use_pre,
+                                                        const int* stop, ReduceSlot rs, ZetaArgs z = {}) {
+    if (stopped(stop)) return;
+    const double rz = sc[i_rz];
+    const T alpha = (T)(rz / sc[i_rz + 2]);
+    const double ad = (double)alpha;
+    const double rz_id = sc[i_rz + 5] - 2.0 * ad * sc[i_rz + 3] + ad * ad * sc[i_rz + 4];
+    const T beta = (T)(rz_id / rz);
+    if (blockIdx.x == 0 && threadIdx.x == 0) sc[id_out] = rz_id;
+    double acc = 0;
+    T accq = 0;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (long long)gridDim.x * blockDim.x) {
+        const T po = p[e];
+        const T rr = r[e] - alpha * Ap[e];
+        const T d = FIRST ? alpha * po : delta[e] + alpha * po;
+        delta[e] = d;
+        r[e] = rr;
+        const T w = use_pre ? pre[e] : (T)1;
+        const T zz = use_pre ? w * rr : rr;
+        acc += (double)w * (double)rr * (double)rr;
+        if (LM) accq += (T)0.5 * (d * (rr + b[e]));
+        p[e] = zz + beta * po;
+    }
+    double v[2] = {acc, (double)accq};
+    double tot[2];
+    if (block_reduce_publish<2>(v, rs, blockIdx.x, tot) && LM && z.on) zeta_test<T>(z, tot[1]);
+}
+
 // Residual reset, LM only (:738-801): first half delta += alpha p ...
 template <typename T>
 __global__ __launch_bounds__(kBlock) void half1_kernel(long long n, const T* __restrict__ p,

@@ -110,6 +110,20 @@ struct HasApplySplit : std::false_type {};
 template <class Op>
 struct HasApplySplit<Op, std::void_t<decltype(std::declval<const Op&>().can_split())>> : std::true_type {};
 
+// Ops whose apply can also reduce the fused PCG step's sums (shape_from_shading):
+// apply_sums(part, p, Ap, dadd, stop, rs, r, w, stream, e0, e1) reduces {p.Ap, r.W Ap,
+// Ap.W Ap, r.W r} (fp64) into rs; the driver then runs PCGStep2 + PCGStep3 as ONE pass
+// (step23_kernel, beta's numerator from the identity over those sums) and, on row slabs,
+// one all-reduce per PCG iteration.
+template <class Op, class = void>
+struct HasApplySums : std::false_type {};
+template <class Op>
+struct HasApplySums<Op, std::void_t<decltype(std::declval<Op&>().apply_sums(
+                            0, (const typename Op::T*)nullptr, (typename Op::T*)nullptr, (const typename Op::T*)nullptr,
+                            (const int*)nullptr, ReduceSlot{}, (const typename Op::T*)nullptr,
+                            (const typename Op::T*)nullptr, hipStream_t{}, hipEvent_t{}, hipEvent_t{}))>>
+    : std::true_type {};
+
 // Ops that fold PCGStep3 into the first pass of their next apply (ARAP: p = z + beta p
 // per vertex, then K of the new p): step3_fused(pre, r, p, sc, i_num, i_den, use_pre,
 // stop, s) replaces step3_kernel; apply_prepared(...apply's arguments) is the apply
@@ -215,7 +229,7 @@ public:
         op_->bind(params, stream_);
         exchange_unknowns();
         const int Lit = std::max(0, sp_.lIterations);
-        red_.ensure(std::max(op_->stencil_blocks(), 4096), 2, kScBase + 3 * (Lit + 2));
+        red_.ensure(std::max(op_->stencil_blocks(), 4096), 4, kScBase + kSlots * (Lit + 2));
         OPT_HIP_CHECK(hipMemsetAsync(stop_, 0, 64, stream_));
         OPT_HIP_CHECK(hipMemsetAsync(delta_, 0, sizeof(T) * n_, stream_));   // PCGInit1: delta = 0
         const int use_pre = spec_.use_preconditioner ? 1 : 0;
@@ -267,6 +281,11 @@ public:
 
     // PCG inner loop (PCGStep1-3, :607-845) of one step; launches only, no host sync.
     void pcg_loop(int Lit, int use_pre, const int* stop) {
+        if constexpr (HasApplySums<Op>::value)
+            if (!mat_ && (fuse23_ == 1 || (fuse23_ == 2 && distributed()))) {
+                pcg_loop_fused(Lit, use_pre, stop);
+                return;
+            }
         const bool fuse3 = !distributed() && !mat_ && fuse3_on_;
         // GN with step3_kernel: the delta update rides in PCGStep3 (reads p_old anyway)
         bool d3 = !lm_ && delta3_on_;
@@ -354,6 +373,83 @@ public:
                 hipLaunchKernelGGL((zeta_kernel<T>), dim3(1), dim3(1), 0, stream_, red_.scalars, q(i + 1),
                                    red_.scalars + kScQ0, i, sp_.q_tolerance, stop_);
             OPT_HIP_CHECK(hipGetLastError());
+        }
+    }
+
+    // The PCG loop with PCGStep2 + PCGStep3 as one pass (HasApplySums, UsePreconditioner):
+    // per iteration the apply (+ its four sums) and step23_kernel; on row slabs ONE
+    // all-reduce per iteration — step23's rz / q ride in the next apply's call — and LM's
+    // zeta test on the all-reduced q before the next step23 (the apply in between is
+    // wasted when it stops: the reference would have left the loop before it). Residual-reset
+    // iterations (LM) run the classic sequence.
+    void pcg_loop_fused(int Lit, int use_pre, const int* stop) {
+        const T* w = use_pre ? pre_ : nullptr;   // PCGStep2's weighting W (1 without a preconditioner)
+        bool pending = false;   // rz(i) / q(i) of the previous step23 not all-reduced yet
+        for (int i = 0; i < Lit; ++i) {
+            const ZetaArgs z{red_.scalars + kScQ0, stop_, i, sp_.q_tolerance, (lm_ && !distributed()) ? 1 : 0};
+            bool split = false;
+            if constexpr (HasApplySplit<Op>::value)
+                split = distributed() && overlap_ && comm_->concurrent_halo() && op_->can_split();
+            const ReduceSlot rs = red_.slot(nb(), pap(i));
+            auto launch = [&](int part) {
+                hipEvent_t e0 = nullptr, e1 = nullptr;
+                const bool ev = part == 0 && timer_.mode && timer_.ext_pair(Op::kApplyName, &e0, &e1);
+                if (!ev) tbegin(Op::kApplyName);
+                op_->apply_sums(part, p_, Ap_, lm_ ? CtC_ : nullptr, stop, rs, r_, w, stream_, e0, e1);
+                if (ev) timer_.ext_record(Op::kApplyName, e0, e1);
+                else tend();
+            };
+            if (split) {
+                halo_mark();
+                launch(1);
+                halo_begin(comm_, vec_planes(p_), dom_, op_->halo());
+                halo_join();
+                launch(2);
+            } else {
+                exchange_vec(p_);
+                launch(0);
+            }
+            if (distributed()) {
+                allreduce(pending ? rz(i) : pap(i), pending ? 6 : 4);
+                if (pending && lm_)   // the previous iteration's exit test on the global q
+                    hipLaunchKernelGGL((zeta_kernel<T>), dim3(1), dim3(1), 0, stream_, red_.scalars, q(i),
+                                       red_.scalars + kScQ0, i - 1, sp_.q_tolerance, stop_);
+                pending = false;
+            }
+            const bool reset = lm_ && ((i + 1) % std::max(1, sp_.residual_reset_period)) == 0;
+            if (reset) {
+                hipLaunchKernelGGL((half1_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)p_, delta_,
+                                   red_.scalars, rz(i), pap(i), stop);
+                exchange_vec(delta_);
+                op_->apply(delta_, Adelta_, CtC_, stop, red_.slot(nb(), kScTmp), stream_);
+                hipLaunchKernelGGL((half2_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)Adelta_,
+                                   (const T*)b_, (const T*)pre_, (const T*)delta_, r_, use_pre, stop,
+                                   red_.slot(fg(), rz(i + 1)), z);
+                allreduce(rz(i + 1), 2);
+                tbegin("step3");
+                hipLaunchKernelGGL((step3_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)pre_,
+                                   (const T*)r_, p_, red_.scalars, rz(i + 1), rz(i), use_pre, stop);
+                tend();
+                if (!z.on)
+                    hipLaunchKernelGGL((zeta_kernel<T>), dim3(1), dim3(1), 0, stream_, red_.scalars, q(i + 1),
+                                       red_.scalars + kScQ0, i, sp_.q_tolerance, stop_);
+                OPT_HIP_CHECK(hipGetLastError());
+                continue;
+            }
+            tbegin("step23");
+            const ReduceSlot rs2 = red_.slot(fg(), rz(i + 1));
+#define S23(F, L)                                                                                              \
+    hipLaunchKernelGGL((step23_kernel<T, F, L>), dim3(fg()), dim3(kBlock), 0, stream_, n_, p_, (const T*)Ap_,      \
+                       (const T*)pre_, (const T*)b_, r_, delta_, red_.scalars, rz(i), rz(i + 1) + 6, use_pre, stop, rs2, \
+                       z)
+            if (i == 0 && lm_) S23(true, true);
+            else if (lm_) S23(false, true);
+            else if (i == 0) S23(true, false);
+            else S23(false, false);
+#undef S23
+            OPT_HIP_CHECK(hipGetLastError());
+            tend();
+            if (distributed()) pending = true;
         }
     }
 
@@ -571,9 +667,12 @@ private:
     static constexpr int kScCost = 1, kScModel = 0, kScTmp = 2, kScQ0 = 3, kScBase = 8;
     // cost sits right after model cost so one 16-byte copy (and one all-reduce) takes both
     // per PCG iteration: rz[i], q[i] (written together by step2 as a pair), pAp[i]
-    int rz(int i) const { return kScBase + 3 * i; }
-    int q(int i) const { return kScBase + 3 * i + 1; }
-    int pap(int i) const { return kScBase + 3 * i + 2; }
+    // iteration i's slots: rz, q, pAp, then (fused PCG step) r.W Ap, Ap.W Ap, r.W r and
+    // step23's identity value of rz
+    static constexpr int kSlots = 7;
+    int rz(int i) const { return kScBase + kSlots * i; }
+    int q(int i) const { return kScBase + kSlots * i + 1; }
+    int pap(int i) const { return kScBase + kSlots * i + 2; }
     int nb() const { return op_->stencil_blocks(); }
     int fg() const { return flat_grid(n_, 1); }
     long long pix_lo() const { return dom_.off(0, dom_.y_lo); }
@@ -735,6 +834,12 @@ private:
     const bool graph_off_ = getenv("OPT_AMD_NO_GRAPH") && atoi(getenv("OPT_AMD_NO_GRAPH"));
     const bool overlap_ = env_int("OPT_AMD_HALO_OVERLAP", 1) != 0;   // 0: blocking halo before each apply
     const bool fuse3_on_ = env_int("OPT_AMD_FUSE_STEP3", 1) != 0;
+    // Ops with apply_sums: OPT_AMD_FUSE23=0 the classic apply / step2 / step3 loop, 1 the
+    // fused loop, 2 (default) the fused loop on row slabs only. One GPU, shape_from_shading
+    // 4096^2 LM: the apply with the four sums takes 175 us against 131 (r read back, 6
+    // instead of 7 waves per SIMD), more than step3's pass saves: 3.56 vs 3.36 ms per step
+    // (tools/r03_fuse23.sh). On slabs the fused loop saves an all-reduce per iteration.
+    const int fuse23_ = env_int("OPT_AMD_FUSE23", 2);
     const bool delta3_on_ = env_int("OPT_AMD_DELTA_IN_STEP3", 1) != 0;   // 0: delta updated by step2    // 0: step3_kernel + the whole apply
     std::unique_ptr<MaterializedJacobian<T>> mat_;
     float radius_ = 1e4f, decrease_ = 2.0f;

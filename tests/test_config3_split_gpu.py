@@ -40,7 +40,11 @@ def sfs4096():
     return workloads.shape_from_shading(N, N, seed=3)
 
 
-def test_sfs_lm_4096_split_8_ways_matches_single_domain(sfs4096):
+def test_sfs_lm_4096_split_8_ways_matches_single_domain(monkeypatch, sfs4096):
+    # the same PCG loop on one domain and on the slabs: the fused PCGStep2+3 (the slabs'
+    # default; its agreement with the classic loop is test_sfs_gpu.py's
+    # test_fused_pcg_step_matches_classic)
+    monkeypatch.setenv("OPT_AMD_FUSE23", "1")
     w = sfs4096
     nit, lit = 3, 10
 

@@ -301,3 +301,38 @@ def test_precompute_strip_equals_per_pixel(monkeypatch, W, H, double):
         s.close()
     assert out["1"][0] == pytest.approx(out["0"][0], rel=1e-12 if double else 1e-6)
     np.testing.assert_allclose(out["1"][1], out["0"][1], rtol=1e-12 if double else 5e-5)
+
+
+@pytest.mark.parametrize("kind", ["LMGPU", "gaussNewtonGPU"])
+@pytest.mark.parametrize("double", [False, True])
+@pytest.mark.parametrize("W,H,lit", [(97, 61, 10), (64, 48, 4), (130, 9, 1)])
+def test_fused_pcg_step_matches_classic(monkeypatch, kind, double, W, H, lit):
+    """PCGStep2 + PCGStep3 as one pass (step23_kernel, beta's numerator from the identity
+    over the apply's fp64 sums r.W Ap, Ap.W Ap, r.W r) against the classic apply / step2 /
+    step3 loop (OPT_AMD_FUSE23=0): energy trajectories within 1e-5 (fp32: the classic loop
+    sums p.Ap and r.z per thread in fp32, the fused one in fp64 — 1.2e-6 measured after
+    three GN steps of 10 PCG iterations) / 1e-11 (fp64);
+    and in every fused iteration the identity agrees with the direct rz (fp64 sums of the
+    same r) to 1e-7 relative (fp32 rounds r_{i+1} once more than the identity sees)."""
+    import torch
+
+    w = synthetic(W, H, seed=2 * W + H)
+    out = {}
+    for f in ("0", "1"):
+        monkeypatch.setenv("OPT_AMD_FUSE23", f)
+        s = OptSolver([W, H], ENERGY, kind, double_precision=double)
+        s.set_solver_params({"nIterations": 3, "lIterations": lit})
+        prm = params(w)
+        if double:
+            prm[16] = prm[16].double()
+        out[f] = (np.array(s.profiled_solve(prm)), to_np(prm[16]).astype(np.float64), s.scalars(8 + 7 * (lit + 2)))
+        s.close()
+    tol = 1e-11 if double else 1e-5
+    np.testing.assert_allclose(out["1"][0], out["0"][0], rtol=tol)
+    assert rel_err(out["1"][1], out["0"][1]) < (1e-10 if double else 1e-4)
+    sc = np.array(out["1"][2])
+    for i in range(1, lit):
+        rz, rz_id = sc[8 + 7 * i], sc[8 + 7 * i + 6]
+        if rz == 0:
+            continue
+        assert abs(rz_id - rz) <= (1e-12 if double else 1e-7) * abs(rz) + 1e-300, (i, rz, rz_id)
