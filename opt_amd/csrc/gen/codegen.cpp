@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <functional>
 #include <map>
 #include <set>
@@ -60,11 +61,28 @@ const char* elem_type(const std::string& e, bool unknown) {
 // the cached values are the bits the kernels would compute.
 using CacheMap = std::map<std::tuple<int, int, int>, int>;
 const CacheMap* g_cache = nullptr;
+// Graph energies: the same values for slot reads, packed per vertex into one record image
+// (channel k of the record = key k) — a gather pass evaluates every incident edge, so the
+// other slot's sin / cos would be re-evaluated once per edge (ARAP's angles: three
+// sincos per edge in the reverse pass); the record is one 32-byte line per vertex.
+struct GraphCache {
+    int img = -1, width = 0;
+    std::map<std::tuple<int, int, int>, int> ch;
+};
+const GraphCache* g_gcache = nullptr;
 
+bool transcendental(const Node& n) {
+    return n.op == Op::Sin || n.op == Op::Cos || n.op == Op::Exp || n.op == Op::Log || n.op == Op::Sqrt;
+}
 bool cacheable(const Pool& P, const Node& n) {
-    if (n.op != Op::Sin && n.op != Op::Cos && n.op != Op::Exp && n.op != Op::Log && n.op != Op::Sqrt) return false;
+    if (!transcendental(n)) return false;
     const Node c = P.at(n.a);
     return c.op == Op::Read && c.slot < 0;
+}
+bool cacheable_slot(const Pool& P, const Node& n) {
+    if (!transcendental(n)) return false;
+    const Node c = P.at(n.a);
+    return c.op == Op::Read && c.slot >= 0;
 }
 
 class Body {
@@ -99,6 +117,34 @@ public:
         auto it = done_.find(id);
         if (it != done_.end()) return it->second;
         const Node n = P_.at(id);
+        if (g_gcache && cacheable_slot(P_, n)) {
+            const Node c = P_.at(n.a);
+            auto ci = g_gcache->ch.find(std::make_tuple((int)n.op, c.i, c.ch));
+            if (ci != g_gcache->ch.end()) {
+                const int W = g_gcache->width, k = ci->second;
+                const std::string rec = "((const T*)a.img[" + std::to_string(g_gcache->img) + "]) + (long long)v" +
+                                        std::to_string(c.slot) + " * " + std::to_string(W);
+                std::string name;
+                // the slot's whole record once as 16-byte vectors (per-edge kernels: gen_cost
+                // 51.7 -> 41.5 us on 1M-vertex ARAP); the vertex gathers read the fields they use
+                // (their edge loops: 83.8 us scalar, 90.0 us as records)
+                if (W >= 4 && !pre_) {
+                    const std::string kr = "kr" + std::to_string(c.slot);
+                    if (!rec_.count(c.slot)) {
+                        for (int g = 0; g < W; g += 4)
+                            out(id) << "        const OptV4 " << kr << "_" << g / 4 << " = *(const OptV4*)(" << rec << " + "
+                                    << g << ");\n";
+                        rec_.insert(c.slot);
+                    }
+                    name = kr + "_" + std::to_string(k / 4) + "." + "xyzw"[k % 4];
+                } else {
+                    name = "k" + std::to_string(id);
+                    out(id) << "        const T " << name << " = (" << rec << ")[" << k << "];\n";
+                }
+                done_[id] = name;
+                return name;
+            }
+        }
         if (g_cache && cacheable(P_, n)) {
             const Node c = P_.at(n.a);
             auto ci = g_cache->find(std::make_tuple((int)n.op, c.i, c.ch));
@@ -235,7 +281,7 @@ private:
     int nd_;
     const std::vector<int>& uslot_;
     std::map<int, std::string> done_;
-    std::set<int> sincos_;
+    std::set<int> sincos_, rec_;
     std::map<std::string, std::string> vdone_;
     std::ostringstream* pre_ = nullptr;
     int self_ = -1, graph_ = -1;
@@ -267,6 +313,7 @@ GenSource generate(GModel& m, bool dbl) {
     std::ostringstream o;
     o << "// generated by opt_amd's energy front end (gen/codegen.cpp)\n";
     o << "typedef " << (dbl ? "double" : "float") << " T;\n";
+    o << "typedef T OptV4 __attribute__((ext_vector_type(4)));\n";
     o << OPTAMD_STR(OPTAMD_GENARGS_BODY) << "\n";
     o << kReduceDevSrc << "\n";
     o << "#define OPT_COORDS const int W = a.dims[0], H = a.dims[1], D = a.dims[2]; (void)D;\n";
@@ -409,6 +456,64 @@ GenSource generate(GModel& m, bool dbl) {
         }
     }
     g_cache = cache.empty() ? nullptr : &cache;
+
+    // graph record cache (see g_gcache): transcendentals of slot reads of arrays on the
+    // unknowns' domain, one record per vertex, filled by one more precompute kernel
+    GraphCache gcache;
+    {
+        const char* ev = getenv("OPT_AMD_GEN_GRAPH_CACHE");
+        const bool on = !ev || atoi(ev) != 0;
+        const int uimg = unk.empty() ? -1 : unk[0];
+        std::vector<std::pair<std::tuple<int, int, int>, int>> want;
+        if (on && uimg >= 0 && m.images.size() < 16)
+            for (auto& r : m.residuals) {
+                if (r.graph < 0) continue;
+                P.visit(r.expr, [&](int, const Node& n) {
+                    if (!cacheable_slot(P, n)) return;
+                    const Node c = P.at(n.a);
+                    if (m.images[c.i].dims != m.images[uimg].dims) return;
+                    auto key = std::make_tuple((int)n.op, c.i, c.ch);
+                    for (auto& w : want)
+                        if (w.first == key) return;
+                    const int z0[3] = {0, 0, 0};
+                    want.push_back({key, P.un(n.op, P.read(c.i, c.ch, z0))});
+                });
+            }
+        if (!want.empty()) {
+            int width = 1;
+            while (width < (int)want.size()) width *= 2;   // aligned records
+            GImage ci;
+            ci.name = "graph_cache";
+            ci.dims = m.images[uimg].dims;
+            ci.channels = width;
+            ci.internal = ci.tvalued = true;
+            m.images.push_back(ci);
+            gcache.img = (int)m.images.size() - 1;
+            gcache.width = width;
+            o << "extern \"C\" __global__ __launch_bounds__(256) void gen_precompute_" << gs.n_precompute << "(GenArgs a) {\n"
+                 "    OPT_COORDS\n"
+                 "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
+              << coords;
+            Body b(m, o, nd, uslot);
+            std::vector<std::string> val(width, "(T)0");
+            for (size_t k = 0; k < want.size(); ++k) {
+                gcache.ch[want[k].first] = (int)k;
+                val[k] = b.v(want[k].second);
+            }
+            // whole 16-byte vectors per record (width >= 4), scalar stores below that
+            const std::string base = "((T*)a.img[" + std::to_string(gcache.img) + "]) + lin * " + std::to_string(width);
+            if (width >= 4) {
+                for (int g = 0; g < width; g += 4)
+                    b.line("*(OptV4*)(" + base + " + " + std::to_string(g) + ") = OptV4{" + val[g] + ", " + val[g + 1] + ", " +
+                           val[g + 2] + ", " + val[g + 3] + "};");
+            } else {
+                for (int k = 0; k < width; ++k) b.line("(" + base + ")[" + std::to_string(k) + "] = " + val[k] + ";");
+            }
+            o << "    }\n}\n";
+            ++gs.n_precompute;
+        }
+    }
+    g_gcache = gcache.img < 0 ? nullptr : &gcache;
 
     // ---------------------------------------------------------------- gen_jtf
     {
@@ -1281,6 +1386,7 @@ GenSource generate(GModel& m, bool dbl) {
     }
     (void)zero3;
     g_cache = nullptr;
+    g_gcache = nullptr;
     char note[128];
     snprintf(note, sizeof(note), "// apply: %s (%.2f residual instances per centred residual)\n",
              gs.has_strip ? "gen_apply_strip" : gs.prefer_tiled ? "gen_apply_tiled" : "gen_apply",
