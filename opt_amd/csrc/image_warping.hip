@@ -1275,6 +1275,14 @@ __global__ __launch_bounds__(kBlock) void iw_flags(Args<T> a) {
 }
 
 // --------------------------------------------------------------- update kernel
+// delta_L of one element: (the deferred alpha_{L-2} p_{L-2} term first, E2), then
+// alpha_{L-1} p_{L-1}; every term an explicit fma onto the pending delta (shared by
+// iw_update and iw_update_cost, so both form the same bits)
+template <typename T, bool HAS_DELTA, bool E2>
+__device__ __forceinline__ T upd_delta(T alpha, T q, T alpha2, T q2, T d) {
+    if (E2) d = HAS_DELTA ? fmad(alpha2, q2, d) : alpha2 * q2;
+    return (HAS_DELTA || E2) ? fmad(alpha, q, d) : alpha * q;
+}
 // X += delta_L on active pixels of the owned rows (PCGLinearUpdate, :854-859), where
 // delta_L = delta_{L-1} + alpha_{L-1} p_{L-1} is the last PCG iteration's delta update
 // (HAS_DELTA = false when lIterations == 1: delta_0 = 0).
@@ -1294,23 +1302,19 @@ __global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O
         const Vec2<T> o = reinterpret_cast<const Vec2<T>*>(O)[i];
         const Vec2<T> pp = reinterpret_cast<const Vec2<T>*>(p)[i];
         const T t = A[i], pt = p[2 * N + i];
-        Vec2<T> d;
-        T dt;
+        Vec2<T> d{}, q2{};
+        T dt = 0, q2t = 0;
         if (HAS_DELTA) {
             d = reinterpret_cast<const Vec2<T>*>(delta)[i];
             dt = delta[2 * N + i];
         }
-        if (E2) {   // the deferred alpha_{L-2} p_{L-2} term first
-            const Vec2<T> q2 = reinterpret_cast<const Vec2<T>*>(p2)[i];
-            const T q2t = p2[2 * N + i];
-            if (HAS_DELTA) { d.x = fmad(alpha2, q2.x, d.x); d.y = fmad(alpha2, q2.y, d.y); dt = fmad(alpha2, q2t, dt); }
-            else { d.x = alpha2 * q2.x; d.y = alpha2 * q2.y; dt = alpha2 * q2t; }
+        if (E2) {
+            q2 = reinterpret_cast<const Vec2<T>*>(p2)[i];
+            q2t = p2[2 * N + i];
         }
-        if (HAS_DELTA || E2) {
-            d.x = fmad(alpha, pp.x, d.x); d.y = fmad(alpha, pp.y, d.y); dt = fmad(alpha, pt, dt);
-        } else {
-            d.x = alpha * pp.x; d.y = alpha * pp.y; dt = alpha * pt;
-        }
+        d.x = upd_delta<T, HAS_DELTA, E2>(alpha, pp.x, alpha2, q2.x, d.x);
+        d.y = upd_delta<T, HAS_DELTA, E2>(alpha, pp.y, alpha2, q2.y, d.y);
+        dt = upd_delta<T, HAS_DELTA, E2>(alpha, pt, alpha2, q2t, dt);
         if (f & 1) {
             reinterpret_cast<Vec2<T>*>(O)[i] = Vec2<T>{o.x + d.x, o.y + d.y};
             A[i] = t + dt;
@@ -1318,6 +1322,136 @@ __global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O
     }
 }
 
+// ------------------------------------------------- update + cost in one strip pass
+// iw_update followed by iw_cost (PCGLinearUpdate, then computeCost at the updated
+// unknowns, solverGPUGaussNewton.t:854-859, :2245) as one pass over the cost's strips:
+// each row is loaded once with delta / p_{L-1} / p_{L-2}, updated in registers (the same
+// upd_delta fmas and o + d as iw_update) and the cost is evaluated from the updated rows
+// (the same expressions and order as iw_cost, the same tiles and reduction slots, so
+// the cost is bitwise iw_cost's). Neighbouring waves read a wave's first / last row and
+// its strip's outer columns (halo rows, edge records) before or after it updates them:
+// those pixels' new Offsets go to `ob` and iw_update_fixup copies them after the pass;
+// every other Offset and every Angle (nobody else reads a pixel's angle) is written in
+// place. O / A alias a.O / a.A: no __restrict__ on them.
+#ifndef IW_UC_DEPTH
+#define IW_UC_DEPTH 1   // rows in flight beyond y + 1
+#endif
+template <typename T>
+struct URaw {
+    VRaw<T> v;
+    Vec2<T> d, q, q2, ed, eq, eq2;
+    T dt, qt, q2t;
+};
+template <typename T, bool HAS_DELTA, bool E2>
+__global__ __launch_bounds__(kBlock) void iw_update_cost(Args<T> a, T* O, T* A, const T* __restrict__ delta,
+                                                         const T* __restrict__ p, const double* __restrict__ sc,
+                                                         int ia_num, int ia_den, const T* __restrict__ p2,
+                                                         int ia2_num, int ia2_den, T* __restrict__ ob,
+                                                         ReduceSlot rs) {
+    const WaveGeom g = geom(a);
+    const long long N = a.dom.npix_mem();
+    const T alpha = (T)(sc[ia_num] / sc[ia_den]);
+    const T alpha2 = E2 ? (T)(sc[ia2_num] / sc[ia2_den]) : (T)0;
+    const T wr = a.wr, wf = a.wf;
+    auto raw = [&](int y) {
+        URaw<T> q;
+        q.v = raw_vrow<T, false>(a, g, y);
+        const long long i = q.v.in ? a.dom.off(g.x, y) : 0;
+        q.q = reinterpret_cast<const Vec2<T>*>(p)[i];
+        q.qt = p[2 * N + i];
+        if (HAS_DELTA) { q.d = reinterpret_cast<const Vec2<T>*>(delta)[i]; q.dt = delta[2 * N + i]; }
+        if (E2) { q.q2 = reinterpret_cast<const Vec2<T>*>(p2)[i]; q.q2t = p2[2 * N + i]; }
+        if (g.edge_lane) {
+            const long long e = q.v.ein ? a.dom.off(g.ex, y) : 0;
+            q.eq = reinterpret_cast<const Vec2<T>*>(p)[e];
+            if (HAS_DELTA) q.ed = reinterpret_cast<const Vec2<T>*>(delta)[e];
+            if (E2) q.eq2 = reinterpret_cast<const Vec2<T>*>(p2)[e];
+        }
+        return q;
+    };
+    auto fin = [&](URaw<T> q) {
+        if (!HAS_DELTA) { q.d = Vec2<T>{0, 0}; q.dt = 0; q.ed = Vec2<T>{0, 0}; }
+        if (!E2) { q.q2 = Vec2<T>{0, 0}; q.q2t = 0; q.eq2 = Vec2<T>{0, 0}; }
+        if (q.v.in && q.v.m == 0.f) {   // flags bit 0: inside and Mask == 0
+            q.v.o.x = q.v.o.x + upd_delta<T, HAS_DELTA, E2>(alpha, q.q.x, alpha2, q.q2.x, q.d.x);
+            q.v.o.y = q.v.o.y + upd_delta<T, HAS_DELTA, E2>(alpha, q.q.y, alpha2, q.q2.y, q.d.y);
+            q.v.t = q.v.t + upd_delta<T, HAS_DELTA, E2>(alpha, q.qt, alpha2, q.q2t, q.dt);
+        }
+        if (g.edge_lane && q.v.ein && q.v.em == 0.f) {
+            q.v.eo.x = q.v.eo.x + upd_delta<T, HAS_DELTA, E2>(alpha, q.eq.x, alpha2, q.eq2.x, q.ed.x);
+            q.v.eo.y = q.v.eo.y + upd_delta<T, HAS_DELTA, E2>(alpha, q.eq.y, alpha2, q.eq2.y, q.ed.y);
+        }
+        return finish_vrow<T, false>(q.v);
+    };
+    T acc = 0;
+    if (g.y0 < g.y1) {
+        VRow<T> up = fin(raw(g.y0 - 1)), cur = fin(raw(g.y0)), dn = fin(raw(g.y0 + 1));
+#if IW_UC_DEPTH == 2
+        URaw<T> n1 = raw(g.y0 + 2);
+#endif
+        for (int y = g.y0; y < g.y1; ++y) {
+#if IW_UC_DEPTH == 2
+            const URaw<T> nx = n1;
+            n1 = raw(y + 3);
+#else
+            const URaw<T> nx = raw(y + 2);
+#endif
+            if (g.out_lane && y < a.dom.H) {
+                // shared pixels: parked whether active or not (the unchanged Offset then),
+                // so the fix-up copies without looking at the flags
+                const long long k = a.dom.off(g.x, y);
+                const bool shared = y == g.y0 || y == g.y1 - 1 || g.edge_lane;
+                if (shared) reinterpret_cast<Vec2<T>*>(ob)[k] = Vec2<T>{cur.ox, cur.oy};
+                else if (cur.act) reinterpret_cast<Vec2<T>*>(O)[k] = Vec2<T>{cur.ox, cur.oy};
+                if (cur.act) A[k] = cur.t;
+            }
+            const T lox = from_left(cur.ox, cur.eox), loy = from_left(cur.oy, cur.eoy);
+            const T rox = from_right(cur.ox, cur.eox), roy = from_right(cur.oy, cur.eoy);
+            const float lux = from_left(cur.ux, cur.eux), luy = from_left(cur.uy, cur.euy);
+            const float rux = from_right(cur.ux, cur.eux), ruy = from_right(cur.uy, cur.euy);
+            const int lact = from_left_i(cur.act, cur.eact), ract = from_right_i(cur.act, cur.eact);
+            T ex, ey, ax, ay, sum = 0;
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, rox, roy, rux, ruy,
+                  cur.act && ract, wr, ex, ey, ax, ay);
+            sum += ex * ex + ey * ey;
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, lox, loy, lux, luy,
+                  cur.act && lact, wr, ex, ey, ax, ay);
+            sum += ex * ex + ey * ey;
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, dn.ox, dn.oy, dn.ux, dn.uy,
+                  cur.act && dn.act, wr, ex, ey, ax, ay);
+            sum += ex * ex + ey * ey;
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, up.ox, up.oy, up.ux, up.uy,
+                  cur.act && up.act, wr, ex, ey, ax, ay);
+            sum += ex * ex + ey * ey;
+            if (cur.fit) {
+                const T fx = wf * (cur.ox - (T)cur.cx), fy = wf * (cur.oy - (T)cur.cy);
+                sum += fx * fx + fy * fy;
+            }
+            if (g.out_lane && cur.act) acc += (T)0.5 * sum;
+            up = cur; cur = dn;
+            dn = fin(nx);
+        }
+    }
+    double v[1] = {(double)acc};
+    block_reduce_publish<1>(v, rs, blockIdx.x);
+}
+// The Offsets iw_update_cost parked in `ob`: each wave's first and last row and its
+// strip's outer two columns (inactive pixels hold their unchanged value).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void iw_update_fixup(Args<T> a, T* __restrict__ O, const T* __restrict__ ob) {
+    const WaveGeom g = geom(a);
+    if (g.y0 >= g.y1) return;
+    auto copy = [&](int x, int y) {
+        if (x >= a.dom.W || !present(a.dom, x, y)) return;
+        const long long k = a.dom.off(x, y);
+        reinterpret_cast<Vec2<T>*>(O)[k] = reinterpret_cast<const Vec2<T>*>(ob)[k];
+    };
+    copy(g.x, g.y0);
+    if (g.y1 - 1 > g.y0) copy(g.x, g.y1 - 1);
+    const int x0 = g.x - g.lane;
+    for (int j = g.lane; j < 2 * (g.y1 - g.y0 - 2); j += kWave)
+        copy(x0 + ((j & 1) ? kWave - 1 : 0), g.y0 + 1 + (j >> 1));
+}
 
 // ---------------------------------------------------- materialized Jacobian
 // saveJToCRS (solverGPUGaussNewton.t:1004-1022) with generateDumpJ (:385-442): every
@@ -1592,12 +1726,41 @@ public:
             }
         }
         // PCGLinearUpdate (with the last delta += alpha p) + cost
+        bool cost_done = false;
         if (L > 0 && defer) {
             // pending: p_{L-1}, and p_{L-2} too when L-1 is odd (the even iterations fold pairs)
             const int ub = flat_grid(dom_.npix_mem(), 1);
             const T* pl = pb[(L - 1) % 3];
             const T* pl2 = L >= 2 ? pb[(L - 2) % 3] : nullptr;
             const bool e2 = L % 2 == 0, has = L >= 3;
+            if (fused_uc_ && !distributed()) {   // update + cost in one strip pass
+                if (!ob_) ob_ = (T*)dmalloc(sizeof(T) * 2 * dom_.npix_mem());
+                const int nb = stencil_blocks();
+                const ReduceSlot rs = red_.slot(nb, kScCost);
+                tbegin("iw_update_cost");
+                if (e2 && has)
+                    hipLaunchKernelGGL((iw::iw_update_cost<T, true, true>), dim3(nb), dim3(kBlock), 0, stream_, args(),
+                                       cur_O_, cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1), pl2,
+                                       rz(L - 2), pap(L - 2), ob_, rs);
+                else if (e2)
+                    hipLaunchKernelGGL((iw::iw_update_cost<T, false, true>), dim3(nb), dim3(kBlock), 0, stream_, args(),
+                                       cur_O_, cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1), pl2,
+                                       rz(L - 2), pap(L - 2), ob_, rs);
+                else if (has)
+                    hipLaunchKernelGGL((iw::iw_update_cost<T, true, false>), dim3(nb), dim3(kBlock), 0, stream_, args(),
+                                       cur_O_, cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1),
+                                       (const T*)nullptr, 0, 0, ob_, rs);
+                else
+                    hipLaunchKernelGGL((iw::iw_update_cost<T, false, false>), dim3(nb), dim3(kBlock), 0, stream_, args(),
+                                       cur_O_, cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1),
+                                       (const T*)nullptr, 0, 0, ob_, rs);
+                OPT_HIP_CHECK(hipGetLastError());
+                hipLaunchKernelGGL(iw::iw_update_fixup<T>, dim3(nb), dim3(kBlock), 0, stream_, args(), cur_O_,
+                                   (const T*)ob_);
+                OPT_HIP_CHECK(hipGetLastError());
+                tend();
+                cost_done = true;
+            } else {
             tbegin("iw_update");
             if (e2 && has)
                 hipLaunchKernelGGL((iw::iw_update<T, true, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
@@ -1618,6 +1781,7 @@ public:
             OPT_HIP_CHECK(hipGetLastError());
             tend();
             exchange_unknowns();
+            }
         } else if (L > 0) {
             const int ub = flat_grid(dom_.npix_mem(), 1);
             tbegin("iw_update");
@@ -1634,7 +1798,7 @@ public:
             exchange_unknowns();
         }
         // computeCost at the updated unknowns (:2245)
-        tbegin("iw_cost"); launch_cost(kScCost); tend();
+        if (!cost_done) { tbegin("iw_cost"); launch_cost(kScCost); tend(); }
         allreduce(kScCost);
         const double c = read_scalar(kScCost);
         unbind_after_step();
@@ -1718,6 +1882,10 @@ private:
         fused_init_ = env_int("OPT_AMD_IW_FUSED_INIT", 1) != 0;
         fused_res_ = env_int("OPT_AMD_IW_FUSED_RES", 1) != 0;
         defer_ = env_int("OPT_AMD_IW_DEFER", 1) != 0;
+        // measured without gain (round 3): iw_update_cost + fix-up 307 + 28 us against
+        // iw_update + iw_cost 192 + 141 us — the strip walk holds ~4.4 TB/s where the flat
+        // update streams at 6.2, so the 24 B/px it saves do not show
+        fused_uc_ = env_int("OPT_AMD_IW_FUSED_COST", 0) != 0;
         res_nt_ = env_int("OPT_AMD_IW_RES_NT", 2);
     }
     // A zeroed plan vector with kSlack spare bytes: place() may move each vector's base
@@ -1768,7 +1936,7 @@ private:
         raw_.clear();
         for (T** v : {&r_, &pre_, &p0_, &p1_, &Ap_, &delta_, &r1_, &Ap1_, &p2_}) *v = nullptr;
         flags_ = nullptr;
-        for (T** v : {&dO_, &dA_}) { dfree(*v); *v = nullptr; }
+        for (T** v : {&dO_, &dA_, &ob_}) { dfree(*v); *v = nullptr; }
         for (float** v : {&dU_, &dC_, &dM_}) { dfree(*v); *v = nullptr; }
     }
 
@@ -2025,6 +2193,8 @@ private:
     T *r_ = nullptr, *pre_ = nullptr, *p0_ = nullptr, *p1_ = nullptr, *Ap_ = nullptr, *delta_ = nullptr;
     T *r1_ = nullptr, *Ap1_ = nullptr;   // iw_apply_res ping-pongs r and Ap (neighbours read the old ones)
     T* p2_ = nullptr;                    // p_i in {p0_, p1_, p2_}[i % 3] with the deferred delta
+    T* ob_ = nullptr;                    // iw_update_cost's parked shared Offsets (2 per px, lazily)
+    bool fused_uc_ = false;              // OPT_AMD_IW_FUSED_COST=1: update + cost in one pass
     std::vector<char*> raw_;             // the plan vectors' allocations (vec_alloc)
     long long stagger_ = env_int("OPT_AMD_STAGGER", kStagger) & ~255LL;
     bool print_addr_ = env_int("OPT_AMD_PRINT_ADDR", 0) != 0;
