@@ -402,3 +402,4 @@ def test_fused_update_cost_is_bitwise_update_then_cost(monkeypatch, W, H, lit, r
         out.append((c, to_np(prm[0]), to_np(prm[1]), np.array(s.scalars(2 + 5 * (lit + 2)))))
     for a, b in zip(out[0], out[1]):
         np.testing.assert_array_equal(a, b)
+
