@@ -1277,6 +1277,8 @@ GenSource generate(GModel& m, bool dbl) {
     // the edges whose slot k is this vertex, ascending): no atomics, a fixed summation
     // order (bitwise reproducible), each edge evaluated once per incident slot. The same
     // kernel finishes the element (exclusion mask, LM diagonal, p.Ap).
+    const char* pfv = getenv("OPT_AMD_GEN_NB_PREFETCH");
+    const bool prefetch_nb = !pfv || atoi(pfv) != 0;
     auto graph_gather = [&](bool apply) {
         // accumulators per output (unknown image, channel)
         for (int k : unk)
@@ -1331,19 +1333,31 @@ GenSource generate(GModel& m, bool dbl) {
                 // { own-vertex values; for each incident edge { the other slots; the rest } }
                 // the other slots' vertices come from per-incidence-order copies (one load
                 // each instead of the edge id, then the slot array)
-                o << "        {\n        const int v" << k << " = (int)vtx;\n" << pre.str()
-                  << "        for (int q = a.goff[" << sbk << "][vtx]; q < a.goff[" << sbk << "][vtx + 1]; ++q) {\n";
+                // the next edge's other-slot vertex ids are loaded one edge ahead (prefetch_nb),
+                // so an edge's gathers do not wait behind its id load
+                std::ostringstream head, loop;
                 for (size_t s2 = 0; s2 < nslots; ++s2)
                     if (s2 != k) {
                         const std::pair<int, int> key(sbk, gs.slot_base[g] + (int)s2);
                         auto it = std::find(gs.nb_pairs.begin(), gs.nb_pairs.end(), key);
                         int idx = (int)(it - gs.nb_pairs.begin());
                         if (it == gs.nb_pairs.end()) gs.nb_pairs.push_back(key);
-                        if (idx < 32)   // GenArgs::gnb capacity; past it, through the edge id
-                            o << "        const int v" << s2 << " = a.gnb[" << idx << "][q];\n";
-                        else
-                            o << "        const int v" << s2 << " = a.slot[" << key.second << "][a.geid[" << sbk << "][q]];\n";
+                        const std::string vs = "v" + std::to_string(s2), ns = "n" + std::to_string(s2);
+                        const std::string gnb = "a.gnb[" + std::to_string(idx) + "]";
+                        if (idx < 32 && prefetch_nb) {
+                            head << "        int " << ns << " = q0 < q1 ? " << gnb << "[q0] : 0;\n";
+                            loop << "        const int " << vs << " = " << ns << ";\n"
+                                 << "        if (q + 1 < q1) " << ns << " = " << gnb << "[q + 1];\n";
+                        } else if (idx < 32) {   // GenArgs::gnb capacity; past it, through the edge id
+                            loop << "        const int " << vs << " = " << gnb << "[q];\n";
+                        } else {
+                            loop << "        const int " << vs << " = a.slot[" << key.second << "][a.geid[" << sbk
+                                 << "][q]];\n";
+                        }
                     }
+                o << "        {\n        const int v" << k << " = (int)vtx;\n" << pre.str()
+                  << "        const int q0 = a.goff[" << sbk << "][vtx], q1 = a.goff[" << sbk << "][vtx + 1];\n"
+                  << head.str() << "        for (int q = q0; q < q1; ++q) {\n" << loop.str();
                 o << body.str() << "        }\n        }\n";
             }
         }
