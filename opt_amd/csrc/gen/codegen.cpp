@@ -309,6 +309,12 @@ GenSource generate(GModel& m, bool dbl) {
         sb += (int)m.graphs[g].slot_names.size();
     }
     for (auto& r : m.residuals) (r.graph < 0 ? gs.has_centered : gs.has_graph) = true;
+    // graph edge loops: vertex ids one edge ahead (OPT_AMD_GEN_NB_PREFETCH=0: at use);
+    // OPT_AMD_GEN_EDGE_UNROLL=k: unroll the gathers' edge loops k times (measurement knob)
+    const char* pfv = getenv("OPT_AMD_GEN_NB_PREFETCH");
+    const bool prefetch_nb = !pfv || atoi(pfv) != 0;
+    const char* urv = getenv("OPT_AMD_GEN_EDGE_UNROLL");
+    const std::string unroll = urv && atoi(urv) > 1 ? "#pragma unroll " + std::to_string(atoi(urv)) + "\n" : "";
 
     std::ostringstream o;
     o << "// generated by opt_amd's energy front end (gen/codegen.cpp)\n";
@@ -1234,10 +1240,21 @@ GenSource generate(GModel& m, bool dbl) {
             bool any = false;
             for (auto& r : m.residuals) any |= r.graph == (int)g;
             if (!any) continue;
-            o << "    for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < a.nedge[" << g
-              << "]; e += (long long)gridDim.x * 256) {\n";
-            for (size_t s = 0; s < m.graphs[g].slot_names.size(); ++s)
-                o << "        const int v" << s << " = a.slot[" << gs.slot_base[g] + s << "][e];\n";
+            // the next edge's vertex ids are loaded one edge ahead (as the gathers' edge loops)
+            const size_t ns = m.graphs[g].slot_names.size();
+            auto sl = [&](size_t s) { return "a.slot[" + std::to_string(gs.slot_base[g] + s) + "]"; };
+            o << "    {\n    const long long es = (long long)gridDim.x * 256, ne = a.nedge[" << g << "];\n"
+              << "    long long e = (long long)blockIdx.x * 256 + threadIdx.x;\n";
+            if (prefetch_nb)
+                for (size_t s = 0; s < ns; ++s) o << "    int n" << s << " = e < ne ? " << sl(s) << "[e] : 0;\n";
+            o << "    for (; e < ne; e += es) {\n";
+            for (size_t s = 0; s < ns; ++s)
+                o << "        const int v" << s << " = " << (prefetch_nb ? "n" + std::to_string(s) : sl(s) + "[e]") << ";\n";
+            if (prefetch_nb) {
+                o << "        if (e + es < ne) {";
+                for (size_t s = 0; s < ns; ++s) o << " n" << s << " = " << sl(s) << "[e + es];";
+                o << " }\n";
+            }
             Body b(m, o, nd, uslot);
             std::string sum = "(T)0";
             int idx = 0;
@@ -1264,7 +1281,7 @@ GenSource generate(GModel& m, bool dbl) {
             }
             b.line("}");
             b.line("acc += (T)0.5 * (" + sum + ");");
-            o << "    }\n";
+            o << "    }\n    }\n";
         }
         o << "    double v[1] = {(double)acc};\n    block_reduce_publish<1>(v, rs, blockIdx.x);\n}\n";
     }
@@ -1277,8 +1294,6 @@ GenSource generate(GModel& m, bool dbl) {
     // the edges whose slot k is this vertex, ascending): no atomics, a fixed summation
     // order (bitwise reproducible), each edge evaluated once per incident slot. The same
     // kernel finishes the element (exclusion mask, LM diagonal, p.Ap).
-    const char* pfv = getenv("OPT_AMD_GEN_NB_PREFETCH");
-    const bool prefetch_nb = !pfv || atoi(pfv) != 0;
     auto graph_gather = [&](bool apply) {
         // accumulators per output (unknown image, channel)
         for (int k : unk)
@@ -1357,7 +1372,7 @@ GenSource generate(GModel& m, bool dbl) {
                     }
                 o << "        {\n        const int v" << k << " = (int)vtx;\n" << pre.str()
                   << "        const int q0 = a.goff[" << sbk << "][vtx], q1 = a.goff[" << sbk << "][vtx + 1];\n"
-                  << head.str() << "        for (int q = q0; q < q1; ++q) {\n" << loop.str();
+                  << head.str() << unroll << "        for (int q = q0; q < q1; ++q) {\n" << loop.str();
                 o << body.str() << "        }\n        }\n";
             }
         }
