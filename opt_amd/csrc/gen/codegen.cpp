@@ -310,11 +310,14 @@ GenSource generate(GModel& m, bool dbl) {
     }
     for (auto& r : m.residuals) (r.graph < 0 ? gs.has_centered : gs.has_graph) = true;
     // graph edge loops: vertex ids one edge ahead (OPT_AMD_GEN_NB_PREFETCH=0: at use);
-    // OPT_AMD_GEN_EDGE_UNROLL=k: unroll the gathers' edge loops k times (measurement knob)
+    // OPT_AMD_GEN_EDGE_UNROLL=k: unroll the gathers' edge loops k times
     const char* pfv = getenv("OPT_AMD_GEN_NB_PREFETCH");
     const bool prefetch_nb = !pfv || atoi(pfv) != 0;
+    // (generated ARAP 1M vertices, profiles/r03_unroll_ab.json: apply 89 / 82-83 / 81 us at
+    // 1 / 2 / 4, GN step 1.63 / 1.63 / 1.56-1.58 ms; 4 by default, 1 = no pragma)
     const char* urv = getenv("OPT_AMD_GEN_EDGE_UNROLL");
-    const std::string unroll = urv && atoi(urv) > 1 ? "#pragma unroll " + std::to_string(atoi(urv)) + "\n" : "";
+    const int unr = urv ? atoi(urv) : 4;
+    const std::string unroll = unr > 1 ? "#pragma unroll " + std::to_string(unr) + "\n" : "";
 
     std::ostringstream o;
     o << "// generated by opt_amd's energy front end (gen/codegen.cpp)\n";
