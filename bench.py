@@ -14,11 +14,15 @@ cost). Inputs are resident in HBM before the timed region starts.
               as backend_cpu_mt) timing one whole GN step on this host's cores, in the
               same unit, plus apply-only rates on all cores and on one; rank 0 at N=1
 
-Multi-GPU (--gpus N under torch.distributed.run): the 4096² image is split into N
-row slabs, one per rank (OptAMD_PlanSetDecomposition over an RCCL communicator):
-per PCG iteration one all-reduce of four fp64 scalars (r.z, p.Ap, r.W Ap, Ap.W Ap: the
-fused pass takes beta's numerator from their identity) and one halo-row exchange.
-Total work is fixed, so the scaling is strong.
+Multi-GPU (--gpus N): the 4096² image is split into N row slabs, one per rank
+(OptAMD_PlanSetDecomposition over an RCCL communicator; the reference's outer-dimension
+split, backend_cpu_mt.t:716-737): per PCG iteration one all-reduce of four fp64 scalars
+(r.z, p.Ap, r.W Ap, Ap.W Ap: the fused pass takes beta's numerator from their identity)
+and one halo-row exchange. Total work is fixed, so the scaling is strong. Launch either
+under torch.distributed.run (WORLD_SIZE must then equal --gpus, else the script exits
+with status 2), or plainly: `python bench.py --gpus N` then starts the N rank processes
+itself (before anything touches the GPU) and exits with the worst child status.
+`--dry-run` prints each rank's environment and slab as JSON and touches no GPU.
 
 --workload shape_from_shading: BASELINE config 3 (4096² fp32 LM + PCG, the config
 north_star tiles across the node) through the same slabs (halo 2, ComputedArray planes
@@ -35,7 +39,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
 
 METRIC = "PCG JᵀJ·p throughput (unknowns/s) + GN iters/s, image_warping 4096² fp32"
 METRIC_SFS = "PCG JᵀJ·p throughput (unknowns/s) + LM iters/s, shape_from_shading 4096² fp32"
@@ -146,7 +149,79 @@ def parse():
     ap.add_argument("--liter", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", default="image_warping", choices=["image_warping", "shape_from_shading"])
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print each rank's launch environment and slab rows as JSON; no GPU work")
     return ap.parse_args()
+
+
+# stencil radius (halo rows) of each workload's energy; checked against the plan's
+# OptAMD_PlanHalo in the real run
+HALO = {"image_warping": 1, "shape_from_shading": 2}
+
+
+def rank_env():
+    """(world, rank, local_rank) from the launcher's environment (torch.distributed.run or
+    spawn_ranks)."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: start N copies of this script, one per GPU, with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (what
+    torch.distributed.run sets). This process never touches the GPU (it only waits), so the
+    children own their devices; if any child fails the others are stopped and the worst
+    status is returned. Rank 0 prints the JSON line."""
+    import subprocess
+
+    n = args.gpus
+    if not args.dry_run:
+        import torch   # device_count() does not initialise the GPU on this image
+
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
+            return 2
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    status = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            rc = p.poll()
+            if rc is None:
+                continue
+            pending.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 1
+                for q in pending:   # a failed rank leaves the others blocked in a collective
+                    q.kill()
+        time.sleep(0.05)
+    return status
+
+
+def dry_run(args, world, rank, local):
+    """One JSON line per rank: what the real run would use (no torch, no GPU)."""
+    from opt_amd import distributed as dd
+
+    sl = dd.slab(args.size, rank, world, HALO[args.workload]) if world > 1 else None
+    print(json.dumps({"rank": rank, "local_rank": local, "world": world, "device": f"cuda:{local}",
+                      "master": f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}",
+                      "workload": args.workload, "size": args.size,
+                      "slab": ([sl.y_lo, sl.y_hi] if sl else [0, args.size]),
+                      "mem_rows": ([sl.mem_lo, sl.mem_hi] if sl else [0, args.size])}), flush=True)
 
 
 def host_cores():
@@ -216,37 +291,46 @@ def cpu_baseline(w, n_unknowns, liter):
     }
 
 
-def cpu_baseline_sfs(W, liter, rows=256):
+def cpu_baseline_sfs(w, W, H, liter):
     """Config 3's comparator: the oracle (oracle/sfs_impl.h, the reference's
-    shape_from_shading energy and LM/PCG loop restated in C, single-threaded) timing ONE
-    LM step (precompute, J^T F, `liter` PCG iterations, model cost, cost) of a W x `rows`
-    crop of the same seeded workload, in the headline's unit (unknowns x lIterations per
-    second). The reference's backend_cpu_mt splits the same loops over rows across
-    threads (backend_cpu_mt.t:716-737); this comparator uses one core."""
+    shape_from_shading energy and LM/PCG loop restated in C) timing ONE LM step
+    (precompute, J^T F, `liter` PCG iterations, model cost, cost) of the full W x H
+    workload, every stencil pass split over row slabs on all the host cores this process
+    may use, per-thread sums added in thread order (backend_cpu_mt.t:350-414, 716-737), in
+    the headline's unit (unknowns x lIterations per second)."""
     from oracle import oracle
-    from opt_amd import workloads
 
-    w = workloads.shape_from_shading(W, rows, seed=3)
+    cores = host_cores()
     t0 = time.perf_counter()
-    oracle.sfs_solve(w, 1, liter, lm=True)
+    oracle.sfs_solve(w, 1, liter, lm=True, nthreads=cores)
     dt = time.perf_counter() - t0
     return {
-        "value": W * rows * liter / dt,
+        "value": W * H * liter / dt,
         "unit": "unknowns/s",
-        "cores": 1,
+        "cores": cores,
         "kind": "port",
-        "sample": f"one LM step ({liter} PCG iterations, incl. precompute and both costs) of a {W}x{rows} crop "
-                  f"of the seeded workload, oracle/sfs_impl.h on 1 thread: {dt:.2f} s",
-        "lm_iters_per_s_at_crop": 1.0 / dt,
+        "sample": f"one LM step ({liter} PCG iterations, incl. precompute and both costs) of the full {W}x{H} "
+                  f"workload, oracle/sfs_impl.h over row slabs on {cores} threads: {dt:.2f} s",
+        "lm_iters_per_s": 1.0 / dt,
         "cpu_model": cpu_model(),
     }
-
-
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr, flush=True)
+        return 2
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args)
+    world, rank, local = rank_env()
+    if world != args.gpus:
+        print(f"bench.py: launched with WORLD_SIZE={world} but --gpus {args.gpus}; refusing to report "
+              f"a {world}-rank run as {args.gpus}", file=sys.stderr, flush=True)
+        return 2
+    if args.dry_run:
+        dry_run(args, world, rank, local)
+        return 0
+    import torch
+
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -282,6 +366,8 @@ def main():
         idraw = (ctypes.c_uint8 * 128)(*idbuf.cpu().tolist())
         comm = lib.OptAMD_CommCreateRccl(idraw, rank, world)
         assert comm, "RCCL communicator"
+        assert lib.OptAMD_CommSize(comm) == world and lib.OptAMD_CommRank(comm) == rank
+        assert s.halo() == HALO[args.workload], (s.halo(), args.workload)
         sl = dd.slab(H, rank, world, s.halo())
         s.set_decomposition(comm, sl.y_lo, sl.y_hi)
         lw = dd.local_image(w, sl, dd.SFS_CHANNELS if sfs else dd.IW_CHANNELS)
@@ -345,11 +431,13 @@ def main():
     Ap = torch.empty_like(p)
     pure_us = s.time_apply(prm, p, Ap, 20)
     kind = "LM" if sfs else "GN"
+    n_ranks = api.load_library().OptAMD_CommSize(comm) if comm else 1   # what the solver ran on
+    rows = [H // world] * (world - 1) + [H - (world - 1) * (H // world)]
     result = {
         "metric": METRIC_SFS if sfs else METRIC,
         "value": n_unknowns * args.liter * args.steps / dt,
         "unit": "unknowns/s",
-        "n_gpus": world,
+        "n_gpus": n_ranks,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": 1000.0 * dt / args.steps,
@@ -361,8 +449,9 @@ def main():
         "config": {
             "workload": f"{args.workload} {W}x{H} fp32 {kind}+PCG, lIterations={args.liter}",
             "unknowns": n_unknowns,
-            "parallelism": (f"row-slabs x{world} (RCCL: {2 if sfs else 1} allreduce + 1 halo exchange per PCG iteration)"
-                            if world > 1 else "single"),
+            "parallelism": (f"row-slabs x{n_ranks} of {rows[0]}" + (f"/{rows[-1]}" if rows[-1] != rows[0] else "")
+                            + f" rows (halo {HALO[args.workload]}; RCCL: {2 if sfs else 1} allreduce + 1 halo "
+                              "exchange per PCG iteration)" if n_ranks > 1 else "single"),
         },
         f"{kind.lower()}_iters_per_s": args.steps / dt,
         "apply_unknowns_per_s": ch * npx * world / avg_apply_s,
@@ -391,7 +480,7 @@ def main():
                                  "bytes_per_px": INIT_BYTES_PER_PX, "achieved": ach,
                                  "frac": ach / PEAK_HBM_GBS}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = (cpu_baseline_sfs(W, args.liter) if sfs
+        result["cpu_baseline"] = (cpu_baseline_sfs(w, W, H, args.liter) if sfs
                                   else cpu_baseline(w, n_unknowns, args.liter))
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -400,7 +489,8 @@ def main():
         api.load_library().OptAMD_CommDestroy(comm)
     if dist:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

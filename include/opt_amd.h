@@ -102,6 +102,10 @@ int OptAMD_RcclUniqueId(void* out128);
 /* RCCL communicator over `nranks` processes, one GPU each (the current HIP device). */
 OptAMD_Comm* OptAMD_CommCreateRccl(const void* id128, int rank, int nranks);
 void OptAMD_CommDestroy(OptAMD_Comm* comm);
+/* Number of ranks / this rank of a communicator (-1 for NULL): bench.py reports the
+ * world size the solver actually runs on from here, not from the launcher's env. */
+int OptAMD_CommSize(OptAMD_Comm* comm);
+int OptAMD_CommRank(OptAMD_Comm* comm);
 /* All ranks as threads of one process (shared device or peer devices): for testing
  * the decomposition on one GPU. The rank handles belong to the group. */
 OptAMD_LocalGroup* OptAMD_LocalGroupCreate(int nranks);

@@ -70,6 +70,8 @@ _SIGNATURES = [
     ("OptAMD_RcclUniqueId", ctypes.c_int, [_VP]),
     ("OptAMD_CommCreateRccl", _VP, [_VP, ctypes.c_int, ctypes.c_int]),
     ("OptAMD_CommDestroy", None, [_VP]),
+    ("OptAMD_CommSize", ctypes.c_int, [_VP]),
+    ("OptAMD_CommRank", ctypes.c_int, [_VP]),
     ("OptAMD_LocalGroupCreate", _VP, [ctypes.c_int]),
     ("OptAMD_LocalGroupRank", _VP, [_VP, ctypes.c_int]),
     ("OptAMD_LocalGroupDestroy", None, [_VP]),

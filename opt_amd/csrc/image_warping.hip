@@ -666,7 +666,11 @@ __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_apply_res(Args<T> a, 
     const T alpha = (T)(rzp / papp);
     const double alpha_d = (double)alpha;
     const double rz_id = base_scale * rzp - 2.0 * alpha_d * sc[prev + 2] + alpha_d * alpha_d * sc[prev + 3];
-    const T beta = (T)(rz_id / rzp);
+    // The identity subtracts fp64 sums of size rz_{i-1}: its absolute error is ~1e-14 rz_{i-1},
+    // i.e. ~1e-14 in beta whatever rz_i / rz_{i-1} is, negligible in p_i. It cancels to <= 0
+    // only where the true beta is itself below that error: beta_i = 0 there (the direct
+    // r_i.z_i of this pass is >= 0 by construction, so a negative beta is never right).
+    const T beta = rz_id > 0.0 ? (T)(rz_id / rzp) : (T)0;
     // E: p_{i-2}'s delta term was deferred by the previous pass; alpha_{i-2} from its slots
     const T alpha2 = E ? (T)(sc[prev - kSlots] / sc[prev - kSlots + 1]) : (T)0;
     if (blockIdx.x == 0 && threadIdx.x == 0) sc[prev + kSlots + 4] = rz_id;

@@ -290,6 +290,8 @@ void OptAMD_CommDestroy(OptAMD_Comm* comm) {
     if (!comm) return;
     if (comm->owned) { delete comm->impl; delete comm; }
 }
+int OptAMD_CommSize(OptAMD_Comm* comm) { return comm ? comm->impl->size() : -1; }
+int OptAMD_CommRank(OptAMD_Comm* comm) { return comm ? comm->impl->rank() : -1; }
 OptAMD_LocalGroup* OptAMD_LocalGroupCreate(int nranks) {
     if (nranks < 1) return nullptr;
     auto* g = new OptAMD_LocalGroup();

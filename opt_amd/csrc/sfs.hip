@@ -619,11 +619,14 @@ __global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restri
                         else dot += pk * acc;
                     }
                 }
-                if (SUMS) {   // inactive pixels: Ap = 0 (r is 0 there too); T products, fp64 sums
-                    const T wr_ = cur.w * cur.rr;
-                    rapd += (double)(wr_ * acc);
-                    apapd += (double)(cur.w * acc * acc);
-                    rwrd += (double)(wr_ * cur.rr);
+                if (SUMS) {   // inactive pixels: Ap = 0 (r is 0 there too)
+                    // fp64 products and sums, as step23's direct rz (w r r in fp64) and
+                    // iw_apply_res's wdot3: the identity r.W r - 2 a r.W Ap + a^2 Ap.W Ap
+                    // cancels, so both sides must be rounded alike
+                    const double w_ = (double)cur.w, r_ = (double)cur.rr, ap_ = (double)acc;
+                    rapd += w_ * r_ * ap_;
+                    apapd += w_ * ap_ * ap_;
+                    rwrd += w_ * r_ * r_;
                 }
                 if constexpr (JTF) {
                     Ap[i] = -acc;   // r

@@ -244,7 +244,9 @@ __global__ __launch_bounds__(kBlock) void step23_kernel(long long n, T* __restri
     const T alpha = (T)(rz / sc[i_rz + 2]);
     const double ad = (double)alpha;
     const double rz_id = sc[i_rz + 5] - 2.0 * ad * sc[i_rz + 3] + ad * ad * sc[i_rz + 4];
-    const T beta = (T)(rz_id / rz);
+    // non-positive only where the true beta is below the identity's ~1e-14 absolute error
+    // (iw_apply_res): beta = 0 there
+    const T beta = rz_id > 0.0 ? (T)(rz_id / rz) : (T)0;
     if (blockIdx.x == 0 && threadIdx.x == 0) sc[id_out] = rz_id;
     double acc = 0;
     T accq = 0;

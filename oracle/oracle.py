@@ -53,19 +53,63 @@ def _args(w):
             _f(w["Mask"]), w["w_fitSqrt"], w["w_regSqrt"])
 
 
-def iw_cost(w, nthreads=1):
+def _iw_double_lib():
+    lib = load()
+    if not getattr(lib, "_iwd", False):
+        i, f, d = ctypes.c_int, ctypes.c_float, ctypes.c_double
+        base = [i, i, _D, _D, _F, _F, _F, f, f]
+        lib.oracle_iw_cost_double.restype, lib.oracle_iw_cost_double.argtypes = d, base + [i]
+        lib.oracle_iw_eval_jtf_double.restype, lib.oracle_iw_eval_jtf_double.argtypes = d, base + [_D, _D, i]
+        lib.oracle_iw_apply_jtj_double.restype, lib.oracle_iw_apply_jtj_double.argtypes = d, base + [_D, _D, i]
+        lib.oracle_iw_solve_double.restype, lib.oracle_iw_solve_double.argtypes = None, base + [i, i, i, _D, _D]
+        lib.oracle_iw_solve_generic_double.restype = i
+        lib.oracle_iw_solve_generic_double.argtypes = base + [i, i, i, i, _D]
+        lib.oracle_iw_model_cost_double.restype, lib.oracle_iw_model_cost_double.argtypes = d, base + [_D]
+        lib.oracle_iw_jtf_diag_double.restype, lib.oracle_iw_jtf_diag_double.argtypes = None, base + [_D, _D]
+        lib._iwd = True
+    return lib
+
+
+def _dd(a):
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_D)
+
+
+def _args_double(w, O=None, A=None):
+    """opt_float = double: the unknowns widened to double (or given), known arrays float."""
+    O = np.ascontiguousarray(w["Offset"] if O is None else O, np.float64)
+    A = np.ascontiguousarray(w["Angle"] if A is None else A, np.float64)
+    return (O, A), (w["W"], w["H"], _dd(O), _dd(A), _f(w["UrShape"]), _f(w["Constraints"]), _f(w["Mask"]),
+                    w["w_fitSqrt"], w["w_regSqrt"])
+
+
+def iw_cost(w, nthreads=1, double=False):
+    if double:
+        keep, a = _args_double(w)
+        return _iw_double_lib().oracle_iw_cost_double(*a, nthreads)
     return load().oracle_iw_cost(*_args(w), nthreads)
 
 
-def iw_eval_jtf(w, nthreads=1):
+def iw_eval_jtf(w, nthreads=1, double=False):
     n = 3 * w["W"] * w["H"]
+    if double:
+        keep, a = _args_double(w)
+        r, pre = np.zeros(n, np.float64), np.zeros(n, np.float64)
+        rz = _iw_double_lib().oracle_iw_eval_jtf_double(*a, _dd(r), _dd(pre), nthreads)
+        return r, pre, rz
     r = np.zeros(n, np.float32)
     pre = np.zeros(n, np.float32)
     rz = load().oracle_iw_eval_jtf(*_args(w), _f(r), _f(pre), nthreads)
     return r, pre, rz
 
 
-def iw_apply_jtj(w, p, nthreads=1):
+def iw_apply_jtj(w, p, nthreads=1, double=False):
+    if double:
+        keep, a = _args_double(w)
+        p = np.ascontiguousarray(p, np.float64)
+        Ap = np.zeros_like(p)
+        pAp = _iw_double_lib().oracle_iw_apply_jtj_double(*a, _dd(p), _dd(Ap), nthreads)
+        return Ap, pAp
     p = np.ascontiguousarray(p, np.float32)
     Ap = np.zeros_like(p)
     pAp = load().oracle_iw_apply_jtj(*_args(w), _f(p), _f(Ap), nthreads)
@@ -79,15 +123,24 @@ def iw_residuals(w):
     return res
 
 
-def iw_solve(w, n_iter, l_iter, nthreads=1, want_scalars=False):
-    """Full GN solve; returns (Offset, Angle, costs[n_iter+1], scalars|None)."""
-    O = w["Offset"].copy()
-    A = w["Angle"].copy()
+def iw_solve(w, n_iter, l_iter, nthreads=1, want_scalars=False, double=False):
+    """Full GN solve; returns (Offset, Angle, costs[n_iter+1], scalars|None). double: the
+    reference's doublePrecision mode (unknowns and solver in double, known arrays float)."""
+    dt = np.float64 if double else np.float32
+    O = w["Offset"].astype(dt)
+    A = w["Angle"].astype(dt)
     costs = np.zeros(n_iter + 1, np.float64)
     sc = np.zeros(max(1, 3 * n_iter * l_iter), np.float64) if want_scalars else None
-    load().oracle_iw_solve(w["W"], w["H"], _f(O), _f(A), _f(w["UrShape"]), _f(w["Constraints"]),
-                           _f(w["Mask"]), w["w_fitSqrt"], w["w_regSqrt"], n_iter, l_iter, nthreads,
-                           costs.ctypes.data_as(_D), sc.ctypes.data_as(_D) if sc is not None else None)
+    scp = sc.ctypes.data_as(_D) if sc is not None else None
+    if double:
+        _iw_double_lib().oracle_iw_solve_double(w["W"], w["H"], _dd(O), _dd(A), _f(w["UrShape"]),
+                                                _f(w["Constraints"]), _f(w["Mask"]), w["w_fitSqrt"],
+                                                w["w_regSqrt"], n_iter, l_iter, nthreads, costs.ctypes.data_as(_D),
+                                                scp)
+    else:
+        load().oracle_iw_solve(w["W"], w["H"], _f(O), _f(A), _f(w["UrShape"]), _f(w["Constraints"]),
+                               _f(w["Mask"]), w["w_fitSqrt"], w["w_regSqrt"], n_iter, l_iter, nthreads,
+                               costs.ctypes.data_as(_D), scp)
     return O, A, costs, (sc.reshape(n_iter, l_iter, 3) if sc is not None else None)
 
 
@@ -105,22 +158,36 @@ def _iwg_lib():
     return lib
 
 
-def iw_jtf_diag(w):
+def iw_jtf_diag(w, double=False):
     """r = -J^T F and the raw diagonal of J^T J (generic driver layout)."""
     n = 3 * w["W"] * w["H"]
+    if double:
+        keep, a = _args_double(w)
+        r, dg = np.zeros(n, np.float64), np.zeros(n, np.float64)
+        _iw_double_lib().oracle_iw_jtf_diag_double(*a, _dd(r), _dd(dg))
+        return r, dg
     r = np.zeros(n, np.float32)
     dg = np.zeros(n, np.float32)
     _iwg_lib().oracle_iw_jtf_diag(*_args(w), _f(r), _f(dg))
     return r, dg
 
 
-def iw_model_cost(w, delta):
+def iw_model_cost(w, delta, double=False):
+    if double:
+        keep, a = _args_double(w)
+        return _iw_double_lib().oracle_iw_model_cost_double(*a, _dd(np.ascontiguousarray(delta, np.float64)))
     delta = np.ascontiguousarray(delta, np.float32)
     return _iwg_lib().oracle_iw_model_cost(*_args(w), _f(delta))
 
 
-def iw_solve_generic(w, n_iter, l_iter, lm=False, nthreads=1):
+def iw_solve_generic(w, n_iter, l_iter, lm=False, nthreads=1, double=False):
     """GN or LM solve through the generic loop (solver_impl.h); returns (O, A, costs)."""
+    if double:
+        (O, A), a = _args_double(w, w["Offset"].astype(np.float64), w["Angle"].astype(np.float64))
+        costs = np.zeros(n_iter + 1, np.float64)
+        k = _iw_double_lib().oracle_iw_solve_generic_double(*a, int(lm), n_iter, l_iter, nthreads,
+                                                            costs.ctypes.data_as(_D))
+        return O, A, costs[: k + 1]
     O = w["Offset"].copy()
     A = w["Angle"].copy()
     costs = np.zeros(n_iter + 1, np.float64)
@@ -143,34 +210,57 @@ def _pie_lib():
         lib.oracle_pie_apply.argtypes = [i, i, _F, _F, _F, _F, _F]
         lib.oracle_pie_solve.restype = i
         lib.oracle_pie_solve.argtypes = [i, i, _F, _F, _F, i, i, i, _D]
+        lib.oracle_pie_cost_double.restype = d
+        lib.oracle_pie_cost_double.argtypes = [i, i, _D, _F, _F]
+        lib.oracle_pie_jtf_double.restype = None
+        lib.oracle_pie_jtf_double.argtypes = [i, i, _D, _F, _F, _D, _D]
+        lib.oracle_pie_apply_double.restype = d
+        lib.oracle_pie_apply_double.argtypes = [i, i, _D, _F, _F, _D, _D]
+        lib.oracle_pie_solve_double.restype = i
+        lib.oracle_pie_solve_double.argtypes = [i, i, _D, _F, _F, i, i, i, _D]
         lib._pie = True
     return lib
 
 
-def pie_cost(w):
-    return _pie_lib().oracle_pie_cost(w["W"], w["H"], _f(w["X"]), _f(w["T"]), _f(w["M"]))
+def _pie_x(w, double, X=None):
+    X = np.ascontiguousarray(w["X"] if X is None else X, np.float64 if double else np.float32)
+    return X, (X.ctypes.data_as(_D if double else _F))
 
 
-def pie_jtf(w):
+def pie_cost(w, double=False):
+    X, xp = _pie_x(w, double)
+    fn = _pie_lib().oracle_pie_cost_double if double else _pie_lib().oracle_pie_cost
+    return fn(w["W"], w["H"], xp, _f(w["T"]), _f(w["M"]))
+
+
+def pie_jtf(w, double=False):
+    dt = np.float64 if double else np.float32
     n = 4 * w["W"] * w["H"]
-    r = np.zeros(n, np.float32)
-    dg = np.zeros(n, np.float32)
-    _pie_lib().oracle_pie_jtf(w["W"], w["H"], _f(w["X"]), _f(w["T"]), _f(w["M"]), _f(r), _f(dg))
+    r = np.zeros(n, dt)
+    dg = np.zeros(n, dt)
+    X, xp = _pie_x(w, double)
+    P = _D if double else _F
+    fn = _pie_lib().oracle_pie_jtf_double if double else _pie_lib().oracle_pie_jtf
+    fn(w["W"], w["H"], xp, _f(w["T"]), _f(w["M"]), r.ctypes.data_as(P), dg.ctypes.data_as(P))
     return r, dg
 
 
-def pie_apply(w, p):
-    p = np.ascontiguousarray(p, np.float32)
+def pie_apply(w, p, double=False):
+    dt = np.float64 if double else np.float32
+    P = _D if double else _F
+    p = np.ascontiguousarray(p, dt)
     Ap = np.zeros_like(p)
-    pAp = _pie_lib().oracle_pie_apply(w["W"], w["H"], _f(w["X"]), _f(w["T"]), _f(w["M"]), _f(p), _f(Ap))
+    X, xp = _pie_x(w, double)
+    fn = _pie_lib().oracle_pie_apply_double if double else _pie_lib().oracle_pie_apply
+    pAp = fn(w["W"], w["H"], xp, _f(w["T"]), _f(w["M"]), p.ctypes.data_as(P), Ap.ctypes.data_as(P))
     return Ap, pAp
 
 
-def pie_solve(w, n_iter, l_iter, lm=False):
-    X = w["X"].copy()
+def pie_solve(w, n_iter, l_iter, lm=False, double=False):
+    X, xp = _pie_x(w, double, w["X"].astype(np.float64 if double else np.float32))
     costs = np.zeros(n_iter + 1, np.float64)
-    k = _pie_lib().oracle_pie_solve(w["W"], w["H"], _f(X), _f(w["T"]), _f(w["M"]), int(lm), n_iter, l_iter,
-                                    costs.ctypes.data_as(_D))
+    fn = _pie_lib().oracle_pie_solve_double if double else _pie_lib().oracle_pie_solve
+    k = fn(w["W"], w["H"], xp, _f(w["T"]), _f(w["M"]), int(lm), n_iter, l_iter, costs.ctypes.data_as(_D))
     return X, costs[: k + 1]
 
 
@@ -255,7 +345,7 @@ def _sfs_lib():
         for suf, R in (("", _F), ("_double", _D)):
             base = [i, i, R, _F, _F, _U8, _U8, _F]
             for name, res, extra in (("precompute", None, [R]), ("cost", d, []), ("jtf", None, [R, R]),
-                                     ("apply", d, [R, R]), ("model_cost", d, [R]), ("solve", i, [i, i, i, _D])):
+                                     ("apply", d, [R, R]), ("model_cost", d, [R]), ("solve", i, [i, i, i, _D, i])):
                 fn = getattr(lib, "oracle_sfs_" + name + suf)
                 fn.restype, fn.argtypes = res, base + extra
         lib._sfs = True
@@ -319,10 +409,12 @@ def sfs_model_cost(w, d, X=None, double=False):
     return _sfs_fn("model_cost", double)(*a, d.ctypes.data_as(R))
 
 
-def sfs_solve(w, n_iter, l_iter, lm=True, double=False):
+def sfs_solve(w, n_iter, l_iter, lm=True, double=False, nthreads=1):
+    """LM (or GN) solve; nthreads: the stencil passes split over row slabs on that many
+    threads (backend_cpu_mt.t:716-737), per-thread sums added in thread order."""
     X, keep, a = _sfs_args(w, w["X"].copy(), double)
     costs = np.zeros(n_iter + 1, np.float64)
-    k = _sfs_fn("solve", double)(*a, int(lm), n_iter, l_iter, costs.ctypes.data_as(_D))
+    k = _sfs_fn("solve", double)(*a, int(lm), n_iter, l_iter, costs.ctypes.data_as(_D), nthreads)
     return X, costs[: k + 1]
 
 

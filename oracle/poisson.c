@@ -20,125 +20,27 @@
 #include <string.h>
 #include "solver.h"
 
-typedef struct {
-    int W, H;
-    float* X;          /* 4 per pixel, updated in place */
-    const float* T;
-    const float* M;
-    float* prev;
-} pie_ctx;
-
 static const int PX[4] = {1, -1, 0, 0};
 static const int PY[4] = {0, 0, 1, -1};
-static int pin(const pie_ctx* c, int x, int y) { return x >= 0 && x < c->W && y >= 0 && y < c->H; }
-static int pact(const pie_ctx* c, int k) { return c->M[k] == 0.f; }
-/* residual channel ch centred at (x,y) toward s; valid if both in bounds */
-static float pres(const pie_ctx* c, const float* X, int x, int y, int s, int ch) {
-    const int k = y * c->W + x, j = (y + PY[s]) * c->W + (x + PX[s]);
-    return (X[4 * k + ch] - X[4 * j + ch]) - (c->T[4 * k + ch] - c->T[4 * j + ch]);
-}
 
-static double pie_cost_fn(void* v) {
-    pie_ctx* c = (pie_ctx*)v;
-    double acc = 0.0;
-    for (int y = 0; y < c->H; ++y)
-        for (int x = 0; x < c->W; ++x) {
-            if (!pact(c, y * c->W + x)) continue;
-            float s2 = 0.f;
-            for (int s = 0; s < 4; ++s) {
-                if (!pin(c, x + PX[s], y + PY[s])) continue;
-                for (int ch = 0; ch < 4; ++ch) { const float e = pres(c, c->X, x, y, s, ch); s2 += e * e; }
-            }
-            acc += 0.5f * s2;
-        }
-    return acc;
-}
+#define REAL float
+#include "pie_impl.h"
+#undef REAL
+#define REAL double
+#include "pie_impl.h"
+#undef REAL
 
-static void pie_jtf_fn(void* v, float* r, float* diag) {
-    pie_ctx* c = (pie_ctx*)v;
-    for (int y = 0; y < c->H; ++y)
-        for (int x = 0; x < c->W; ++x) {
-            const int k = y * c->W + x;
-            for (int ch = 0; ch < 4; ++ch) {
-                float F = 0.f, D = 0.f;
-                if (pact(c, k)) {
-                    for (int s = 0; s < 4; ++s) {
-                        if (pin(c, x + PX[s], y + PY[s])) { F += pres(c, c->X, x, y, s, ch); D += 1.f; }
-                        if (pin(c, x - PX[s], y - PY[s])) { F += -1.f * pres(c, c->X, x - PX[s], y - PY[s], s, ch); D += 1.f; }
-                    }
-                }
-                r[4 * k + ch] = -F;
-                diag[4 * k + ch] = D;
-            }
-        }
-}
-
-static double pie_apply_fn(void* v, const float* p, float* Ap) {
-    pie_ctx* c = (pie_ctx*)v;
-    double dot = 0.0;
-    for (int y = 0; y < c->H; ++y)
-        for (int x = 0; x < c->W; ++x) {
-            const int k = y * c->W + x;
-            for (int ch = 0; ch < 4; ++ch) {
-                float a = 0.f;
-                if (pact(c, k)) {
-                    for (int s = 0; s < 4; ++s) {
-                        const int tx = x + PX[s], ty = y + PY[s], jx = x - PX[s], jy = y - PY[s];
-                        if (pin(c, tx, ty)) {
-                            const int t = ty * c->W + tx;
-                            const float pt = pact(c, t) ? p[4 * t + ch] : 0.f;
-                            a += 1.f * (p[4 * k + ch] - pt);
-                        }
-                        if (pin(c, jx, jy)) {
-                            const int j = jy * c->W + jx;
-                            const float pj = pact(c, j) ? p[4 * j + ch] : 0.f;
-                            a += -1.f * (pj - p[4 * k + ch]);
-                        }
-                    }
-                    dot += (double)p[4 * k + ch] * a;
-                }
-                Ap[4 * k + ch] = a;
-            }
-        }
-    return dot;
-}
-
-static double pie_model_fn(void* v, const float* d) {
-    pie_ctx* c = (pie_ctx*)v;
-    double acc = 0.0;
-    for (int y = 0; y < c->H; ++y)
-        for (int x = 0; x < c->W; ++x) {
-            const int k = y * c->W + x;
-            if (!pact(c, k)) continue;
-            float s2 = 0.f;
-            for (int s = 0; s < 4; ++s) {
-                const int tx = x + PX[s], ty = y + PY[s];
-                if (!pin(c, tx, ty)) continue;
-                const int t = ty * c->W + tx;
-                for (int ch = 0; ch < 4; ++ch) {
-                    const float dt = pact(c, t) ? d[4 * t + ch] : 0.f;
-                    const float e = pres(c, c->X, x, y, s, ch) + (d[4 * k + ch] - dt);
-                    s2 += e * e;
-                }
-            }
-            acc += 0.5f * s2;
-        }
-    return acc;
-}
-static void pie_update_fn(void* v, const float* d) {
-    pie_ctx* c = (pie_ctx*)v;
-    for (int k = 0; k < c->W * c->H; ++k)
-        if (pact(c, k)) for (int ch = 0; ch < 4; ++ch) c->X[4 * k + ch] += d[4 * k + ch];
-}
-static void pie_save_fn(void* v) {
-    pie_ctx* c = (pie_ctx*)v;
-    memcpy(c->prev, c->X, sizeof(float) * 4 * c->W * c->H);
-}
-static void pie_revert_fn(void* v) {
-    pie_ctx* c = (pie_ctx*)v;
-    for (int k = 0; k < c->W * c->H; ++k)
-        if (pact(c, k)) for (int ch = 0; ch < 4; ++ch) c->X[4 * k + ch] = c->prev[4 * k + ch];
-}
+/* the float instantiation under the names the rest of this file uses */
+typedef pie_ctx_float pie_ctx;
+#define pin pin_float
+#define pact pact_float
+#define pie_cost_fn pie_cost_fn_float
+#define pie_jtf_fn pie_jtf_fn_float
+#define pie_apply_fn pie_apply_fn_float
+#define pie_model_fn pie_model_fn_float
+#define pie_update_fn pie_update_fn_float
+#define pie_save_fn pie_save_fn_float
+#define pie_revert_fn pie_revert_fn_float
 
 /* ------------------------------------------------------------- public API ---- */
 double oracle_pie_cost(int W, int H, float* X, const float* T, const float* M) {
@@ -167,6 +69,38 @@ int oracle_pie_solve(int W, int H, float* X, const float* T, const float* M, int
     sp.nIterations = nIter;
     sp.lIterations = lIter;
     const int k = oracle_solve_f32(&P, lm, &sp, costs);
+    free(act);
+    free(c.prev);
+    return k;
+}
+
+/* opt_float = double: X and the solver in double, T / M float */
+double oracle_pie_cost_double(int W, int H, double* X, const float* T, const float* M) {
+    pie_ctx_double c = {W, H, X, T, M, NULL};
+    return pie_cost_fn_double(&c);
+}
+void oracle_pie_jtf_double(int W, int H, double* X, const float* T, const float* M, double* r, double* diag) {
+    pie_ctx_double c = {W, H, X, T, M, NULL};
+    pie_jtf_fn_double(&c, r, diag);
+}
+double oracle_pie_apply_double(int W, int H, double* X, const float* T, const float* M, const double* p,
+                               double* Ap) {
+    pie_ctx_double c = {W, H, X, T, M, NULL};
+    return pie_apply_fn_double(&c, p, Ap);
+}
+int oracle_pie_solve_double(int W, int H, double* X, const float* T, const float* M, int lm, int nIter, int lIter,
+                            double* costs) {
+    pie_ctx_double c = {W, H, X, T, M, NULL};
+    const long long n = 4LL * W * H;
+    unsigned char* act = malloc(n);
+    for (long long e = 0; e < n; ++e) act[e] = M[e / 4] == 0.f;
+    c.prev = malloc(sizeof(double) * n);
+    oracle_problem_double P = {n, act, 0, &c, pie_cost_fn_double, pie_jtf_fn_double, pie_apply_fn_double,
+                               pie_model_fn_double, pie_update_fn_double, pie_save_fn_double, pie_revert_fn_double};
+    oracle_params sp = oracle_default_params();
+    sp.nIterations = nIter;
+    sp.lIterations = lIter;
+    const int k = oracle_solve_f64(&P, lm, &sp, costs);
     free(act);
     free(c.prev);
     return k;

@@ -29,6 +29,7 @@
  * Image reads outside the image are 0 (Image:get, o.t:856-862).
  */
 #include <math.h>
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 #include "solver.h"
@@ -100,10 +101,12 @@
         free_ctx_##R(&c);                                                                                         \
         return v;                                                                                                 \
     }                                                                                                             \
+    /* nthreads: row slabs of every stencil pass over that many threads (backend_cpu_mt) */                    \
     int oracle_sfs_solve##SUF(int W, int H, R* X, const float* D, const float* Im, const unsigned char* mR,      \
                               const unsigned char* mC, const float* prm, int lm, int nIter, int lIter,            \
-                              double* costs) {                                                                    \
+                              double* costs, int nthreads) {                                                      \
         sfs_ctx_##R c = make_ctx_##R(W, H, X, D, Im, mR, mC, prm);                                                \
+        c.nthreads = nthreads;                                                                                    \
         const long long n = (long long)W * H;                                                                     \
         unsigned char* act = malloc(n);                                                                           \
         for (long long k = 0; k < n; ++k) act[k] = !excl_##R(&c, k);                                              \

@@ -19,6 +19,7 @@ typedef struct {
     /* precomputed */
     REAL *BI, *G00, *Gm0, *G0m, *VAL;
     REAL* prev;
+    int nthreads;   /* row slabs over pthreads (backend_cpu_mt.t:716-737); 0 or 1: one thread */
 } FN(sfs_ctx);
 
 static int FN(sin_)(const FN(sfs_ctx) * c, int x, int y) { return x >= 0 && x < c->W && y >= 0 && y < c->H; }
@@ -68,8 +69,8 @@ static void FN(bi_eval)(const FN(sfs_ctx)* c, const REAL* X, int x, int y, REAL*
     }
 }
 
-static void FN(sfs_precompute)(FN(sfs_ctx)* c) {
-    for (int y = 0; y < c->H; ++y)
+static void FN(pre_rows)(FN(sfs_ctx)* c, int y0, int y1) {
+    for (int y = y0; y < y1; ++y)
         for (int x = 0; x < c->W; ++x) {
             const long long k = (long long)y * c->W + x;
             REAL g[3];
@@ -158,10 +159,9 @@ static int FN(eval_res)(const FN(sfs_ctx)* c, int t, int x, int y, FN(res_t)* r)
 
 static int FN(excl)(const FN(sfs_ctx)* c, long long k) { return !(c->D[k] > (REAL)0.); }
 
-static double FN(sfs_cost_fn)(void* v) {
-    FN(sfs_ctx)* c = (FN(sfs_ctx)*)v;
+static double FN(cost_rows)(FN(sfs_ctx)* c, int y0, int y1) {
     double acc = 0.0;
-    for (int y = 0; y < c->H; ++y)
+    for (int y = y0; y < y1; ++y)
         for (int x = 0; x < c->W; ++x) {
             if (FN(excl)(c, (long long)y * c->W + x)) continue;
             REAL s2 = (REAL)0.;
@@ -175,10 +175,9 @@ static double FN(sfs_cost_fn)(void* v) {
     return acc;
 }
 
-static double FN(sfs_model_fn)(void* v, const REAL* dl) {
-    FN(sfs_ctx)* c = (FN(sfs_ctx)*)v;
+static double FN(model_rows)(FN(sfs_ctx)* c, const REAL* dl, int y0, int y1) {
     double acc = 0.0;
-    for (int y = 0; y < c->H; ++y)
+    for (int y = y0; y < y1; ++y)
         for (int x = 0; x < c->W; ++x) {
             if (FN(excl)(c, (long long)y * c->W + x)) continue;
             REAL s2 = (REAL)0.;
@@ -233,9 +232,8 @@ static void FN(gather)(const FN(sfs_ctx)* c, int x, int y, const REAL* p, REAL* 
     else *out0 = A;
 }
 
-static void FN(sfs_jtf_fn)(void* v, REAL* r, REAL* diag) {
-    FN(sfs_ctx)* c = (FN(sfs_ctx)*)v;
-    for (int y = 0; y < c->H; ++y)
+static void FN(jtf_rows)(FN(sfs_ctx)* c, REAL* r, REAL* diag, int y0, int y1) {
+    for (int y = y0; y < y1; ++y)
         for (int x = 0; x < c->W; ++x) {
             const long long k = (long long)y * c->W + x;
             REAL F = (REAL)0., D = (REAL)0.;
@@ -244,10 +242,9 @@ static void FN(sfs_jtf_fn)(void* v, REAL* r, REAL* diag) {
             diag[k] = D;
         }
 }
-static double FN(sfs_apply_fn)(void* v, const REAL* p, REAL* Ap) {
-    FN(sfs_ctx)* c = (FN(sfs_ctx)*)v;
+static double FN(apply_rows)(FN(sfs_ctx)* c, const REAL* p, REAL* Ap, int y0, int y1) {
     double dot = 0.0;
-    for (int y = 0; y < c->H; ++y)
+    for (int y = y0; y < y1; ++y)
         for (int x = 0; x < c->W; ++x) {
             const long long k = (long long)y * c->W + x;
             REAL a = (REAL)0.;
@@ -259,6 +256,53 @@ static double FN(sfs_apply_fn)(void* v, const REAL* p, REAL* Ap) {
         }
     return dot;
 }
+/* ---- row slabs over threads, per-thread partial sums added in thread order
+ * (backend_cpu_mt.t:350-414, 716-737); one thread is the whole image in row order ---- */
+typedef struct {
+    FN(sfs_ctx) * c;
+    int op, y0, y1;
+    const REAL* in;
+    REAL *o0, *o1;
+    double acc;
+} FN(sjob);
+static void* FN(sjob_run)(void* v) {
+    FN(sjob)* j = (FN(sjob)*)v;
+    switch (j->op) {
+        case 0: FN(pre_rows)(j->c, j->y0, j->y1); break;
+        case 1: j->acc = FN(cost_rows)(j->c, j->y0, j->y1); break;
+        case 2: j->acc = FN(model_rows)(j->c, j->in, j->y0, j->y1); break;
+        case 3: FN(jtf_rows)(j->c, j->o0, j->o1, j->y0, j->y1); break;
+        default: j->acc = FN(apply_rows)(j->c, j->in, j->o0, j->y0, j->y1); break;
+    }
+    return NULL;
+}
+static double FN(spar)(FN(sfs_ctx)* c, int op, const REAL* in, REAL* o0, REAL* o1) {
+    int nt = c->nthreads < 1 ? 1 : c->nthreads;
+    if (nt > c->H) nt = c->H;
+    FN(sjob)* J = (FN(sjob)*)calloc(nt, sizeof(FN(sjob)));
+    pthread_t* th = (pthread_t*)calloc(nt, sizeof(pthread_t));
+    for (int t = 0; t < nt; ++t) {
+        J[t].c = c; J[t].op = op; J[t].in = in; J[t].o0 = o0; J[t].o1 = o1;
+        J[t].y0 = t * (c->H / nt);
+        J[t].y1 = t == nt - 1 ? c->H : (t + 1) * (c->H / nt);
+    }
+    if (nt == 1) FN(sjob_run)(&J[0]);
+    else {
+        for (int t = 0; t < nt; ++t) pthread_create(&th[t], NULL, FN(sjob_run), &J[t]);
+        for (int t = 0; t < nt; ++t) pthread_join(th[t], NULL);
+    }
+    double acc = 0.0;
+    for (int t = 0; t < nt; ++t) acc += J[t].acc;
+    free(J);
+    free(th);
+    return acc;
+}
+static void FN(sfs_precompute)(FN(sfs_ctx)* c) { FN(spar)(c, 0, NULL, NULL, NULL); }
+static double FN(sfs_cost_fn)(void* v) { return FN(spar)((FN(sfs_ctx)*)v, 1, NULL, NULL, NULL); }
+static double FN(sfs_model_fn)(void* v, const REAL* dl) { return FN(spar)((FN(sfs_ctx)*)v, 2, dl, NULL, NULL); }
+static void FN(sfs_jtf_fn)(void* v, REAL* r, REAL* diag) { FN(spar)((FN(sfs_ctx)*)v, 3, NULL, r, diag); }
+static double FN(sfs_apply_fn)(void* v, const REAL* p, REAL* Ap) { return FN(spar)((FN(sfs_ctx)*)v, 4, p, Ap, NULL); }
+
 static void FN(sfs_update_fn)(void* v, const REAL* d) {
     FN(sfs_ctx)* c = (FN(sfs_ctx)*)v;
     for (long long k = 0; k < (long long)c->W * c->H; ++k)

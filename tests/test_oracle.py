@@ -15,10 +15,13 @@ from oracle import oracle
 DIRS = [(1, 0), (-1, 0), (0, 1), (0, -1)]
 
 
-def residuals64(w, O, A):
-    """image_warping.t, restated independently in float64 (10 residuals per pixel)."""
+def residuals64(w, O, A, u_float_diff=False):
+    """image_warping.t, restated independently in float64 (10 residuals per pixel).
+    u_float_diff: UrShape differences as float subtractions (the generated code's Terra
+    operation on two float loads, o.t:2418-2470), as in the reference's doublePrecision."""
     W, H = w["W"], w["H"]
-    U = w["UrShape"].reshape(H, W, 2).astype(np.float64)
+    U32 = w["UrShape"].reshape(H, W, 2)
+    U = U32.astype(np.float64)
     C = w["Constraints"].reshape(H, W, 2).astype(np.float64)
     M = w["Mask"].reshape(H, W)
     O = O.reshape(H, W, 2)
@@ -35,7 +38,7 @@ def residuals64(w, O, A):
                 tx, ty = x + sx, y + sy
                 if not (0 <= tx < W and 0 <= ty < H) or not act[ty, tx]:
                     continue
-                d = U[y, x] - U[ty, tx]
+                d = (U32[y, x] - U32[ty, tx]).astype(np.float64) if u_float_diff else U[y, x] - U[ty, tx]
                 rot = np.array([c * d[0] - s * d[1], s * d[0] + c * d[1]])
                 res[y, x, 2 * k:2 * k + 2] = wr * ((O[y, x] - O[ty, tx]) - rot)
             if C[y, x, 0] >= 0 and C[y, x, 1] >= 0:
@@ -62,17 +65,18 @@ def unknown_vec(w):
     return np.concatenate([w["Offset"].astype(np.float64), w["Angle"].astype(np.float64)]), N
 
 
-def jacobian64(w):
+def jacobian64(w, u_float_diff=False):
     x0, N = unknown_vec(w)
     n = x0.size
-    r0 = residuals64(w, x0[:2 * N], x0[2 * N:])
+    res = lambda O, A: residuals64(w, O, A, u_float_diff)   # noqa: E731
+    r0 = res(x0[:2 * N], x0[2 * N:])
     J = np.zeros((r0.size, n))
     h = 1e-6
     for j in range(n):
         xp, xm = x0.copy(), x0.copy()
         xp[j] += h
         xm[j] -= h
-        J[:, j] = (residuals64(w, xp[:2 * N], xp[2 * N:]) - residuals64(w, xm[:2 * N], xm[2 * N:])) / (2 * h)
+        J[:, j] = (res(xp[:2 * N], xp[2 * N:]) - res(xm[:2 * N], xm[2 * N:])) / (2 * h)
     return J, r0
 
 
@@ -186,3 +190,58 @@ def test_fp32_noise_floor_of_the_gn_trajectory():
     _, _, s0, _ = oracle.iw_solve(w, 1, 2)
     _, _, s1, _ = oracle.iw_solve(w2, 1, 2)
     assert abs(s1[1] - s0[1]) / s0[1] < 1e-4   # one short-PCG step stays tight
+
+
+# ---------------------------------------------------------------- opt_float = double
+def test_double_oracle_matches_the_float64_restatement():
+    """doublePrecision (Opt.h:11-14): the double instantiation of the same body
+    (oracle/iw_impl.h) against the float64 restatement and its central-difference
+    Jacobian at fp64 tolerances (the float form meets them only at 1e-5)."""
+    w = small_problem()
+    x0, N = unknown_vec(w)
+    r64 = residuals64(w, x0[:2 * N], x0[2 * N:], u_float_diff=True)
+    assert oracle.iw_cost(w, double=True) == pytest.approx(0.5 * np.sum(r64 ** 2), rel=1e-13)
+    J, r0 = jacobian64(w, u_float_diff=True)
+    act = active_unknowns(w)
+    g = J.T @ r0
+    r, pre, rz = oracle.iw_eval_jtf(w, double=True)
+    assert r.dtype == np.float64
+    np.testing.assert_allclose(r[act], -g[act], atol=1e-7 * np.abs(g).max())
+    diag = np.sum(J * J, axis=0)
+    np.testing.assert_allclose(pre[act], 1.0 / (1.0 + np.sqrt(diag[act])) ** 2, rtol=1e-7)
+    assert rz == pytest.approx(float(np.sum(r * pre * r)), rel=1e-13)
+    p = np.random.default_rng(7).normal(size=J.shape[1])
+    p[~act] = 0
+    Ap, pAp = oracle.iw_apply_jtj(w, p, double=True)
+    ref = J.T @ (J @ p)
+    np.testing.assert_allclose(Ap[act], ref[act], atol=1e-7 * np.abs(ref).max())
+    assert np.all(Ap[~act] == 0)
+    assert pAp == pytest.approx(float(p @ ref), rel=1e-8)
+    # the double form of the GN-quadratic model cost and the raw diagonal
+    d = 0.05 * np.random.default_rng(5).normal(size=act.size)
+    d[~act] = 0
+    rg, dg = oracle.iw_jtf_diag(w, double=True)
+    Ad, _ = oracle.iw_apply_jtj(w, d, double=True)
+    quad = oracle.iw_cost(w, double=True) - float(rg @ d) + 0.5 * float(d @ Ad)
+    assert oracle.iw_model_cost(w, d, double=True) == pytest.approx(quad, rel=1e-12)
+    np.testing.assert_allclose(dg[act], diag[act], rtol=1e-7)
+
+
+def test_double_gn_loops_agree_and_track_the_float_loop():
+    w = workloads.image_warping(40, 30, seed=5, n_handles=5)
+    O1, A1, c1, _ = oracle.iw_solve(w, 3, 10, double=True)
+    O2, A2, c2 = oracle.iw_solve_generic(w, 3, 10, lm=False, double=True)
+    # the same double operations; only the dot products' summation order differs (pixel
+    # order vs vector-layout order), which float's rounding of alpha / beta hides and
+    # double's does not (a 1e-16 change moves this trajectory by ~1e-12)
+    np.testing.assert_allclose(c2, c1, rtol=1e-10)
+    np.testing.assert_allclose(O2, O1, rtol=0, atol=1e-10 * np.abs(O1).max())
+    _, _, c4, _ = oracle.iw_solve(w, 3, 10, nthreads=4, double=True)
+    np.testing.assert_allclose(c4, c1, rtol=1e-10)
+    assert c1[0] > c1[1] > c1[2] > c1[3]
+    # one short-PCG GN step: float and double agree to the float rounding of the inputs
+    _, _, s32, _ = oracle.iw_solve(w, 1, 2)
+    _, _, s64, _ = oracle.iw_solve(w, 1, 2, double=True)
+    assert abs(s32[1] - s64[1]) / s64[1] < 1e-5
+    _, _, cl = oracle.iw_solve_generic(w, 4, 10, lm=True, double=True)
+    assert cl[-1] < cl[0]

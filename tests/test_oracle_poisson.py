@@ -70,3 +70,37 @@ def test_gn_and_lm_decrease_cost():
     assert len(c) == 3 and c[1] < c[0] and c[2] <= c[1]
     _, c = oracle.pie_solve(w, 3, 10, lm=True)
     assert c[-1] < c[0]
+
+
+def test_double_oracle_against_fd():
+    """opt_float = double: X and the solver in double, T / M float (oracle/pie_impl.h)."""
+    w = small()
+    W, H = w["W"], w["H"]
+    act_px = w["M"] == 0
+    act = np.repeat(act_px, 4)
+    x0 = w["X"].astype(np.float64)
+    res = residuals64(w, x0)
+    assert oracle.pie_cost(w, double=True) == pytest.approx(0.5 * float(np.sum(res.reshape(H * W, 16)[act_px] ** 2)),
+                                                           rel=1e-13)
+    n = x0.size
+    J = np.zeros((res.size, n))
+    for j in range(n):   # the residuals are linear: central differences are exact up to rounding
+        xp, xm = x0.copy(), x0.copy()
+        xp[j] += 0.5
+        xm[j] -= 0.5
+        J[:, j] = (residuals64(w, xp) - residuals64(w, xm)).ravel()
+    g = J.T @ res.ravel()
+    r, dg = oracle.pie_jtf(w, double=True)
+    assert r.dtype == np.float64
+    np.testing.assert_allclose(r[act], -g[act], atol=1e-12 * np.abs(g).max())
+    np.testing.assert_array_equal(dg[act], np.sum(J * J, axis=0)[act])
+    p = np.random.default_rng(1).normal(size=n)
+    p[~act] = 0
+    Ap, pAp = oracle.pie_apply(w, p, double=True)
+    ref = J.T @ (J @ p)
+    np.testing.assert_allclose(Ap[act], ref[act], atol=1e-12 * np.abs(ref).max())
+    assert pAp == pytest.approx(float(p @ ref), rel=1e-12)
+    Xd, cd = oracle.pie_solve(w, 2, 10, double=True)
+    _, cf = oracle.pie_solve(w, 2, 10)
+    assert Xd.dtype == np.float64 and cd[-1] < cd[0]
+    np.testing.assert_allclose(cf, cd, rtol=1e-5)

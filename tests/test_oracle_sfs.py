@@ -171,3 +171,15 @@ def test_lm_and_gn_decrease_cost_on_reference_inputs():
     assert np.all(np.diff(c) <= 0) and c[-1] < c[0]
     _, c = oracle.sfs_solve(w, 2, 10, lm=False)
     assert c[-1] < c[0]
+
+
+@pytest.mark.parametrize("double", [False, True])
+def test_threaded_solve_matches_one_thread(double):
+    """The row-slab split over threads (bench.py's config-3 CPU comparator,
+    backend_cpu_mt.t:716-737): same per-pixel values, only the sums' order changes."""
+    w = workloads.shape_from_shading(96, 72, seed=3)
+    X1, c1 = oracle.sfs_solve(w, 3, 10, lm=True, double=double)
+    X4, c4 = oracle.sfs_solve(w, 3, 10, lm=True, double=double, nthreads=4)
+    assert len(c1) == len(c4)
+    np.testing.assert_allclose(c4, c1, rtol=1e-10 if double else 1e-5)
+    np.testing.assert_allclose(X4, X1, rtol=0, atol=(1e-10 if double else 1e-5) * np.abs(X1).max())

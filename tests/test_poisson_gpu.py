@@ -78,3 +78,39 @@ def test_config1_cpu_backend_512():
     np.testing.assert_allclose(costs, c_ref, rtol=1e-5)
     assert costs[1] < costs[0]
     assert rel_err(X, X_ref) < 1e-5
+
+
+@pytest.mark.parametrize("kind,nit,lit", [("gaussNewtonGPU", 3, 10), ("LMGPU", 4, 10)])
+@pytest.mark.parametrize("W,H", [(64, 48), (97, 61), (130, 7)])
+def test_double_precision_matches_double_oracle(kind, nit, lit, W, H):
+    """doublePrecision (Opt.h:11-14): X and the solver in double, T / M float, against the
+    double oracle (oracle/pie_impl.h): J^T F, J^T J p within 1e-10 of their largest
+    magnitude, the cost within 1e-12, GN / LM trajectories and X within 1e-8."""
+    import torch
+
+    w = workloads.poisson_image_editing(W, H, seed=W + 2 * H)
+    rng = np.random.default_rng(4)
+    w["X"] = (w["X"] + rng.normal(0, 2, w["X"].shape)).astype(np.float32)
+    s = OptSolver([W, H], ENERGY, kind, double_precision=True)
+    prm = [torch.from_numpy(w["X"].astype(np.float64)).cuda()] + dev(w)[1:]
+    assert s.eval_cost(prm) == pytest.approx(oracle.pie_cost(w, double=True), rel=1e-12, abs=1e-12)
+    n = 4 * W * H
+    r = torch.zeros(n, device="cuda", dtype=torch.float64)
+    pre = torch.zeros(n, device="cuda", dtype=torch.float64)
+    s.eval_jtf(prm, r, pre)
+    r_ref, _ = oracle.pie_jtf(w, double=True)
+    assert rel_err(to_np(r), r_ref) < 1e-10
+    act = np.repeat(w["M"] == 0, 4)
+    p = rng.normal(size=n)
+    p[~act] = 0
+    Ap = torch.zeros(n, device="cuda", dtype=torch.float64)
+    pAp = s.apply_jtj(prm, torch.from_numpy(p).cuda(), Ap)
+    Ap_ref, pAp_ref = oracle.pie_apply(w, p, double=True)
+    assert rel_err(to_np(Ap), Ap_ref) < 1e-10
+    assert pAp == pytest.approx(pAp_ref, rel=1e-10)
+    s.set_solver_params({"nIterations": nit, "lIterations": lit})
+    costs = s.profiled_solve(prm)
+    X_ref, c_ref = oracle.pie_solve(w, nit, lit, lm=(kind == "LMGPU"), double=True)
+    assert len(costs) == len(c_ref)
+    np.testing.assert_allclose(costs, c_ref, rtol=1e-8)
+    assert rel_err(to_np(prm[0]), X_ref) < 1e-8
