@@ -921,9 +921,11 @@ std::unique_ptr<Plan> make_arap_plan(const ProblemSpec& spec, const StateOptions
         if (d.name == spec.graphs[0].dims[0]) E = dims[d.index];
     }
     if (N == 0) { *err = "arap_mesh_deformation: zero vertices"; return nullptr; }
-    // 24 N bytes (arap::gld3) and 9 N sizeof(T) bytes (arap::gldq, the K planes) must fit the
-    // gathers' 32-bit offsets: at most 2^25 vertices
-    if (N > (1u << 25) || E > (1u << 30)) { *err = "arap_mesh_deformation: graph too large"; return nullptr; }
+    // 3 N sizeof(T) bytes (arap::gld3 of p / delta; UrShape and Constraints are float) and
+    // 9 N sizeof(T) bytes (arap::gldq, the K planes) must fit the gathers' 32-bit offsets:
+    // at most ~119 M vertices in fp32, ~59.6 M in fp64
+    const unsigned long long kbytes = 9ULL * N * (opts.double_precision ? sizeof(double) : sizeof(float));
+    if (kbytes >= (1ULL << 32) || E > (1u << 30)) { *err = "arap_mesh_deformation: graph too large"; return nullptr; }
     Domain dom{(int)N, 1, 0, 1, 0, 1};
     dom.edges = (int)E;
     if (opts.double_precision) return make_stencil_plan<ArapOp<double>>(spec, opts, dom, err);

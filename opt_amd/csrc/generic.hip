@@ -358,6 +358,13 @@ public:
     void precompute(hipStream_t s) {
         for (hipFunction_t f : k_pre_) launch(f, s, {&a_});
     }
+    // The transcendental caches (the precompute kernels after the ComputedArrays' ones:
+    // the centred cache image, the graph record cache) from the arrays bound at this Step
+    // (StencilPlan::step; HasRefreshCaches). Returns whether any ran.
+    bool refresh_caches(hipStream_t s) {
+        for (size_t k = m_.computed.size(); k < k_pre_.size(); ++k) launch(k_pre_[k], s, {&a_});
+        return k_pre_.size() > m_.computed.size();
+    }
     // ComputedArray values and gradient images: exchanged after every precompute
     void computed_planes(std::vector<HaloPlane>& v) const {
         for (size_t i = 0; i < m_.images.size(); ++i)

@@ -205,7 +205,7 @@ __device__ __forceinline__ acc_t wdot3(T w0, T a0, T b0, T w1, T a1, T b1, T w2,
 
 // ------------------------------------------------------------ row records
 // Every stencil kernel keeps rows y-1, y, y+1 finished in registers and has row y+2
-// (DEPTH 2: also y+3) in flight: a raw row is issued as pure loads (no arithmetic on
+// in flight: a raw row is issued as pure loads (no arithmetic on
 // the loaded values, so no s_waitcnt there) and finished — combined, masked,
 // sin/cos — only after the current row has been computed, so each load has at least
 // a full row of compute to land. The strip's two outside neighbours (x0-1 for lane
@@ -349,7 +349,7 @@ __device__ __forceinline__ PRow<T> finish_prow(const Args<T>& a, const PRaw<T>& 
 // NT bit 0: streaming loads of the PCG vectors (raw_prow); bit 1: streaming stores.
 // SUMS (MODE 1): iteration 0 of iw_apply_res's loop when PCGInit1 is not fused with it
 // (row slabs): sc[rs.out + 0..2] = {p.Ap, r.W Ap, Ap.W Ap} in fp64, as iw_jtf_apply sums them.
-template <typename T, int MODE, int DM, int DEPTH, bool LMX = false, int NT = 0, bool SUMS = false>
+template <typename T, int MODE, int DM, bool LMX = false, int NT = 0, bool SUMS = false>
 __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restrict__ pin,
                                                    const T* __restrict__ r,
                                                    const T* __restrict__ pre, T* __restrict__ pout,
@@ -378,13 +378,10 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
         jedge(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, up.px, up.py, up.ux, up.uy,
               up.act && cur.act, wr, my_x, my_y, ax, ay);
         thm = -wr * (ax * my_x + ay * my_y);
-        PRaw<T> nx;
-        if (DEPTH == 2) nx = raw_prow<T, MODE, DM, (NT & 1) != 0>(a, g, g.y0 + 2, pin, r, pre, delta);
         for (int y = g.y0; y < g.y1; ++y) {
-            // DEPTH 1: row y+2 in flight during row y; DEPTH 2: rows y+2 and y+3
-            PRaw<T> nn;
-            if (DEPTH == 1) nx = raw_prow<T, MODE, DM, (NT & 1) != 0>(a, g, y + 2, pin, r, pre, delta);
-            else nn = raw_prow<T, MODE, DM, (NT & 1) != 0>(a, g, y + 3, pin, r, pre, delta);
+            // row y+2 in flight during row y (a second row in flight, y+3, was measured
+            // slower: more VGPRs, fewer waves)
+            const PRaw<T> nx = raw_prow<T, MODE, DM, (NT & 1) != 0>(a, g, y + 2, pin, r, pre, delta);
             // horizontal neighbours; the strip's outside columns enter at lanes 0 / 63
             const T lpx = from_left(cur.px, cur.epx), lpy = from_left(cur.py, cur.epy);
             const T rpx = from_right(cur.px, cur.epx), rpy = from_right(cur.py, cur.epy);
@@ -442,7 +439,6 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
             thm = -wr * (adn_x * jdn_x + adn_y * jdn_y);
             up = cur; cur = dn;
             dn = finish_prow<T, MODE, DM>(a, nx, beta, alpha);
-            if (DEPTH == 2) nx = nn;
         }
     }
     if constexpr (SUMS) {
@@ -501,7 +497,21 @@ __device__ __forceinline__ void stb(T* base, unsigned off, V v) {
     if constexpr (NT) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
-constexpr int kFStrip = 62;
+// iw_apply_res addresses an unknown-layout vector (3 N values), UrShape (8 B per pixel)
+// and the flags through 32-bit byte offsets: the plan runs it only when these fit
+template <typename T>
+constexpr bool offsets_fit_32(long long npix) {
+    return 3 * npix * (long long)sizeof(T) < (1LL << 32) && 8 * npix < (1LL << 32);
+}
+static_assert(offsets_fit_32<float>(4096LL * 4096) && offsets_fit_32<double>(4096LL * 4096), "headline sizes");
+static_assert(!offsets_fit_32<double>(180000000LL) && offsets_fit_32<float>(357000000LL) &&
+              !offsets_fit_32<float>(358000000LL), "fp64 bound ~179 M px, fp32 ~358 M px");
+// iw_jtf_apply's strips: 60 output columns per wavefront, x = 60 strip - 2 + lane. J^T F
+// is valid at lanes 1..62 (lanes 0 / 63 lack a lane neighbour), the apply at lanes 2..61:
+// no edge record at all (round 3's 62-column form carried one for J^T F at lanes 0 / 63,
+// which cost a second sincos per lane, five more loads per row and 21 VGPRs: 146 VGPRs,
+// 3 waves per SIMD)
+constexpr int kFStrip = 60;
 template <typename T>
 __device__ __forceinline__ WaveGeom geom_fused(const Args<T>& a) {
     WaveGeom g;
@@ -510,12 +520,12 @@ __device__ __forceinline__ WaveGeom geom_fused(const Args<T>& a) {
     const int strip = t % a.nstrips, rb = t / a.nstrips;
     g.lane = threadIdx.x & (kWave - 1);
     const int w = threadIdx.x / kWave;
-    g.x = strip * kFStrip - 1 + g.lane;
-    g.edge_lane = (g.lane == 0) || (g.lane == kWave - 1);
-    g.ex = g.lane == 0 ? g.x - 1 : g.x + 1;
+    g.x = strip * kFStrip - 2 + g.lane;
+    g.edge_lane = false;
+    g.ex = g.x;
     g.y0 = a.dom.y_lo + (rb * (kBlock / kWave) + w) * a.rows;
     g.y1 = min(g.y0 + a.rows, a.dom.y_hi);
-    g.out_lane = g.lane >= 1 && g.lane <= kFStrip && g.x < a.dom.W;
+    g.out_lane = g.lane >= 2 && g.lane < 2 + kFStrip && g.x < a.dom.W;
     return g;
 }
 template <typename T>
@@ -774,7 +784,9 @@ struct VRow {
     int eact;
     T ec, es;          // its cos / sin (only the J^T F kernel needs them)
 };
-template <typename T, bool EDGE_ANGLE>
+// EDGE: the strip's two outside columns ride along (lanes 0 / 63); EDGE_ANGLE: with
+// their angle (only J^T F needs it)
+template <typename T, bool EDGE_ANGLE, bool EDGE = true>
 __device__ __forceinline__ VRaw<T> raw_vrow(const Args<T>& a, const WaveGeom& g, int y) {
     VRaw<T> q;
     q.in = present(a.dom, g.x, y);
@@ -785,7 +797,7 @@ __device__ __forceinline__ VRaw<T> raw_vrow(const Args<T>& a, const WaveGeom& g,
     q.c = reinterpret_cast<const float2*>(a.C)[i];
     q.m = a.M[i];
     q.ein = 0;
-    if (g.edge_lane) {
+    if (EDGE && g.edge_lane) {
         q.ein = present(a.dom, g.ex, y);
         const long long e = q.ein ? a.dom.off(g.ex, y) : 0;
         q.eo = reinterpret_cast<const Vec2<T>*>(a.O)[e];
@@ -795,7 +807,7 @@ __device__ __forceinline__ VRaw<T> raw_vrow(const Args<T>& a, const WaveGeom& g,
     }
     return q;
 }
-template <typename T, bool EDGE_ANGLE>
+template <typename T, bool EDGE_ANGLE, bool EDGE = true>
 __device__ __forceinline__ VRow<T> finish_vrow(const VRaw<T>& r) {
     VRow<T> q;
     q.ox = r.in ? r.o.x : (T)0;
@@ -806,6 +818,10 @@ __device__ __forceinline__ VRow<T> finish_vrow(const VRaw<T>& r) {
     q.act = r.in && (r.m == 0.f);
     q.fit = (q.cx >= 0.f) && (q.cy >= 0.f);
     sc_of(q.t, &q.c, &q.s);
+    if (!EDGE) {
+        q.eox = 0; q.eoy = 0; q.eux = 0.f; q.euy = 0.f; q.eact = 0; q.ec = 0; q.es = 0;
+        return q;
+    }
     q.eox = r.ein ? r.eo.x : (T)0;
     q.eoy = r.ein ? r.eo.y : (T)0;
     q.eux = r.ein ? r.eu.x : 0.f; q.euy = r.ein ? r.eu.y : 0.f;
@@ -845,7 +861,9 @@ struct JRow {
     T fx, fy, ft, dt;
     int nv;
 };
-template <typename T>
+// EDGE = false (iw_jtf_apply): no outside columns; the values at lanes 0 / 63 are
+// meaningless and unused.
+template <typename T, bool EDGE = true>
 __device__ __forceinline__ JRow<T> jtf_row(const Args<T>& a, const VRow<T>& cur, const VRow<T>& dn,
                                            JCarry<T>& k) {
     const T wr = a.wr, wf = a.wf, wr2 = a.wr * a.wr;
@@ -868,8 +886,12 @@ __device__ __forceinline__ JRow<T> jtf_row(const Args<T>& a, const VRow<T>& cur,
     eedge(dn.ox, dn.oy, dn.c, dn.s, dn.ux, dn.uy, cur.ox, cur.oy, cur.ux, cur.uy, vpy, wr,
           edn_x, edn_y, adn_x, adn_y);
     // the strip's outside neighbour's residual pointing at lane 0 / 63
-    eedge(cur.eox, cur.eoy, cur.ec, cur.es, cur.eux, cur.euy, cur.ox, cur.oy, cur.ux, cur.uy,
-          cur.eact && cur.act, wr, ee_x, ee_y, ax, ay);
+    if (EDGE) {
+        eedge(cur.eox, cur.eoy, cur.ec, cur.es, cur.eux, cur.euy, cur.ox, cur.oy, cur.ux, cur.uy,
+              cur.eact && cur.act, wr, ee_x, ee_y, ax, ay);
+    } else {
+        ee_x = 0; ee_y = 0;
+    }
     const T inpx_x = from_right(emx_x, ee_x), inpx_y = from_right(emx_y, ee_y);
     const T inmx_x = from_left(epx_x, ee_x), inmx_y = from_left(epx_y, ee_y);
     o.fx = wr * ((epx_x + emx_x + epy_x + k.my_x) - (inpx_x + inmx_x + edn_x + k.inup_x));
@@ -993,11 +1015,16 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
 // rz[0] down to rz[1], 2e4 x smaller on the test problems).
 template <typename T>
 struct FRow {          // a finished row of the fused kernel's apply window
-    T px, py, pt, c, s;
-    T rx, ry, rt;      // r_0
-    T w0, w2;          // PCGStep2's weights (pre, or 1 without a preconditioner)
+    T rx, ry, rt;      // r_0 (0 on inactive pixels)
+    T wo, wt;          // the preconditioner of the Offset / angle channels
+    T c, s;
     float ux, uy;
-    int act, fit;
+    bool act, fit;
+    // p_0 = pre r_0, formed where it is used (iw_apply<1>'s make_p: zero on inactive pixels,
+    // where r_0 = pre = 0): three multiplies instead of three more VGPRs per held row
+    __device__ __forceinline__ T px() const { return wo * rx; }
+    __device__ __forceinline__ T py() const { return wo * ry; }
+    __device__ __forceinline__ T pt() const { return wt * rt; }
 };
 template <typename T, int NT = 2>
 __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_jtf_apply(Args<T> a, T* __restrict__ r, T* __restrict__ pre,
@@ -1011,7 +1038,7 @@ __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_jtf_apply(Args<T> a, 
     // J^T F of row y from the window (cur = row y, dn = row y+1): stores r / pre / flags
     // when the row is this wave's, returns the apply's view of the row (p = pre r)
     auto jrow = [&](const VRow<T>& cur, const VRow<T>& dn, JCarry<T>& k, int y, bool own) {
-        const JRow<T> j = jtf_row(a, cur, dn, k);
+        const JRow<T> j = jtf_row<T, false>(a, cur, dn, k);
         const JOut<T> o = jtf_out(a, cur, j);
         if (own && g.out_lane) {
             const long long i = a.dom.off(g.x, y);
@@ -1022,57 +1049,53 @@ __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_jtf_apply(Args<T> a, 
             if (cur.act) rzdot += wdot3(o.wo, o.rx, o.rx, o.wo, o.ry, o.ry, o.wt, o.rt, o.rt);
         }
         FRow<T> p;
-        // iw_apply<1>'s make_p: p = pre r per channel (zero on inactive pixels)
-        p.px = o.wo * o.rx; p.py = o.wo * o.ry; p.pt = o.wt * o.rt;
-        if (!cur.act) { p.px = 0; p.py = 0; p.pt = 0; }
+        p.rx = o.rx; p.ry = o.ry; p.rt = o.rt; p.wo = o.wo; p.wt = o.wt;
         p.c = cur.c; p.s = cur.s; p.ux = cur.ux; p.uy = cur.uy; p.act = cur.act; p.fit = cur.fit;
-        p.w0 = a.use_pre ? o.wo : (T)1;
-        p.w2 = a.use_pre ? o.wt : (T)1;
-        p.rx = o.rx; p.ry = o.ry; p.rt = o.rt;
         return p;
     };
     if (g.y0 < g.y1) {
-        const VRow<T> vm2 = finish_vrow<T, true>(raw_vrow<T, true>(a, g, g.y0 - 2));
-        VRow<T> vcur = finish_vrow<T, true>(raw_vrow<T, true>(a, g, g.y0 - 1));
-        VRow<T> vdn = finish_vrow<T, true>(raw_vrow<T, true>(a, g, g.y0));
+        const VRow<T> vm2 = finish_vrow<T, false, false>(raw_vrow<T, false, false>(a, g, g.y0 - 2));
+        VRow<T> vcur = finish_vrow<T, false, false>(raw_vrow<T, false, false>(a, g, g.y0 - 1));
+        VRow<T> vdn = finish_vrow<T, false, false>(raw_vrow<T, false, false>(a, g, g.y0));
         JCarry<T> k = jcarry_init(vm2, vcur, wr);
         FRow<T> up = jrow(vcur, vdn, k, g.y0 - 1, false);
         vcur = vdn;
-        vdn = finish_vrow<T, true>(raw_vrow<T, true>(a, g, g.y0 + 1));
+        vdn = finish_vrow<T, false, false>(raw_vrow<T, false, false>(a, g, g.y0 + 1));
         FRow<T> cur = jrow(vcur, vdn, k, g.y0, true);
         vcur = vdn;
-        vdn = finish_vrow<T, true>(raw_vrow<T, true>(a, g, g.y0 + 2));
+        vdn = finish_vrow<T, false, false>(raw_vrow<T, false, false>(a, g, g.y0 + 2));
         // apply carries from the row above: J(up->cur) and J(cur->up) with its angle term
         T in_up_x, in_up_y, my_x, my_y, thm, ax, ay;
-        jedge(up.px, up.py, up.pt, up.c, up.s, up.ux, up.uy, cur.px, cur.py, cur.ux, cur.uy,
+        jedge(up.px(), up.py(), up.pt(), up.c, up.s, up.ux, up.uy, cur.px(), cur.py(), cur.ux, cur.uy,
               up.act && cur.act, wr, in_up_x, in_up_y, ax, ay);
-        jedge(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, up.px, up.py, up.ux, up.uy,
+        jedge(cur.px(), cur.py(), cur.pt(), cur.c, cur.s, cur.ux, cur.uy, up.px(), up.py(), up.ux, up.uy,
               up.act && cur.act, wr, my_x, my_y, ax, ay);
         thm = -wr * (ax * my_x + ay * my_y);
         for (int y = g.y0; y < g.y1; ++y) {
-            const VRaw<T> nx = raw_vrow<T, true>(a, g, y + 3);
+            const VRaw<T> nx = raw_vrow<T, false, false>(a, g, y + 3);
             const FRow<T> dn = jrow(vcur, vdn, k, y + 1, y + 1 < g.y1);
-            // iw_apply's row body; lanes 0 / 63 are not outputs, so no edge operand
-            const T lpx = from_left(cur.px, (T)0), lpy = from_left(cur.py, (T)0);
-            const T rpx = from_right(cur.px, (T)0), rpy = from_right(cur.py, (T)0);
+            const T cpx = cur.px(), cpy = cur.py(), cpt = cur.pt(), dpx = dn.px(), dpy = dn.py(), dpt = dn.pt();
+            // iw_apply's row body; lanes 0, 1, 62, 63 are not outputs, so no edge operand
+            const T lpx = from_left(cpx, (T)0), lpy = from_left(cpy, (T)0);
+            const T rpx = from_right(cpx, (T)0), rpy = from_right(cpy, (T)0);
             const float lux = from_left(cur.ux, 0.f), luy = from_left(cur.uy, 0.f);
             const float rux = from_right(cur.ux, 0.f), ruy = from_right(cur.uy, 0.f);
             const int lact = from_left_i(cur.act, 0), ract = from_right_i(cur.act, 0);
             T jpx_x, jpx_y, apx_x, apx_y, jmx_x, jmx_y, amx_x, amx_y;
             T jpy_x, jpy_y, apy_x, apy_y, jdn_x, jdn_y, adn_x, adn_y;
-            jedge(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, rpx, rpy, rux, ruy,
+            jedge(cpx, cpy, cpt, cur.c, cur.s, cur.ux, cur.uy, rpx, rpy, rux, ruy,
                   cur.act && ract, wr, jpx_x, jpx_y, apx_x, apx_y);
-            jedge(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, lpx, lpy, lux, luy,
+            jedge(cpx, cpy, cpt, cur.c, cur.s, cur.ux, cur.uy, lpx, lpy, lux, luy,
                   cur.act && lact, wr, jmx_x, jmx_y, amx_x, amx_y);
-            jedge(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, dn.px, dn.py, dn.ux, dn.uy,
+            jedge(cpx, cpy, cpt, cur.c, cur.s, cur.ux, cur.uy, dpx, dpy, dn.ux, dn.uy,
                   cur.act && dn.act, wr, jpy_x, jpy_y, apy_x, apy_y);
-            jedge(dn.px, dn.py, dn.pt, dn.c, dn.s, dn.ux, dn.uy, cur.px, cur.py, cur.ux, cur.uy,
+            jedge(dpx, dpy, dpt, dn.c, dn.s, dn.ux, dn.uy, cpx, cpy, cur.ux, cur.uy,
                   cur.act && dn.act, wr, jdn_x, jdn_y, adn_x, adn_y);
             const T inpx_x = from_right(jmx_x, (T)0), inpx_y = from_right(jmx_y, (T)0);
             const T inmx_x = from_left(jpx_x, (T)0), inmx_y = from_left(jpx_y, (T)0);
             T aox = wr * ((jpx_x + jmx_x + jpy_x + my_x) - (inpx_x + inmx_x + jdn_x + in_up_x));
             T aoy = wr * ((jpx_y + jmx_y + jpy_y + my_y) - (inpx_y + inmx_y + jdn_y + in_up_y));
-            if (cur.fit) { aox += wf2 * cur.px; aoy += wf2 * cur.py; }
+            if (cur.fit) { aox += wf2 * cpx; aoy += wf2 * cpy; }
             T aot = thm - wr * ((apx_x * jpx_x + apx_y * jpx_y) + (amx_x * jmx_x + amx_y * jmx_y) +
                                 (apy_x * jpy_x + apy_y * jpy_y));
             if (!cur.act) { aox = 0; aoy = 0; aot = 0; }
@@ -1082,18 +1105,20 @@ __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_jtf_apply(Args<T> a, 
                     st_v<(NT & 2) != 0>(Ap + 2 * i, aox); st_v<(NT & 2) != 0>(Ap + 2 * i + 1, aoy);
                     st_v<(NT & 2) != 0>(Ap + 2 * N + i, aot);
                 }
-                st_v<(NT & 2) != 0>(pout + 2 * i, cur.px); st_v<(NT & 2) != 0>(pout + 2 * i + 1, cur.py);
-                st_v<(NT & 2) != 0>(pout + 2 * N + i, cur.pt);
-                papdot += (acc_t)(cur.px * aox + cur.py * aoy + cur.pt * aot);
-                rapd += wdot3(cur.w0, cur.rx, aox, cur.w0, cur.ry, aoy, cur.w2, cur.rt, aot);
-                apapd += wdot3(cur.w0, aox, aox, cur.w0, aoy, aoy, cur.w2, aot, aot);
+                st_v<(NT & 2) != 0>(pout + 2 * i, cpx); st_v<(NT & 2) != 0>(pout + 2 * i + 1, cpy);
+                st_v<(NT & 2) != 0>(pout + 2 * N + i, cpt);
+                papdot += (acc_t)(cpx * aox + cpy * aoy + cpt * aot);
+                // PCGStep2's weights: pre, or 1 without a preconditioner
+                const T w0 = a.use_pre ? cur.wo : (T)1, w2 = a.use_pre ? cur.wt : (T)1;
+                rapd += wdot3(w0, cur.rx, aox, w0, cur.ry, aoy, w2, cur.rt, aot);
+                apapd += wdot3(w0, aox, aox, w0, aoy, aoy, w2, aot, aot);
             }
             in_up_x = jpy_x; in_up_y = jpy_y;
             my_x = jdn_x; my_y = jdn_y;
             thm = -wr * (adn_x * jdn_x + adn_y * jdn_y);
             cur = dn;
             vcur = vdn;
-            vdn = finish_vrow<T, true>(nx);
+            vdn = finish_vrow<T, false, false>(nx);
         }
     }
     double v[4] = {(double)rzdot, (double)papdot, (double)rapd, (double)apapd};
@@ -1280,8 +1305,9 @@ __global__ __launch_bounds__(kBlock) void iw_flags(Args<T> a) {
 
 // --------------------------------------------------------------- update kernel
 // delta_L of one element: (the deferred alpha_{L-2} p_{L-2} term first, E2), then
-// alpha_{L-1} p_{L-1}; every term an explicit fma onto the pending delta (shared by
-// iw_update and iw_update_cost, so both form the same bits)
+// alpha_{L-1} p_{L-1}; every term an explicit fma onto the pending delta, as
+// iw_apply_res forms the terms it folds, so the deferred delta is bitwise the
+// per-iteration one
 template <typename T, bool HAS_DELTA, bool E2>
 __device__ __forceinline__ T upd_delta(T alpha, T q, T alpha2, T q2, T d) {
     if (E2) d = HAS_DELTA ? fmad(alpha2, q2, d) : alpha2 * q2;
@@ -1324,137 +1350,6 @@ __global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O
             A[i] = t + dt;
         }
     }
-}
-
-// ------------------------------------------------- update + cost in one strip pass
-// iw_update followed by iw_cost (PCGLinearUpdate, then computeCost at the updated
-// unknowns, solverGPUGaussNewton.t:854-859, :2245) as one pass over the cost's strips:
-// each row is loaded once with delta / p_{L-1} / p_{L-2}, updated in registers (the same
-// upd_delta fmas and o + d as iw_update) and the cost is evaluated from the updated rows
-// (the same expressions and order as iw_cost, the same tiles and reduction slots, so
-// the cost is bitwise iw_cost's). Neighbouring waves read a wave's first / last row and
-// its strip's outer columns (halo rows, edge records) before or after it updates them:
-// those pixels' new Offsets go to `ob` and iw_update_fixup copies them after the pass;
-// every other Offset and every Angle (nobody else reads a pixel's angle) is written in
-// place. O / A alias a.O / a.A: no __restrict__ on them.
-#ifndef IW_UC_DEPTH
-#define IW_UC_DEPTH 1   // rows in flight beyond y + 1
-#endif
-template <typename T>
-struct URaw {
-    VRaw<T> v;
-    Vec2<T> d, q, q2, ed, eq, eq2;
-    T dt, qt, q2t;
-};
-template <typename T, bool HAS_DELTA, bool E2>
-__global__ __launch_bounds__(kBlock) void iw_update_cost(Args<T> a, T* O, T* A, const T* __restrict__ delta,
-                                                         const T* __restrict__ p, const double* __restrict__ sc,
-                                                         int ia_num, int ia_den, const T* __restrict__ p2,
-                                                         int ia2_num, int ia2_den, T* __restrict__ ob,
-                                                         ReduceSlot rs) {
-    const WaveGeom g = geom(a);
-    const long long N = a.dom.npix_mem();
-    const T alpha = (T)(sc[ia_num] / sc[ia_den]);
-    const T alpha2 = E2 ? (T)(sc[ia2_num] / sc[ia2_den]) : (T)0;
-    const T wr = a.wr, wf = a.wf;
-    auto raw = [&](int y) {
-        URaw<T> q;
-        q.v = raw_vrow<T, false>(a, g, y);
-        const long long i = q.v.in ? a.dom.off(g.x, y) : 0;
-        q.q = reinterpret_cast<const Vec2<T>*>(p)[i];
-        q.qt = p[2 * N + i];
-        if (HAS_DELTA) { q.d = reinterpret_cast<const Vec2<T>*>(delta)[i]; q.dt = delta[2 * N + i]; }
-        if (E2) { q.q2 = reinterpret_cast<const Vec2<T>*>(p2)[i]; q.q2t = p2[2 * N + i]; }
-        if (g.edge_lane) {
-            const long long e = q.v.ein ? a.dom.off(g.ex, y) : 0;
-            q.eq = reinterpret_cast<const Vec2<T>*>(p)[e];
-            if (HAS_DELTA) q.ed = reinterpret_cast<const Vec2<T>*>(delta)[e];
-            if (E2) q.eq2 = reinterpret_cast<const Vec2<T>*>(p2)[e];
-        }
-        return q;
-    };
-    auto fin = [&](URaw<T> q) {
-        if (!HAS_DELTA) { q.d = Vec2<T>{0, 0}; q.dt = 0; q.ed = Vec2<T>{0, 0}; }
-        if (!E2) { q.q2 = Vec2<T>{0, 0}; q.q2t = 0; q.eq2 = Vec2<T>{0, 0}; }
-        if (q.v.in && q.v.m == 0.f) {   // flags bit 0: inside and Mask == 0
-            q.v.o.x = q.v.o.x + upd_delta<T, HAS_DELTA, E2>(alpha, q.q.x, alpha2, q.q2.x, q.d.x);
-            q.v.o.y = q.v.o.y + upd_delta<T, HAS_DELTA, E2>(alpha, q.q.y, alpha2, q.q2.y, q.d.y);
-            q.v.t = q.v.t + upd_delta<T, HAS_DELTA, E2>(alpha, q.qt, alpha2, q.q2t, q.dt);
-        }
-        if (g.edge_lane && q.v.ein && q.v.em == 0.f) {
-            q.v.eo.x = q.v.eo.x + upd_delta<T, HAS_DELTA, E2>(alpha, q.eq.x, alpha2, q.eq2.x, q.ed.x);
-            q.v.eo.y = q.v.eo.y + upd_delta<T, HAS_DELTA, E2>(alpha, q.eq.y, alpha2, q.eq2.y, q.ed.y);
-        }
-        return finish_vrow<T, false>(q.v);
-    };
-    T acc = 0;
-    if (g.y0 < g.y1) {
-        VRow<T> up = fin(raw(g.y0 - 1)), cur = fin(raw(g.y0)), dn = fin(raw(g.y0 + 1));
-#if IW_UC_DEPTH == 2
-        URaw<T> n1 = raw(g.y0 + 2);
-#endif
-        for (int y = g.y0; y < g.y1; ++y) {
-#if IW_UC_DEPTH == 2
-            const URaw<T> nx = n1;
-            n1 = raw(y + 3);
-#else
-            const URaw<T> nx = raw(y + 2);
-#endif
-            if (g.out_lane && y < a.dom.H) {
-                // shared pixels: parked whether active or not (the unchanged Offset then),
-                // so the fix-up copies without looking at the flags
-                const long long k = a.dom.off(g.x, y);
-                const bool shared = y == g.y0 || y == g.y1 - 1 || g.edge_lane;
-                if (shared) reinterpret_cast<Vec2<T>*>(ob)[k] = Vec2<T>{cur.ox, cur.oy};
-                else if (cur.act) reinterpret_cast<Vec2<T>*>(O)[k] = Vec2<T>{cur.ox, cur.oy};
-                if (cur.act) A[k] = cur.t;
-            }
-            const T lox = from_left(cur.ox, cur.eox), loy = from_left(cur.oy, cur.eoy);
-            const T rox = from_right(cur.ox, cur.eox), roy = from_right(cur.oy, cur.eoy);
-            const float lux = from_left(cur.ux, cur.eux), luy = from_left(cur.uy, cur.euy);
-            const float rux = from_right(cur.ux, cur.eux), ruy = from_right(cur.uy, cur.euy);
-            const int lact = from_left_i(cur.act, cur.eact), ract = from_right_i(cur.act, cur.eact);
-            T ex, ey, ax, ay, sum = 0;
-            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, rox, roy, rux, ruy,
-                  cur.act && ract, wr, ex, ey, ax, ay);
-            sum += ex * ex + ey * ey;
-            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, lox, loy, lux, luy,
-                  cur.act && lact, wr, ex, ey, ax, ay);
-            sum += ex * ex + ey * ey;
-            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, dn.ox, dn.oy, dn.ux, dn.uy,
-                  cur.act && dn.act, wr, ex, ey, ax, ay);
-            sum += ex * ex + ey * ey;
-            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, up.ox, up.oy, up.ux, up.uy,
-                  cur.act && up.act, wr, ex, ey, ax, ay);
-            sum += ex * ex + ey * ey;
-            if (cur.fit) {
-                const T fx = wf * (cur.ox - (T)cur.cx), fy = wf * (cur.oy - (T)cur.cy);
-                sum += fx * fx + fy * fy;
-            }
-            if (g.out_lane && cur.act) acc += (T)0.5 * sum;
-            up = cur; cur = dn;
-            dn = fin(nx);
-        }
-    }
-    double v[1] = {(double)acc};
-    block_reduce_publish<1>(v, rs, blockIdx.x);
-}
-// The Offsets iw_update_cost parked in `ob`: each wave's first and last row and its
-// strip's outer two columns (inactive pixels hold their unchanged value).
-template <typename T>
-__global__ __launch_bounds__(kBlock) void iw_update_fixup(Args<T> a, T* __restrict__ O, const T* __restrict__ ob) {
-    const WaveGeom g = geom(a);
-    if (g.y0 >= g.y1) return;
-    auto copy = [&](int x, int y) {
-        if (x >= a.dom.W || !present(a.dom, x, y)) return;
-        const long long k = a.dom.off(x, y);
-        reinterpret_cast<Vec2<T>*>(O)[k] = reinterpret_cast<const Vec2<T>*>(ob)[k];
-    };
-    copy(g.x, g.y0);
-    if (g.y1 - 1 > g.y0) copy(g.x, g.y1 - 1);
-    const int x0 = g.x - g.lane;
-    for (int j = g.lane; j < 2 * (g.y1 - g.y0 - 2); j += kWave)
-        copy(x0 + ((j & 1) ? kWave - 1 : 0), g.y0 + 1 + (j >> 1));
 }
 
 // ---------------------------------------------------- materialized Jacobian
@@ -1560,9 +1455,6 @@ public:
         // by declared index: the routing matched this file's structural signature, in which
         // each parameter is identified by its problemparams index (generic.hip: generic_signature),
         // against the canonical energy's (fit weight declared first), so names play no part
-        rows_ = env_int("OPT_AMD_ROWS", 0);   // 0: iw::rows_for (per domain)
-        depth_ = env_int("OPT_AMD_DEPTH", 1);
-        nt_ = env_int("OPT_AMD_IW_NT", 6);
         read_knobs();
         timer_.apply_name = apply_kernel_name();
         timer_.aux_names = {"iw_jtf_apply", "iw_apply_res"};
@@ -1608,7 +1500,6 @@ public:
     }
 
     int step(void** params) override {
-        read_knobs();   // per Step: an A/B of the loop structure on one plan (same allocations)
         if (!initialised_) init(params);
         if (n_iter_ >= sp_.nIterations) {
             cleanup_log();
@@ -1636,7 +1527,9 @@ public:
         // iterations 1.. as iw_apply_res (the residual update folded into the next apply;
         // needs the sums r_0.W Ap_0, Ap_0.W Ap_0 of iteration 0), on one domain and on row
         // slabs: ONE all-reduce of four scalars per PCG iteration instead of two
-        const bool res = fused_res_ && L >= 1;
+        // (its 32-bit byte offsets must fit: above ~358 M pixels in fp32 / ~179 M in fp64 the
+        // separate passes, which index with 64 bits, run instead)
+        const bool res = fused_res_ && offsets32_ && L >= 1;
         // res with defer_: p_i in pb[i % 3]; the delta terms of odd iterations are folded
         // in pairs by the next even iteration (or the update), which reads p_{i-2} again
         const bool defer = res && defer_;
@@ -1730,41 +1623,12 @@ public:
             }
         }
         // PCGLinearUpdate (with the last delta += alpha p) + cost
-        bool cost_done = false;
         if (L > 0 && defer) {
             // pending: p_{L-1}, and p_{L-2} too when L-1 is odd (the even iterations fold pairs)
             const int ub = flat_grid(dom_.npix_mem(), 1);
             const T* pl = pb[(L - 1) % 3];
             const T* pl2 = L >= 2 ? pb[(L - 2) % 3] : nullptr;
             const bool e2 = L % 2 == 0, has = L >= 3;
-            if (fused_uc_ && !distributed()) {   // update + cost in one strip pass
-                if (!ob_) ob_ = (T*)dmalloc(sizeof(T) * 2 * dom_.npix_mem());
-                const int nb = stencil_blocks();
-                const ReduceSlot rs = red_.slot(nb, kScCost);
-                tbegin("iw_update_cost");
-                if (e2 && has)
-                    hipLaunchKernelGGL((iw::iw_update_cost<T, true, true>), dim3(nb), dim3(kBlock), 0, stream_, args(),
-                                       cur_O_, cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1), pl2,
-                                       rz(L - 2), pap(L - 2), ob_, rs);
-                else if (e2)
-                    hipLaunchKernelGGL((iw::iw_update_cost<T, false, true>), dim3(nb), dim3(kBlock), 0, stream_, args(),
-                                       cur_O_, cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1), pl2,
-                                       rz(L - 2), pap(L - 2), ob_, rs);
-                else if (has)
-                    hipLaunchKernelGGL((iw::iw_update_cost<T, true, false>), dim3(nb), dim3(kBlock), 0, stream_, args(),
-                                       cur_O_, cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1),
-                                       (const T*)nullptr, 0, 0, ob_, rs);
-                else
-                    hipLaunchKernelGGL((iw::iw_update_cost<T, false, false>), dim3(nb), dim3(kBlock), 0, stream_, args(),
-                                       cur_O_, cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1),
-                                       (const T*)nullptr, 0, 0, ob_, rs);
-                OPT_HIP_CHECK(hipGetLastError());
-                hipLaunchKernelGGL(iw::iw_update_fixup<T>, dim3(nb), dim3(kBlock), 0, stream_, args(), cur_O_,
-                                   (const T*)ob_);
-                OPT_HIP_CHECK(hipGetLastError());
-                tend();
-                cost_done = true;
-            } else {
             tbegin("iw_update");
             if (e2 && has)
                 hipLaunchKernelGGL((iw::iw_update<T, true, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
@@ -1785,7 +1649,6 @@ public:
             OPT_HIP_CHECK(hipGetLastError());
             tend();
             exchange_unknowns();
-            }
         } else if (L > 0) {
             const int ub = flat_grid(dom_.npix_mem(), 1);
             tbegin("iw_update");
@@ -1802,7 +1665,7 @@ public:
             exchange_unknowns();
         }
         // computeCost at the updated unknowns (:2245)
-        if (!cost_done) { tbegin("iw_cost"); launch_cost(kScCost); tend(); }
+        tbegin("iw_cost"); launch_cost(kScCost); tend();
         allreduce(kScCost);
         const double c = read_scalar(kScCost);
         unbind_after_step();
@@ -1870,27 +1733,18 @@ public:
     }
 
 private:
+    // Measurement / A-B knobs, read once when the plan is created (never inside a Step):
+    // OPT_AMD_ROWS rows per wave (0: iw::rows_for), OPT_AMD_STAGGER the vectors' placement,
+    // and the separate-pass forms the tests compare bitwise with the fused loop
+    // (OPT_AMD_IW_FUSED_INIT / _FUSED_RES / _DEFER = 0).
     void read_knobs() {
-        const int rw = env_int("OPT_AMD_ROWS", 0);   // 0: iw::rows_for (per domain)
-        if (rw > 0 && rw != rows_) {
-            rows_ = rw;
-            rows_auto_ = false;
-            nrowblocks_ = (dom_.y_hi - dom_.y_lo + rows_ * 4 - 1) / (rows_ * 4);
-        }
-        const long long st = env_int("OPT_AMD_STAGGER", kStagger) & ~255LL;
-        if (st != stagger_) {
-            stagger_ = st;
-            OPT_HIP_CHECK(hipStreamSynchronize(stream_));
-            place();
-        }
+        const int rw = env_int("OPT_AMD_ROWS", 0);
+        if (rw > 0) { rows_ = rw; rows_auto_ = false; }
+        stagger_ = env_int("OPT_AMD_STAGGER", kStagger) & ~255LL;
+        print_addr_ = env_int("OPT_AMD_PRINT_ADDR", 0) != 0;
         fused_init_ = env_int("OPT_AMD_IW_FUSED_INIT", 1) != 0;
         fused_res_ = env_int("OPT_AMD_IW_FUSED_RES", 1) != 0;
         defer_ = env_int("OPT_AMD_IW_DEFER", 1) != 0;
-        // measured without gain (round 3): iw_update_cost + fix-up 307 + 28 us against
-        // iw_update + iw_cost 192 + 141 us — the strip walk holds ~4.4 TB/s where the flat
-        // update streams at 6.2, so the 24 B/px it saves do not show
-        fused_uc_ = env_int("OPT_AMD_IW_FUSED_COST", 0) != 0;
-        res_nt_ = env_int("OPT_AMD_IW_RES_NT", 2);
     }
     // A zeroed plan vector with kSlack spare bytes: place() may move each vector's base
     // within them between Steps (every vector is rewritten before it is read in a Step).
@@ -1917,6 +1771,7 @@ private:
     void allocate() {
         const long long N = dom_.npix_mem();
         nvec_ = 3 * N;
+        offsets32_ = iw::offsets_fit_32<T>(N);
         for (T** v : {&r_, &p0_, &p1_, &Ap_, &delta_, &r1_, &Ap1_})
             *v = (T*)vec_alloc(sizeof(T) * nvec_);
         pre_ = (T*)vec_alloc(sizeof(T) * N);   // angle channel only (Args::preO)
@@ -1940,7 +1795,7 @@ private:
         raw_.clear();
         for (T** v : {&r_, &pre_, &p0_, &p1_, &Ap_, &delta_, &r1_, &Ap1_, &p2_}) *v = nullptr;
         flags_ = nullptr;
-        for (T** v : {&dO_, &dA_, &ob_}) { dfree(*v); *v = nullptr; }
+        for (T** v : {&dO_, &dA_}) { dfree(*v); *v = nullptr; }
         for (float** v : {&dU_, &dC_, &dM_}) { dfree(*v); *v = nullptr; }
     }
 
@@ -2084,7 +1939,7 @@ private:
         }
         if constexpr (MODE == 1) {
             if (sums) {   // iteration 0 of the fused loop (iw_apply_res's identity needs its sums)
-                launch_timed("iw_apply", iw::iw_apply<T, 1, 0, 1, false, 2, true>, grid, a, pin, (const T*)r_,
+                launch_timed("iw_apply", iw::iw_apply<T, 1, 0, false, 2, true>, grid, a, pin, (const T*)r_,
                              (const T*)pre_, pout, Ap, delta_, (const double*)red_.scalars, ib_num, ib_den, ia_num,
                              ia_den, red_.slot(nb, sc_out), (const T*)nullptr, (const int*)nullptr);
                 return;
@@ -2096,39 +1951,11 @@ private:
     void launch_apply_grid(const iw::Args<T>& a, int grid, const T* pin, T* pout, int sc_out, int ib_num,
                            int ib_den, int ia_num, int ia_den, T* Ap) {
         const int nb = stencil_blocks();   // the reduction slot spans every tile
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (nt_ == 6 && depth_ == 1 && timer_.ext_pair("iw_apply", &e0, &e1)) {   // the default variant
-            hipExtLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 2>), dim3(grid), dim3(kBlock), 0, stream_, e0,
-                                  e1, 0, a, pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
-                                  ib_num, ib_den, ia_num, ia_den, red_.slot(nb, sc_out), (const T*)nullptr,
-                                  (const int*)nullptr);
-            OPT_HIP_CHECK(hipGetLastError());
-            timer_.ext_record("iw_apply", e0, e1);
-            return;
-        }
-        tbegin("iw_apply");   // the other variants: event records around the launch
-        if (depth_ == 2)
-            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 2>), dim3(grid), dim3(kBlock), 0, stream_, a, pin,
-                               (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars, ib_num,
-                               ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
-        else if ((nt_ & 3) == 1)
-            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 1>), dim3(grid), dim3(kBlock), 0, stream_,
-                               a, pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
-                               ib_num, ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
-        else if ((nt_ & 3) == 2)
-            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 2>), dim3(grid), dim3(kBlock), 0, stream_,
-                               a, pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
-                               ib_num, ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
-        else if ((nt_ & 3) == 3)
-            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1, false, 3>), dim3(grid), dim3(kBlock), 0, stream_,
-                               a, pin, (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars,
-                               ib_num, ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
-        else
-            hipLaunchKernelGGL((iw::iw_apply<T, MODE, DM, 1>), dim3(grid), dim3(kBlock), 0, stream_, a, pin,
-                               (const T*)r_, (const T*)pre_, pout, Ap, delta_, red_.scalars, ib_num,
-                               ib_den, ia_num, ia_den, red_.slot(nb, sc_out));
-        tend();
-        OPT_HIP_CHECK(hipGetLastError());
+        // streaming (nontemporal) stores of the PCG vectors (NT = 2); streaming loads as
+        // well, or plain stores, measured +1-5 % (round 3)
+        launch_timed("iw_apply", iw::iw_apply<T, MODE, DM, false, 2>, grid, a, pin, (const T*)r_, (const T*)pre_,
+                     pout, Ap, delta_, (const double*)red_.scalars, ib_num, ib_den, ia_num, ia_den,
+                     red_.slot(nb, sc_out), (const T*)nullptr, (const int*)nullptr);
     }
     // PCG iteration i >= 1 of the fused loop: r_{i-1} / Ap_{i-1} in buffer (i-1) & 1 (r_ / Ap_
     // for even), r_i / Ap_i into the other one (none in the last iteration)
@@ -2156,28 +1983,19 @@ private:
             launch_timed("iw_apply_res", kern, grid, a, pin, rin, Apin, (const T*)pre_, pout, rout, Apout, delta_,
                          red_.scalars, rz(i - 1), base_scale, rs, pin2);
         };
-        if (res_nt_ == 3) go_res<3>(go, i, pin2);
-        else if (res_nt_ == 0) go_res<0>(go, i, pin2);
-        else go_res<2>(go, i, pin2);
-    }
-    // OPT_AMD_IW_RES_NT: streaming (nontemporal) loads (bit 0) / stores (bit 1) of the PCG vectors
-    template <int NT, typename G>
-    void go_res(G&& go, int i, const T* pin2) {
+        // streaming stores of the PCG vectors (NT = 2; streaming loads too, or plain
+        // stores, measured +1-5 %, round 3)
         if (pin2 || (defer_ && i == 1)) {   // deferred delta: odd i none, i = 2 starts it, even i > 2 folds a pair
-            if (i % 2 == 1) go(iw::iw_apply_res<T, 0, NT, 0>);
-            else if (i == 2) go(iw::iw_apply_res<T, 1, NT, 1>);
-            else go(iw::iw_apply_res<T, 2, NT, 1>);
-        } else if (i == 1) go(iw::iw_apply_res<T, 1, NT>);
-        else go(iw::iw_apply_res<T, 2, NT>);
+            if (i % 2 == 1) go(iw::iw_apply_res<T, 0, 2, 0>);
+            else if (i == 2) go(iw::iw_apply_res<T, 1, 2, 1>);
+            else go(iw::iw_apply_res<T, 2, 2, 1>);
+        } else if (i == 1) go(iw::iw_apply_res<T, 1, 2>);
+        else go(iw::iw_apply_res<T, 2, 2>);
     }
     void launch_residual(int i_num, int i_den, int sc_out) {
         const int nb = flat_grid(dom_.npix_mem(), 2);
-        if (nt_ & 4)
-            hipLaunchKernelGGL((iw::iw_residual<T, true>), dim3(nb), dim3(kBlock), 0, stream_, args(), (const T*)Ap_,
-                               (const T*)pre_, r_, red_.scalars, i_num, i_den, red_.slot(nb, sc_out));
-        else
-            hipLaunchKernelGGL((iw::iw_residual<T>), dim3(nb), dim3(kBlock), 0, stream_, args(), (const T*)Ap_,
-                               (const T*)pre_, r_, red_.scalars, i_num, i_den, red_.slot(nb, sc_out));
+        hipLaunchKernelGGL((iw::iw_residual<T, true>), dim3(nb), dim3(kBlock), 0, stream_, args(), (const T*)Ap_,
+                           (const T*)pre_, r_, red_.scalars, i_num, i_den, red_.slot(nb, sc_out));
         OPT_HIP_CHECK(hipGetLastError());
     }
     void launch_cost(int sc_out) {
@@ -2197,19 +2015,16 @@ private:
     T *r_ = nullptr, *pre_ = nullptr, *p0_ = nullptr, *p1_ = nullptr, *Ap_ = nullptr, *delta_ = nullptr;
     T *r1_ = nullptr, *Ap1_ = nullptr;   // iw_apply_res ping-pongs r and Ap (neighbours read the old ones)
     T* p2_ = nullptr;                    // p_i in {p0_, p1_, p2_}[i % 3] with the deferred delta
-    T* ob_ = nullptr;                    // iw_update_cost's parked shared Offsets (2 per px, lazily)
-    bool fused_uc_ = false;              // OPT_AMD_IW_FUSED_COST=1: update + cost in one pass
     std::vector<char*> raw_;             // the plan vectors' allocations (vec_alloc)
-    long long stagger_ = env_int("OPT_AMD_STAGGER", kStagger) & ~255LL;
-    bool print_addr_ = env_int("OPT_AMD_PRINT_ADDR", 0) != 0;
+    long long stagger_ = kStagger;
+    bool print_addr_ = false;
     uint8_t* flags_ = nullptr;
     bool fused_init_ = true;            // OPT_AMD_IW_FUSED_INIT=0: iw_jtf, then iw_apply<1,0>
     bool fused_res_ = true;             // OPT_AMD_IW_FUSED_RES=0: iw_apply<2> + iw_residual per iteration
     bool defer_ = true;                 // OPT_AMD_IW_DEFER=0: iw_apply_res updates delta in every iteration
-    int res_nt_ = 2;                    // iw_apply_res NT template argument (0, 2, 3)
-    int rows_ = 16, depth_ = 1, nstrips_ = 0, nrowblocks_ = 0;
-    bool rows_auto_ = false;
-    int nt_ = 6;   // streaming PCG-vector access: bit 0 iw_apply loads, bit 1 iw_apply stores, bit 2 iw_residual
+    bool offsets32_ = true;             // iw_apply_res's 32-bit byte offsets cover every plan vector
+    int rows_ = 0, nstrips_ = 0, nrowblocks_ = 0;
+    bool rows_auto_ = true;
     Comm* comm_ = nullptr;
     const bool overlap_ = env_int("OPT_AMD_HALO_OVERLAP", 1) != 0;   // 0: blocking halo before each apply
     float wf_ = 0, wr_ = 0;
@@ -2316,7 +2131,7 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
     void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
-        hipLaunchKernelGGL((iw::iw_apply<T, 0, 0, 1, true>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p,
+        hipLaunchKernelGGL((iw::iw_apply<T, 0, 0, true>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p,
                            (const T*)nullptr, (const T*)nullptr, (T*)nullptr, Ap, (T*)nullptr,
                            (const double*)nullptr, 0, 0, 0, 0, rs, dadd, stop);
         OPT_HIP_CHECK(hipGetLastError());

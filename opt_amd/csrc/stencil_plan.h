@@ -150,6 +150,18 @@ struct HasSlabRefusal : std::false_type {};
 template <class Op>
 struct HasSlabRefusal<Op, std::void_t<decltype(std::declval<const Op&>().slab_refusal())>> : std::true_type {};
 
+// Ops that keep private per-step caches of values derived from the bound arrays
+// (GenericOp: transcendentals of centred and graph-slot reads): refresh_caches(stream)
+// recomputes them from the arrays as bound at THIS Step. The reference evaluates those
+// values inline from the arrays at every Step (setGPUptr, solverGPUGaussNewton.t:2001), so
+// a caller may rewrite or rebind arrays between Steps (Opt.h:64-65); ComputedArrays
+// themselves keep the reference's schedule (init, after update, after revert).
+template <class Op, class = void>
+struct HasRefreshCaches : std::false_type {};
+template <class Op>
+struct HasRefreshCaches<Op, std::void_t<decltype(std::declval<Op&>().refresh_caches(hipStream_t{}))>>
+    : std::true_type {};
+
 // Ops that describe their own hipGraph capture gate and key (GenericOp: the kernel
 // argument block the generated launches receive) instead of the declaration parser's.
 template <class Op, class = void>
@@ -228,6 +240,9 @@ public:
         begin_call();
         op_->bind(params, stream_);
         exchange_unknowns();
+        if constexpr (HasRefreshCaches<Op>::value) {
+            if (op_->refresh_caches(stream_)) exchange_computed();
+        }
         const int Lit = std::max(0, sp_.lIterations);
         red_.ensure(std::max(op_->stencil_blocks(), 4096), 4, kScBase + kSlots * (Lit + 2));
         OPT_HIP_CHECK(hipMemsetAsync(stop_, 0, 64, stream_));

@@ -472,28 +472,3 @@ def test_deferred_delta_is_bitwise_the_per_iteration_update(monkeypatch, W, H, l
         out.append((c, to_np(prm[0]), to_np(prm[1]), np.array(s.scalars(2 + 5 * (lit + 2)))))
     for a, b in zip(out[0], out[1]):
         np.testing.assert_array_equal(a, b)
-
-
-@pytest.mark.parametrize("W,H,lit,rows", [(150, 110, 10, 0), (37, 29, 1, 0), (64, 64, 2, 0), (5, 3, 3, 0),
-                                          (200, 1, 4, 0), (700, 300, 7, 0), (130, 40, 4, 1), (130, 40, 3, 2),
-                                          (129, 47, 2, 3)])
-def test_fused_update_cost_is_bitwise_update_then_cost(monkeypatch, W, H, lit, rows):
-    """iw_update_cost (the update formed per row in registers, the cost evaluated from the
-    updated rows; the Offsets of each wave's first / last row and outer columns parked and
-    copied by iw_update_fixup) against iw_update + iw_cost: energies, Offset, Angle and PCG
-    scalars bitwise equal over three GN steps. lIterations 1..4 reach all four pending-delta
-    variants; 1-3 rows per wave put every pixel on a wave's first or last row."""
-    if rows:
-        monkeypatch.setenv("OPT_AMD_ROWS", str(rows))
-    out = []
-    for val in (0, 1):
-        monkeypatch.setenv("OPT_AMD_IW_FUSED_COST", str(val))
-        w = perturbed(W, H, seed=3 * W + H)
-        s = OptSolver([W, H], ENERGY, "gaussNewtonGPU")
-        s.set_solver_params({"nIterations": 3, "lIterations": lit})
-        prm = device_params(w)
-        c = np.array(s.profiled_solve(prm))
-        out.append((c, to_np(prm[0]), to_np(prm[1]), np.array(s.scalars(2 + 5 * (lit + 2)))))
-    for a, b in zip(out[0], out[1]):
-        np.testing.assert_array_equal(a, b)
-

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Run a list of GPU test files (through gpurun): tools/r03_tests.sh <outdir> <pytest args...>
+# Run a list of GPU test files (through gpurun): tools/run_gpu_tests.sh <outdir> <pytest args...>
 R=$(pwd)
 O=$R/gpurun_out/$1
 shift
