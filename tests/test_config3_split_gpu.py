@@ -57,7 +57,7 @@ def test_sfs_lm_4096_split_8_ways_matches_single_domain(monkeypatch, sfs4096):
 
     ref, Xref = single(w["X"])
     pert, _ = single(_ulp(w["X"], 1))
-    costs, X = run_generic(SFS, w, WORLD, nit, lit)
+    costs, X, sc = run_generic(SFS, w, WORLD, nit, lit, scalars=8 + 7 * (lit + 2))
     for r in range(WORLD):
         assert costs[r] == costs[0]           # every rank reports the global energy
     c = np.array(costs[0])
@@ -65,6 +65,16 @@ def test_sfs_lm_4096_split_8_ways_matches_single_domain(monkeypatch, sfs4096):
     assert np.all(np.abs(c - ref) / ref <= _floor_bar(ref, pert)), (c, ref, pert)
     act = np.abs(Xref) < 1e3
     assert np.abs(X - Xref)[act].max() <= 1e-4 * np.abs(Xref[act]).max()
+    # the fused step23's beta numerator (identity over the apply's fp64 sums, products in
+    # fp64 on both sides) against the direct r.z of the same pass, every PCG
+    # iteration of the last LM step on the 8 all-reduced slabs (stencil_plan.h slots:
+    # rz(i) = 8 + 7 i, its identity value at rz(i) + 6; LM's residual-reset iteration 9
+    # takes the classic sequence; a zeta exit leaves later slots unwritten)
+    for i in range(1, lit):
+        rz, rzx, rzp = sc[8 + 7 * i], sc[8 + 7 * i + 6], sc[8 + 7 * (i - 1)]
+        if i == 9 or rz == 0:
+            continue
+        assert abs(rzx - rz) <= 1e-4 * rz + 1e-12 * rzp, (i, rz, rzx, rzp)
 
 
 def test_sfs_4096_split_halo_overlap_is_bitwise_the_blocking_exchange(monkeypatch, sfs4096):
@@ -88,16 +98,24 @@ def test_image_warping_gn_4096_split_8_ways_matches_single_domain(iw4096):
     def single(off):
         s = solver(N, N)
         s.set_solver_params({"nIterations": nit, "lIterations": lit})
-        return np.array(s.profiled_solve(device_params(dict(w, Offset=off))))
+        prm = device_params(dict(w, Offset=off))
+        c = np.array(s.profiled_solve(prm))
+        return c, prm[0].cpu().numpy().astype(np.float64), prm[1].cpu().numpy().astype(np.float64)
 
-    ref = single(w["Offset"])
-    pert = single(_ulp(w["Offset"], 1))
+    ref, Oref, Aref = single(w["Offset"])
+    pert, Op, Ap = single(_ulp(w["Offset"], 1))
     costs, O, A = run_decomposed(w, WORLD, nit, lit)
     for r in range(WORLD):
         assert costs[r] == costs[0]
     c = np.array(costs[0])
     assert len(c) == len(ref)
     assert np.all(np.abs(c - ref) / ref <= _floor_bar(ref, pert)), (c, ref, pert)
+    # the unknowns too: within 4x the single-domain solve's own response to
+    # a 1-ulp input change, or 1e-5 of the largest magnitude
+    dO = np.abs(O.astype(np.float64) - Oref).max()
+    dA = np.abs(A.astype(np.float64) - Aref).max()
+    assert dO <= max(4 * np.abs(Op - Oref).max(), 1e-5 * np.abs(Oref).max()), (dO, np.abs(Op - Oref).max())
+    assert dA <= max(4 * np.abs(Ap - Aref).max(), 1e-5 * max(1.0, np.abs(Aref).max())), (dA, np.abs(Ap - Aref).max())
 
 
 def test_image_warping_4096_split_halo_overlap_is_bitwise_the_blocking_exchange(monkeypatch, iw4096):

@@ -46,7 +46,9 @@ SFS = Family(os.path.join(ROOT, "energies", "shape_from_shading.t"), "LMGPU",
              [("X", 1), ("D_i", 1), ("Im", 1), ("edgeMaskR", 1), ("edgeMaskC", 1)], ["X"])
 
 
-def run(fam, w, world, nit, lit):
+def run(fam, w, world, nit, lit, scalars=0):
+    """scalars > 0: also return rank 0's first `scalars` plan scalar slots after the solve
+    (its last step's PCG sums, stencil_plan.h rz / pap / identity slots)."""
     W, H = w["W"], w["H"]
     lib = api.load_library()
     group = lib.OptAMD_LocalGroupCreate(world)
@@ -74,10 +76,11 @@ def run(fam, w, world, nit, lit):
     assert not errors, errors
     nscal = len(w.get("params", []))
     X = np.concatenate([dd.owned(to_np(prms[r][nscal]), W, fam.arrays[0][1], slabs[r]) for r in range(world)])
+    sc = np.array(solvers[0].scalars(scalars)) if scalars else None
     for sv in solvers:
         sv.close()
     lib.OptAMD_LocalGroupDestroy(group)
-    return results, X
+    return (results, X, sc) if scalars else (results, X)
 
 
 @pytest.mark.parametrize("fam,world,W,H", [(POISSON, 1, 96, 64), (POISSON, 2, 96, 64), (POISSON, 3, 130, 77),

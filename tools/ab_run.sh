@@ -1,14 +1,14 @@
 #!/bin/bash
 # On the GPU box: the headline bench line for each A/B variant, twice, interleaved:
 #   tools/ab_run.sh <outdir> v1 v2 ...
-# a variant is <name> (build_exp/<name>/libopt_amd.so; "tree" = opt_amd/libopt_amd.so)
+# a variant is <name> (build_ab/<name>/libopt_amd.so; "tree" = opt_amd/libopt_amd.so)
 # optionally followed by @VAR=value[@VAR=value...] environment settings.
 O=gpurun_out/$1; shift
 mkdir -p $O
 for round in 1 2; do
   for v in "$@"; do
     n=${v%%@*}
-    lib=build_exp/$n/libopt_amd.so
+    lib=build_ab/$n/libopt_amd.so
     [ "$n" = tree ] && lib=opt_amd/libopt_amd.so
     envs=""
     [ "$v" != "$n" ] && envs=$(echo "${v#*@}" | tr '@' ' ')

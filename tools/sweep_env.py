@@ -23,7 +23,7 @@ def main():
     configs = [c for c in os.environ.get("SWEEP_CONFIGS", "").split(";")]
     w = workloads.image_warping(W, H, seed=1234)
     base = [torch.from_numpy(w[k]).cuda() for k in ("Offset", "Angle", "UrShape", "Constraints", "Mask")]
-    names = ["iw_apply", "iw_residual", "iw_jtf", "iw_jtf_apply", "iw_update", "iw_cost"]
+    names = ["iw_apply", "iw_apply_res", "iw_residual", "iw_jtf", "iw_jtf_apply", "iw_update", "iw_cost"]
     solvers = []
     for c in configs:
         for kv in filter(None, c.split(",")):
