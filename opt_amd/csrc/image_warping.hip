@@ -790,6 +790,17 @@ template <typename T, bool EDGE_ANGLE, bool EDGE = true>
 __device__ __forceinline__ VRaw<T> raw_vrow(const Args<T>& a, const WaveGeom& g, int y) {
     VRaw<T> q;
     q.in = present(a.dom, g.x, y);
+    if (!EDGE) {   // iw_jtf_apply: 32-bit byte offsets from uniform bases (offsets_fit_32)
+        const unsigned i = q.in ? (unsigned)a.dom.off(g.x, y) : 0u;
+        const vec2_t<T> o = ldb<false, vec2_t<T>>(a.O, i * 2u * (unsigned)sizeof(T));
+        q.o = Vec2<T>{o.x, o.y};
+        q.t = ldb<false, T>(a.A, i * (unsigned)sizeof(T));
+        q.u = ldb<false, float2>(a.U, 8u * i);
+        q.c = ldb<false, float2>(a.C, 8u * i);
+        q.m = ldb<false, float>(a.M, 4u * i);
+        q.ein = 0;
+        return q;
+    }
     const long long i = q.in ? a.dom.off(g.x, y) : 0;
     q.o = reinterpret_cast<const Vec2<T>*>(a.O)[i];
     q.t = a.A[i];
@@ -1027,13 +1038,12 @@ struct FRow {          // a finished row of the fused kernel's apply window
     __device__ __forceinline__ T pt() const { return wt * rt; }
 };
 template <typename T, int NT = 2>
-__global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_jtf_apply(Args<T> a, T* __restrict__ r, T* __restrict__ pre,
-                                                       T* __restrict__ pout, T* __restrict__ Ap,
-                                                       ReduceSlot rs) {
+__device__ __forceinline__ void iw_jtf_apply_body(const Args<T>& a, T* __restrict__ r, T* __restrict__ pre,
+                                                  T* __restrict__ pout, T* __restrict__ Ap, ReduceSlot rs) {
     IW_PRE_TABLE(a);
     const WaveGeom g = geom_fused(a);
     const T wr = a.wr, wf2 = a.wf * a.wf;
-    const long long N = a.dom.npix_mem();
+    const unsigned tb = (unsigned)(2 * a.dom.npix_mem() * (long long)sizeof(T));
     acc_t rzdot = 0, papdot = 0, rapd = 0, apapd = 0;
     // J^T F of row y from the window (cur = row y, dn = row y+1): stores r / pre / flags
     // when the row is this wave's, returns the apply's view of the row (p = pre r)
@@ -1041,11 +1051,14 @@ __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_jtf_apply(Args<T> a, 
         const JRow<T> j = jtf_row<T, false>(a, cur, dn, k);
         const JOut<T> o = jtf_out(a, cur, j);
         if (own && g.out_lane) {
-            const long long i = a.dom.off(g.x, y);
-            a.flags[i] = (uint8_t)o.f;
-            st_v<(NT & 2) != 0>(r + 2 * i, o.rx); st_v<(NT & 2) != 0>(r + 2 * i + 1, o.ry);
-            st_v<(NT & 2) != 0>(r + 2 * N + i, o.rt);
-            st_v<(NT & 2) != 0>(pre + i, o.wt);
+            // 32-bit byte offsets from uniform bases (the plan takes this kernel only when
+            // they fit, offsets_fit_32), the Offset pair as one 8/16-byte store
+            const unsigned i = (unsigned)a.dom.off(g.x, y);
+            const POff<T> off(i, tb);
+            stb<false>(a.flags, i, (uint8_t)o.f);
+            vec2_t<T> rv; rv.x = o.rx; rv.y = o.ry;
+            stb<(NT & 2) != 0>(r, off.xy, rv); stb<(NT & 2) != 0>(r, off.t, o.rt);
+            stb<(NT & 2) != 0>(pre, off.s, o.wt);
             if (cur.act) rzdot += wdot3(o.wo, o.rx, o.rx, o.wo, o.ry, o.ry, o.wt, o.rt, o.rt);
         }
         FRow<T> p;
@@ -1100,13 +1113,13 @@ __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_jtf_apply(Args<T> a, 
                                 (apy_x * jpy_x + apy_y * jpy_y));
             if (!cur.act) { aox = 0; aoy = 0; aot = 0; }
             if (g.out_lane) {
-                const long long i = a.dom.off(g.x, y);
+                const POff<T> off((unsigned)a.dom.off(g.x, y), tb);
                 if (Ap) {   // null when lIterations == 1: nothing reads that Ap
-                    st_v<(NT & 2) != 0>(Ap + 2 * i, aox); st_v<(NT & 2) != 0>(Ap + 2 * i + 1, aoy);
-                    st_v<(NT & 2) != 0>(Ap + 2 * N + i, aot);
+                    vec2_t<T> v; v.x = aox; v.y = aoy;
+                    stb<(NT & 2) != 0>(Ap, off.xy, v); stb<(NT & 2) != 0>(Ap, off.t, aot);
                 }
-                st_v<(NT & 2) != 0>(pout + 2 * i, cpx); st_v<(NT & 2) != 0>(pout + 2 * i + 1, cpy);
-                st_v<(NT & 2) != 0>(pout + 2 * N + i, cpt);
+                vec2_t<T> pv; pv.x = cpx; pv.y = cpy;
+                stb<(NT & 2) != 0>(pout, off.xy, pv); stb<(NT & 2) != 0>(pout, off.t, cpt);
                 papdot += (acc_t)(cpx * aox + cpy * aoy + cpt * aot);
                 // PCGStep2's weights: pre, or 1 without a preconditioner
                 const T w0 = a.use_pre ? cur.wo : (T)1, w2 = a.use_pre ? cur.wt : (T)1;
@@ -1124,6 +1137,23 @@ __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_jtf_apply(Args<T> a, 
     double v[4] = {(double)rzdot, (double)papdot, (double)rapd, (double)apapd};
     block_reduce_publish<4>(v, rs, g.tile);
 }
+// minimum waves per SIMD of the fp32 kernel (0: the compiler's choice; its 112 VGPRs give 4)
+#ifndef OPTAMD_IW_JA_WPE
+#define OPTAMD_IW_JA_WPE 0
+#endif
+template <typename T, int NT = 2>
+__global__ __launch_bounds__(kBlock) void iw_jtf_apply(Args<T> a, T* __restrict__ r, T* __restrict__ pre,
+                                                       T* __restrict__ pout, T* __restrict__ Ap, ReduceSlot rs) {
+    iw_jtf_apply_body<T, NT>(a, r, pre, pout, Ap, rs);
+}
+#if OPTAMD_IW_JA_WPE > 0
+template <>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OPTAMD_IW_JA_WPE))) void
+iw_jtf_apply<float, 2>(Args<float> a, float* __restrict__ r, float* __restrict__ pre, float* __restrict__ pout,
+                       float* __restrict__ Ap, ReduceSlot rs) {
+    iw_jtf_apply_body<float, 2>(a, r, pre, pout, Ap, rs);
+}
+#endif
 
 // ----------------------------------------------------------------- cost kernel
 // sc[rs.out] = sum over active pixels of 1/2 (sum_s |e_reg(k,s)|^2 + |e_fit(k)|^2).
@@ -1523,7 +1553,7 @@ public:
         // reference does on every Step (:2001, :2028): problem parameters may be updated
         // in place between Steps (Opt.h:64-65). On one domain it is fused with the first
         // PCG iteration's apply (iw_jtf_apply: the first p = pre r needs no global scalar).
-        const bool fused = fused_init_ && !distributed() && L >= 1;
+        const bool fused = fused_init_ && offsets32_ && !distributed() && L >= 1;
         // iterations 1.. as iw_apply_res (the residual update folded into the next apply;
         // needs the sums r_0.W Ap_0, Ap_0.W Ap_0 of iteration 0), on one domain and on row
         // slabs: ONE all-reduce of four scalars per PCG iteration instead of two
