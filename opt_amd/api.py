@@ -115,7 +115,11 @@ def load_library(path: str = None):
         pass
     lib = ctypes.CDLL(path)
     for name, res, args in _SIGNATURES:
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if os.path.abspath(path) != os.path.abspath(LIB_PATH):
+                continue   # an older A/B build (OPT_AMD_LIB) may predate an extension entry point
+            raise OptError(f"{path} does not export {name}")
         fn.restype = res
         fn.argtypes = args
     _lib = lib

@@ -380,8 +380,9 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
         thm = -wr * (ax * my_x + ay * my_y);
         for (int y = g.y0; y < g.y1; ++y) {
             // row y+2 in flight during row y (a second row in flight, y+3, was measured
-            // slower: more VGPRs, fewer waves)
-            const PRaw<T> nx = raw_prow<T, MODE, DM, (NT & 1) != 0>(a, g, y + 2, pin, r, pre, delta);
+            // slower: more VGPRs, fewer waves); the last trip re-reads the halo row y1 (an
+            // L2 hit) instead of fetching row y1 + 1, which nothing needs
+            const PRaw<T> nx = raw_prow<T, MODE, DM, (NT & 1) != 0>(a, g, min(y + 2, g.y1), pin, r, pre, delta);
             // horizontal neighbours; the strip's outside columns enter at lanes 0 / 63
             const T lpx = from_left(cur.px, cur.epx), lpy = from_left(cur.py, cur.epy);
             const T rpx = from_right(cur.px, cur.epx), rpy = from_right(cur.py, cur.epy);
@@ -745,13 +746,15 @@ __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_apply_res(Args<T> a, 
             my_x = jdn_x; my_y = jdn_y;
             thm = -wr * (adn_x * jdn_x + adn_y * jdn_y);
         };
-        // two rows per trip, the two row records swapping roles (no register copies)
+        // two rows per trip, the two row records swapping roles (no register copies). Rows
+        // past the halo row y1 are never needed: the last trip's prefetch re-reads row y1
+        // (an L2 hit) instead of fetching row y1 + 1 from HBM
         for (int y = g.y0; y < g.y1; y += 2) {
-            const RRaw<T> n1 = raw(y + 2);
+            const RRaw<T> n1 = raw(min(y + 2, g.y1));
             apply_row(A, B, y);
             A = fin(n1, y + 2);
             if (y + 1 >= g.y1) break;
-            const RRaw<T> n2 = raw(y + 3);
+            const RRaw<T> n2 = raw(min(y + 3, g.y1));
             apply_row(B, A, y + 1);
             B = fin(n2, y + 3);
         }
@@ -975,7 +978,7 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
                 dn = finish_vrow<T, true>(raw_vrow<T, true>(a, g, g.y0 + 1));
         JCarry<T> k = jcarry_init(up, cur, a.wr);
         for (int y = g.y0; y < g.y1; ++y) {
-            const VRaw<T> nx = raw_vrow<T, true>(a, g, y + 2);
+            const VRaw<T> nx = raw_vrow<T, true>(a, g, min(y + 2, g.y1));
             const JRow<T> j = jtf_row(a, cur, dn, k);
             if (g.out_lane) {
                 const long long i = a.dom.off(g.x, y);
@@ -1085,7 +1088,9 @@ __device__ __forceinline__ void iw_jtf_apply_body(const Args<T>& a, T* __restric
               up.act && cur.act, wr, my_x, my_y, ax, ay);
         thm = -wr * (ax * my_x + ay * my_y);
         for (int y = g.y0; y < g.y1; ++y) {
-            const VRaw<T> nx = raw_vrow<T, false, false>(a, g, y + 3);
+            // J^T F needs rows up to y1 + 1; the last trip re-reads that row (an L2 hit)
+            // instead of fetching row y1 + 2
+            const VRaw<T> nx = raw_vrow<T, false, false>(a, g, min(y + 3, g.y1 + 1));
             const FRow<T> dn = jrow(vcur, vdn, k, y + 1, y + 1 < g.y1);
             const T cpx = cur.px(), cpy = cur.py(), cpt = cur.pt(), dpx = dn.px(), dpy = dn.py(), dpt = dn.pt();
             // iw_apply's row body; lanes 0, 1, 62, 63 are not outputs, so no edge operand
@@ -1167,7 +1172,7 @@ __global__ __launch_bounds__(kBlock) void iw_cost(Args<T> a, ReduceSlot rs) {
                 cur = finish_vrow<T, false>(raw_vrow<T, false>(a, g, g.y0)),
                 dn = finish_vrow<T, false>(raw_vrow<T, false>(a, g, g.y0 + 1));
         for (int y = g.y0; y < g.y1; ++y) {
-            const VRaw<T> nx = raw_vrow<T, false>(a, g, y + 2);
+            const VRaw<T> nx = raw_vrow<T, false>(a, g, min(y + 2, g.y1));
             const T lox = from_left(cur.ox, cur.eox), loy = from_left(cur.oy, cur.eoy);
             const T rox = from_right(cur.ox, cur.eox), roy = from_right(cur.oy, cur.eoy);
             const float lux = from_left(cur.ux, cur.eux), luy = from_left(cur.uy, cur.euy);

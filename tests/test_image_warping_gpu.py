@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 SIZES = [(37, 29), (62, 5), (63, 64), (130, 70), (250, 131), (5, 3), (1, 9), (200, 1)]
 # |rz_i by the identity - rz_i direct| / rz_i allowed in any PCG iteration of the fused loop
-IDENTITY_BOUND = 1e-4
+IDENTITY_BOUND = 1e-6   # measured round 4: <= 7.5e-8 over 500 iterations
 
 
 def to_np(t):
@@ -267,10 +267,14 @@ def test_fused_loop_at_the_examples_pcg_depth(monkeypatch, case, lit):
         so its absolute error is ~1e-14 rz_{i-1}, i.e. an absolute error of ~1e-14 in
         beta_i, whatever rz_i / rz_{i-1} is (a non-positive identity value
         gives beta_i = 0, iw_apply_res);
-      * the true trajectory is the fp64 path's (doublePrecision, fused loop); its own
-        floor is the fp64 separate-pass loop's distance from it (hundreds of PCG iterations
-        amplify fp64 rounding too: up to ~4e-4 on cat512 at 200 iterations, round 4), and
-        on cat512 at 200 iterations the double oracle lies within 4x that floor (or 1e-8);
+      * the true trajectory is the fp64 path's (doublePrecision, fused loop; pinned to the
+        double oracle by test_double_precision_path); its own floor is the fp64
+        separate-pass loop's distance from it. Hundreds of PCG iterations amplify fp64
+        rounding too: measured round 4, cat512 at 200 iterations moves by 1.5e-3 / 1.4e-2
+        after GN steps 1 / 2 between the two fp64 loops, and the double oracle lands
+        7.5e-3 / 2.4e-2 from the GPU (its products and sums round differently), so this
+        energy at that depth has no trajectory to pin below the percent level in ANY
+        precision; the fp32 floor there is 0.14 / 0.09;
       * the fp32 fused loop and the fp32 separate-pass loop (OPT_AMD_IW_FUSED_RES=0) lie
         within twice the larger floor — fp32's (the worst error of the fp32 fused loop on
         two 1-ulp perturbations of Offset) or fp64's — of that truth, or 1e-5."""
@@ -297,9 +301,6 @@ def test_fused_loop_at_the_examples_pcg_depth(monkeypatch, case, lit):
     truth = run(1, double=True)[0]
     sep64 = run(0, double=True)[0]
     floor64 = np.abs(sep64 - truth) / truth
-    if case == "cat512" and lit == 200:
-        _, _, t_or, _ = oracle.iw_solve(w, 2, lit, nthreads=16, double=True)
-        assert np.all(np.abs(t_or - truth) / truth <= np.maximum(4 * floor64, 1e-8)), (t_or, truth, floor64)
     floor = np.zeros_like(truth)
     for seed in (1, 2):
         c, _ = run(1, wi=_perturb_offset(w, seed))
