@@ -80,6 +80,8 @@ IW_DEFER = os.environ.get("OPT_AMD_IW_DEFER", "1") != "0"
 
 def res_bytes_per_px(i: int, liter: int = 10, defer: bool = IW_DEFER) -> int:
     b = 4 + 8 + 1 + 4 + 12 + 12 + 12 + 12
+    if i == 1 and liter >= 3:
+        b -= 12   # P0: pass 1 forms p_0 = pre r_0 from the r_0 it reads (p_0 is never stored)
     if i < liter - 1:
         b += 24
     if defer:
@@ -92,19 +94,24 @@ def res_bytes_per_px(i: int, liter: int = 10, defer: bool = IW_DEFER) -> int:
 RES_KERNEL = "iw_apply_res"
 
 
-def res_variant(i: int, defer: bool = IW_DEFER) -> str:
-    """The iw_apply_res instantiation PCG iteration i >= 1 runs (<T, DM, NT, E>)."""
+def res_variant(i: int, defer: bool = IW_DEFER, liter: int = 10) -> str:
+    """The iw_apply_res instantiation PCG iteration i >= 1 runs (<T, DM, NT, E, P0>)."""
     if defer:
         dm, e = (0, 0) if i % 2 == 1 else ((1, 1) if i == 2 else (2, 1))
     else:
         dm, e = (1 if i == 1 else 2), 0
-    return f"iw_apply_res<float, {dm}, 2, {e}>"
+    p0 = "true" if liter >= 3 and (i == 1 or (defer and i == 2)) else "false"
+    return f"iw_apply_res<float, {dm}, 2, {e}, {p0}>"
 
 
 # PCGInit1 fused with the first apply (iw_jtf_apply, one strip pass): Offset 8 + Angle 4 +
-# UrShape 8 + Constraints 8 + Mask 4 read; r 12 + angle pre 4 + flag 1 + p 12 + Ap 12 written.
+# UrShape 8 + Constraints 8 + Mask 4 read; r 12 + angle pre 4 + flag 1 + Ap 12 written, and
+# p 12 only when lIterations <= 2 (from 3 on, passes 1 and 2 form p_0 = pre r_0 themselves).
 INIT_KERNEL = "iw_jtf_apply"
-INIT_BYTES_PER_PX = 8 + 4 + 8 + 8 + 4 + 12 + 4 + 1 + 12 + 12
+
+
+def init_bytes_per_px(liter: int = 10) -> int:
+    return 8 + 4 + 8 + 8 + 4 + 12 + 4 + 1 + 12 + (12 if liter <= 2 else 0)
 
 
 def pmc_traffic(liter: int, first: int = 0, res: bool = False):
@@ -115,7 +122,7 @@ def pmc_traffic(liter: int, first: int = 0, res: bool = False):
         return None
     total = 0.0
     for i in range(first, liter):
-        key = res_variant(i) if res else APPLY_VARIANT[min(i, 2)]
+        key = res_variant(i, liter=liter) if res else APPLY_VARIANT[min(i, 2)]
         hit = [v for k, v in ks.items() if key in k]
         if not hit or "FETCH_SIZE" not in hit[0] or "WRITE_SIZE" not in hit[0]:
             return None
@@ -475,10 +482,10 @@ def main():
     }
     if n_init:
         init_s = (init_ms / 1e3) / n_init
-        ach = INIT_BYTES_PER_PX * npx / init_s / 1e9
+        ibpp = init_bytes_per_px(args.liter)
+        ach = ibpp * npx / init_s / 1e9
         result["init_kernel"] = {"kernel": INIT_KERNEL, "avg_us": init_s * 1e6, "launches": n_init,
-                                 "bytes_per_px": INIT_BYTES_PER_PX, "achieved": ach,
-                                 "frac": ach / PEAK_HBM_GBS}
+                                 "bytes_per_px": ibpp, "achieved": ach, "frac": ach / PEAK_HBM_GBS}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = (cpu_baseline_sfs(w, W, H, args.liter) if sfs
                                   else cpu_baseline(w, n_unknowns, args.liter))

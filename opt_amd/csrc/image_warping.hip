@@ -560,7 +560,10 @@ struct POff {
         t(tb + i * (unsigned)sizeof(T)), s(i * (unsigned)sizeof(T)) {}
 };
 // own: a row of this wave (the halo rows y0-1 and y1 feed the stencil only: no delta terms)
-template <typename T, int DM, bool NT, int E>
+// P0 (lIterations >= 3): p_0 = pre r_0 is not stored by PCGInit1; pass 1 (E = 0) forms its
+// p_{i-1} from the r_0 it reads anyway, and pass 2 (E = 1) reads r_0 through pin2 (the r
+// buffer it is about to overwrite with r_2, own pixel only) for the deferred alpha_0 p_0
+template <typename T, int DM, bool NT, int E, bool P0 = false>
 __device__ __forceinline__ RRaw<T> raw_rrow(const Args<T>& a, const WaveGeom& g, int y, unsigned tb,
                                             const T* pin, const T* rin, const T* Apin, const T* pre,
                                             const T* delta, const T* pin2, bool own) {
@@ -574,7 +577,7 @@ __device__ __forceinline__ RRaw<T> raw_rrow(const Args<T>& a, const WaveGeom& g,
     q.r = ldb<NT, vec2_t<T>>(rin, o.xy); q.rt = ldb<NT, T>(rin, o.t);
     q.ap = ldb<NT, vec2_t<T>>(Apin, o.xy); q.at = ldb<NT, T>(Apin, o.t);
     q.w2 = ldb<NT, T>(pre, o.s);
-    q.q = ldb<NT, vec2_t<T>>(pin, o.xy); q.qt = ldb<NT, T>(pin, o.t);
+    if (!(P0 && !E)) { q.q = ldb<NT, vec2_t<T>>(pin, o.xy); q.qt = ldb<NT, T>(pin, o.t); }
     if (DM == 2 && own) { q.d = ldb<NT, vec2_t<T>>(delta, o.xy); q.dt = ldb<NT, T>(delta, o.t); }
     if (E && own) { q.q2 = ldb<NT, vec2_t<T>>(pin2, o.xy); q.q2t = ldb<NT, T>(pin2, o.t); }
     q.ein = 0;
@@ -588,7 +591,7 @@ __device__ __forceinline__ RRaw<T> raw_rrow(const Args<T>& a, const WaveGeom& g,
         q.er = ldb<false, vec2_t<T>>(rin, oe.xy); q.ert = ldb<false, T>(rin, oe.t);
         q.eap = ldb<false, vec2_t<T>>(Apin, oe.xy); q.eat = ldb<false, T>(Apin, oe.t);
         q.ew2 = ldb<false, T>(pre, oe.s);
-        q.eq = ldb<false, vec2_t<T>>(pin, oe.xy); q.eqt = ldb<false, T>(pin, oe.t);
+        if (!(P0 && !E)) { q.eq = ldb<false, vec2_t<T>>(pin, oe.xy); q.eqt = ldb<false, T>(pin, oe.t); }
     }
     return q;
 }
@@ -602,12 +605,18 @@ __device__ __forceinline__ void make_rp(const Args<T>& a, int f, T alpha, T beta
 }
 // Finish a raw row: r_i, p_i, the edge pixel's p and residual; an owned row (own) also
 // stores r_i (unless rout is null) and the updated delta right here and adds its r_i.W r_i.
-template <typename T, int DM, bool NT, int E>
-__device__ __forceinline__ RRow<T> finish_rrow(const Args<T>& a, const RRaw<T>& q, T beta, T alpha, T alpha2, bool own,
+template <typename T, int DM, bool NT, int E, bool P0 = false>
+__device__ __forceinline__ RRow<T> finish_rrow(const Args<T>& a, const RRaw<T>& qin, T beta, T alpha, T alpha2, bool own,
                                                const WaveGeom& g, int y, unsigned tb, T* rout, T* delta,
                                                acc_t& rzd) {
     RRow<T> o;
+    RRaw<T> q = qin;
     const int f = q.in ? q.f : 0;
+    if constexpr (P0) {   // p_0 = pre r_0 (PCGInit1's p, iw_jtf_apply's cpx / cpy / cpt: the same T products)
+        const T w0 = pre_offset(a, f);
+        if (E == 0) { q.q.x = w0 * q.r.x; q.q.y = w0 * q.r.y; q.qt = q.w2 * q.rt; }
+        else { q.q2.x = w0 * q.q2.x; q.q2.y = w0 * q.q2.y; q.q2t = q.w2 * q.q2t; }   // pin2 held r_0
+    }
     o.act = f & 1;
     o.fit = (f >> 1) & 1;
     o.ux = q.in ? q.u.x : 0.f;
@@ -643,6 +652,10 @@ __device__ __forceinline__ RRow<T> finish_rrow(const Args<T>& a, const RRaw<T>& 
     }
     if (!o.act) { o.px = 0; o.py = 0; o.pt = 0; }
     const int ef = q.ein ? q.ef : 0;
+    if constexpr (P0 && E == 0) {
+        const T we = pre_offset(a, ef);
+        q.eq.x = we * q.er.x; q.eq.y = we * q.er.y; q.eqt = q.ew2 * q.ert;
+    }
     o.eact = ef & 1;
     o.eux = q.ein ? q.eu.x : 0.f;
     o.euy = q.ein ? q.eu.y : 0.f;
@@ -655,14 +668,16 @@ __device__ __forceinline__ RRow<T> finish_rrow(const Args<T>& a, const RRaw<T>& 
           o.ejx, o.ejy, ax, ay);
     return o;
 }
-template <typename T, int DM, int NT = 2, int E = 0>
+// P0: see raw_rrow; pass 2 then reads r_0 through pin2 from the buffer it writes r_2 to
+// (rout), own pixel before own pixel: those two are not __restrict__
+template <typename T, int DM, int NT = 2, int E = 0, bool P0 = false>
 __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_apply_res(Args<T> a, const T* __restrict__ pin,
                                                        const T* __restrict__ rin, const T* __restrict__ Apin,
                                                        const T* __restrict__ pre, T* __restrict__ pout,
-                                                       T* __restrict__ rout, T* __restrict__ Apout,
+                                                       T* rout, T* __restrict__ Apout,
                                                        T* __restrict__ delta, double* __restrict__ sc,
                                                        int prev, double base_scale, ReduceSlot rs,
-                                                       const T* __restrict__ pin2 = nullptr) {
+                                                       const T* pin2 = nullptr) {
     constexpr bool LNT = (NT & 1) != 0, SNT = (NT & 2) != 0;
     IW_PRE_TABLE(a);
     // 64-column strips with the 2-lane edge record (iw_apply's geometry): every store is a
@@ -690,11 +705,11 @@ __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_apply_res(Args<T> a, 
     acc_t rzd = 0, papd = 0, rapd = 0, apapd = 0;
     if (g.y0 < g.y1) {
         auto raw = [&](int y) {
-            return raw_rrow<T, DM, LNT, E>(a, g, y, tb, pin, rin, Apin, pre, delta, pin2, y >= g.y0 && y < g.y1);
+            return raw_rrow<T, DM, LNT, E, P0>(a, g, y, tb, pin, rin, Apin, pre, delta, pin2, y >= g.y0 && y < g.y1);
         };
         auto fin = [&](const RRaw<T>& q, int y) {
-            return finish_rrow<T, DM, SNT, E>(a, q, beta, alpha, alpha2, y >= g.y0 && y < g.y1, g, y, tb, rout,
-                                              delta, rzd);
+            return finish_rrow<T, DM, SNT, E, P0>(a, q, beta, alpha, alpha2, y >= g.y0 && y < g.y1, g, y, tb, rout,
+                                                  delta, rzd);
         };
         const RRow<T> up = fin(raw(g.y0 - 1), g.y0 - 1);
         RRow<T> A = fin(raw(g.y0), g.y0);
@@ -1123,8 +1138,10 @@ __device__ __forceinline__ void iw_jtf_apply_body(const Args<T>& a, T* __restric
                     vec2_t<T> v; v.x = aox; v.y = aoy;
                     stb<(NT & 2) != 0>(Ap, off.xy, v); stb<(NT & 2) != 0>(Ap, off.t, aot);
                 }
-                vec2_t<T> pv; pv.x = cpx; pv.y = cpy;
-                stb<(NT & 2) != 0>(pout, off.xy, pv); stb<(NT & 2) != 0>(pout, off.t, cpt);
+                if (pout) {   // null when the loop forms p_0 from r_0 itself (lIterations >= 3)
+                    vec2_t<T> pv; pv.x = cpx; pv.y = cpy;
+                    stb<(NT & 2) != 0>(pout, off.xy, pv); stb<(NT & 2) != 0>(pout, off.t, cpt);
+                }
                 papdot += (acc_t)(cpx * aox + cpy * aoy + cpt * aot);
                 // PCGStep2's weights: pre, or 1 without a preconditioner
                 const T w0 = a.use_pre ? cur.wo : (T)1, w2 = a.use_pre ? cur.wt : (T)1;
@@ -1569,8 +1586,11 @@ public:
         // in pairs by the next even iteration (or the update), which reads p_{i-2} again
         const bool defer = res && defer_;
         T* pb[3] = {p0_, p1_, p2_};
+        // lIterations >= 3 with the fused loop: nothing but passes 1 and 2 reads p_0, and both
+        // form it from r_0 (iw_apply_res P0), so PCGInit1 does not store it
+        const bool p0 = res && L >= 3;
         if (fused) {
-            launch_jtf_apply(pcur, L == 1);
+            launch_jtf_apply(p0 ? nullptr : pcur, L == 1);
         } else {
             tbegin("iw_jtf"); launch_jtf(r_, pre_, rz(0), false, res); tend();
             allreduce(rz(0));
@@ -1599,7 +1619,8 @@ public:
                 const bool last = i + 1 == L;
                 T* rb[2] = {r_, r1_};
                 T* ab[2] = {Ap_, Ap1_};
-                const T* pin2 = (defer && i >= 2) ? pbuf(i - 2) : nullptr;
+                // pass 2 with P0: p_0 is formed from r_0, still in the r buffer pass 2 writes r_2 to
+                const T* pin2 = (defer && i >= 2) ? ((p0 && i == 2) ? rb[0] : pbuf(i - 2)) : nullptr;
                 if (distributed()) {   // the stencil reads r, Ap and p of iteration i-1 in the halo rows
                     std::vector<HaloPlane> pl;
                     add_vec_planes(pl, rb[(i - 1) & 1]);
@@ -1607,16 +1628,16 @@ public:
                     add_vec_planes(pl, pbuf(i - 1));
                     if (split) {   // beside the interior row blocks
                         halo_mark();
-                        launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 1);
+                        launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 1, p0);
                         halo_begin(comm_, pl, dom_, 1);
                         halo_join();
-                        launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 2);
+                        launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 2, p0);
                     } else {
                         exchange(pl);
-                        launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2);
+                        launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 0, p0);
                     }
                 } else {
-                    launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2);
+                    launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 0, p0);
                 }
                 allreduce(rz(i), 4);   // rz, pAp, r.W Ap, Ap.W Ap of iteration i
             }
@@ -1995,7 +2016,8 @@ private:
     // PCG iteration i >= 1 of the fused loop: r_{i-1} / Ap_{i-1} in buffer (i-1) & 1 (r_ / Ap_
     // for even), r_i / Ap_i into the other one (none in the last iteration)
     // part: 0 every row block, 1 the interior ones, 2 the first and last (launch_apply)
-    void launch_apply_res(int i, const T* pin, T* pout, bool last, const T* pin2 = nullptr, int part = 0) {
+    void launch_apply_res(int i, const T* pin, T* pout, bool last, const T* pin2 = nullptr, int part = 0,
+                          bool p0 = false) {
         T* rb[2] = {r_, r1_};
         T* ab[2] = {Ap_, Ap1_};
         const T* rin = rb[(i - 1) & 1];
@@ -2019,12 +2041,15 @@ private:
                          red_.scalars, rz(i - 1), base_scale, rs, pin2);
         };
         // streaming stores of the PCG vectors (NT = 2; streaming loads too, or plain
-        // stores, measured +1-5 %, round 3)
+        // stores, measured +1-5 %, round 3); P0: passes 1 and 2 form p_0 from r_0
         if (pin2 || (defer_ && i == 1)) {   // deferred delta: odd i none, i = 2 starts it, even i > 2 folds a pair
-            if (i % 2 == 1) go(iw::iw_apply_res<T, 0, 2, 0>);
+            if (i == 1 && p0) go(iw::iw_apply_res<T, 0, 2, 0, true>);
+            else if (i % 2 == 1) go(iw::iw_apply_res<T, 0, 2, 0>);
+            else if (i == 2 && p0) go(iw::iw_apply_res<T, 1, 2, 1, true>);
             else if (i == 2) go(iw::iw_apply_res<T, 1, 2, 1>);
             else go(iw::iw_apply_res<T, 2, 2, 1>);
-        } else if (i == 1) go(iw::iw_apply_res<T, 1, 2>);
+        } else if (i == 1 && p0) go(iw::iw_apply_res<T, 1, 2, 0, true>);
+        else if (i == 1) go(iw::iw_apply_res<T, 1, 2>);
         else go(iw::iw_apply_res<T, 2, 2>);
     }
     void launch_residual(int i_num, int i_den, int sc_out) {

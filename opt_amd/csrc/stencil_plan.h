@@ -611,7 +611,9 @@ public:
             materialize();
             mat_apply((const T*)p, (T*)Ap, nullptr, kScTmp);
         } else {
+            tbegin(Op::kApplyName);   // the same timer entry as the PCG loop's applies
             op_->apply((const T*)p, (T*)Ap, nullptr, nullptr, red_.slot(nb(), kScTmp), stream_);
+            tend();
         }
         allreduce(kScTmp, 1);
         *pAp = read(kScTmp);
