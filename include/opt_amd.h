@@ -168,8 +168,10 @@ int OptAMD_CsrSpMV(int nRowsA, int nColsA, long long nnz, const int* rowPtrA, co
 
 /* General energy front end (the reference's energy compiler, API/src/o.t:1295-1348 and
  * 2669-3235): the HIP source generated for the energy file `filename` (float kernels, or
- * double with doublePrecision = 1), copied into buf (NUL-terminated, truncated to n).
- * Returns the full length, or -1 with the front end's message in buf. No device needed. */
+ * double with bit 0 of doublePrecision set; bit 1 selects the 32-bit gather addressing a
+ * plan takes when its arrays are below 2 GiB), copied into buf (NUL-terminated, truncated
+ * to n). Returns the full length, or -1 with the front end's message in buf. No device
+ * needed. */
 int OptAMD_GenericSource(const char* filename, int doublePrecision, char* buf, int n);
 
 /* The residual templates the front end lowered `filename` to, one line each:

@@ -394,9 +394,10 @@ def _text_call(fn, *args, cap: int = 1 << 23):
     return r, buf.value.decode(errors="replace")
 
 
-def generic_source(energy_file: str, double: bool = False) -> str:
-    """HIP source the front end generates for `energy_file` (OptAMD_GenericSource)."""
-    r, txt = _text_call(load_library().OptAMD_GenericSource, energy_file.encode(), int(double))
+def generic_source(energy_file: str, double: bool = False, off32: bool = False) -> str:
+    """HIP source the front end generates for `energy_file` (OptAMD_GenericSource); off32:
+    the 32-bit gather addressing plans take for arrays below 2 GiB."""
+    r, txt = _text_call(load_library().OptAMD_GenericSource, energy_file.encode(), int(double) | (2 if off32 else 0))
     if r < 0:
         raise OptError(txt)
     return txt

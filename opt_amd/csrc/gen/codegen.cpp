@@ -70,6 +70,10 @@ struct GraphCache {
     std::map<std::tuple<int, int, int>, int> ch;
 };
 const GraphCache* g_gcache = nullptr;
+// Slot reads (graph gathers) as uniform base + 32-bit byte offset (generate's off32): the
+// saddr form of global_load, one 32-bit multiply per neighbour instead of a 64-bit address
+// per gathered array
+bool g_off32 = false;
 
 bool transcendental(const Node& n) {
     return n.op == Op::Sin || n.op == Op::Cos || n.op == Op::Exp || n.op == Op::Log || n.op == Op::Sqrt;
@@ -124,6 +128,8 @@ public:
                 const int W = g_gcache->width, k = ci->second;
                 const std::string rec = "((const T*)a.img[" + std::to_string(g_gcache->img) + "]) + (long long)v" +
                                         std::to_string(c.slot) + " * " + std::to_string(W);
+                const std::string rec32 = "opt_g32((const T*)a.img[" + std::to_string(g_gcache->img) + "], v" +
+                                          std::to_string(c.slot) + ", " + std::to_string(W) + ", ";
                 std::string name;
                 // the slot's whole record once as 16-byte vectors (per-edge kernels: gen_cost
                 // 51.7 -> 41.5 us on 1M-vertex ARAP); the vertex gathers read the fields they use
@@ -139,7 +145,10 @@ public:
                     name = kr + "_" + std::to_string(k / 4) + "." + "xyzw"[k % 4];
                 } else {
                     name = "k" + std::to_string(id);
-                    out(id) << "        const T " << name << " = (" << rec << ")[" << k << "];\n";
+                    if (g_off32 && W <= 16)   // (the plan's size check assumes <= 16 fields)
+                        out(id) << "        const T " << name << " = " << rec32 << k << ");\n";
+                    else
+                        out(id) << "        const T " << name << " = (" << rec << ")[" << k << "];\n";
                 }
                 done_[id] = name;
                 return name;
@@ -267,6 +276,7 @@ private:
             base = "((const " + std::string(elem_type(im.elem, im.tvalued)) + "*)a.img[" + std::to_string(n.i) + "])";
         }
         if (n.slot >= 0) {
+            if (g_off32) return "(T)opt_g32(" + base + ", v" + std::to_string(n.slot) + ", " + ch + ", " + c + ")";
             idx = "(long long)v" + std::to_string(n.slot) + " * " + ch + " + " + c;
             return "(T)(" + base + ")[" + idx + "]";
         }
@@ -296,8 +306,9 @@ struct Instance {   // a centred residual shifted so that it contains unknown (i
 
 }  // namespace
 
-GenSource generate(GModel& m, bool dbl) {
+GenSource generate(GModel& m, bool dbl, bool off32) {
     GenSource gs;
+    g_off32 = off32;
     Pool& P = m.pool;
     const int nd = m.unknown_dims();
     const std::vector<int> unk = m.unknown_images();
@@ -342,6 +353,19 @@ GenSource generate(GModel& m, bool dbl) {
          "__device__ __forceinline__ T opt_sh(T v, int d) { for (; d > 0; --d) v = opt_lr(v); for (; d < 0; ++d) v = opt_ll(v); return v; }\n";
     // masked read without a branch: the load always issues (at element 0 of the array when
     // the access is outside), the value is selected afterwards
+    // XCD-contiguous block order for the graph kernels: the hardware deals blocks to the 8
+    // XCDs round robin, so with blockIdx order a vertex's mesh neighbours (v +- 1, v +- a
+    // row) are gathered on several XCDs and cached in each one's L2; with this order each
+    // XCD walks one contiguous eighth of the vertices (of each grid-stride pass)
+    o << "__device__ __forceinline__ long long opt_xcd_block() {\n"
+         "    const int nb = gridDim.x, b = blockIdx.x, q = nb / 8, r = nb % 8, x = b % 8;\n"
+         "    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;\n}\n";
+    // element v * stride + c of b, addressed as b + a 32-bit byte offset to element v's
+    // record (generate's off32) + c: the channel stays a constant offset of the same
+    // address, so a record's channels merge into one multi-dword load (a channel inside
+    // the 32-bit sum cannot: the compiler must allow for its wrap-around)
+    o << "template <typename E> __device__ __forceinline__ E opt_g32(const E* b, int v, unsigned stride, unsigned c) {\n"
+         "    return ((const E*)((const char*)b + (unsigned)v * (stride * (unsigned)sizeof(E))))[c];\n}\n";
     o << "template <typename E> __device__ __forceinline__ T opt_ldm(const E* b, long long i, bool c) {\n"
          "    const E v = b[c ? i : 0]; return c ? (T)v : (T)0;\n}\n"
          // both channels of a 2-channel element (i = its first channel) in one access when
@@ -618,16 +642,11 @@ GenSource generate(GModel& m, bool dbl) {
 
 
     // -------------------------------------------------------------- gen_apply
-    {
-        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_apply(GenArgs a, const T* __restrict__ p, T* __restrict__ Ap,\n"
-             "        const T* __restrict__ dadd, const int* stop, ReduceSlot rs, int finish) {\n"
-             "    if (stop && *stop) return;\n"
-             "    OPT_COORDS\n"
-             "    T dot = 0;\n";
-        o << "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
-              << coords;
-        Body b(m, o, nd, uslot);
-        b.line("const bool act = (a.flags[lin] & 1) != 0;");
+    // The gather form of the centred J^T J p at pixel `lin` (coordinates in scope). fused:
+    // inside gen_apply_graph, the sum of output (k, c) goes to cacc<slot>_<c> (declared by
+    // the caller) instead of Ap
+    auto centred_apply = [&](Body& b, bool fused) {
+        if (!fused) b.line("const bool act = (a.flags[lin] & 1) != 0;");
         std::map<std::string, std::string> jp;   // (residual, shift) -> J p of that instance
         for (int k : unk) {
             const GImage& im = m.images[k];
@@ -654,15 +673,30 @@ GenSource generate(GModel& m, bool dbl) {
                     }
                     terms.push_back(b.v(g) + " * " + jp[key]);
                 }
-                const std::string e = "a.uoff[" + std::to_string(uslot[k]) + "] + lin * " + std::to_string(im.channels) +
-                                      " + " + std::to_string(c);
                 std::string acc = "(T)0";
                 for (auto& t : terms) acc += " + " + t;
+                if (fused) {
+                    b.line("cacc" + std::to_string(uslot[k]) + "_" + std::to_string(c) + " = " + acc + ";");
+                    continue;
+                }
+                const std::string e = "a.uoff[" + std::to_string(uslot[k]) + "] + lin * " + std::to_string(im.channels) +
+                                      " + " + std::to_string(c);
                 b.line("{ const long long e = " + e + "; const T acc = " + acc + ";");
                 b.line("  if (finish) { const T pe = p[e]; const T o = act ? acc + (dadd ? dadd[e] * pe : (T)0) : (T)0; Ap[e] = o; dot += pe * o; }");
                 b.line("  else Ap[e] = acc; }");
             }
         }
+    };
+    {
+        o << "extern \"C\" __global__ __launch_bounds__(256) void gen_apply(GenArgs a, const T* __restrict__ p, T* __restrict__ Ap,\n"
+             "        const T* __restrict__ dadd, const int* stop, ReduceSlot rs, int finish) {\n"
+             "    if (stop && *stop) return;\n"
+             "    OPT_COORDS\n"
+             "    T dot = 0;\n";
+        o << "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
+              << coords;
+        Body b(m, o, nd, uslot);
+        centred_apply(b, false);
         o << "    }\n"
              "    if (finish) { double v[1] = {(double)dot}; block_reduce_publish<1>(v, rs, blockIdx.x); }\n}\n";
     }
@@ -1247,7 +1281,7 @@ GenSource generate(GModel& m, bool dbl) {
             const size_t ns = m.graphs[g].slot_names.size();
             auto sl = [&](size_t s) { return "a.slot[" + std::to_string(gs.slot_base[g] + s) + "]"; };
             o << "    {\n    const long long es = (long long)gridDim.x * 256, ne = a.nedge[" << g << "];\n"
-              << "    long long e = (long long)blockIdx.x * 256 + threadIdx.x;\n";
+              << "    long long e = opt_xcd_block() * 256 + threadIdx.x;\n";
             if (prefetch_nb)
                 for (size_t s = 0; s < ns; ++s) o << "    int n" << s << " = e < ne ? " << sl(s) << "[e] : 0;\n";
             o << "    for (; e < ne; e += es) {\n";
@@ -1362,12 +1396,15 @@ GenSource generate(GModel& m, bool dbl) {
                         if (it == gs.nb_pairs.end()) gs.nb_pairs.push_back(key);
                         const std::string vs = "v" + std::to_string(s2), ns = "n" + std::to_string(s2);
                         const std::string gnb = "a.gnb[" + std::to_string(idx) + "]";
+                        auto at = [&](const std::string& q) {
+                            return off32 ? "opt_g32(" + gnb + ", " + q + ", 1, 0)" : gnb + "[" + q + "]";
+                        };
                         if (idx < 32 && prefetch_nb) {
-                            head << "        int " << ns << " = q0 < q1 ? " << gnb << "[q0] : 0;\n";
+                            head << "        int " << ns << " = q0 < q1 ? " << at("q0") << " : 0;\n";
                             loop << "        const int " << vs << " = " << ns << ";\n"
-                                 << "        if (q + 1 < q1) " << ns << " = " << gnb << "[q + 1];\n";
+                                 << "        if (q + 1 < q1) " << ns << " = " << at("q + 1") << ";\n";
                         } else if (idx < 32) {   // GenArgs::gnb capacity; past it, through the edge id
-                            loop << "        const int " << vs << " = " << gnb << "[q];\n";
+                            loop << "        const int " << vs << " = " << at("q") << ";\n";
                         } else {
                             loop << "        const int " << vs << " = a.slot[" << key.second << "][a.geid[" << sbk
                                  << "][q]];\n";
@@ -1383,7 +1420,7 @@ GenSource generate(GModel& m, bool dbl) {
     {
         o << "extern \"C\" __global__ __launch_bounds__(256) void gen_jtf_graph(GenArgs a, T* __restrict__ r, T* __restrict__ diag) {\n"
              "    OPT_COORDS\n"
-             "    for (long long vtx = (long long)blockIdx.x * 256 + threadIdx.x; vtx < a.npix; vtx += (long long)gridDim.x * 256) {\n";
+             "    for (long long vtx = opt_xcd_block() * 256 + threadIdx.x; vtx < a.npix; vtx += (long long)gridDim.x * 256) {\n";
         graph_gather(false);
         o << "        const bool act = (a.flags[vtx] & 1) != 0;\n";
         for (int k : unk)
@@ -1400,16 +1437,31 @@ GenSource generate(GModel& m, bool dbl) {
              "    if (stop && *stop) return;\n"
              "    OPT_COORDS\n"
              "    T dot = 0;\n"
-             "    for (long long vtx = (long long)blockIdx.x * 256 + threadIdx.x; vtx < a.npix; vtx += (long long)gridDim.x * 256) {\n";
+             "    for (long long vtx = opt_xcd_block() * 256 + threadIdx.x; vtx < a.npix; vtx += (long long)gridDim.x * 256) {\n";
         graph_gather(true);
+        // 1-D vertex domains: the centred terms at this vertex too (after the edge loops,
+        // whose registers are free by then), instead of a gen_apply pass that stores them
+        // for this kernel to read back
+        gs.graph_apply_centred = gs.has_centered && nd == 1;
+        if (gs.graph_apply_centred) {
+            std::string decl = "        T";
+            for (int k : unk)
+                for (int c = 0; c < m.images[k].channels; ++c)
+                    decl += std::string(decl.size() > 9 ? "," : "") + " cacc" + std::to_string(uslot[k]) + "_" + std::to_string(c) + " = 0";
+            o << decl << ";\n        {\n        const long long lin = vtx;\n" << coords;
+            Body b(m, o, nd, uslot);
+            centred_apply(b, true);
+            o << "        }\n";
+        }
         o << "        const bool act = (a.flags[vtx] & 1) != 0;\n";
         for (int k : unk)
             for (int c = 0; c < m.images[k].channels; ++c) {
                 const std::string e = "a.uoff[" + std::to_string(uslot[k]) + "] + vtx * " +
                                       std::to_string(m.images[k].channels) + " + " + std::to_string(c);
                 const std::string sfx = std::to_string(uslot[k]) + "_" + std::to_string(c);
+                const std::string cen = gs.graph_apply_centred ? "cacc" + sfx : "(has_centred ? Ap[i] : (T)0)";
                 o << "        { const long long i = " << e << "; const T pe = p[i];\n"
-                  << "          const T o = act ? (has_centred ? Ap[i] : (T)0) + acc" << sfx
+                  << "          const T o = act ? " << cen << " + acc" << sfx
                   << " + (dadd ? dadd[i] * pe : (T)0) : (T)0;\n"
                   << "          Ap[i] = o; dot += pe * o; }\n";
             }

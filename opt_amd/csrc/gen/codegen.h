@@ -53,10 +53,16 @@ struct GenSource {
     // GenArgs::gnb[i] = slot nb_pairs[i].second's vertex of each edge in slot
     // nb_pairs[i].first's incidence order (the graph gathers read neighbours through it)
     std::vector<std::pair<int, int>> nb_pairs;
+    // gen_apply_graph adds the centred residuals' terms itself (1-D vertex domains): the
+    // plan launches no gen_apply before it
+    bool graph_apply_centred = false;
 };
 
-// Generate the kernels for `m` in float (dbl = false) or double.
-GenSource generate(GModel& m, bool dbl);
+// Generate the kernels for `m` in float (dbl = false) or double. off32: every array a
+// graph gather reads (the unknown vectors, known and internal images, the incidence
+// copies) is below 2 GiB, so slot reads address it as a uniform base plus a 32-bit byte
+// offset (the plan checks the sizes).
+GenSource generate(GModel& m, bool dbl, bool off32 = false);
 
 }  // namespace gen
 }  // namespace optamd

@@ -82,6 +82,25 @@ size_t elem_size(const gen::GImage& im, bool dbl) {
     return 4;
 }
 
+// gen::generate's off32: every array the graph gathers read is below 2 GiB — the unknown
+// vectors, the images (all allocated at the unknowns' domain size), the graph record cache
+// (at most 16 fields per vertex in the 32-bit form, codegen.cpp) and the per-edge
+// incidence copies. The same answer at the admission compile and in the plan.
+bool gather_offsets_fit_32(const gen::GModel& m, const ProblemSpec& s, bool dbl) {
+    const long long lim = 1LL << 31, t = dbl ? 8 : 4;
+    long long npix = 1, chans = 0;
+    for (int d : m.images[m.unknown_images()[0]].dims) npix *= (long long)s.dim_values.at(m.dims[d].index);
+    for (int k : m.unknown_images()) chans += m.images[k].channels;
+    bool ok = npix * chans * t < lim && npix * 16 * t < lim;
+    for (auto& im : m.images) ok &= npix * im.channels * (long long)elem_size(im, dbl) < lim;
+    for (auto& g : m.graphs) {
+        long long e = 1;
+        for (int d : g.dims) e *= (long long)s.dim_values.at(m.dims[d].index);
+        ok &= e * 4 < lim;
+    }
+    return ok;
+}
+
 }  // namespace
 
 // Front-end admission check for Opt_ProblemDefine: lower the energy and check it fits the
@@ -238,7 +257,7 @@ public:
             off += npix_ * m_.images[unk_[k]].channels;
         }
         n_ = off;
-        src_ = gen::generate(m_, sizeof(T) == 8);
+        src_ = gen::generate(m_, sizeof(T) == 8, gather_offsets_fit_32(m_, spec, sizeof(T) == 8));
         load_module();
         for (size_t i = 0; i < m_.images.size(); ++i)
             if (m_.images[i].internal) {   // ComputedArray values and gradient images
@@ -383,7 +402,7 @@ public:
             launch(k_apply_, s, {&a_, &p, &Ap, &dadd, &stop, &rs, &finish});
             return;
         }
-        int finish = 0, centred = src_.has_centered ? 1 : 0;
+        int finish = 0, centred = src_.has_centered && !src_.graph_apply_centred ? 1 : 0;
         if (centred) launch(k_apply_, s, {&a_, &p, &Ap, &dadd, &stop, &rs, &finish});
         launch(k_apply_graph_, s, {&a_, &p, &Ap, &dadd, &stop, &rs, &centred});
     }
@@ -657,7 +676,7 @@ std::unique_ptr<Plan> make_generic_plan(const ProblemSpec& spec, const StateOpti
         gen::GModel mc;
         std::string e2;
         gen::build_model(spec.text, &mc, &e2);
-        const std::string code = gen::generate(mc, opts.double_precision).code;
+        const std::string code = gen::generate(mc, opts.double_precision, gather_offsets_fit_32(mc, s, opts.double_precision)).code;
         std::lock_guard<std::mutex> lk(g_mu);
         if (!code_cache().count(code)) {
             std::string obj, log;
@@ -678,12 +697,12 @@ std::unique_ptr<Plan> make_generic_plan(const ProblemSpec& spec, const StateOpti
 }
 
 // Generated source for `text` (tests / inspection): length, or -1 + message in buf.
-int generic_source(const std::string& text, bool dbl, std::string* out) {
+int generic_source(const std::string& text, bool dbl, std::string* out, bool off32) {
     gen::GModel m;
     std::string err;
     if (!gen::build_model(text, &m, &err)) { *out = err; return -1; }
     if (!m.unsupported.empty()) { *out = "unsupported: " + m.unsupported; return -1; }
-    *out = gen::generate(m, dbl).code;
+    *out = gen::generate(m, dbl, off32).code;
     return (int)out->size();
 }
 

@@ -417,7 +417,7 @@ static bool read_file(const char* filename, std::string* text) {
 int OptAMD_GenericSource(const char* filename, int doublePrecision, char* buf, int n) {
     std::string text, out;
     if (!read_file(filename, &text)) return copy_name("cannot read energy file", buf, n), -1;
-    const int r = optamd::generic_source(text, doublePrecision != 0, &out);
+    const int r = optamd::generic_source(text, (doublePrecision & 1) != 0, &out, (doublePrecision & 2) != 0);
     copy_name(out, buf, n);
     return r;
 }

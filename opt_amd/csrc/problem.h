@@ -63,7 +63,7 @@ bool parse_energy(const std::string& text, ProblemSpec* spec, std::string* err);
 bool classify(ProblemSpec* spec, std::string* err);
 // General front end (generic.hip): accept any energy gen/ lowers; sets family "generic".
 bool generic_accepts(const std::string& text, ProblemSpec* spec, std::string* err);
-int generic_source(const std::string& text, bool dbl, std::string* out);
+int generic_source(const std::string& text, bool dbl, std::string* out, bool off32 = false);
 int generic_describe(const std::string& text, std::string* out);
 int generic_compile_check(const std::string& text, bool dbl, std::string* log);
 // Structural signature of the lowered energy (declarations + residual templates, names
