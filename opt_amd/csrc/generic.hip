@@ -725,6 +725,10 @@ int generic_compile_check(const std::string& text, bool dbl, std::string* log) {
     std::string code;
     if (generic_source(text, dbl, &code) < 0) { *log = code; return -1; }
     std::string obj;
+    if (!rtc_compile(code, &obj, log)) return -1;
+    // graph energies: also the 32-bit gather form plans take below 2 GiB
+    if (code.find("a.gnb[") == std::string::npos) return 0;
+    if (generic_source(text, dbl, &code, true) < 0) { *log = code; return -1; }
     return rtc_compile(code, &obj, log) ? 0 : -1;
 }
 

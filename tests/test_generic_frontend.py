@@ -57,6 +57,11 @@ def test_generated_source_compiles(name):
         assert k in src
     assert "typedef float T;" in src
     assert "typedef double T;" in api.generic_source(E(name), double=True)
+    # graph energies: the 32-bit gather form (plans with arrays below 2 GiB) differs only
+    # in the slot reads; generic_compile_check compiles it too
+    if "a.gnb[" in src:
+        s32 = api.generic_source(E(name), off32=True)
+        assert "opt_g32(p + a.uoff[" in s32 and "opt_g32(p + a.uoff[" not in src
     api.generic_compile_check(E(name))
 
 
