@@ -347,6 +347,12 @@ __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restr
 // per SIMD) 50.6-50.9 us against 3 slots (110 VGPRs, 4 waves) 52.4-52.5 us for kdir +
 // apply at 1 M vertices (profiles/r03_arap_eb.txt); OPT_AMD_ARAP_EB=3 restores 3
 constexpr int kEBM = 2;
+#ifndef OPTAMD_ARAP_IDPF
+#define OPTAMD_ARAP_IDPF 1
+#endif
+#ifndef OPTAMD_ARAP_OWNK
+#define OPTAMD_ARAP_OWNK 0
+#endif
 template <typename T, int EB = kEBM>
 __global__ __launch_bounds__(kBlock) void arap_apply_merged(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
                                                             const T* __restrict__ Kall, const T* __restrict__ dadd,
@@ -361,25 +367,47 @@ __global__ __launch_bounds__(kBlock) void arap_apply_merged(Args<T> a, const T* 
         const V3<T> Av = ld3<T>(a.A, v);
         const V3<float> Uv = ld3<float>(a.U, v);
         T K[9];
+#if OPTAMD_ARAP_OWNK
+#pragma unroll
+        for (int q = 0; q < 9; ++q) K[q] = Kall[q * N + v];   // this vertex's K from the K pass
+#else
         {
             T R[9], dR[3][9];
             rotation(Av, R, dR);
             directional(dR, pA, K);
         }
+#endif
         T M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         V3<T> aO = {0, 0, 0}, aA = {0, 0, 0};
         if (fit_valid(a, v)) aO = {wf * (wf * pO.x), wf * (wf * pO.y), wf * (wf * pO.z)};
         const int lane = v & 63;
         const int* nel = a.nb_ell + a.nb_eoff[v >> 6] + lane;
         const int nw = a.nb_ew[v >> 6];
+#if OPTAMD_ARAP_IDPF
+        // the next batch's slots are loaded while this batch gathers (one dependent load
+        // latency per batch instead of two)
+        int xn[EB];
+#pragma unroll
+        for (int b = 0; b < EB; ++b) xn[b] = nw > 0 ? nel[64 * b] : -1;
+#endif
         for (int i0 = 0; i0 < nw; i0 += EB) {
             int u[EB], kind[EB];
 #pragma unroll
             for (int b = 0; b < EB; ++b) {
+#if OPTAMD_ARAP_IDPF
+                const int x = xn[b];
+#else
                 const int x = nel[64 * (i0 + b)];
+#endif
                 kind[b] = x < 0 ? 0 : (x >> 28);
                 u[b] = x < 0 ? v : (x & 0x0FFFFFFF);
             }
+#if OPTAMD_ARAP_IDPF
+            if (i0 + EB < nw) {
+#pragma unroll
+                for (int b = 0; b < EB; ++b) xn[b] = nel[64 * (i0 + EB + b)];
+            }
+#endif
             V3<T> pu[EB];
             V3<float> Uu[EB];
             T Ku[EB][9];
