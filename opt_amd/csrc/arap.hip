@@ -347,8 +347,8 @@ __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restr
 // per SIMD) 50.6-50.9 us against 3 slots (110 VGPRs, 4 waves) 52.4-52.5 us for kdir +
 // apply at 1 M vertices (profiles/r03_arap_eb.txt); OPT_AMD_ARAP_EB=3 restores 3
 constexpr int kEBM = 2;
-#ifndef OPTAMD_ARAP_IDPF
-#define OPTAMD_ARAP_IDPF 1
+#ifndef OPTAMD_ARAP_DPF
+#define OPTAMD_ARAP_DPF 0
 #endif
 #ifndef OPTAMD_ARAP_OWNK
 #define OPTAMD_ARAP_OWNK 0
@@ -383,64 +383,83 @@ __global__ __launch_bounds__(kBlock) void arap_apply_merged(Args<T> a, const T* 
         const int lane = v & 63;
         const int* nel = a.nb_ell + a.nb_eoff[v >> 6] + lane;
         const int nw = a.nb_ew[v >> 6];
-#if OPTAMD_ARAP_IDPF
-        // the next batch's slots are loaded while this batch gathers (one dependent load
+        // one merged slot: the neighbour's p_O, UrShape and K (kind 0: padding, the vertex
+        // itself, contributing exact zeros through the selects below)
+        struct Slot { int kind; V3<T> pu; V3<float> Uu; T Ku[9]; };
+        auto gather = [&](int x, Slot& sl) {
+            sl.kind = x < 0 ? 0 : (x >> 28);
+            const int u = x < 0 ? v : (x & 0x0FFFFFFF);
+            sl.pu = gld3<T>(p, u);
+            sl.Uu = gld3<float>(a.U, u);
+#pragma unroll
+            for (int q = 0; q < 9; ++q) sl.Ku[q] = gldq(Kall, (unsigned)q * (unsigned)N, u);
+        };
+        auto use = [&](const Slot& sl) {
+            const bool out = sl.kind & 1, in = sl.kind & 2;
+            const V3<T> d = {(T)(Uv.x - sl.Uu.x), (T)(Uv.y - sl.Uu.y), (T)(Uv.z - sl.Uu.z)};
+            {   // out-edge v -> u
+                const V3<T> Kd = mv(K, d);
+                const V3<T> jp = {out ? wr * (pO.x - sl.pu.x - Kd.x) : (T)0, out ? wr * (pO.y - sl.pu.y - Kd.y) : (T)0,
+                                  out ? wr * (pO.z - sl.pu.z - Kd.z) : (T)0};
+                const V3<T> dd = {out ? d.x : (T)0, out ? d.y : (T)0, out ? d.z : (T)0};
+                aO.x += wr * jp.x; aO.y += wr * jp.y; aO.z += wr * jp.z;
+                M[0] += jp.x * dd.x; M[1] += jp.x * dd.y; M[2] += jp.x * dd.z;
+                M[3] += jp.y * dd.x; M[4] += jp.y * dd.y; M[5] += jp.y * dd.z;
+                M[6] += jp.z * dd.x; M[7] += jp.z * dd.y; M[8] += jp.z * dd.z;
+            }
+            {   // in-edge u -> v
+                const V3<T> di = {(T)(sl.Uu.x - Uv.x), (T)(sl.Uu.y - Uv.y), (T)(sl.Uu.z - Uv.z)};
+                const V3<T> Kd = mv(sl.Ku, di);
+                const V3<T> jp = {in ? wr * (sl.pu.x - pO.x - Kd.x) : (T)0, in ? wr * (sl.pu.y - pO.y - Kd.y) : (T)0,
+                                  in ? wr * (sl.pu.z - pO.z - Kd.z) : (T)0};
+                aO.x -= wr * jp.x; aO.y -= wr * jp.y; aO.z -= wr * jp.z;
+            }
+        };
+#if OPTAMD_ARAP_DPF
+        // software pipeline: batch k+1's neighbour data and batch k+2's slot ids are in
+        // flight while batch k computes
+        Slot cur[EB], nxt[EB];
+        int xn[EB];
+        if (nw > 0) {
+#pragma unroll
+            for (int b = 0; b < EB; ++b) gather(nel[64 * b], cur[b]);
+        }
+        if (EB < nw) {
+#pragma unroll
+            for (int b = 0; b < EB; ++b) xn[b] = nel[64 * (EB + b)];
+        }
+        for (int i0 = 0; i0 < nw; i0 += EB) {
+            if (i0 + EB < nw) {
+#pragma unroll
+                for (int b = 0; b < EB; ++b) gather(xn[b], nxt[b]);
+                if (i0 + 2 * EB < nw) {
+#pragma unroll
+                    for (int b = 0; b < EB; ++b) xn[b] = nel[64 * (i0 + 2 * EB + b)];
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < EB; ++b) use(cur[b]);
+#pragma unroll
+            for (int b = 0; b < EB; ++b) cur[b] = nxt[b];
+        }
+#else
+        // the next batch's slot ids are loaded while this batch gathers (one dependent load
         // latency per batch instead of two)
         int xn[EB];
 #pragma unroll
         for (int b = 0; b < EB; ++b) xn[b] = nw > 0 ? nel[64 * b] : -1;
-#endif
         for (int i0 = 0; i0 < nw; i0 += EB) {
-            int u[EB], kind[EB];
+            Slot sl[EB];
 #pragma unroll
-            for (int b = 0; b < EB; ++b) {
-#if OPTAMD_ARAP_IDPF
-                const int x = xn[b];
-#else
-                const int x = nel[64 * (i0 + b)];
-#endif
-                kind[b] = x < 0 ? 0 : (x >> 28);
-                u[b] = x < 0 ? v : (x & 0x0FFFFFFF);
-            }
-#if OPTAMD_ARAP_IDPF
+            for (int b = 0; b < EB; ++b) gather(xn[b], sl[b]);
             if (i0 + EB < nw) {
 #pragma unroll
                 for (int b = 0; b < EB; ++b) xn[b] = nel[64 * (i0 + EB + b)];
             }
-#endif
-            V3<T> pu[EB];
-            V3<float> Uu[EB];
-            T Ku[EB][9];
 #pragma unroll
-            for (int b = 0; b < EB; ++b) {
-                pu[b] = gld3<T>(p, u[b]);
-                Uu[b] = gld3<float>(a.U, u[b]);
-#pragma unroll
-                for (int q = 0; q < 9; ++q) Ku[b][q] = gldq(Kall, (unsigned)q * (unsigned)N, u[b]);
-            }
-#pragma unroll
-            for (int b = 0; b < EB; ++b) {
-                const bool out = kind[b] & 1, in = kind[b] & 2;
-                const V3<T> d = {(T)(Uv.x - Uu[b].x), (T)(Uv.y - Uu[b].y), (T)(Uv.z - Uu[b].z)};
-                {   // out-edge v -> u
-                    const V3<T> Kd = mv(K, d);
-                    const V3<T> jp = {out ? wr * (pO.x - pu[b].x - Kd.x) : (T)0, out ? wr * (pO.y - pu[b].y - Kd.y) : (T)0,
-                                      out ? wr * (pO.z - pu[b].z - Kd.z) : (T)0};
-                    const V3<T> dd = {out ? d.x : (T)0, out ? d.y : (T)0, out ? d.z : (T)0};
-                    aO.x += wr * jp.x; aO.y += wr * jp.y; aO.z += wr * jp.z;
-                    M[0] += jp.x * dd.x; M[1] += jp.x * dd.y; M[2] += jp.x * dd.z;
-                    M[3] += jp.y * dd.x; M[4] += jp.y * dd.y; M[5] += jp.y * dd.z;
-                    M[6] += jp.z * dd.x; M[7] += jp.z * dd.y; M[8] += jp.z * dd.z;
-                }
-                {   // in-edge u -> v
-                    const V3<T> di = {(T)(Uu[b].x - Uv.x), (T)(Uu[b].y - Uv.y), (T)(Uu[b].z - Uv.z)};
-                    const V3<T> Kd = mv(Ku[b], di);
-                    const V3<T> jp = {in ? wr * (pu[b].x - pO.x - Kd.x) : (T)0, in ? wr * (pu[b].y - pO.y - Kd.y) : (T)0,
-                                      in ? wr * (pu[b].z - pO.z - Kd.z) : (T)0};
-                    aO.x -= wr * jp.x; aO.y -= wr * jp.y; aO.z -= wr * jp.z;
-                }
-            }
+            for (int b = 0; b < EB; ++b) use(sl[b]);
         }
+#endif
         {
             T R[9], dR[3][9];
             rotation(Av, R, dR);
@@ -765,7 +784,10 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
     void apply_prepared(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
-        if (merged_on_ && eb_ == 3)
+        if (merged_on_ && eb_ == 1)
+            hipLaunchKernelGGL((arap::arap_apply_merged<T, 1>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap,
+                               (const T*)K_, dadd, stop, rs);
+        else if (merged_on_ && eb_ == 3)
             hipLaunchKernelGGL((arap::arap_apply_merged<T, 3>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap,
                                (const T*)K_, dadd, stop, rs);
         else if (merged_on_)
@@ -931,7 +953,7 @@ private:
     T* K_ = nullptr;   // per-vertex directional rotation derivative of the current p
     const bool merged_on_ = env_int("OPT_AMD_ARAP_MERGED", 1) != 0;   // 0: separate out / in lists
     // merged slots per batch of arap_apply_merged (the merged ELL widths are padded to it)
-    const int eb_ = env_int("OPT_AMD_ARAP_EB", arap::kEBM) == 3 ? 3 : 2;
+    const int eb_ = std::min(3, std::max(1, env_int("OPT_AMD_ARAP_EB", arap::kEBM)));
     T *userO_ = nullptr, *userA_ = nullptr, *dO_ = nullptr, *dA_ = nullptr;
     float *dU_ = nullptr, *dC_ = nullptr;
     int *dv0_ = nullptr, *dv1_ = nullptr;
