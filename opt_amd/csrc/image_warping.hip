@@ -192,10 +192,19 @@ typedef float acc_t;
 #else
 typedef double acc_t;
 #endif
-// w0 a0 b0 + w1 a1 b1 + w2 a2 b2 at the accumulation precision
+// w0 a0 b0 + w1 a1 b1 + w2 a2 b2 at the accumulation precision. Every caller passes
+// w1 == w0 (the Offset channels share one preconditioner value), so the fp64 form
+// factors it: w0 (a0 b0 + a1 b1) + w2 a2 b2 — five fp64 operations instead of eight (fp64
+// VALU issues at half the fp32 rate, and the fused passes form three of these per pixel)
+#ifndef OPTAMD_IW_WFACT
+#define OPTAMD_IW_WFACT 1
+#endif
 template <typename T>
 __device__ __forceinline__ acc_t wdot3(T w0, T a0, T b0, T w1, T a1, T b1, T w2, T a2, T b2) {
-#if OPTAMD_IW_ACC == 2
+#if OPTAMD_IW_ACC == 2 && OPTAMD_IW_WFACT
+    (void)w1;
+    return (double)w0 * ((double)a0 * (double)b0 + (double)a1 * (double)b1) + (double)w2 * ((double)a2 * (double)b2);
+#elif OPTAMD_IW_ACC == 2
     return (double)w0 * (double)a0 * (double)b0 + (double)w1 * (double)a1 * (double)b1 +
            (double)w2 * (double)a2 * (double)b2;
 #else
