@@ -347,12 +347,6 @@ __global__ __launch_bounds__(kBlock) void arap_apply(Args<T> a, const T* __restr
 // per SIMD) 50.6-50.9 us against 3 slots (110 VGPRs, 4 waves) 52.4-52.5 us for kdir +
 // apply at 1 M vertices (profiles/r03_arap_eb.txt); OPT_AMD_ARAP_EB=3 restores 3
 constexpr int kEBM = 2;
-#ifndef OPTAMD_ARAP_DPF
-#define OPTAMD_ARAP_DPF 0
-#endif
-#ifndef OPTAMD_ARAP_OWNK
-#define OPTAMD_ARAP_OWNK 0
-#endif
 template <typename T, int EB = kEBM>
 __global__ __launch_bounds__(kBlock) void arap_apply_merged(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
                                                             const T* __restrict__ Kall, const T* __restrict__ dadd,
@@ -367,16 +361,11 @@ __global__ __launch_bounds__(kBlock) void arap_apply_merged(Args<T> a, const T* 
         const V3<T> Av = ld3<T>(a.A, v);
         const V3<float> Uv = ld3<float>(a.U, v);
         T K[9];
-#if OPTAMD_ARAP_OWNK
-#pragma unroll
-        for (int q = 0; q < 9; ++q) K[q] = Kall[q * N + v];   // this vertex's K from the K pass
-#else
         {
             T R[9], dR[3][9];
             rotation(Av, R, dR);
             directional(dR, pA, K);
         }
-#endif
         T M[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         V3<T> aO = {0, 0, 0}, aA = {0, 0, 0};
         if (fit_valid(a, v)) aO = {wf * (wf * pO.x), wf * (wf * pO.y), wf * (wf * pO.z)};
@@ -415,34 +404,6 @@ __global__ __launch_bounds__(kBlock) void arap_apply_merged(Args<T> a, const T* 
                 aO.x -= wr * jp.x; aO.y -= wr * jp.y; aO.z -= wr * jp.z;
             }
         };
-#if OPTAMD_ARAP_DPF
-        // software pipeline: batch k+1's neighbour data and batch k+2's slot ids are in
-        // flight while batch k computes
-        Slot cur[EB], nxt[EB];
-        int xn[EB];
-        if (nw > 0) {
-#pragma unroll
-            for (int b = 0; b < EB; ++b) gather(nel[64 * b], cur[b]);
-        }
-        if (EB < nw) {
-#pragma unroll
-            for (int b = 0; b < EB; ++b) xn[b] = nel[64 * (EB + b)];
-        }
-        for (int i0 = 0; i0 < nw; i0 += EB) {
-            if (i0 + EB < nw) {
-#pragma unroll
-                for (int b = 0; b < EB; ++b) gather(xn[b], nxt[b]);
-                if (i0 + 2 * EB < nw) {
-#pragma unroll
-                    for (int b = 0; b < EB; ++b) xn[b] = nel[64 * (i0 + 2 * EB + b)];
-                }
-            }
-#pragma unroll
-            for (int b = 0; b < EB; ++b) use(cur[b]);
-#pragma unroll
-            for (int b = 0; b < EB; ++b) cur[b] = nxt[b];
-        }
-#else
         // the next batch's slot ids are loaded while this batch gathers (one dependent load
         // latency per batch instead of two)
         int xn[EB];
@@ -459,7 +420,6 @@ __global__ __launch_bounds__(kBlock) void arap_apply_merged(Args<T> a, const T* 
 #pragma unroll
             for (int b = 0; b < EB; ++b) use(sl[b]);
         }
-#endif
         {
             T R[9], dR[3][9];
             rotation(Av, R, dR);
@@ -784,10 +744,7 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
     void apply_prepared(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
-        if (merged_on_ && eb_ == 1)
-            hipLaunchKernelGGL((arap::arap_apply_merged<T, 1>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap,
-                               (const T*)K_, dadd, stop, rs);
-        else if (merged_on_ && eb_ == 3)
+        if (merged_on_ && eb_ == 3)
             hipLaunchKernelGGL((arap::arap_apply_merged<T, 3>), dim3(stencil_blocks()), dim3(kBlock), 0, s, a_, p, Ap,
                                (const T*)K_, dadd, stop, rs);
         else if (merged_on_)
@@ -953,7 +910,7 @@ private:
     T* K_ = nullptr;   // per-vertex directional rotation derivative of the current p
     const bool merged_on_ = env_int("OPT_AMD_ARAP_MERGED", 1) != 0;   // 0: separate out / in lists
     // merged slots per batch of arap_apply_merged (the merged ELL widths are padded to it)
-    const int eb_ = std::min(3, std::max(1, env_int("OPT_AMD_ARAP_EB", arap::kEBM)));
+    const int eb_ = env_int("OPT_AMD_ARAP_EB", arap::kEBM) == 3 ? 3 : 2;
     T *userO_ = nullptr, *userA_ = nullptr, *dO_ = nullptr, *dA_ = nullptr;
     float *dU_ = nullptr, *dC_ = nullptr;
     int *dv0_ = nullptr, *dv1_ = nullptr;

@@ -29,14 +29,6 @@
 #include <tuple>
 #include "reduce_dev_src.h"
 
-#ifndef OPTAMD_GEN_XCD_ALL
-#define OPTAMD_GEN_XCD_ALL 0
-#endif
-#if OPTAMD_GEN_XCD_ALL
-#define OPTAMD_GEN_BLK "opt_xcd_block()"
-#else
-#define OPTAMD_GEN_BLK "(long long)blockIdx.x"
-#endif
 #define OPTAMD_STR2(...) #__VA_ARGS__
 #define OPTAMD_STR(x) OPTAMD_STR2(x)
 
@@ -429,7 +421,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         const GComputed& c = m.computed[k];
         o << "extern \"C\" __global__ __launch_bounds__(256) void gen_precompute_" << k << "(GenArgs a) {\n"
              "    OPT_COORDS\n"
-             "    for (long long lin = a.own_lo + " OPTAMD_GEN_BLK " * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
+             "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
           << coords;
         Body b(m, o, nd, uslot);
         const int nch = (int)c.expr.size();
@@ -476,7 +468,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         if (!want.empty()) {
             o << "extern \"C\" __global__ __launch_bounds__(256) void gen_precompute_" << gs.n_precompute << "(GenArgs a) {\n"
                  "    OPT_COORDS\n"
-                 "    for (long long lin = a.own_lo + " OPTAMD_GEN_BLK " * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
+                 "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
               << coords;
             Body b(m, o, nd, uslot);
             const int uimg = unk.empty() ? 0 : unk[0];
@@ -533,7 +525,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
             gcache.width = width;
             o << "extern \"C\" __global__ __launch_bounds__(256) void gen_precompute_" << gs.n_precompute << "(GenArgs a) {\n"
                  "    OPT_COORDS\n"
-                 "    for (long long lin = a.own_lo + " OPTAMD_GEN_BLK " * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
+                 "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
               << coords;
             Body b(m, o, nd, uslot);
             std::vector<std::string> val(width, "(T)0");
@@ -560,7 +552,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
     {
         o << "extern \"C\" __global__ __launch_bounds__(256) void gen_jtf(GenArgs a, T* __restrict__ r, T* __restrict__ diag) {\n"
              "    OPT_COORDS\n"
-             "    for (long long lin = a.own_lo + " OPTAMD_GEN_BLK " * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
+             "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
           << coords;
         Body b(m, o, nd, uslot);
         const std::string act = m.exclude >= 0 ? "(" + b.v(m.exclude) + " == (T)0)" : "true";
@@ -701,7 +693,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
              "    if (stop && *stop) return;\n"
              "    OPT_COORDS\n"
              "    T dot = 0;\n";
-        o << "    for (long long lin = a.own_lo + " OPTAMD_GEN_BLK " * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
+        o << "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
               << coords;
         Body b(m, o, nd, uslot);
         centred_apply(b, false);
@@ -1188,7 +1180,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
                  "        long long row_base, long long nnz_base, long long nunk) {\n"
                  "    OPT_COORDS\n";
             if (g < 0) {
-                o << "    for (long long lin = a.own_lo + " OPTAMD_GEN_BLK " * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
+                o << "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
                   << coords << "        const long long el = lin;\n";
             } else {
                 o << "    for (long long el = (long long)blockIdx.x * 256 + threadIdx.x; el < a.nedge[" << g
@@ -1247,7 +1239,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
              "    OPT_COORDS\n"
              "    T acc = 0;\n";
         if (gs.has_centered) {
-            o << "    for (long long lin = a.own_lo + " OPTAMD_GEN_BLK " * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
+            o << "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
               << coords;
             Body b(m, o, nd, uslot);
             if (m.exclude >= 0) b.line("if (" + b.v(m.exclude) + " != (T)0) continue;");
