@@ -60,11 +60,11 @@ def apply_bytes_per_px(i: int, liter: int = 10) -> int:
 
 
 # HBM traffic of the in-loop apply from the committed rocprofv3 PMC summary of the same
-# kernels (tools/measure.sh: separate --pmc FETCH_SIZE / WRITE_SIZE passes over this
+# kernels (tools/measure_r04.sh: separate --pmc FETCH_SIZE / WRITE_SIZE passes over this
 # bench). FETCH_SIZE reads exactly 1/2 of the bytes on gfx950 for 1/4/8/16-B-per-lane
 # streaming reads and WRITE_SIZE is exact (profiles/r01_fetchcal.json, 1 GiB arrays), so
 # traffic = 2 FETCH_SIZE + WRITE_SIZE, averaged over the lIterations in-loop launches.
-PMC_FILE = os.path.join(ROOT, "profiles", "r03_final_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r04_final_pmc.json")
 APPLY_VARIANT = {0: "iw_apply<float, 1, 0,", 1: "iw_apply<float, 2, 1,", 2: "iw_apply<float, 2, 2,"}
 
 
@@ -130,18 +130,18 @@ def pmc_traffic(liter: int, first: int = 0, res: bool = False):
     return total / (liter - first)
 
 
-PMC_FILE_SFS = os.path.join(ROOT, "profiles", "r02_pmc_sfs.json")
+PMC_FILE_SFS = os.path.join(ROOT, "profiles", "r04_final_pmc_sfs.json")
 
 
 def pmc_traffic_sfs():
     """The same for the shape_from_shading leg: the in-loop J^T J p strip (sfs_strip<float,
-    false>) from the committed PMC summary of that workload (tools/measure_r02.sh)."""
+    false, false>) from the committed PMC summary of that workload (tools/measure_r04.sh)."""
     try:
         with open(PMC_FILE_SFS) as f:
             ks = json.load(f)["kernels"]
     except (OSError, ValueError, KeyError):
         return None
-    hit = [v for k, v in ks.items() if "sfs_strip<float, false>" in k]
+    hit = [v for k, v in ks.items() if "sfs_strip<float, false, false>" in k]
     if not hit or "FETCH_SIZE" not in hit[0] or "WRITE_SIZE" not in hit[0]:
         return None
     return (2.0 * hit[0]["FETCH_SIZE"] + hit[0]["WRITE_SIZE"]) * 1024.0

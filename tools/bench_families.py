@@ -51,7 +51,9 @@ def sfs():
     w = workloads.shape_from_shading(4096, 4096, seed=3)
     prm = [float(v) for v in w["params"]] + [cuda(w[k]) for k in ("X", "D_i", "Im", "edgeMaskR", "edgeMaskC")]
     return dict(name="shape_from_shading 4096x4096 fp32 LM", dims=[4096, 4096], energy=E("shape_from_shading"),
-                kind="LMGPU", double=False, prm=prm, units=4096 * 4096, unit="px", bytes_per_unit=34,
+                # the timed apply alone (time_apply) gets no LM diagonal: 30 B/px; the PCG loop's
+                # apply also reads CtC (34 B/px, bench.py --workload shape_from_shading)
+                kind="LMGPU", double=False, prm=prm, units=4096 * 4096, unit="px", bytes_per_unit=30,
                 dtype=torch.float32)
 
 
