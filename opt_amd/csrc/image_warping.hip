@@ -192,21 +192,36 @@ typedef float acc_t;
 #else
 typedef double acc_t;
 #endif
+// alpha = rz / pAp of the fused loop, 0 when pAp is not positive. The reference divides
+// unguarded (solverGPUGaussNewton.t:696), which far past convergence meets 0 / 0 or x / 0
+// once p and Ap underflow: NaN unknowns. The fused loop takes a zero step there instead
+// (bitwise the plain division whenever pAp > 0).
+template <typename T>
+__device__ __forceinline__ T pcg_alpha(double rz, double pap) {
+    return pap > 0.0 ? (T)(rz / pap) : (T)0;
+}
+// a0 b0 + a1 b1 + a2 b2 at the accumulation precision: p.Ap of the fused passes. Its
+// products must be formed as rz's are (wdot3): far past convergence (hundreds of PCG
+// iterations on a small problem) p and Ap reach ~1e-40, their fp32 products underflow to 0
+// while rz's fp64 products do not, and alpha = rz / pAp blew up (a 9x7 image at 400
+// iterations: energy 1.6e20; test_pcg_far_past_convergence_stays_finite)
+template <typename T>
+__device__ __forceinline__ acc_t dot3(T a0, T b0, T a1, T b1, T a2, T b2) {
+#if OPTAMD_IW_ACC == 2
+    return (double)a0 * (double)b0 + (double)a1 * (double)b1 + (double)a2 * (double)b2;
+#else
+    return (acc_t)(a0 * b0 + a1 * b1 + a2 * b2);
+#endif
+}
 // w0 a0 b0 + w1 a1 b1 + w2 a2 b2 at the accumulation precision. Every caller passes
 // w1 == w0 (the Offset channels share one preconditioner value), so the fp64 form
-// factors it: w0 (a0 b0 + a1 b1) + w2 a2 b2 — five fp64 operations instead of eight (fp64
-// VALU issues at half the fp32 rate, and the fused passes form three of these per pixel)
-#ifndef OPTAMD_IW_WFACT
-#define OPTAMD_IW_WFACT 1
-#endif
+// factors it: w0 (a0 b0 + a1 b1) + w2 a2 b2 — five fp64 operations instead of eight
+// (measured round 4: the same step time either way, `profiles/r04_arap_ab.json` "iw")
 template <typename T>
 __device__ __forceinline__ acc_t wdot3(T w0, T a0, T b0, T w1, T a1, T b1, T w2, T a2, T b2) {
-#if OPTAMD_IW_ACC == 2 && OPTAMD_IW_WFACT
+#if OPTAMD_IW_ACC == 2
     (void)w1;
     return (double)w0 * ((double)a0 * (double)b0 + (double)a1 * (double)b1) + (double)w2 * ((double)a2 * (double)b2);
-#elif OPTAMD_IW_ACC == 2
-    return (double)w0 * (double)a0 * (double)b0 + (double)w1 * (double)a1 * (double)b1 +
-           (double)w2 * (double)a2 * (double)b2;
 #else
     return (acc_t)(w0 * a0 * b0 + w1 * a1 * b1 + w2 * a2 * b2);
 #endif
@@ -436,7 +451,7 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
                     st_v<(NT & 2) != 0>(delta + 2 * N + i, on ? cur.dt : (T)0);
                 }
                 if (SUMS) {
-                    papd += (acc_t)(cur.px * aox + cur.py * aoy + cur.pt * aot);
+                    papd += dot3(cur.px, aox, cur.py, aoy, cur.pt, aot);
                     rapd += wdot3(cur.ww0, cur.rx, aox, cur.ww0, cur.ry, aoy, cur.ww2, cur.rt, aot);
                     apapd += wdot3(cur.ww0, aox, aox, cur.ww0, aoy, aoy, cur.ww2, aot, aot);
                 } else {
@@ -698,16 +713,16 @@ __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_apply_res(Args<T> a, 
     const double rzp = sc[prev], papp = sc[prev + 1];
     // the identity takes alpha as the pixels apply it (rounded to T): with the cancellation
     // in it (rz_i << rz_{i-1}) the fp64 alpha would be off by ~1e-7 x rz_{i-1} / rz_i
-    const T alpha = (T)(rzp / papp);
+    const T alpha = pcg_alpha<T>(rzp, papp);
     const double alpha_d = (double)alpha;
     const double rz_id = base_scale * rzp - 2.0 * alpha_d * sc[prev + 2] + alpha_d * alpha_d * sc[prev + 3];
     // The identity subtracts fp64 sums of size rz_{i-1}: its absolute error is ~1e-14 rz_{i-1},
     // i.e. ~1e-14 in beta whatever rz_i / rz_{i-1} is, negligible in p_i. It cancels to <= 0
     // only where the true beta is itself below that error: beta_i = 0 there (the direct
     // r_i.z_i of this pass is >= 0 by construction, so a negative beta is never right).
-    const T beta = rz_id > 0.0 ? (T)(rz_id / rzp) : (T)0;
+    const T beta = rz_id > 0.0 && rzp > 0.0 ? (T)(rz_id / rzp) : (T)0;
     // E: p_{i-2}'s delta term was deferred by the previous pass; alpha_{i-2} from its slots
-    const T alpha2 = E ? (T)(sc[prev - kSlots] / sc[prev - kSlots + 1]) : (T)0;
+    const T alpha2 = E ? pcg_alpha<T>(sc[prev - kSlots], sc[prev - kSlots + 1]) : (T)0;
     if (blockIdx.x == 0 && threadIdx.x == 0) sc[prev + kSlots + 4] = rz_id;
     const T wr = a.wr, wf2 = a.wf * a.wf;
     const unsigned tb = (unsigned)(2 * a.dom.npix_mem() * (long long)sizeof(T));
@@ -762,7 +777,7 @@ __global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_apply_res(Args<T> a, 
                 }
                 vec2_t<T> pv; pv.x = cur.px; pv.y = cur.py;
                 stb<SNT>(pout, off.xy, pv); stb<SNT>(pout, off.t, cur.pt);
-                papd += (acc_t)(cur.px * aox + cur.py * aoy + cur.pt * aot);
+                papd += dot3(cur.px, aox, cur.py, aoy, cur.pt, aot);
                 rapd += wdot3(cur.w0, cur.rx, aox, cur.w0, cur.ry, aoy, cur.w2, cur.rt, aot);
                 apapd += wdot3(cur.w0, aox, aox, cur.w0, aoy, aoy, cur.w2, aot, aot);
             }
@@ -1151,7 +1166,7 @@ __device__ __forceinline__ void iw_jtf_apply_body(const Args<T>& a, T* __restric
                     vec2_t<T> pv; pv.x = cpx; pv.y = cpy;
                     stb<(NT & 2) != 0>(pout, off.xy, pv); stb<(NT & 2) != 0>(pout, off.t, cpt);
                 }
-                papdot += (acc_t)(cpx * aox + cpy * aoy + cpt * aot);
+                papdot += dot3(cpx, aox, cpy, aoy, cpt, aot);
                 // PCGStep2's weights: pre, or 1 without a preconditioner
                 const T w0 = a.use_pre ? cur.wo : (T)1, w2 = a.use_pre ? cur.wt : (T)1;
                 rapd += wdot3(w0, cur.rx, aox, w0, cur.ry, aoy, w2, cur.rt, aot);
@@ -1168,23 +1183,12 @@ __device__ __forceinline__ void iw_jtf_apply_body(const Args<T>& a, T* __restric
     double v[4] = {(double)rzdot, (double)papdot, (double)rapd, (double)apapd};
     block_reduce_publish<4>(v, rs, g.tile);
 }
-// minimum waves per SIMD of the fp32 kernel (0: the compiler's choice; its 112 VGPRs give 4)
-#ifndef OPTAMD_IW_JA_WPE
-#define OPTAMD_IW_JA_WPE 0
-#endif
+// (the compiler's 112-114 VGPRs give 4 waves per SIMD; forcing 5 spills: 504 vs 373 us)
 template <typename T, int NT = 2>
 __global__ __launch_bounds__(kBlock) void iw_jtf_apply(Args<T> a, T* __restrict__ r, T* __restrict__ pre,
                                                        T* __restrict__ pout, T* __restrict__ Ap, ReduceSlot rs) {
     iw_jtf_apply_body<T, NT>(a, r, pre, pout, Ap, rs);
 }
-#if OPTAMD_IW_JA_WPE > 0
-template <>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(OPTAMD_IW_JA_WPE))) void
-iw_jtf_apply<float, 2>(Args<float> a, float* __restrict__ r, float* __restrict__ pre, float* __restrict__ pout,
-                       float* __restrict__ Ap, ReduceSlot rs) {
-    iw_jtf_apply_body<float, 2>(a, r, pre, pout, Ap, rs);
-}
-#endif
 
 // ----------------------------------------------------------------- cost kernel
 // sc[rs.out] = sum over active pixels of 1/2 (sum_s |e_reg(k,s)|^2 + |e_fit(k)|^2).
@@ -1384,8 +1388,8 @@ __global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O
                                                     const T* __restrict__ p2 = nullptr, int ia2_num = 0,
                                                     int ia2_den = 0) {
     const long long N = a.dom.npix_mem();
-    const T alpha = (T)(sc[ia_num] / sc[ia_den]);
-    const T alpha2 = E2 ? (T)(sc[ia2_num] / sc[ia2_den]) : (T)0;
+    const T alpha = pcg_alpha<T>(sc[ia_num], sc[ia_den]);
+    const T alpha2 = E2 ? pcg_alpha<T>(sc[ia2_num], sc[ia2_den]) : (T)0;
     const long long b = a.dom.off(0, a.dom.y_lo), e = a.dom.off(0, a.dom.y_hi);
     for (long long i = b + (long long)blockIdx.x * blockDim.x + threadIdx.x; i < e;
          i += (long long)gridDim.x * blockDim.x) {

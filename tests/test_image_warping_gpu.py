@@ -313,6 +313,42 @@ def test_fused_loop_at_the_examples_pcg_depth(monkeypatch, case, lit):
     assert np.all(e_f <= bar) and np.all(e_s <= bar), (e_f, e_s, floor)
 
 
+@pytest.mark.parametrize("W,H,lit", [(5, 4, 120), (9, 7, 400)])
+def test_pcg_far_past_convergence_stays_finite(monkeypatch, W, H, lit):
+    """lIterations far past convergence on tiny problems (60 and 189 unknowns, CG's
+    exact-arithmetic bound): once rz reaches the rounding floor, the identity
+    r_i.W r_i = rz_{i-1} - 2 alpha rAp + alpha^2 ApAp is a difference of fp64 sums of size
+    rz_{i-1}; should it cancel to <= 0, iw_apply_res takes beta_i = 0 (a restart) instead
+    of a negative or huge beta. The fused loop must stay finite and land where it lands
+    with just enough iterations to converge (the 2 GN steps are then the same Newton
+    steps up to fp32 rounding). The reference's own PCGStep2/3 divide without a guard
+    (alpha = rz / pAp, beta = rz_new / rz_old, solverGPUGaussNewton.t:696,842), and so does
+    our separate-pass loop (OPT_AMD_IW_FUSED_RES=0), which measured NaN energies on the
+    5x4 case (round 4): past convergence those divisions meet 0 / 0. The count of
+    non-positive identity values (kept raw in the scalar slot at +4) is printed."""
+    from opt_amd import workloads
+
+    w = workloads.image_warping(W, H, seed=7)
+    n = 3 * W * H
+
+    def run(lit_):
+        monkeypatch.setenv("OPT_AMD_IW_FUSED_RES", "1")
+        s = solver(W, H)
+        prm = device_params(w)
+        costs, sc = _step_scalars(s, prm, 2, lit_)
+        return costs, sc, [t.cpu().numpy() for t in prm[0:2]]   # Offset, Angle after the steps
+
+    cf, scf, xf = run(lit)
+    cn, _, xn = run(n)
+    restarts = sum(int(sc[2 + 5 * i + 4] <= 0.0) for sc in scf for i in range(1, lit))
+    print(f"{W}x{H} lIterations={lit}: {restarts} iterations with a non-positive identity value; "
+          f"energies {cf}, at lIterations={n}: {cn}")
+    assert np.all(np.isfinite(cf)) and all(np.all(np.isfinite(x)) for x in xf)
+    np.testing.assert_allclose(cf, cn, rtol=1e-4, atol=1e-6 * cn[0])
+    for a, b in zip(xf, xn):
+        np.testing.assert_allclose(a, b, rtol=1e-3, atol=1e-3)
+
+
 # ---- Step-time rebinding (Opt.h:64-65, solverGPUGaussNewton.t:2001,2028): every Step
 # evaluates PCGInit1 from the arrays as they are at that Step, so a caller may update
 # problem parameters IN PLACE (same pointers) between Steps. The oracle replays the
