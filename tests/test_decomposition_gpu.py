@@ -80,7 +80,7 @@ def test_decomposed_solve_matches_single_domain(monkeypatch, world, W, H):
         # trajectories differ in rounding only, and this energy amplifies rounding: a
         # 1-ulp input change moves one GN step's energy by 1e-3..4e-2 (DESIGN.md §5,
         # test_fp32_noise_floor_of_the_gn_trajectory). 256x200 at 4 ranks lands at
-        # 1.8e-4 of max|A| after 3 steps (tools/dbg_dec4.py: deterministic, independent of
+        # 1.8e-4 of max|A| after 3 steps (tools/history/dbg_dec4.py: deterministic, independent of
         # freed-memory contents), the energies at 5e-6; that case alone gets its measured
         # floor plus margin, the smaller worlds keep 1e-4.
         ra = to_np(prm[1])
