@@ -353,10 +353,14 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
          "__device__ __forceinline__ T opt_sh(T v, int d) { for (; d > 0; --d) v = opt_lr(v); for (; d < 0; ++d) v = opt_ll(v); return v; }\n";
     // masked read without a branch: the load always issues (at element 0 of the array when
     // the access is outside), the value is selected afterwards
-    // XCD-contiguous block order for the graph kernels: the hardware deals blocks to the 8
-    // XCDs round robin, so with blockIdx order a vertex's mesh neighbours (v +- 1, v +- a
-    // row) are gathered on several XCDs and cached in each one's L2; with this order each
-    // XCD walks one contiguous eighth of the vertices (of each grid-stride pass)
+    // XCD-contiguous block order for the graph kernels and the register strips: the
+    // hardware deals blocks to the 8 XCDs round robin, so with blockIdx order a vertex's
+    // mesh neighbours (v +- 1, v +- a row) are gathered on several XCDs and cached in each
+    // one's L2; with this order each XCD walks one contiguous eighth of the vertices (of
+    // each grid-stride pass), and neighbouring strips, which share their halo columns, run
+    // on the same XCD (generated image_warping / shape_from_shading GN / LM steps 6.91-6.92 ->
+    // 6.86 / 3.87-3.89 -> 3.84-3.85 ms, same box; the grid-stride centred kernels gained
+    // nothing, poisson's lost: they keep blockIdx order)
     o << "__device__ __forceinline__ long long opt_xcd_block() {\n"
          "    const int nb = gridDim.x, b = blockIdx.x, q = nb / 8, r = nb % 8, x = b % 8;\n"
          "    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;\n}\n";
@@ -912,7 +916,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         o << "    const int lane = threadIdx.x & 63, z = 0; (void)z;\n"
              "    const int nsx = (W + " << nout - 1 << ") / " << nout << ", G = gridDim.x * 4;\n"
              "    const int RB = max(8, (int)(((long long)H * nsx + G - 1) / G)), nby = (H + RB - 1) / RB;\n"
-             "    for (int wid = blockIdx.x * 4 + (threadIdx.x >> 6); wid < nsx * nby; wid += G) {\n"
+             "    for (int wid = (int)opt_xcd_block() * 4 + (threadIdx.x >> 6); wid < nsx * nby; wid += G) {\n"
              "        const int x = (wid % nsx) * " << nout << " + lane - " << loff << ";\n"
              "        const int y0 = (wid / nsx) * RB, y1 = min(H, y0 + RB);\n"
              "        const bool xin = x >= 0 && x < W, xout = xin && lane >= " << loff << " && lane < " << loff + nout << ";\n";
@@ -1093,7 +1097,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
              "    const int lane = threadIdx.x & 63, z = 0; (void)z;\n"
              "    const int nsx = (W + " << nout - 1 << ") / " << nout << ", G = gridDim.x * 4;\n"
              "    const int RB = max(8, (int)(((long long)H * nsx + G - 1) / G)), nby = (H + RB - 1) / RB;\n"
-             "    for (int wid = blockIdx.x * 4 + (threadIdx.x >> 6); wid < nsx * nby; wid += G) {\n"
+             "    for (int wid = (int)opt_xcd_block() * 4 + (threadIdx.x >> 6); wid < nsx * nby; wid += G) {\n"
              "        const int x = (wid % nsx) * " << nout << " + lane - " << loff << ";\n"
              "        const int y0 = (wid / nsx) * RB, y1 = min(H, y0 + RB);\n"
              "        const bool xin = x >= 0 && x < W, xout = xin && lane >= " << loff << " && lane < " << loff + nout << ";\n";
