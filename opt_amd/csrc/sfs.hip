@@ -534,7 +534,12 @@ __global__ __launch_bounds__(kBlock) void sfs_strip(Args<T> a, const T* __restri
     const int lane = threadIdx.x & (kWave - 1);
     // this launch's blocks: local b < bn0 -> bb0 + b, else bb1 + b - bn0 (whole slab: the
     // identity; the slab plans launch interior and boundary block ranges separately)
-    const int gb = (int)blockIdx.x < bn0 ? bb0 + (int)blockIdx.x : bb1 + (int)blockIdx.x - bn0;
+    // XCD-contiguous block order: neighbouring strips (which share halo columns) and row
+    // blocks run on the same XCD's L2; the reduction stays indexed by gb, so the sums are
+    // bitwise those of blockIdx order (round 4, same box: LM step 3.36-3.37 -> 3.29-3.30 ms,
+    // in-loop apply 131 -> 128 us; profiles/r04_sfs_xcd_ab.json)
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int gb = lb < bn0 ? bb0 + lb : bb1 + lb - bn0;
     const int wave = gb * (kBlock / kWave) + (threadIdx.x >> 6);
     const int strip = wave % nstrips, rb = wave / nstrips;
     const int gx = strip * kStripOut - 2 + lane;
