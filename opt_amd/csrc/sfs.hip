@@ -146,7 +146,7 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void sfs_precompute_strip(Args<T> a, int nstrips, int rows) {
     const Domain& d = a.dom;
     const int lane = threadIdx.x & (kWave - 1);
-    const int wave = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    const int wave = xcd_remap(blockIdx.x, gridDim.x) * (kBlock / kWave) + (threadIdx.x >> 6);   // XCD-contiguous
     const int strip = wave % nstrips, rb = wave / nstrips;
     const int x = strip * kPreOut - 1 + lane;
     const int y0 = d.y_lo + rb * rows, y1 = min(y0 + rows, d.y_hi);
@@ -751,7 +751,8 @@ __global__ __launch_bounds__(kBlock) void sfs_cost_strip(Args<T> a, const T* __r
                                                          int nstrips, int rows) {
     const Domain& d = a.dom;
     const int lane = threadIdx.x & (kWave - 1);
-    const int wave = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);   // XCD-contiguous, as sfs_strip
+    const int wave = lb * (kBlock / kWave) + (threadIdx.x >> 6);
     const int strip = wave % nstrips, rb = wave / nstrips;
     const int gx = strip * kCostOut - 1 + lane;
     const int y0 = d.y_lo + rb * rows, y1 = min(y0 + rows, d.y_hi);
@@ -844,7 +845,7 @@ __global__ __launch_bounds__(kBlock) void sfs_cost_strip(Args<T> a, const T* __r
         }
     }
     double v[1] = {(double)acc};
-    block_reduce_publish<1>(v, rs, blockIdx.x);
+    block_reduce_publish<1>(v, rs, lb);   // slot of the logical block: the sums of blockIdx order
 }
 
 }  // namespace sfs
