@@ -241,12 +241,14 @@ __global__ __launch_bounds__(kBlock) void step23_kernel(long long n, T* __restri
                                                         const int* stop, ReduceSlot rs, ZetaArgs z = {}) {
     if (stopped(stop)) return;
     const double rz = sc[i_rz];
-    const T alpha = (T)(rz / sc[i_rz + 2]);
+    // a zero step where p.Ap is not positive (far past convergence, once p and Ap
+    // underflow; the reference's unguarded division gives NaN there: iw_apply_res)
+    const T alpha = sc[i_rz + 2] > 0.0 ? (T)(rz / sc[i_rz + 2]) : (T)0;
     const double ad = (double)alpha;
     const double rz_id = sc[i_rz + 5] - 2.0 * ad * sc[i_rz + 3] + ad * ad * sc[i_rz + 4];
     // non-positive only where the true beta is below the identity's ~1e-14 absolute error
     // (iw_apply_res): beta = 0 there
-    const T beta = rz_id > 0.0 ? (T)(rz_id / rz) : (T)0;
+    const T beta = rz_id > 0.0 && rz > 0.0 ? (T)(rz_id / rz) : (T)0;
     if (blockIdx.x == 0 && threadIdx.x == 0) sc[id_out] = rz_id;
     double acc = 0;
     T accq = 0;
