@@ -181,17 +181,10 @@ __device__ __forceinline__ void eedge(T ojx, T ojy, T cj, T sj, float ujx, float
     ey = v ? wr * (ojy - oty - ry) : (T)0;
 }
 
-// Accumulation of the fused passes' sums: 0 fp32 products and lane sums, 1 fp32 products
-// summed in fp64, 2 fp64 products summed in fp64 (the identity's terms cancel: their
-// rounding is amplified by rz_{i-1} / rz_i).
-#ifndef OPTAMD_IW_ACC
-#define OPTAMD_IW_ACC 2
-#endif
-#if OPTAMD_IW_ACC == 0
-typedef float acc_t;
-#else
+// Accumulation of the fused passes' sums: fp64 products summed in fp64 (the identity's
+// terms cancel, so their rounding is amplified by rz_{i-1} / rz_i; round 2 measured fp32
+// products ~1e-7 of rz off, enough to matter there)
 typedef double acc_t;
-#endif
 // alpha = rz / pAp of the fused loop, 0 when pAp is not positive. The reference divides
 // unguarded (solverGPUGaussNewton.t:696), which far past convergence meets 0 / 0 or x / 0
 // once p and Ap underflow: NaN unknowns. The fused loop takes a zero step there instead
@@ -207,11 +200,7 @@ __device__ __forceinline__ T pcg_alpha(double rz, double pap) {
 // iterations: energy 1.6e20; test_pcg_far_past_convergence_stays_finite)
 template <typename T>
 __device__ __forceinline__ acc_t dot3(T a0, T b0, T a1, T b1, T a2, T b2) {
-#if OPTAMD_IW_ACC == 2
     return (double)a0 * (double)b0 + (double)a1 * (double)b1 + (double)a2 * (double)b2;
-#else
-    return (acc_t)(a0 * b0 + a1 * b1 + a2 * b2);
-#endif
 }
 // w0 a0 b0 + w1 a1 b1 + w2 a2 b2 at the accumulation precision. Every caller passes
 // w1 == w0 (the Offset channels share one preconditioner value), so the fp64 form
@@ -219,12 +208,8 @@ __device__ __forceinline__ acc_t dot3(T a0, T b0, T a1, T b1, T a2, T b2) {
 // (measured round 4: the same step time either way, `profiles/r04_arap_ab.json` "iw")
 template <typename T>
 __device__ __forceinline__ acc_t wdot3(T w0, T a0, T b0, T w1, T a1, T b1, T w2, T a2, T b2) {
-#if OPTAMD_IW_ACC == 2
     (void)w1;
     return (double)w0 * ((double)a0 * (double)b0 + (double)a1 * (double)b1) + (double)w2 * ((double)a2 * (double)b2);
-#else
-    return (acc_t)(w0 * a0 * b0 + w1 * a1 * b1 + w2 * a2 * b2);
-#endif
 }
 
 // ------------------------------------------------------------ row records
@@ -496,15 +481,6 @@ __global__ __launch_bounds__(kBlock) void iw_apply(Args<T> a, const T* __restric
 // in the last iteration (nothing reads r_L or Ap_L).
 // Scalar slots of iteration j (ImageWarpingPlan: kScBase + kSlots * j): rz, pAp, rAp, ApAp, rz by the identity
 constexpr int kSlots = 5;
-// minimum waves per SIMD the fused passes are compiled for (0: the compiler's choice)
-#ifndef OPTAMD_IW_WPE
-#define OPTAMD_IW_WPE 0
-#endif
-#if OPTAMD_IW_WPE > 0
-#define IW_FUSED_ATTR __attribute__((amdgpu_waves_per_eu(OPTAMD_IW_WPE)))
-#else
-#define IW_FUSED_ATTR
-#endif
 // 32-bit byte offsets from a uniform base: global_load / global_store with an SGPR base and
 // a VGPR offset, no 64-bit address arithmetic per access (the plan takes these kernels
 // only when 3 N sizeof(T) < 2^32). Vec2 = the two interleaved Offset channels of a pixel.
@@ -695,7 +671,7 @@ __device__ __forceinline__ RRow<T> finish_rrow(const Args<T>& a, const RRaw<T>& 
 // P0: see raw_rrow; pass 2 then reads r_0 through pin2 from the buffer it writes r_2 to
 // (rout), own pixel before own pixel: those two are not __restrict__
 template <typename T, int DM, int NT = 2, int E = 0, bool P0 = false>
-__global__ __launch_bounds__(kBlock) IW_FUSED_ATTR void iw_apply_res(Args<T> a, const T* __restrict__ pin,
+__global__ __launch_bounds__(kBlock) void iw_apply_res(Args<T> a, const T* __restrict__ pin,
                                                        const T* __restrict__ rin, const T* __restrict__ Apin,
                                                        const T* __restrict__ pre, T* __restrict__ pout,
                                                        T* rout, T* __restrict__ Apout,
