@@ -87,6 +87,7 @@ size_t elem_size(const gen::GImage& im, bool dbl) {
 // (at most 16 fields per vertex in the 32-bit form, codegen.cpp) and the per-edge
 // incidence copies. The same answer at the admission compile and in the plan.
 bool gather_offsets_fit_32(const gen::GModel& m, const ProblemSpec& s, bool dbl) {
+    if (env_int("OPT_AMD_GEN_OFF32", 1) == 0) return false;   // tests: force the 64-bit form
     const long long lim = 1LL << 31, t = dbl ? 8 : 4;
     long long npix = 1, chans = 0;
     for (int d : m.images[m.unknown_images()[0]].dims) npix *= (long long)s.dim_values.at(m.dims[d].index);
