@@ -27,8 +27,11 @@
 #include "solver.h"
 
 #define REAL float
+#define OACC double
 #include "arap_impl.h"
 #undef REAL
+#undef OACC
+#define OACC long double
 #define REAL double
 #include "arap_impl.h"
 #undef REAL

@@ -59,7 +59,7 @@ static void FN(edge_res)(const FN(arap_ctx)* c, int e, REAL r[3], REAL col[3][3]
 
 static double FN(arap_cost_fn)(void* v) {
     FN(arap_ctx)* c = (FN(arap_ctx)*)v;
-    double acc = 0.0;
+    OACC acc = 0.0;
     for (int i = 0; i < c->N; ++i) {
         if (!FN(fit_valid)(c, i)) continue;
         REAL s = (REAL)0.;
@@ -116,7 +116,7 @@ static double FN(arap_apply_fn)(void* v, const REAL* p, REAL* Ap) {
     const REAL* pO = p; const REAL* pA = p + 3 * N;
     REAL* aO = Ap; REAL* aA = Ap + 3 * N;
     memset(Ap, 0, sizeof(REAL) * 6 * N);
-    double dot = 0.0;
+    OACC dot = 0.0;
     for (int i = 0; i < N; ++i)   /* centred fit (PCGStep1) */
         if (FN(fit_valid)(c, i))
             for (int k = 0; k < 3; ++k) {
@@ -145,7 +145,7 @@ static double FN(arap_model_fn)(void* v, const REAL* d) {
     FN(arap_ctx)* c = (FN(arap_ctx)*)v;
     const int N = c->N;
     const REAL* dO = d; const REAL* dA = d + 3 * N;
-    double acc = 0.0;
+    OACC acc = 0.0;
     for (int i = 0; i < N; ++i) {
         if (!FN(fit_valid)(c, i)) continue;
         REAL s = (REAL)0.;

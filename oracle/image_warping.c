@@ -45,6 +45,7 @@ static const int SX[4] = {1, -1, 0, 0};
 static const int SY[4] = {0, 0, 1, -1};
 
 #define REAL float
+#define OACC double
 #define RCOS cosf
 #define RSIN sinf
 #define RSQRT sqrtf
@@ -55,6 +56,8 @@ static const int SY[4] = {0, 0, 1, -1};
 #undef RSIN
 #undef RSQRT
 #undef SOLVE_FN
+#undef OACC
+#define OACC long double
 #define REAL double
 #define RCOS cos
 #define RSIN sin

@@ -13,6 +13,14 @@
  * float (the generated code emits the Terra operation on the loaded values, o.t:2418-2470):
  * UrShape differences are float subtractions promoted afterwards; Constraints are
  * promoted where they meet an Offset.
+ *
+ * OACC, the accumulator of every sum (rz, p.Ap, cost), is double for REAL = float and
+ * long double for REAL = double (oracle/image_warping.c). The reference's reductions are
+ * atomics in no fixed order (backend_cuda.t:366-495), so its fp64 trajectory is defined
+ * only up to summation order; this trajectory (10 PCG iterations on the bench workload)
+ * amplifies one rounding of a PCG scalar ~1e9-fold, so a double accumulator made the
+ * "double oracle" itself move by up to 3.5e-7 between slab counts at 1024^2 (round 5,
+ * DESIGN.md §5). The 80-bit sums are the fp64 truth the GPU paths are held to.
  */
 #define CAT2(a, b) a##b
 #define CAT(a, b) CAT2(a, b)
@@ -68,7 +76,7 @@ typedef struct {
     int y0, y1;
     const REAL* p;
     REAL *out0, *out1;   /* Ap | (r, pre) */
-    double acc;
+    OACC acc;
     int use_pre;
 } FN(slab);
 
@@ -158,7 +166,7 @@ static void* FN(w_apply)(void* v) {
     FN(slab)* S = (FN(slab)*)v;
     const FN(iw_problem)* P = S->P;
     const int N = P->W * P->H;
-    double acc = 0.0;
+    OACC acc = 0.0;
     for (int y = S->y0; y < S->y1; ++y)
         for (int x = 0; x < P->W; ++x) {
             const int k = y * P->W + x;
@@ -180,7 +188,7 @@ static void* FN(w_jtf)(void* v) {
     FN(slab)* S = (FN(slab)*)v;
     const FN(iw_problem)* P = S->P;
     const int N = P->W * P->H;
-    double acc = 0.0;
+    OACC acc = 0.0;
     for (int y = S->y0; y < S->y1; ++y)
         for (int x = 0; x < P->W; ++x) {
             const int k = y * P->W + x;
@@ -203,7 +211,7 @@ static void* FN(w_jtf)(void* v) {
 static void* FN(w_cost)(void* v) {
     FN(slab)* S = (FN(slab)*)v;
     const FN(iw_problem)* P = S->P;
-    double acc = 0.0;
+    OACC acc = 0.0;
     for (int y = S->y0; y < S->y1; ++y)
         for (int x = 0; x < P->W; ++x)
             if (!FN(excluded)(P, x, y)) acc += FN(cost_px)(P, x, y);
@@ -211,7 +219,7 @@ static void* FN(w_cost)(void* v) {
     return NULL;
 }
 
-static double FN(run_slabs)(const FN(iw_problem) * P, int nthreads, void* (*fn)(void*), const REAL* p,
+static OACC FN(run_slabs)(const FN(iw_problem) * P, int nthreads, void* (*fn)(void*), const REAL* p,
                             REAL* o0, REAL* o1) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > P->H) nthreads = P->H;
@@ -228,7 +236,7 @@ static double FN(run_slabs)(const FN(iw_problem) * P, int nthreads, void* (*fn)(
         for (int t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, fn, &S[t]);
         for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
     }
-    double acc = 0.0;
+    OACC acc = 0.0;
     for (int t = 0; t < nthreads; ++t) acc += S[t].acc;   /* thread order (backend_cpu_mt.t:402-410) */
     free(S);
     free(th);
@@ -250,14 +258,14 @@ static void FN(iw_solve)(int W, int H, REAL* O, REAL* A, const float* U, const f
     costs[0] = FN(run_slabs)(&P, nthreads, FN(w_cost), NULL, NULL, NULL);
     for (int it = 0; it < nIter; ++it) {
         /* PCGInit1 */
-        double alpha_num = FN(run_slabs)(&P, nthreads, FN(w_jtf), NULL, r, pre);
+        OACC alpha_num = FN(run_slabs)(&P, nthreads, FN(w_jtf), NULL, r, pre);
         for (size_t e = 0; e < n3; ++e) { d[e] = (REAL)0; p[e] = pre[e] * r[e]; }
         for (int li = 0; li < lIter; ++li) {
             /* PCGStep1 */
-            double alpha_den = FN(run_slabs)(&P, nthreads, FN(w_apply), p, Ap, NULL);
+            OACC alpha_den = FN(run_slabs)(&P, nthreads, FN(w_apply), p, Ap, NULL);
             /* PCGStep2 (excluded elements hold r = pre = p = Ap = 0) */
             const REAL alpha = (REAL)(alpha_num / alpha_den);
-            double beta_num = 0.0;
+            OACC beta_num = 0.0;
             for (size_t e = 0; e < n3; ++e) {
                 d[e] = d[e] + alpha * p[e];
                 r[e] = r[e] - alpha * Ap[e];
@@ -321,7 +329,7 @@ static double FN(iwg_model)(void* v, const REAL* d) {
     FN(iw_ctx)* c = (FN(iw_ctx)*)v;
     const FN(iw_problem)* P = &c->P;
     const int N = P->W * P->H;
-    double acc = 0.0;
+    OACC acc = 0.0;
     for (int y = 0; y < P->H; ++y)
         for (int x = 0; x < P->W; ++x) {
             if (FN(excluded)(P, x, y)) continue;

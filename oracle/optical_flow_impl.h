@@ -59,7 +59,7 @@ static REAL FN(of_fit)(const FN(of_ctx) * c, const REAL* X, int x, int y, REAL* 
 
 static double FN(of_cost)(void* v) {
     FN(of_ctx)* c = (FN(of_ctx)*)v;
-    double acc = 0.0;
+    OACC acc = 0.0;
     for (int y = 0; y < c->H; ++y)
         for (int x = 0; x < c->W; ++x) {
             const long long k = (long long)y * c->W + x;
@@ -114,7 +114,7 @@ static void FN(of_jtf)(void* v, REAL* r, REAL* diag) {
 
 static double FN(of_apply)(void* v, const REAL* p, REAL* Ap) {
     FN(of_ctx)* c = (FN(of_ctx)*)v;
-    double dot = 0.0;
+    OACC dot = 0.0;
     for (int y = 0; y < c->H; ++y)
         for (int x = 0; x < c->W; ++x) {
             const long long k = (long long)y * c->W + x;
@@ -143,7 +143,7 @@ static double FN(of_apply)(void* v, const REAL* p, REAL* Ap) {
 
 static double FN(of_model)(void* v, const REAL* d) {
     FN(of_ctx)* c = (FN(of_ctx)*)v;
-    double acc = 0.0;
+    OACC acc = 0.0;
     for (int y = 0; y < c->H; ++y)
         for (int x = 0; x < c->W; ++x) {
             const long long k = (long long)y * c->W + x;

@@ -29,7 +29,7 @@ static REAL FN(pres)(const FN(pie_ctx)* c, const REAL* X, int x, int y, int s, i
 
 static double FN(pie_cost_fn)(void* v) {
     FN(pie_ctx)* c = (FN(pie_ctx)*)v;
-    double acc = 0.0;
+    OACC acc = 0.0;
     for (int y = 0; y < c->H; ++y)
         for (int x = 0; x < c->W; ++x) {
             if (!FN(pact)(c, y * c->W + x)) continue;
@@ -64,7 +64,7 @@ static void FN(pie_jtf_fn)(void* v, REAL* r, REAL* diag) {
 
 static double FN(pie_apply_fn)(void* v, const REAL* p, REAL* Ap) {
     FN(pie_ctx)* c = (FN(pie_ctx)*)v;
-    double dot = 0.0;
+    OACC dot = 0.0;
     for (int y = 0; y < c->H; ++y)
         for (int x = 0; x < c->W; ++x) {
             const int k = y * c->W + x;
@@ -94,7 +94,7 @@ static double FN(pie_apply_fn)(void* v, const REAL* p, REAL* Ap) {
 
 static double FN(pie_model_fn)(void* v, const REAL* d) {
     FN(pie_ctx)* c = (FN(pie_ctx)*)v;
-    double acc = 0.0;
+    OACC acc = 0.0;
     for (int y = 0; y < c->H; ++y)
         for (int x = 0; x < c->W; ++x) {
             const int k = y * c->W + x;

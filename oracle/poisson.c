@@ -24,8 +24,11 @@ static const int PX[4] = {1, -1, 0, 0};
 static const int PY[4] = {0, 0, 1, -1};
 
 #define REAL float
+#define OACC double
 #include "pie_impl.h"
 #undef REAL
+#undef OACC
+#define OACC long double
 #define REAL double
 #include "pie_impl.h"
 #undef REAL

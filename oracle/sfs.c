@@ -36,8 +36,11 @@
 
 
 #define REAL float
+#define OACC double
 #include "sfs_impl.h"
 #undef REAL
+#undef OACC
+#define OACC long double
 #define REAL double
 #include "sfs_impl.h"
 #undef REAL

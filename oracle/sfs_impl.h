@@ -160,7 +160,7 @@ static int FN(eval_res)(const FN(sfs_ctx)* c, int t, int x, int y, FN(res_t)* r)
 static int FN(excl)(const FN(sfs_ctx)* c, long long k) { return !(c->D[k] > (REAL)0.); }
 
 static double FN(cost_rows)(FN(sfs_ctx)* c, int y0, int y1) {
-    double acc = 0.0;
+    OACC acc = 0.0;
     for (int y = y0; y < y1; ++y)
         for (int x = 0; x < c->W; ++x) {
             if (FN(excl)(c, (long long)y * c->W + x)) continue;
@@ -176,7 +176,7 @@ static double FN(cost_rows)(FN(sfs_ctx)* c, int y0, int y1) {
 }
 
 static double FN(model_rows)(FN(sfs_ctx)* c, const REAL* dl, int y0, int y1) {
-    double acc = 0.0;
+    OACC acc = 0.0;
     for (int y = y0; y < y1; ++y)
         for (int x = 0; x < c->W; ++x) {
             if (FN(excl)(c, (long long)y * c->W + x)) continue;
@@ -243,7 +243,7 @@ static void FN(jtf_rows)(FN(sfs_ctx)* c, REAL* r, REAL* diag, int y0, int y1) {
         }
 }
 static double FN(apply_rows)(FN(sfs_ctx)* c, const REAL* p, REAL* Ap, int y0, int y1) {
-    double dot = 0.0;
+    OACC dot = 0.0;
     for (int y = y0; y < y1; ++y)
         for (int x = 0; x < c->W; ++x) {
             const long long k = (long long)y * c->W + x;
@@ -263,7 +263,7 @@ typedef struct {
     int op, y0, y1;
     const REAL* in;
     REAL *o0, *o1;
-    double acc;
+    OACC acc;
 } FN(sjob);
 static void* FN(sjob_run)(void* v) {
     FN(sjob)* j = (FN(sjob)*)v;
@@ -291,7 +291,7 @@ static double FN(spar)(FN(sfs_ctx)* c, int op, const REAL* in, REAL* o0, REAL* o
         for (int t = 0; t < nt; ++t) pthread_create(&th[t], NULL, FN(sjob_run), &J[t]);
         for (int t = 0; t < nt; ++t) pthread_join(th[t], NULL);
     }
-    double acc = 0.0;
+    OACC acc = 0.0;
     for (int t = 0; t < nt; ++t) acc += J[t].acc;
     free(J);
     free(th);

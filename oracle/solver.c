@@ -6,8 +6,11 @@
 #include "solver.h"
 
 #define REAL float
+#define OACC double
 #include "solver_impl.h"
 #undef REAL
+#undef OACC
+#define OACC long double
 #define REAL double
 #include "solver_impl.h"
 #undef REAL

@@ -10,7 +10,8 @@
  *   residual-reset halves :738-801, PCGStep3, alpha_num = beta_num, LM zeta exit
  *   :2211-2220}, LM model cost, savePreviousUnknowns, PCGLinearUpdate, cost, LM
  *   accept / reject with the trust-region update (:2247-2292).
- * Scalar sums are accumulated in double; opt_float arithmetic elsewhere.
+ * Scalar sums are accumulated in OACC (double for REAL = float, long double for REAL =
+ * double: the fp64 truth, see oracle/iw_impl.h); opt_float arithmetic elsewhere.
  */
 #ifndef REAL
 #error define REAL
@@ -37,7 +38,7 @@ static int CAT(oracle_solve_, REAL)(CAT(oracle_problem_, REAL)* P, int lm, const
     for (int it = 0; it < sp->nIterations; ++it) {
         /* PCGInit1 */
         P->jtf(P->ctx, r, diag);
-        double alpha_num = 0.0;
+        OACC alpha_num = 0.0;
         for (long long e = 0; e < n; ++e) {
             d[e] = 0;
             REAL w = P->act[e] ? CAT(ginv_, REAL)(P->use_pre ? diag[e] : (REAL)1) : (REAL)0;
@@ -67,7 +68,7 @@ static int CAT(oracle_solve_, REAL)(CAT(oracle_problem_, REAL)* P, int lm, const
         if (P->materialize) P->materialize(P->ctx);
         for (int li = 0; li < sp->lIterations; ++li) {
             /* PCGStep1 (+ CtC p for LM), or the materialized SpMV + PCGStep1_Finish */
-            double alpha_den = P->apply_mat ? P->apply_mat(P->ctx, p, Ap) : P->apply(P->ctx, p, Ap);
+            OACC alpha_den = P->apply_mat ? P->apply_mat(P->ctx, p, Ap) : P->apply(P->ctx, p, Ap);
             if (lm && !P->apply_mat) {
                 for (long long e = 0; e < n; ++e) {
                     Ap[e] += CtC[e] * p[e];
@@ -75,7 +76,7 @@ static int CAT(oracle_solve_, REAL)(CAT(oracle_problem_, REAL)* P, int lm, const
                 }
             }
             const REAL alpha = (REAL)(alpha_num / alpha_den);
-            double beta_num = 0.0, q = 0.0;
+            OACC beta_num = 0.0, q = 0.0;
             const int reset = lm && ((li + 1) % (sp->residual_reset_period > 0 ? sp->residual_reset_period : 1)) == 0;
             if (reset) {
                 for (long long e = 0; e < n; ++e) d[e] = d[e] + alpha * p[e];
