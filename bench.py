@@ -104,17 +104,49 @@ def res_variant(i: int, defer: bool = IW_DEFER, liter: int = 10) -> str:
     return f"iw_apply_res<float, {dm}, 2, {e}, {p0}>"
 
 
+# PCG iteration i >= 1 as iw_pcg (the default on one GPU, round 5): iw_apply_res with
+# Ap_{i-1} recomputed from p_{i-1} instead of read back, and Ap_i never stored: Angle 4 +
+# UrShape 8 + flag 1 + angle pre 4 + r_{i-1} 12 + p_{i-1} 12 read, p_i 12 written, r_i 12
+# written except in the last iteration; P0 and the deferred delta as iw_apply_res.
+PCG_KERNEL = "iw_pcg"
+
+
+def pcg_bytes_per_px(i: int, liter: int = 10, defer: bool = IW_DEFER) -> int:
+    b = 4 + 8 + 1 + 4 + 12 + 12 + 12
+    if i == 1 and liter >= 3:
+        b -= 12   # P0: p_0 = pre r_0 from the r_0 the pass reads
+    if i < liter - 1:
+        b += 12
+    if defer:
+        b += 0 if i % 2 == 1 else (24 if i == 2 else 36)
+    else:
+        b += 12 if i == 1 else 24
+    return b
+
+
+def pcg_variant(i: int, defer: bool = IW_DEFER, liter: int = 10) -> str:
+    """The iw_pcg instantiation PCG iteration i >= 1 runs (<T, DM, E, P0, SNT>)."""
+    if defer:
+        dm, e = (0, 0) if i % 2 == 1 else ((1, 1) if i == 2 else (2, 1))
+    else:
+        dm, e = (1 if i == 1 else 2), 0
+    p0 = "true" if liter >= 3 and (i == 1 or (defer and i == 2)) else "false"
+    return f"iw_pcg<float, {dm}, {e}, {p0}, false>"
+
+
 # PCGInit1 fused with the first apply (iw_jtf_apply, one strip pass): Offset 8 + Angle 4 +
 # UrShape 8 + Constraints 8 + Mask 4 read; r 12 + angle pre 4 + flag 1 + Ap 12 written, and
 # p 12 only when lIterations <= 2 (from 3 on, passes 1 and 2 form p_0 = pre r_0 themselves).
 INIT_KERNEL = "iw_jtf_apply"
 
 
-def init_bytes_per_px(liter: int = 10) -> int:
-    return 8 + 4 + 8 + 8 + 4 + 12 + 4 + 1 + 12 + (12 if liter <= 2 else 0)
+def init_bytes_per_px(liter: int = 10, ap: bool = True) -> int:
+    """ap: Ap_0 stored (iw_apply_res reads it back); iw_pcg recomputes it, so with the
+    iw_pcg loop iw_jtf_apply stores no Ap."""
+    return 8 + 4 + 8 + 8 + 4 + 12 + 4 + 1 + (12 if ap else 0) + (12 if liter <= 2 else 0)
 
 
-def pmc_traffic(liter: int, first: int = 0, res: bool = False):
+def pmc_traffic(liter: int, first: int = 0, res=False):
     try:
         with open(PMC_FILE) as f:
             ks = json.load(f)["kernels"]
@@ -122,7 +154,8 @@ def pmc_traffic(liter: int, first: int = 0, res: bool = False):
         return None
     total = 0.0
     for i in range(first, liter):
-        key = res_variant(i, liter=liter) if res else APPLY_VARIANT[min(i, 2)]
+        key = (pcg_variant(i, liter=liter) if res == "pcg" else res_variant(i, liter=liter) if res
+               else APPLY_VARIANT[min(i, 2)])
         hit = [v for k, v in ks.items() if key in k]
         if not hit or "FETCH_SIZE" not in hit[0] or "WRITE_SIZE" not in hit[0]:
             return None
@@ -417,7 +450,10 @@ def main():
     res = False
     if not sfs:
         n_res, res_ms = s.kernel_stat(RES_KERNEL)
-        if n_res:   # the loop ran as iw_apply_res passes: that is the dominant kernel
+        n_pcg, pcg_ms = s.kernel_stat(PCG_KERNEL)
+        if n_pcg:   # the loop ran as iw_pcg passes (one GPU): the dominant kernel
+            kname, n_apply, apply_ms, res = PCG_KERNEL, n_pcg, pcg_ms, "pcg"
+        elif n_res:   # as iw_apply_res passes (row slabs, OPT_AMD_IW_APFREE=0)
             kname, n_apply, apply_ms, res = RES_KERNEL, n_res, res_ms, True
     s.set_kernel_timing(0)
     # the in-loop applies of one step: PCG iterations first..liter-1 (first = 1 when the
@@ -429,7 +465,7 @@ def main():
     if sfs:   # sfs_strip: SURVEY.md §8d's per-pixel apply bytes
         bpp = SFS_APPLY_BYTES_PER_PX
     else:
-        per = res_bytes_per_px if res else apply_bytes_per_px
+        per = pcg_bytes_per_px if res == "pcg" else res_bytes_per_px if res else apply_bytes_per_px
         bpp = sum(per(i, args.liter) for i in range(first, args.liter)) / (args.liter - first)
     achieved = bpp * npx / avg_apply_s / 1e9
     # the pure apply (reads p) timed separately for the kernel-only unknowns/s
@@ -482,7 +518,7 @@ def main():
     }
     if n_init:
         init_s = (init_ms / 1e3) / n_init
-        ibpp = init_bytes_per_px(args.liter)
+        ibpp = init_bytes_per_px(args.liter, ap=res != "pcg")
         ach = ibpp * npx / init_s / 1e9
         result["init_kernel"] = {"kernel": INIT_KERNEL, "avg_us": init_s * 1e6, "launches": n_init,
                                  "bytes_per_px": ibpp, "achieved": ach, "frac": ach / PEAK_HBM_GBS}

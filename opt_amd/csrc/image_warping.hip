@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -73,6 +74,9 @@ struct Args {
     // tb1 + t - tn0 (whole domain: 0, nstrips * nrowblocks, 0; the slab plans launch the
     // interior row blocks and the two boundary row blocks separately to overlap the halo)
     int tb0, tn0, tb1;
+    // side != 0 (geom): the block's four waves walk the SAME rows over four adjacent strips
+    // (tile = row chunk x group of 4 strips) instead of four stacked row ranges of one strip
+    int side;
     // Jacobi preconditioner of the two Offset channels: diag(J^T J) there is
     // 2 wr^2 (#valid edges) + wf^2 [fit], so pre = 1/(1+sqrt(diag))^2 takes one of ten
     // values (host-computed once per step; 0.25 everywhere for UsePreconditioner(false)).
@@ -125,6 +129,17 @@ __device__ __forceinline__ void sc_of(double t, double* c, double* s) { sincos(t
 __device__ __forceinline__ float fmad(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 __device__ __forceinline__ double fmad(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
+// A rounded value the compiler may not see through: p_0 = pre r_0 is a product that the
+// reference stores (PCGInit1) and reads back (PCGStep1); used in place, the compiler would
+// contract it into the apply's subtractions (fma(pre, r, -p_t)) and the apply would act on
+// an unrounded p_0. Every kernel that forms p_0 from r_0 passes it through opaque(), so
+// iw_jtf_apply's Ap_0 and iw_pcg's recomputed Ap_0 act on the same rounded p_0.
+template <typename T>
+__device__ __forceinline__ T opaque(T v) {
+    asm("" : "+v"(v));
+    return v;
+}
+
 struct WaveGeom {
     int x, ex, lane, y0, y1, tile;
     bool out_lane, edge_lane;
@@ -135,14 +150,22 @@ __device__ __forceinline__ WaveGeom geom(const Args<T>& a) {
     const int lt = xcd_remap(blockIdx.x, gridDim.x);
     const int t = lt < a.tn0 ? a.tb0 + lt : a.tb1 + (lt - a.tn0);
     g.tile = t;
-    const int strip = t % a.nstrips, rb = t / a.nstrips;
     g.lane = threadIdx.x & (kWave - 1);
     const int w = threadIdx.x / kWave;
+    int strip, ychunk;
+    if (a.side) {
+        const int ng = (a.nstrips + kBlock / kWave - 1) / (kBlock / kWave);
+        strip = (t % ng) * (kBlock / kWave) + w;
+        ychunk = t / ng;
+    } else {
+        strip = t % a.nstrips;
+        ychunk = (t / a.nstrips) * (kBlock / kWave) + w;
+    }
     g.x = strip * kStrip + g.lane;
     // lane 0 fetches the column left of the strip, lane 63 the column right of it
     g.edge_lane = (g.lane == 0) || (g.lane == kWave - 1);
     g.ex = g.lane == 0 ? g.x - 1 : g.x + 1;
-    g.y0 = a.dom.y_lo + (rb * (kBlock / kWave) + w) * a.rows;
+    g.y0 = a.dom.y_lo + ychunk * a.rows;
     g.y1 = min(g.y0 + a.rows, a.dom.y_hi);
     g.out_lane = g.x < a.dom.W;
     return g;
@@ -614,8 +637,8 @@ __device__ __forceinline__ RRow<T> finish_rrow(const Args<T>& a, const RRaw<T>& 
     const int f = q.in ? q.f : 0;
     if constexpr (P0) {   // p_0 = pre r_0 (PCGInit1's p, iw_jtf_apply's cpx / cpy / cpt: the same T products)
         const T w0 = pre_offset(a, f);
-        if (E == 0) { q.q.x = w0 * q.r.x; q.q.y = w0 * q.r.y; q.qt = q.w2 * q.rt; }
-        else { q.q2.x = w0 * q.q2.x; q.q2.y = w0 * q.q2.y; q.q2t = q.w2 * q.q2t; }   // pin2 held r_0
+        if (E == 0) { q.q.x = opaque(w0 * q.r.x); q.q.y = opaque(w0 * q.r.y); q.qt = opaque(q.w2 * q.rt); }
+        else { q.q2.x = opaque(w0 * q.q2.x); q.q2.y = opaque(w0 * q.q2.y); q.q2t = opaque(q.w2 * q.q2t); }   // pin2 held r_0
     }
     o.act = f & 1;
     o.fit = (f >> 1) & 1;
@@ -654,7 +677,7 @@ __device__ __forceinline__ RRow<T> finish_rrow(const Args<T>& a, const RRaw<T>& 
     const int ef = q.ein ? q.ef : 0;
     if constexpr (P0 && E == 0) {
         const T we = pre_offset(a, ef);
-        q.eq.x = we * q.er.x; q.eq.y = we * q.er.y; q.eqt = q.ew2 * q.ert;
+        q.eq.x = opaque(we * q.er.x); q.eq.y = opaque(we * q.er.y); q.eqt = opaque(q.ew2 * q.ert);
     }
     o.eact = ef & 1;
     o.eux = q.ein ? q.eu.x : 0.f;
@@ -772,6 +795,233 @@ __global__ __launch_bounds__(kBlock) void iw_apply_res(Args<T> a, const T* __res
             const RRaw<T> n2 = raw(min(y + 3, g.y1));
             apply_row(B, A, y + 1);
             B = fin(n2, y + 3);
+        }
+    }
+    double v[4] = {(double)rzd, (double)papd, (double)rapd, (double)apapd};
+    block_reduce_publish<4>(v, rs, g.tile);
+}
+
+// ------------------------------------------- PCG iteration without a stored Ap
+// iw_pcg: iw_apply_res's iteration i >= 1 (PCGStep2 + PCGStep3 of iteration i-1, PCGStep1
+// of iteration i; :665-731, :814-845, :607-632) with Ap_{i-1} RECOMPUTED from p_{i-1}
+// instead of read back: the pass reads r_{i-1} and p_{i-1} (+ the per-pixel angle, UrShape,
+// flags and angle pre) and writes r_i and p_i; Ap is never stored (-24 B/px per pass:
+// the Ap_{i-1} read and the Ap_i write). Ap_{i-1} is the same expression over the same
+// stored p_{i-1} as the previous pass's Ap (apply_ap below is the one body both use), so
+// r_i, p_i, Ap_i and the four sums are bitwise iw_apply_res's.
+// Geometry: iw_jtf_apply's 60-column strips (x = 60 strip - 2 + lane, no edge record): per
+// row, stage A recomputes Ap_{i-1} at every lane from the p_{i-1} window (valid at lanes
+// 1..62), forms r_i and p_i there; stage B applies J^T J to p_i one row behind (lanes
+// 2..61 are the outputs). Stage A runs one row ahead of stage B; a wave reads the unknown
+// rows y0-2 .. y1+1 (p_{i-1} at radius 2).
+template <typename T>
+struct GRow {          // a finished row of p_{i-1} with the pixel's static data
+    T px, py, pt;      // p_{i-1} (0 on inactive pixels)
+    T c, s;            // cos / sin of the angle
+    float ux, uy;
+    int f;             // flag byte
+    vec2_t<T> r;       // r_{i-1}
+    T rt, w2;          // its angle channel, the angle pre
+    vec2_t<T> d, q2;   // own rows: delta, p_{i-2} (E)
+    T dt, q2t;
+    __device__ __forceinline__ bool act() const { return f & 1; }
+    __device__ __forceinline__ bool fit() const { return (f >> 1) & 1; }
+};
+template <typename T>
+struct GRaw {
+    vec2_t<T> p, r, d, q2;
+    T pt, rt, w2, ang, dt, q2t;
+    float2 u;
+    int f, in;
+};
+template <typename T, int DM, int E, bool P0>
+__device__ __forceinline__ GRaw<T> raw_grow(const Args<T>& a, const WaveGeom& g, int y, unsigned tb, const T* pin,
+                                            const T* rin, const T* pre, const T* delta, const T* pin2, bool own) {
+    GRaw<T> q;
+    q.in = present(a.dom, g.x, y);
+    const unsigned i = q.in ? (unsigned)a.dom.off(g.x, y) : 0u;
+    const POff<T> o(i, tb);
+    q.f = ldb<false, uint8_t>(a.flags, i);
+    q.u = ldb<false, float2>(a.U, 8u * i);
+    q.ang = ldb<false, T>(a.A, o.s);
+    q.r = ldb<false, vec2_t<T>>(rin, o.xy); q.rt = ldb<false, T>(rin, o.t);
+    q.w2 = ldb<false, T>(pre, o.s);
+    if (!(P0 && !E)) { q.p = ldb<false, vec2_t<T>>(pin, o.xy); q.pt = ldb<false, T>(pin, o.t); }
+    own = own && g.out_lane;
+    if (DM == 2 && own) { q.d = ldb<false, vec2_t<T>>(delta, o.xy); q.dt = ldb<false, T>(delta, o.t); }
+    if (E && own) { q.q2 = ldb<false, vec2_t<T>>(pin2, o.xy); q.q2t = ldb<false, T>(pin2, o.t); }
+    return q;
+}
+template <typename T, int E, bool P0>
+__device__ __forceinline__ GRow<T> finish_grow(const Args<T>& a, const GRaw<T>& q) {
+    GRow<T> o;
+    o.f = q.in ? q.f : 0;
+    o.ux = q.in ? q.u.x : 0.f;
+    o.uy = q.in ? q.u.y : 0.f;
+    sc_of(q.in ? q.ang : (T)0, &o.c, &o.s);
+    o.r = q.r; o.rt = q.rt; o.w2 = q.w2;
+    o.d = q.d; o.dt = q.dt;
+    o.q2 = q.q2; o.q2t = q.q2t;
+    if constexpr (P0) {   // p_0 = pre r_0 (iw_jtf_apply's FRow::px: the same T products)
+        const T w0 = pre_offset(a, o.f);
+        if (E == 0) { o.px = opaque(w0 * q.r.x); o.py = opaque(w0 * q.r.y); o.pt = opaque(q.w2 * q.rt); }
+        else {
+            o.q2.x = opaque(w0 * q.q2.x); o.q2.y = opaque(w0 * q.q2.y); o.q2t = opaque(q.w2 * q.q2t);
+            o.px = q.p.x; o.py = q.p.y; o.pt = q.pt;
+        }
+    } else {
+        o.px = q.p.x; o.py = q.p.y; o.pt = q.pt;
+    }
+    if (!o.act()) { o.px = 0; o.py = 0; o.pt = 0; }
+    return o;
+}
+// Carries of the apply's row recursion: J(up->cur), J(cur->up) and its angle term
+template <typename T>
+struct ACarry { T in_up_x, in_up_y, my_x, my_y, thm; };
+template <typename T>
+__device__ __forceinline__ ACarry<T> acarry_init(T upx, T upy, T upt, T uc, T us, float uux, float uuy, bool uact,
+                                                 T cpx, T cpy, T cpt, T cc, T cs, float cux, float cuy, bool cact, T wr) {
+    ACarry<T> k;
+    T ax, ay;
+    (void)cpt;
+    jedge(upx, upy, upt, uc, us, uux, uuy, cpx, cpy, cux, cuy, uact && cact, wr, k.in_up_x, k.in_up_y, ax, ay);
+    jedge(cpx, cpy, cpt, cc, cs, cux, cuy, upx, upy, uux, uuy, uact && cact, wr, k.my_x, k.my_y, ax, ay);
+    k.thm = -wr * (ax * k.my_x + ay * k.my_y);
+    return k;
+}
+// Ap = J^T J p of row cur from (cur, dn) and the carry; no edge operand (lanes 0 / 63 are
+// never used). The same expression as iw_apply_res's apply_row, term for term.
+template <typename T>
+__device__ __forceinline__ void apply_ap(T cpx, T cpy, T cpt, T cc, T cs, float cux, float cuy, bool cact, bool cfit,
+                                         T dpx, T dpy, T dpt, T dc, T ds, float dux, float duy, bool dact, T wr, T wf2,
+                                         ACarry<T>& k, T& aox, T& aoy, T& aot) {
+    const T lpx = from_left(cpx, (T)0), lpy = from_left(cpy, (T)0);
+    const T rpx = from_right(cpx, (T)0), rpy = from_right(cpy, (T)0);
+    const float lux = from_left(cux, 0.f), luy = from_left(cuy, 0.f);
+    const float rux = from_right(cux, 0.f), ruy = from_right(cuy, 0.f);
+    const int lact = from_left_i((int)cact, 0), ract = from_right_i((int)cact, 0);
+    T jpx_x, jpx_y, apx_x, apx_y, jmx_x, jmx_y, amx_x, amx_y;
+    T jpy_x, jpy_y, apy_x, apy_y, jdn_x, jdn_y, adn_x, adn_y;
+    jedge(cpx, cpy, cpt, cc, cs, cux, cuy, rpx, rpy, rux, ruy, cact && ract, wr, jpx_x, jpx_y, apx_x, apx_y);
+    jedge(cpx, cpy, cpt, cc, cs, cux, cuy, lpx, lpy, lux, luy, cact && lact, wr, jmx_x, jmx_y, amx_x, amx_y);
+    jedge(cpx, cpy, cpt, cc, cs, cux, cuy, dpx, dpy, dux, duy, cact && dact, wr, jpy_x, jpy_y, apy_x, apy_y);
+    jedge(dpx, dpy, dpt, dc, ds, dux, duy, cpx, cpy, cux, cuy, cact && dact, wr, jdn_x, jdn_y, adn_x, adn_y);
+    const T inpx_x = from_right(jmx_x, (T)0), inpx_y = from_right(jmx_y, (T)0);
+    const T inmx_x = from_left(jpx_x, (T)0), inmx_y = from_left(jpx_y, (T)0);
+    aox = wr * ((jpx_x + jmx_x + jpy_x + k.my_x) - (inpx_x + inmx_x + jdn_x + k.in_up_x));
+    aoy = wr * ((jpx_y + jmx_y + jpy_y + k.my_y) - (inpx_y + inmx_y + jdn_y + k.in_up_y));
+    if (cfit) { aox += wf2 * cpx; aoy += wf2 * cpy; }
+    aot = k.thm - wr * ((apx_x * jpx_x + apx_y * jpx_y) + (amx_x * jmx_x + amx_y * jmx_y) +
+                        (apy_x * jpy_x + apy_y * jpy_y));
+    if (!cact) { aox = 0; aoy = 0; aot = 0; }
+    k.in_up_x = jpy_x; k.in_up_y = jpy_y;
+    k.my_x = jdn_x; k.my_y = jdn_y;
+    k.thm = -wr * (adn_x * jdn_x + adn_y * jdn_y);
+}
+// Stage B's view of a row: p_i, r_i, the weights and the static data
+template <typename T>
+struct HRow {
+    T px, py, pt, c, s;
+    float ux, uy;
+    bool act, fit;
+    T rx, ry, rt, w0, w2;
+};
+// SNT: streaming stores. The 60-column strips store 240-byte row segments that straddle
+// cache lines shared with the neighbouring strips; plain stores let the L2 merge them.
+template <typename T, int DM, int E = 0, bool P0 = false, bool SNT = false>
+__global__ __launch_bounds__(kBlock) void iw_pcg(Args<T> a, const T* __restrict__ pin, const T* __restrict__ rin,
+                                                 const T* __restrict__ pre, T* __restrict__ pout, T* rout,
+                                                 T* __restrict__ delta, double* __restrict__ sc, int prev,
+                                                 double base_scale, ReduceSlot rs, const T* pin2 = nullptr) {
+    IW_PRE_TABLE(a);
+    const WaveGeom g = geom_fused(a);
+    // the scalars exactly as iw_apply_res forms them
+    const double rzp = sc[prev], papp = sc[prev + 1];
+    const T alpha = pcg_alpha<T>(rzp, papp);
+    const double alpha_d = (double)alpha;
+    const double rz_id = base_scale * rzp - 2.0 * alpha_d * sc[prev + 2] + alpha_d * alpha_d * sc[prev + 3];
+    const T beta = rz_id > 0.0 && rzp > 0.0 ? (T)(rz_id / rzp) : (T)0;
+    const T alpha2 = E ? pcg_alpha<T>(sc[prev - kSlots], sc[prev - kSlots + 1]) : (T)0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) sc[prev + kSlots + 4] = rz_id;
+    const T wr = a.wr, wf2 = a.wf * a.wf;
+    const unsigned tb = (unsigned)(2 * a.dom.npix_mem() * (long long)sizeof(T));
+    acc_t rzd = 0, papd = 0, rapd = 0, apapd = 0;
+    if (g.y0 < g.y1) {
+        auto raw = [&](int y) {
+            return raw_grow<T, DM, E, P0>(a, g, y, tb, pin, rin, pre, delta, pin2, y >= g.y0 && y < g.y1);
+        };
+        auto fin = [&](const GRaw<T>& q) { return finish_grow<T, E, P0>(a, q); };
+        // stage A at row y (cur = row y, dn = row y+1, carry from row y-1): Ap_{i-1}, then
+        // r_i and p_i (stores r_i and delta on an owned row)
+        ACarry<T> ka;
+        auto stage_a = [&](const GRow<T>& cur, const GRow<T>& dn, int y) {
+            T ax, ay, at;
+            apply_ap(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, cur.act(), cur.fit(), dn.px, dn.py, dn.pt,
+                     dn.c, dn.s, dn.ux, dn.uy, dn.act(), wr, wf2, ka, ax, ay, at);
+            HRow<T> h;
+            h.c = cur.c; h.s = cur.s; h.ux = cur.ux; h.uy = cur.uy; h.act = cur.act(); h.fit = cur.fit();
+            // make_rp: r_i = r_{i-1} - alpha Ap_{i-1}, z_i = pre r_i, p_i = z_i + beta p_{i-1}
+            make_rp(a, cur.f, alpha, beta, cur.r.x, cur.r.y, cur.rt, ax, ay, at, cur.w2, cur.px, cur.py, cur.pt, h.rx,
+                    h.ry, h.rt, h.px, h.py, h.pt);
+            h.w0 = a.use_pre ? pre_offset(a, cur.f) : (T)1;
+            h.w2 = a.use_pre ? cur.w2 : (T)1;
+            if (y >= g.y0 && y < g.y1 && g.out_lane) {
+                const POff<T> off((unsigned)a.dom.off(g.x, y), tb);
+                if (DM != 0) {   // iw_apply_res's deferred delta terms, term by term
+                    vec2_t<T> d;
+                    T dt;
+                    if (E) {
+                        if (DM == 1) { d.x = alpha2 * cur.q2.x; d.y = alpha2 * cur.q2.y; dt = alpha2 * cur.q2t; }
+                        else { d.x = fmad(alpha2, cur.q2.x, cur.d.x); d.y = fmad(alpha2, cur.q2.y, cur.d.y); dt = fmad(alpha2, cur.q2t, cur.dt); }
+                        d.x = fmad(alpha, cur.px, d.x); d.y = fmad(alpha, cur.py, d.y); dt = fmad(alpha, cur.pt, dt);
+                    } else if (DM == 1) {
+                        d.x = alpha * cur.px; d.y = alpha * cur.py; dt = alpha * cur.pt;
+                    } else {
+                        d.x = fmad(alpha, cur.px, cur.d.x); d.y = fmad(alpha, cur.py, cur.d.y); dt = fmad(alpha, cur.pt, cur.dt);
+                    }
+                    if (!h.act) { d.x = 0; d.y = 0; dt = 0; }
+                    stb<SNT>(delta, off.xy, d); stb<SNT>(delta, off.t, dt);
+                }
+                if (rout) {
+                    vec2_t<T> r; r.x = h.rx; r.y = h.ry;
+                    stb<SNT>(rout, off.xy, r); stb<SNT>(rout, off.t, h.rt);
+                }
+                rzd += wdot3(h.w0, h.rx, h.rx, h.w0, h.ry, h.ry, h.w2, h.rt, h.rt);
+            }
+            if (!h.act) { h.px = 0; h.py = 0; h.pt = 0; }
+            return h;
+        };
+        const GRow<T> g0 = fin(raw(g.y0 - 2));
+        GRow<T> qc = fin(raw(g.y0 - 1));
+        GRow<T> qd = fin(raw(g.y0));
+        ka = acarry_init(g0.px, g0.py, g0.pt, g0.c, g0.s, g0.ux, g0.uy, g0.act(), qc.px, qc.py, qc.pt, qc.c, qc.s,
+                         qc.ux, qc.uy, qc.act(), wr);
+        HRow<T> hup = stage_a(qc, qd, g.y0 - 1);
+        qc = qd;
+        qd = fin(raw(g.y0 + 1));
+        HRow<T> hc = stage_a(qc, qd, g.y0);
+        qc = qd;
+        qd = fin(raw(g.y0 + 2));
+        ACarry<T> kb = acarry_init(hup.px, hup.py, hup.pt, hup.c, hup.s, hup.ux, hup.uy, hup.act, hc.px, hc.py, hc.pt,
+                                   hc.c, hc.s, hc.ux, hc.uy, hc.act, wr);
+        for (int y = g.y0; y < g.y1; ++y) {
+            // stage A needs rows up to y1 + 1; the last trip re-reads that row (an L2 hit)
+            const GRaw<T> nx = raw(min(y + 3, g.y1 + 1));
+            const HRow<T> hd = stage_a(qc, qd, y + 1);
+            T aox, aoy, aot;
+            apply_ap(hc.px, hc.py, hc.pt, hc.c, hc.s, hc.ux, hc.uy, hc.act, hc.fit, hd.px, hd.py, hd.pt, hd.c, hd.s,
+                     hd.ux, hd.uy, hd.act, wr, wf2, kb, aox, aoy, aot);
+            if (g.out_lane) {
+                const POff<T> off((unsigned)a.dom.off(g.x, y), tb);
+                vec2_t<T> pv; pv.x = hc.px; pv.y = hc.py;
+                stb<SNT>(pout, off.xy, pv); stb<SNT>(pout, off.t, hc.pt);
+                papd += dot3(hc.px, aox, hc.py, aoy, hc.pt, aot);
+                rapd += wdot3(hc.w0, hc.rx, aox, hc.w0, hc.ry, aoy, hc.w2, hc.rt, aot);
+                apapd += wdot3(hc.w0, aox, aox, hc.w0, aoy, aoy, hc.w2, aot, aot);
+            }
+            hc = hd;
+            qc = qd;
+            qd = fin(nx);
         }
     }
     double v[4] = {(double)rzd, (double)papd, (double)rapd, (double)apapd};
@@ -1051,9 +1301,9 @@ struct FRow {          // a finished row of the fused kernel's apply window
     bool act, fit;
     // p_0 = pre r_0, formed where it is used (iw_apply<1>'s make_p: zero on inactive pixels,
     // where r_0 = pre = 0): three multiplies instead of three more VGPRs per held row
-    __device__ __forceinline__ T px() const { return wo * rx; }
-    __device__ __forceinline__ T py() const { return wo * ry; }
-    __device__ __forceinline__ T pt() const { return wt * rt; }
+    __device__ __forceinline__ T px() const { return opaque(wo * rx); }
+    __device__ __forceinline__ T py() const { return opaque(wo * ry); }
+    __device__ __forceinline__ T pt() const { return opaque(wt * rt); }
 };
 template <typename T, int NT = 2>
 __device__ __forceinline__ void iw_jtf_apply_body(const Args<T>& a, T* __restrict__ r, T* __restrict__ pre,
@@ -1498,7 +1748,7 @@ public:
         // against the canonical energy's (fit weight declared first), so names play no part
         read_knobs();
         timer_.apply_name = apply_kernel_name();
-        timer_.aux_names = {"iw_jtf_apply", "iw_apply_res"};
+        timer_.aux_names = {"iw_jtf_apply", "iw_apply_res", "iw_pcg"};
         allocate();
     }
     ~ImageWarpingPlan() override {
@@ -1550,7 +1800,7 @@ public:
         bind(params, false);
         exchange_unknowns();
         const int L = std::max(0, sp_.lIterations);
-        red_.ensure(std::max({stencil_blocks(), fused_blocks(), 2048}), 4, kScBase + iw::kSlots * (L + 2));
+        red_.ensure(std::max({stencil_blocks(), fused_blocks(), side_blocks(), 2048}), 4, kScBase + iw::kSlots * (L + 2));
         if (print_addr_) {   // OPT_AMD_PRINT_ADDR=1: placement of every stream (HBM channel study)
             print_addr_ = false;
             fprintf(stderr, "[opt_amd] addr r=%p r1=%p p0=%p p1=%p Ap=%p Ap1=%p delta=%p pre=%p flags=%p "
@@ -1578,8 +1828,10 @@ public:
         // lIterations >= 3 with the fused loop: nothing but passes 1 and 2 reads p_0, and both
         // form it from r_0 (iw_apply_res P0), so PCGInit1 does not store it
         const bool p0 = res && L >= 3;
+        // iterations 1.. as iw_pcg (one domain): Ap_{i-1} recomputed from p_{i-1}, never stored
+        const bool apfree = res && apfree_ && !distributed();
         if (fused) {
-            launch_jtf_apply(p0 ? nullptr : pcur, L == 1);
+            launch_jtf_apply(p0 ? nullptr : pcur, L == 1 || apfree);
         } else {
             tbegin("iw_jtf"); launch_jtf(r_, pre_, rz(0), false, res); tend();
             allreduce(rz(0));
@@ -1625,6 +1877,8 @@ public:
                         exchange(pl);
                         launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 0, p0);
                     }
+                } else if (apfree) {
+                    launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0);
                 } else {
                     launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 0, p0);
                 }
@@ -1790,6 +2044,10 @@ private:
         fused_init_ = env_int("OPT_AMD_IW_FUSED_INIT", 1) != 0;
         fused_res_ = env_int("OPT_AMD_IW_FUSED_RES", 1) != 0;
         defer_ = env_int("OPT_AMD_IW_DEFER", 1) != 0;
+        side_ = env_int("OPT_AMD_IW_SIDE", 0) != 0;
+        apfree_ = env_int("OPT_AMD_IW_APFREE", 1) != 0;
+        pcg_nt_ = env_int("OPT_AMD_IW_PCG_NT", 0) != 0;
+        jtf_nt_ = env_int("OPT_AMD_IW_JTF_NT", 1) != 0;
     }
     // A zeroed plan vector with kSlack spare bytes: place() may move each vector's base
     // within them between Steps (every vector is rewritten before it is read in a Step).
@@ -1872,7 +2130,11 @@ private:
     int pap(int i) const { return rz(i) + 1; }
 
     int stencil_blocks() const { return nstrips_ * nrowblocks_; }
-    // tiles of iw_jtf_apply: 62-column strips
+    // tiles of the side-by-side geometry (Args::side): groups of 4 strips x row chunks
+    int side_blocks() const {
+        return (nstrips_ + kBlock / kWave - 1) / (kBlock / kWave) * ((dom_.y_hi - dom_.y_lo + rows_ - 1) / rows_);
+    }
+    // tiles of iw_jtf_apply: 60-column strips
     int fused_strips() const { return (dom_.W + iw::kFStrip - 1) / iw::kFStrip; }
     int fused_blocks() const { return fused_strips() * nrowblocks_; }
 
@@ -1885,6 +2147,7 @@ private:
         a.use_pre = spec_.use_preconditioner ? 1 : 0;
         a.nstrips = nstrips_; a.nrowblocks = nrowblocks_; a.rows = rows_;
         a.tb0 = 0; a.tn0 = nstrips_ * nrowblocks_; a.tb1 = 0;
+        a.side = 0;
         // same float expression the reference's evalJTF + guardedInvert evaluate
         const T wr2 = (T)wr_ * (T)wr_, wf2 = (T)wf_ * (T)wf_;
         for (int fit = 0; fit < 2; ++fit)
@@ -1963,8 +2226,42 @@ private:
         iw::Args<T> a = args();
         a.nstrips = fused_strips();
         const int nb = fused_blocks();
-        launch_timed("iw_jtf_apply", iw::iw_jtf_apply<T>, nb, a, r_, pre_, pout, no_ap ? nullptr : Ap_,
-                     red_.slot(nb, rz(0)));
+        if (jtf_nt_)
+            launch_timed("iw_jtf_apply", iw::iw_jtf_apply<T, 2>, nb, a, r_, pre_, pout, no_ap ? nullptr : Ap_,
+                         red_.slot(nb, rz(0)));
+        else
+            launch_timed("iw_jtf_apply", iw::iw_jtf_apply<T, 0>, nb, a, r_, pre_, pout, no_ap ? nullptr : Ap_,
+                         red_.slot(nb, rz(0)));
+    }
+    // PCG iteration i >= 1 without a stored Ap (iw_pcg): reads r_{i-1} and p_{i-1}, writes
+    // r_i (unless last) and p_i; the deferred delta and P0 exactly as launch_apply_res
+    void launch_pcg(int i, const T* pin, T* pout, bool last, const T* pin2, bool p0) {
+        T* rb[2] = {r_, r1_};
+        const T* rin = rb[(i - 1) & 1];
+        T* rout = last ? nullptr : rb[i & 1];
+        const double base_scale = (i == 1 && !spec_.use_preconditioner) ? 4.0 : 1.0;
+        iw::Args<T> a = args();
+        a.nstrips = fused_strips();
+        const int nb = fused_blocks();
+        const ReduceSlot rs = red_.slot(nb, rz(i));
+        auto go = [&](auto kern) {
+            launch_timed("iw_pcg", kern, nb, a, pin, rin, (const T*)pre_, pout, rout, delta_, red_.scalars, rz(i - 1),
+                         base_scale, rs, pin2);
+        };
+        auto pick = [&](auto nt) {
+            constexpr bool SNT = decltype(nt)::value;
+            if (pin2 || (defer_ && i == 1)) {
+                if (i == 1 && p0) go(iw::iw_pcg<T, 0, 0, true, SNT>);
+                else if (i % 2 == 1) go(iw::iw_pcg<T, 0, 0, false, SNT>);
+                else if (i == 2 && p0) go(iw::iw_pcg<T, 1, 1, true, SNT>);
+                else if (i == 2) go(iw::iw_pcg<T, 1, 1, false, SNT>);
+                else go(iw::iw_pcg<T, 2, 1, false, SNT>);
+            } else if (i == 1 && p0) go(iw::iw_pcg<T, 1, 0, true, SNT>);
+            else if (i == 1) go(iw::iw_pcg<T, 1, 0, false, SNT>);
+            else go(iw::iw_pcg<T, 2, 0, false, SNT>);
+        };
+        if (pcg_nt_) pick(std::true_type{});
+        else pick(std::false_type{});
     }
     // part 0: every row block; 1: the interior row blocks [1, nrb - 1); 2: the first and
     // last row blocks (the only ones whose stencil reads halo rows)
@@ -2015,8 +2312,10 @@ private:
         T* Apout = last ? nullptr : ab[i & 1];
         const double base_scale = (i == 1 && !spec_.use_preconditioner) ? 4.0 : 1.0;
         iw::Args<T> a = args();
-        const int nb = stencil_blocks();   // the reduction slot spans every tile
+        const bool side = side_ && part == 0;
+        const int nb = side ? side_blocks() : stencil_blocks();   // the reduction slot spans every tile
         int grid = nb;
+        if (side) { a.side = 1; a.tn0 = nb; }
         if (part == 1) {
             a.tb0 = nstrips_; a.tn0 = nstrips_ * (nrowblocks_ - 2);
             grid = a.tn0;
@@ -2071,6 +2370,10 @@ private:
     bool fused_init_ = true;            // OPT_AMD_IW_FUSED_INIT=0: iw_jtf, then iw_apply<1,0>
     bool fused_res_ = true;             // OPT_AMD_IW_FUSED_RES=0: iw_apply<2> + iw_residual per iteration
     bool defer_ = true;                 // OPT_AMD_IW_DEFER=0: iw_apply_res updates delta in every iteration
+    bool side_ = false;                 // OPT_AMD_IW_SIDE=1: iw_apply_res with side-by-side waves (Args::side)
+    bool apfree_ = true;                // OPT_AMD_IW_APFREE=0: iw_apply_res (stored Ap) instead of iw_pcg
+    bool pcg_nt_ = false;               // OPT_AMD_IW_PCG_NT=1: iw_pcg with streaming stores
+    bool jtf_nt_ = true;                // OPT_AMD_IW_JTF_NT=0: iw_jtf_apply with plain stores
     bool offsets32_ = true;             // iw_apply_res's 32-bit byte offsets cover every plan vector
     int rows_ = 0, nstrips_ = 0, nrowblocks_ = 0;
     bool rows_auto_ = true;
@@ -2162,6 +2465,7 @@ public:
         a_.use_pre = use_pre_ ? 1 : 0;
         a_.nstrips = nstrips_; a_.nrowblocks = nrowblocks_; a_.rows = rows_;
         a_.tb0 = 0; a_.tn0 = nstrips_ * nrowblocks_; a_.tb1 = 0;
+        a_.side = 0;
         for (int f = 0; f < 2; ++f)
             for (int v = 0; v < 5; ++v) a_.preO[f][v] = 0;   // MODE 0 never reads them
     }

@@ -518,7 +518,7 @@ def _oracle_trajectory_floor(w, nit, lit):
     return ref, spread
 
 
-def _fused_vs_separate(monkeypatch, env, W, H, lit, seed, energy=ENERGY, oracle_floor=True):
+def _fused_vs_separate(monkeypatch, env, W, H, lit, seed, energy=ENERGY, oracle_floor=True, both=False):
     """One GN step with `env` = 0 and = 1: energies within 1e-6, unknowns within 1e-6 of
     their largest magnitude (the per-pixel values are the same; only reductions group
     differently). Three steps: both settings within 4x the oracle's fp32 noise floor (or
@@ -547,7 +547,7 @@ def _fused_vs_separate(monkeypatch, env, W, H, lit, seed, energy=ENERGY, oracle_
     else:
         np.testing.assert_allclose(b3[0], a3[0], rtol=1e-4)
         assert b3[0][-1] < b3[0][0]
-    return b
+    return (a, b) if both else b
 
 
 @pytest.mark.parametrize("W,H,lit", [(150, 110, 8), (37, 29, 1), (5, 3, 4), (200, 1, 3), (700, 300, 10)])
@@ -613,3 +613,39 @@ def test_side_by_side_waves_match_stacked(monkeypatch, W, H):
         out.append((np.array(s.profiled_solve(prm)), to_np(prm[0]), to_np(prm[1])))
     np.testing.assert_allclose(out[1][0], out[0][0], rtol=1e-6)
     assert rel_err(out[1][1], out[0][1]) < 1e-6 and rel_err(out[1][2], out[0][2]) < 1e-5
+
+
+@pytest.mark.parametrize("W,H,lit", [(150, 110, 8), (5, 3, 4), (200, 1, 3), (700, 300, 10), (64, 64, 2),
+                                     (61, 2, 5), (1, 9, 4), (125, 66, 3)])
+def test_pcg_pass_without_stored_ap_matches_apply_res(monkeypatch, W, H, lit):
+    """iw_pcg (Ap_{i-1} recomputed from p_{i-1} on 60-column strips; Ap never stored)
+    against iw_apply_res (Ap stored and read back, 64-column strips): the same per-pixel
+    expressions, only the reduction's tile partition differs — one GN step within 1e-6,
+    three within the oracle's fp32 floor; beta's identity against the direct sum."""
+    a, b = _fused_vs_separate(monkeypatch, "OPT_AMD_IW_APFREE", W, H, lit, 3 * W + H, both=True)
+    # the identity's distance from the direct sum is fp32 rounding of r_i amplified by
+    # rz_{i-1} / rz_i (1e-5 on the 1 x 9 image, whose first iteration cuts rz 1e4-fold):
+    # no further from it than iw_apply_res's, or 1e-6
+    sa, sb = np.array(a[3]), np.array(b[3])
+    for i in range(1, lit):
+        rz, rzx = sb[2 + 5 * i], sb[2 + 5 * i + 4]
+        old = abs(sa[2 + 5 * i + 4] - sa[2 + 5 * i])
+        assert abs(rzx - rz) <= max(1e-6 * abs(rz), 2 * old) + 1e-30, (i, rz, rzx, old)
+
+
+@pytest.mark.parametrize("W,H", [(90, 70), (130, 5), (256, 190)])
+def test_pcg_pass_without_stored_ap_fp64(monkeypatch, W, H):
+    """The same in fp64 (3 GN x 10 PCG): within 1e-9 of iw_apply_res and of the double
+    oracle's energies."""
+    w = perturbed(W, H, seed=8 + W)
+    out = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("OPT_AMD_IW_APFREE", v)
+        s = solver(W, H, double=True)
+        prm = device_params(w, double=True)
+        s.set_solver_params({"nIterations": 3, "lIterations": 10})
+        out.append((np.array(s.profiled_solve(prm)), to_np(prm[0]), to_np(prm[1])))
+    np.testing.assert_allclose(out[1][0], out[0][0], rtol=1e-9)
+    assert rel_err(out[1][1], out[0][1]) < 1e-9
+    _, _, c_ref, _ = oracle.iw_solve(w, 3, 10, double=True)
+    np.testing.assert_allclose(out[1][0], c_ref, rtol=1e-8)
