@@ -131,7 +131,7 @@ def pcg_variant(i: int, defer: bool = IW_DEFER, liter: int = 10) -> str:
     else:
         dm, e = (1 if i == 1 else 2), 0
     p0 = "true" if liter >= 3 and (i == 1 or (defer and i == 2)) else "false"
-    return f"iw_pcg<float, {dm}, {e}, {p0}, false>"
+    return f"iw_pcg<float, {dm}, {e}, {p0}, false, false>"
 
 
 # PCGInit1 fused with the first apply (iw_jtf_apply, one strip pass): Offset 8 + Angle 4 +

@@ -807,18 +807,127 @@ __global__ __launch_bounds__(kBlock) void iw_apply_res(Args<T> a, const T* __res
 // instead of read back: the pass reads r_{i-1} and p_{i-1} (+ the per-pixel angle, UrShape,
 // flags and angle pre) and writes r_i and p_i; Ap is never stored (-24 B/px per pass:
 // the Ap_{i-1} read and the Ap_i write). Ap_{i-1} is the same expression over the same
-// stored p_{i-1} as the previous pass's Ap (apply_ap below is the one body both use), so
-// r_i, p_i, Ap_i and the four sums are bitwise iw_apply_res's.
+// stored p_{i-1} as the previous pass's Ap_{i-1} (apply_ap2 is the one body every pass and
+// iw_jtf_apply use), so the identity's sums and r_i agree.
 // Geometry: iw_jtf_apply's 60-column strips (x = 60 strip - 2 + lane, no edge record): per
 // row, stage A recomputes Ap_{i-1} at every lane from the p_{i-1} window (valid at lanes
 // 1..62), forms r_i and p_i there; stage B applies J^T J to p_i one row behind (lanes
-// 2..61 are the outputs). Stage A runs one row ahead of stage B; a wave reads the unknown
-// rows y0-2 .. y1+1 (p_{i-1} at radius 2).
+// 2..61 are the outputs). A wave reads the unknown rows y0-2 .. y1+1 (p_{i-1} at radius 2).
+// The (x, y) pairs are two-lane vectors: the Offset channels, the residuals' two
+// components and the rotation derivative become v_pk_{fma,mul,add}_f32 (two fp32 operations
+// per instruction), which the pass needs: with twice iw_apply_res's stencil work per
+// pixel its VALU issue, not HBM, set its time (round 5, profiles/r05_pcg_pmc.json).
+template <typename T>
+__device__ __forceinline__ vec2_t<T> shl2(vec2_t<T> v) {   // lane l gets lane l-1's (0 at lane 0)
+    vec2_t<T> o;
+    o.x = from_left(v.x, (T)0); o.y = from_left(v.y, (T)0);
+    return o;
+}
+template <typename T>
+__device__ __forceinline__ vec2_t<T> shr2(vec2_t<T> v) {   // lane l gets lane l+1's (0 at lane 63)
+    vec2_t<T> o;
+    o.x = from_right(v.x, (T)0); o.y = from_right(v.y, (T)0);
+    return o;
+}
+// jedge in pairs: the residual pair J(j -> t) applied to p, and a = dR(t_j)/dt (U_j - U_t)
+template <typename T>
+__device__ __forceinline__ void jedge2(vec2_t<T> pj, T pjt, T cj, T sj, vec2_t<float> uj, vec2_t<T> pt,
+                                       vec2_t<float> ut, bool v, T wr, vec2_t<T>& J, vec2_t<T>& ad) {
+    const vec2_t<float> du = uj - ut;   // float subtractions, as the reference's Image reads
+    const T dx = (T)du.x, dy = (T)du.y;
+    vec2_t<T> ms, cs;
+    ms.x = -sj; ms.y = cj;
+    cs.x = cj; cs.y = sj;
+    ad = ms * dx - cs * dy;
+    const vec2_t<T> j = wr * ((pj - pt) - ad * pjt);
+    J = v ? j : (vec2_t<T>)0;
+}
+// Carries of the apply's row recursion: J(up->cur), J(cur->up) and its angle term
+template <typename T>
+struct ACarry {
+    vec2_t<T> in_up, my;
+    T thm;
+};
+template <typename T>
+__device__ __forceinline__ ACarry<T> acarry_init(vec2_t<T> up, T upt, T uc, T us, vec2_t<float> uu, bool uact,
+                                                 vec2_t<T> cp, T cpt, T cc, T cs, vec2_t<float> cu, bool cact, T wr) {
+    ACarry<T> k;
+    vec2_t<T> ad;
+    jedge2(up, upt, uc, us, uu, cp, cu, uact && cact, wr, k.in_up, ad);
+    jedge2(cp, cpt, cc, cs, cu, up, uu, uact && cact, wr, k.my, ad);
+    const vec2_t<T> th = ad * k.my;
+    k.thm = -wr * (th.x + th.y);
+    return k;
+}
+// Ap = J^T J p of row cur from (cur, dn) and the carry; no edge operand (lanes 0 / 63 are
+// never used). Leaves the carry of row dn.
+template <typename T>
+__device__ __forceinline__ void apply_ap2(vec2_t<T> cp, T cpt, T cc, T cs, vec2_t<float> cu, bool cact, bool cfit,
+                                          vec2_t<T> dp, T dpt, T dc, T ds, vec2_t<float> du, bool dact, T wr, T wf2,
+                                          ACarry<T>& k, vec2_t<T>& ao, T& aot) {
+    const vec2_t<T> lp = shl2(cp), rp = shr2(cp);
+    const vec2_t<float> lu = shl2(cu), ru = shr2(cu);
+    const int lact = from_left_i((int)cact, 0), ract = from_right_i((int)cact, 0);
+    vec2_t<T> jpx, apx, jmx, amx, jpy, apy, jdn, adn;
+    jedge2(cp, cpt, cc, cs, cu, rp, ru, cact && ract, wr, jpx, apx);
+    jedge2(cp, cpt, cc, cs, cu, lp, lu, cact && lact, wr, jmx, amx);
+    jedge2(cp, cpt, cc, cs, cu, dp, du, cact && dact, wr, jpy, apy);
+    jedge2(dp, dpt, dc, ds, du, cp, cu, cact && dact, wr, jdn, adn);
+    const vec2_t<T> inpx = shr2(jmx), inmx = shl2(jpx);
+    ao = wr * ((jpx + jmx + jpy + k.my) - (inpx + inmx + jdn + k.in_up));
+    if (cfit) ao += wf2 * cp;
+    const vec2_t<T> tt = apx * jpx + amx * jmx + apy * jpy;
+    aot = k.thm - wr * (tt.x + tt.y);
+    if (!cact) { ao = (vec2_t<T>)0; aot = 0; }
+    k.in_up = jpy;
+    k.my = jdn;
+    const vec2_t<T> th = adn * jdn;
+    k.thm = -wr * (th.x + th.y);
+}
+// Raw buffer access (gfx9 V#, dword3 0x00020000): an access at an offset >= num_records is
+// dropped (a store) or returns 0 (a load) by the hardware, without touching memory. iw_pcg
+// issues every conditional store and own-row load this way, at an out-of-range offset where
+// it does not apply, so every row issues the same vector-memory instructions with no branch
+// around them. With exec-masked stores the compiler cannot know how many stores follow the
+// next row's loads and waits for vmcnt(0) — this row's stores included — before it may use
+// them; with a fixed count it waits only for the loads (vmcnt(#stores issued after them)).
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bres(const void* p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, p ? (int)bytes : 0, 0x00020000);
+}
+__device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, unsigned off, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, unsigned off, vec2_t<float> v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, unsigned off, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, 0);
+}
+__device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, unsigned off, vec2_t<double> v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 0);
+}
+template <typename V> __device__ __forceinline__ V bld(__amdgpu_buffer_rsrc_t r, unsigned off);
+template <> __device__ __forceinline__ float bld<float>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+template <> __device__ __forceinline__ vec2_t<float> bld<vec2_t<float>>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(vec2_t<float>, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+template <> __device__ __forceinline__ double bld<double>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+template <> __device__ __forceinline__ vec2_t<double> bld<vec2_t<double>>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+    return __builtin_bit_cast(vec2_t<double>, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
 template <typename T>
 struct GRow {          // a finished row of p_{i-1} with the pixel's static data
-    T px, py, pt;      // p_{i-1} (0 on inactive pixels)
+    vec2_t<T> p;       // p_{i-1} (0 on inactive pixels)
+    T pt;
     T c, s;            // cos / sin of the angle
-    float ux, uy;
+    vec2_t<float> u;
     int f;             // flag byte
     vec2_t<T> r;       // r_{i-1}
     T rt, w2;          // its angle channel, the angle pre
@@ -831,104 +940,64 @@ template <typename T>
 struct GRaw {
     vec2_t<T> p, r, d, q2;
     T pt, rt, w2, ang, dt, q2t;
-    float2 u;
+    vec2_t<float> u;
     int f, in;
 };
 template <typename T, int DM, int E, bool P0>
 __device__ __forceinline__ GRaw<T> raw_grow(const Args<T>& a, const WaveGeom& g, int y, unsigned tb, const T* pin,
-                                            const T* rin, const T* pre, const T* delta, const T* pin2, bool own) {
+                                            const T* rin, const T* pre, __amdgpu_buffer_rsrc_t rdl,
+                                            __amdgpu_buffer_rsrc_t rq2, unsigned oob, bool own) {
     GRaw<T> q;
     q.in = present(a.dom, g.x, y);
     const unsigned i = q.in ? (unsigned)a.dom.off(g.x, y) : 0u;
     const POff<T> o(i, tb);
     q.f = ldb<false, uint8_t>(a.flags, i);
-    q.u = ldb<false, float2>(a.U, 8u * i);
+    q.u = ldb<false, vec2_t<float>>(a.U, 8u * i);
     q.ang = ldb<false, T>(a.A, o.s);
     q.r = ldb<false, vec2_t<T>>(rin, o.xy); q.rt = ldb<false, T>(rin, o.t);
     q.w2 = ldb<false, T>(pre, o.s);
     if (!(P0 && !E)) { q.p = ldb<false, vec2_t<T>>(pin, o.xy); q.pt = ldb<false, T>(pin, o.t); }
     own = own && g.out_lane;
-    if (DM == 2 && own) { q.d = ldb<false, vec2_t<T>>(delta, o.xy); q.dt = ldb<false, T>(delta, o.t); }
-    if (E && own) { q.q2 = ldb<false, vec2_t<T>>(pin2, o.xy); q.q2t = ldb<false, T>(pin2, o.t); }
+    const unsigned oxy = own ? o.xy : oob, ot = own ? o.t : oob;
+    if (DM == 2) { q.d = bld<vec2_t<T>>(rdl, oxy); q.dt = bld<T>(rdl, ot); }
+    if (E) { q.q2 = bld<vec2_t<T>>(rq2, oxy); q.q2t = bld<T>(rq2, ot); }
     return q;
 }
 template <typename T, int E, bool P0>
 __device__ __forceinline__ GRow<T> finish_grow(const Args<T>& a, const GRaw<T>& q) {
     GRow<T> o;
     o.f = q.in ? q.f : 0;
-    o.ux = q.in ? q.u.x : 0.f;
-    o.uy = q.in ? q.u.y : 0.f;
+    o.u = q.in ? q.u : (vec2_t<float>)0.f;
     sc_of(q.in ? q.ang : (T)0, &o.c, &o.s);
     o.r = q.r; o.rt = q.rt; o.w2 = q.w2;
     o.d = q.d; o.dt = q.dt;
     o.q2 = q.q2; o.q2t = q.q2t;
-    if constexpr (P0) {   // p_0 = pre r_0 (iw_jtf_apply's FRow::px: the same T products)
+    if constexpr (P0) {   // p_0 = pre r_0 (iw_jtf_apply's FRow::p: the same rounded T products)
         const T w0 = pre_offset(a, o.f);
-        if (E == 0) { o.px = opaque(w0 * q.r.x); o.py = opaque(w0 * q.r.y); o.pt = opaque(q.w2 * q.rt); }
-        else {
-            o.q2.x = opaque(w0 * q.q2.x); o.q2.y = opaque(w0 * q.q2.y); o.q2t = opaque(q.w2 * q.q2t);
-            o.px = q.p.x; o.py = q.p.y; o.pt = q.pt;
-        }
+        if (E == 0) { o.p = opaque(w0 * q.r); o.pt = opaque(q.w2 * q.rt); }
+        else { o.q2 = opaque(w0 * q.q2); o.q2t = opaque(q.w2 * q.q2t); o.p = q.p; o.pt = q.pt; }
     } else {
-        o.px = q.p.x; o.py = q.p.y; o.pt = q.pt;
+        o.p = q.p; o.pt = q.pt;
     }
-    if (!o.act()) { o.px = 0; o.py = 0; o.pt = 0; }
+    if (!o.act()) { o.p = (vec2_t<T>)0; o.pt = 0; }
     return o;
-}
-// Carries of the apply's row recursion: J(up->cur), J(cur->up) and its angle term
-template <typename T>
-struct ACarry { T in_up_x, in_up_y, my_x, my_y, thm; };
-template <typename T>
-__device__ __forceinline__ ACarry<T> acarry_init(T upx, T upy, T upt, T uc, T us, float uux, float uuy, bool uact,
-                                                 T cpx, T cpy, T cpt, T cc, T cs, float cux, float cuy, bool cact, T wr) {
-    ACarry<T> k;
-    T ax, ay;
-    (void)cpt;
-    jedge(upx, upy, upt, uc, us, uux, uuy, cpx, cpy, cux, cuy, uact && cact, wr, k.in_up_x, k.in_up_y, ax, ay);
-    jedge(cpx, cpy, cpt, cc, cs, cux, cuy, upx, upy, uux, uuy, uact && cact, wr, k.my_x, k.my_y, ax, ay);
-    k.thm = -wr * (ax * k.my_x + ay * k.my_y);
-    return k;
-}
-// Ap = J^T J p of row cur from (cur, dn) and the carry; no edge operand (lanes 0 / 63 are
-// never used). The same expression as iw_apply_res's apply_row, term for term.
-template <typename T>
-__device__ __forceinline__ void apply_ap(T cpx, T cpy, T cpt, T cc, T cs, float cux, float cuy, bool cact, bool cfit,
-                                         T dpx, T dpy, T dpt, T dc, T ds, float dux, float duy, bool dact, T wr, T wf2,
-                                         ACarry<T>& k, T& aox, T& aoy, T& aot) {
-    const T lpx = from_left(cpx, (T)0), lpy = from_left(cpy, (T)0);
-    const T rpx = from_right(cpx, (T)0), rpy = from_right(cpy, (T)0);
-    const float lux = from_left(cux, 0.f), luy = from_left(cuy, 0.f);
-    const float rux = from_right(cux, 0.f), ruy = from_right(cuy, 0.f);
-    const int lact = from_left_i((int)cact, 0), ract = from_right_i((int)cact, 0);
-    T jpx_x, jpx_y, apx_x, apx_y, jmx_x, jmx_y, amx_x, amx_y;
-    T jpy_x, jpy_y, apy_x, apy_y, jdn_x, jdn_y, adn_x, adn_y;
-    jedge(cpx, cpy, cpt, cc, cs, cux, cuy, rpx, rpy, rux, ruy, cact && ract, wr, jpx_x, jpx_y, apx_x, apx_y);
-    jedge(cpx, cpy, cpt, cc, cs, cux, cuy, lpx, lpy, lux, luy, cact && lact, wr, jmx_x, jmx_y, amx_x, amx_y);
-    jedge(cpx, cpy, cpt, cc, cs, cux, cuy, dpx, dpy, dux, duy, cact && dact, wr, jpy_x, jpy_y, apy_x, apy_y);
-    jedge(dpx, dpy, dpt, dc, ds, dux, duy, cpx, cpy, cux, cuy, cact && dact, wr, jdn_x, jdn_y, adn_x, adn_y);
-    const T inpx_x = from_right(jmx_x, (T)0), inpx_y = from_right(jmx_y, (T)0);
-    const T inmx_x = from_left(jpx_x, (T)0), inmx_y = from_left(jpx_y, (T)0);
-    aox = wr * ((jpx_x + jmx_x + jpy_x + k.my_x) - (inpx_x + inmx_x + jdn_x + k.in_up_x));
-    aoy = wr * ((jpx_y + jmx_y + jpy_y + k.my_y) - (inpx_y + inmx_y + jdn_y + k.in_up_y));
-    if (cfit) { aox += wf2 * cpx; aoy += wf2 * cpy; }
-    aot = k.thm - wr * ((apx_x * jpx_x + apx_y * jpx_y) + (amx_x * jmx_x + amx_y * jmx_y) +
-                        (apy_x * jpy_x + apy_y * jpy_y));
-    if (!cact) { aox = 0; aoy = 0; aot = 0; }
-    k.in_up_x = jpy_x; k.in_up_y = jpy_y;
-    k.my_x = jdn_x; k.my_y = jdn_y;
-    k.thm = -wr * (adn_x * jdn_x + adn_y * jdn_y);
 }
 // Stage B's view of a row: p_i, r_i, the weights and the static data
 template <typename T>
 struct HRow {
-    T px, py, pt, c, s;
-    float ux, uy;
+    vec2_t<T> p;
+    T pt, c, s;
+    vec2_t<float> u;
     bool act, fit;
-    T rx, ry, rt, w0, w2;
+    vec2_t<T> r;
+    T rt, w0, w2;
 };
 // SNT: streaming stores. The 60-column strips store 240-byte row segments that straddle
 // cache lines shared with the neighbouring strips; plain stores let the L2 merge them.
-template <typename T, int DM, int E = 0, bool P0 = false, bool SNT = false>
+// U2: two rows per loop trip with the row records swapping roles (no register copies, but
+// more VGPRs live: 138-168 against 120-142, 3 waves per SIMD instead of 4 on the odd passes)
+// PF2 (with U2): two raw rows in flight per wave instead of one.
+template <typename T, int DM, int E = 0, bool P0 = false, bool SNT = false, bool U2 = false, bool PF2 = false>
 __global__ __launch_bounds__(kBlock) void iw_pcg(Args<T> a, const T* __restrict__ pin, const T* __restrict__ rin,
                                                  const T* __restrict__ pre, T* __restrict__ pout, T* rout,
                                                  T* __restrict__ delta, double* __restrict__ sc, int prev,
@@ -945,83 +1014,132 @@ __global__ __launch_bounds__(kBlock) void iw_pcg(Args<T> a, const T* __restrict_
     if (blockIdx.x == 0 && threadIdx.x == 0) sc[prev + kSlots + 4] = rz_id;
     const T wr = a.wr, wf2 = a.wf * a.wf;
     const unsigned tb = (unsigned)(2 * a.dom.npix_mem() * (long long)sizeof(T));
+    // the unknown-layout vectors' byte size: the buffers' range and the drop offset
+    const unsigned oob = (unsigned)(3 * a.dom.npix_mem() * (long long)sizeof(T));
+    const __amdgpu_buffer_rsrc_t r_out = bres(rout, oob), r_p = bres(pout, oob), r_d = bres(delta, oob),
+                                 r_q2 = bres(pin2, oob);
     acc_t rzd = 0, papd = 0, rapd = 0, apapd = 0;
     if (g.y0 < g.y1) {
         auto raw = [&](int y) {
-            return raw_grow<T, DM, E, P0>(a, g, y, tb, pin, rin, pre, delta, pin2, y >= g.y0 && y < g.y1);
+            return raw_grow<T, DM, E, P0>(a, g, y, tb, pin, rin, pre, r_d, r_q2, oob, y >= g.y0 && y < g.y1);
         };
         auto fin = [&](const GRaw<T>& q) { return finish_grow<T, E, P0>(a, q); };
         // stage A at row y (cur = row y, dn = row y+1, carry from row y-1): Ap_{i-1}, then
         // r_i and p_i (stores r_i and delta on an owned row)
         ACarry<T> ka;
         auto stage_a = [&](const GRow<T>& cur, const GRow<T>& dn, int y) {
-            T ax, ay, at;
-            apply_ap(cur.px, cur.py, cur.pt, cur.c, cur.s, cur.ux, cur.uy, cur.act(), cur.fit(), dn.px, dn.py, dn.pt,
-                     dn.c, dn.s, dn.ux, dn.uy, dn.act(), wr, wf2, ka, ax, ay, at);
+            vec2_t<T> ap;
+            T at;
+            apply_ap2(cur.p, cur.pt, cur.c, cur.s, cur.u, cur.act(), cur.fit(), dn.p, dn.pt, dn.c, dn.s, dn.u,
+                      dn.act(), wr, wf2, ka, ap, at);
             HRow<T> h;
-            h.c = cur.c; h.s = cur.s; h.ux = cur.ux; h.uy = cur.uy; h.act = cur.act(); h.fit = cur.fit();
-            // make_rp: r_i = r_{i-1} - alpha Ap_{i-1}, z_i = pre r_i, p_i = z_i + beta p_{i-1}
-            make_rp(a, cur.f, alpha, beta, cur.r.x, cur.r.y, cur.rt, ax, ay, at, cur.w2, cur.px, cur.py, cur.pt, h.rx,
-                    h.ry, h.rt, h.px, h.py, h.pt);
-            h.w0 = a.use_pre ? pre_offset(a, cur.f) : (T)1;
+            h.c = cur.c; h.s = cur.s; h.u = cur.u; h.act = cur.act(); h.fit = cur.fit();
+            // r_i = r_{i-1} - alpha Ap_{i-1}, z_i = pre r_i, p_i = z_i + beta p_{i-1}
+            const T w0 = pre_offset(a, cur.f);
+            h.r = cur.r - alpha * ap;
+            h.rt = cur.rt - alpha * at;
+            vec2_t<T> z = h.r;
+            T zt = h.rt;
+            if (a.use_pre) { z = w0 * h.r; zt = cur.w2 * h.rt; }
+            h.p = z + beta * cur.p;
+            h.pt = zt + beta * cur.pt;
+            h.w0 = a.use_pre ? w0 : (T)1;
             h.w2 = a.use_pre ? cur.w2 : (T)1;
-            if (y >= g.y0 && y < g.y1 && g.out_lane) {
-                const POff<T> off((unsigned)a.dom.off(g.x, y), tb);
-                if (DM != 0) {   // iw_apply_res's deferred delta terms, term by term
+            const bool mine = y >= g.y0 && y < g.y1 && g.out_lane;
+            {
+                const POff<T> off(mine ? (unsigned)a.dom.off(g.x, y) : 0u, tb);
+                const unsigned oxy = mine ? off.xy : oob, ot = mine ? off.t : oob;
+                if (DM != 0) {   // iw_apply_res's deferred delta terms, term by term (explicit fmas)
                     vec2_t<T> d;
                     T dt;
                     if (E) {
-                        if (DM == 1) { d.x = alpha2 * cur.q2.x; d.y = alpha2 * cur.q2.y; dt = alpha2 * cur.q2t; }
-                        else { d.x = fmad(alpha2, cur.q2.x, cur.d.x); d.y = fmad(alpha2, cur.q2.y, cur.d.y); dt = fmad(alpha2, cur.q2t, cur.dt); }
-                        d.x = fmad(alpha, cur.px, d.x); d.y = fmad(alpha, cur.py, d.y); dt = fmad(alpha, cur.pt, dt);
+                        if (DM == 1) { d = alpha2 * cur.q2; dt = alpha2 * cur.q2t; }
+                        else { d = __builtin_elementwise_fma((vec2_t<T>)alpha2, cur.q2, cur.d); dt = fmad(alpha2, cur.q2t, cur.dt); }
+                        d = __builtin_elementwise_fma((vec2_t<T>)alpha, cur.p, d); dt = fmad(alpha, cur.pt, dt);
                     } else if (DM == 1) {
-                        d.x = alpha * cur.px; d.y = alpha * cur.py; dt = alpha * cur.pt;
+                        d = alpha * cur.p; dt = alpha * cur.pt;
                     } else {
-                        d.x = fmad(alpha, cur.px, cur.d.x); d.y = fmad(alpha, cur.py, cur.d.y); dt = fmad(alpha, cur.pt, cur.dt);
+                        d = __builtin_elementwise_fma((vec2_t<T>)alpha, cur.p, cur.d); dt = fmad(alpha, cur.pt, cur.dt);
                     }
-                    if (!h.act) { d.x = 0; d.y = 0; dt = 0; }
-                    stb<SNT>(delta, off.xy, d); stb<SNT>(delta, off.t, dt);
+                    if (!h.act) { d = (vec2_t<T>)0; dt = 0; }
+                    bst(r_d, oxy, d); bst(r_d, ot, dt);
                 }
-                if (rout) {
-                    vec2_t<T> r; r.x = h.rx; r.y = h.ry;
-                    stb<SNT>(rout, off.xy, r); stb<SNT>(rout, off.t, h.rt);
-                }
-                rzd += wdot3(h.w0, h.rx, h.rx, h.w0, h.ry, h.ry, h.w2, h.rt, h.rt);
+                bst(r_out, oxy, h.r); bst(r_out, ot, h.rt);   // rout null (last pass): dropped
+                const acc_t rz = wdot3(h.w0, h.r.x, h.r.x, h.w0, h.r.y, h.r.y, h.w2, h.rt, h.rt);
+                rzd += mine ? rz : 0.0;
             }
-            if (!h.act) { h.px = 0; h.py = 0; h.pt = 0; }
+            if (!h.act) { h.p = (vec2_t<T>)0; h.pt = 0; }
             return h;
         };
         const GRow<T> g0 = fin(raw(g.y0 - 2));
         GRow<T> qc = fin(raw(g.y0 - 1));
         GRow<T> qd = fin(raw(g.y0));
-        ka = acarry_init(g0.px, g0.py, g0.pt, g0.c, g0.s, g0.ux, g0.uy, g0.act(), qc.px, qc.py, qc.pt, qc.c, qc.s,
-                         qc.ux, qc.uy, qc.act(), wr);
+        ka = acarry_init(g0.p, g0.pt, g0.c, g0.s, g0.u, g0.act(), qc.p, qc.pt, qc.c, qc.s, qc.u, qc.act(), wr);
         HRow<T> hup = stage_a(qc, qd, g.y0 - 1);
         qc = qd;
         qd = fin(raw(g.y0 + 1));
         HRow<T> hc = stage_a(qc, qd, g.y0);
         qc = qd;
         qd = fin(raw(g.y0 + 2));
-        ACarry<T> kb = acarry_init(hup.px, hup.py, hup.pt, hup.c, hup.s, hup.ux, hup.uy, hup.act, hc.px, hc.py, hc.pt,
-                                   hc.c, hc.s, hc.ux, hc.uy, hc.act, wr);
-        for (int y = g.y0; y < g.y1; ++y) {
-            // stage A needs rows up to y1 + 1; the last trip re-reads that row (an L2 hit)
-            const GRaw<T> nx = raw(min(y + 3, g.y1 + 1));
-            const HRow<T> hd = stage_a(qc, qd, y + 1);
-            T aox, aoy, aot;
-            apply_ap(hc.px, hc.py, hc.pt, hc.c, hc.s, hc.ux, hc.uy, hc.act, hc.fit, hd.px, hd.py, hd.pt, hd.c, hd.s,
-                     hd.ux, hd.uy, hd.act, wr, wf2, kb, aox, aoy, aot);
-            if (g.out_lane) {
-                const POff<T> off((unsigned)a.dom.off(g.x, y), tb);
-                vec2_t<T> pv; pv.x = hc.px; pv.y = hc.py;
-                stb<SNT>(pout, off.xy, pv); stb<SNT>(pout, off.t, hc.pt);
-                papd += dot3(hc.px, aox, hc.py, aoy, hc.pt, aot);
-                rapd += wdot3(hc.w0, hc.rx, aox, hc.w0, hc.ry, aoy, hc.w2, hc.rt, aot);
-                apapd += wdot3(hc.w0, aox, aox, hc.w0, aoy, aoy, hc.w2, aot, aot);
+        ACarry<T> kb = acarry_init(hup.p, hup.pt, hup.c, hup.s, hup.u, hup.act, hc.p, hc.pt, hc.c, hc.s, hc.u, hc.act, wr);
+        // stage B at row y: Ap_i from (cur = row y, dn = row y+1), stores p_i, the three sums
+        auto stage_b = [&](const HRow<T>& cur, const HRow<T>& dn, int y) {
+            vec2_t<T> ao;
+            T aot;
+            apply_ap2(cur.p, cur.pt, cur.c, cur.s, cur.u, cur.act, cur.fit, dn.p, dn.pt, dn.c, dn.s, dn.u, dn.act, wr,
+                      wf2, kb, ao, aot);
+            {
+                const POff<T> off(g.out_lane ? (unsigned)a.dom.off(g.x, y) : 0u, tb);
+                bst(r_p, g.out_lane ? off.xy : oob, cur.p); bst(r_p, g.out_lane ? off.t : oob, cur.pt);
+                const acc_t s1 = dot3(cur.p.x, ao.x, cur.p.y, ao.y, cur.pt, aot);
+                const acc_t s2 = wdot3(cur.w0, cur.r.x, ao.x, cur.w0, cur.r.y, ao.y, cur.w2, cur.rt, aot);
+                const acc_t s3 = wdot3(cur.w0, ao.x, ao.x, cur.w0, ao.y, ao.y, cur.w2, aot, aot);
+                papd += g.out_lane ? s1 : 0.0;
+                rapd += g.out_lane ? s2 : 0.0;
+                apapd += g.out_lane ? s3 : 0.0;
             }
-            hc = hd;
-            qc = qd;
-            qd = fin(nx);
+        };
+        // two rows per trip, the row records swapping roles (no register copies): entering a
+        // trip at row y, q0 / q1 hold rows y+1 / y+2 and h0 row y
+        if constexpr (!U2) {
+            for (int y = g.y0; y < g.y1; ++y) {
+                const GRaw<T> nx = raw(min(y + 3, g.y1 + 1));
+                const HRow<T> hd = stage_a(qc, qd, y + 1);
+                stage_b(hc, hd, y);
+                hc = hd;
+                qc = qd;
+                qd = fin(nx);
+            }
+        } else if constexpr (PF2) {
+            GRow<T> q0 = qc, q1 = qd;
+            HRow<T> h0 = hc, h1;
+            GRaw<T> na = raw(min(g.y0 + 3, g.y1 + 1)), nb = raw(min(g.y0 + 4, g.y1 + 1));
+            for (int y = g.y0; y < g.y1; y += 2) {
+                h1 = stage_a(q0, q1, y + 1);
+                stage_b(h0, h1, y);
+                q0 = fin(na);
+                if (y + 1 >= g.y1) break;
+                na = raw(min(y + 5, g.y1 + 1));
+                h0 = stage_a(q1, q0, y + 2);
+                stage_b(h1, h0, y + 1);
+                q1 = fin(nb);
+                nb = raw(min(y + 6, g.y1 + 1));
+            }
+        } else {
+        GRow<T> q0 = qc, q1 = qd;
+        HRow<T> h0 = hc, h1;
+        for (int y = g.y0; y < g.y1; y += 2) {
+            // stage A needs rows up to y1 + 1; the last trip re-reads that row (an L2 hit)
+            const GRaw<T> n1 = raw(min(y + 3, g.y1 + 1));
+            h1 = stage_a(q0, q1, y + 1);
+            stage_b(h0, h1, y);
+            q0 = fin(n1);
+            if (y + 1 >= g.y1) break;
+            const GRaw<T> n2 = raw(min(y + 4, g.y1 + 1));
+            h0 = stage_a(q1, q0, y + 2);
+            stage_b(h1, h0, y + 1);
+            q1 = fin(n2);
+        }
         }
     }
     double v[4] = {(double)rzd, (double)papd, (double)rapd, (double)apapd};
@@ -1281,12 +1399,12 @@ __global__ __launch_bounds__(kBlock) void iw_jtf(Args<T> a, T* __restrict__ r, T
 // The first PCG iteration's p = pre r depends on nothing global, so PCGInit1 (J^T F,
 // preconditioner, flags, rz[0] = r.(pre r)) and the first apply (Ap = J^T J p,
 // pAp[0] = p.Ap) run as ONE strip pass from the arrays bound at this Step: the same
-// per-pixel values as iw_jtf<0> followed by iw_apply<1,0> (bitwise), without writing
-// r / pre / flags and reading them back. Geometry: a wavefront owns 62 output columns,
-// x = 62*strip - 1 + lane; J^T F is evaluated at all 64 lanes (iw_jtf's 2-lane edge
-// record supplies columns x-1 of lane 0 and x+1 of lane 63), so the apply at lanes
-// 1..62 finds every horizontal neighbour's p in a lane neighbour (DPP) and needs no
-// second edge ring. Rows: J^T F runs one row ahead of the apply (rows y0-1 .. y1,
+// r / pre / flags as iw_jtf<0> (bitwise) and the same J^T J p as iw_apply<1,0> up to the
+// summation order of the pairs (apply_ap2, round 5), without writing r / pre / flags and
+// reading them back. Geometry: a wavefront owns 60 output columns, x = 60*strip - 2 + lane;
+// J^T F is evaluated at all 64 lanes (valid at lanes 1..62), so the apply at lanes 2..61
+// finds every horizontal neighbour's p in a lane neighbour (DPP) and needs no edge
+// record. Rows: J^T F runs one row ahead of the apply (rows y0-1 .. y1,
 // the outer two for the apply's vertical neighbours only; unknown rows y0-2 .. y1+1).
 // One reduction of four scalars (fp64 per lane): sc[rs.out + 0..3] = {rz[0], pAp[0],
 // r_0.W Ap_0, Ap_0.W Ap_0} — the last two for iw_apply_res's identity for rz[1] (W r_0
@@ -1304,6 +1422,16 @@ struct FRow {          // a finished row of the fused kernel's apply window
     __device__ __forceinline__ T px() const { return opaque(wo * rx); }
     __device__ __forceinline__ T py() const { return opaque(wo * ry); }
     __device__ __forceinline__ T pt() const { return opaque(wt * rt); }
+    __device__ __forceinline__ vec2_t<T> p() const {
+        vec2_t<T> r;
+        r.x = rx; r.y = ry;
+        return opaque(wo * r);
+    }
+    __device__ __forceinline__ vec2_t<float> u() const {
+        vec2_t<float> v;
+        v.x = ux; v.y = uy;
+        return v;
+    }
 };
 template <typename T, int NT = 2>
 __device__ __forceinline__ void iw_jtf_apply_body(const Args<T>& a, T* __restrict__ r, T* __restrict__ pre,
@@ -1345,62 +1473,35 @@ __device__ __forceinline__ void iw_jtf_apply_body(const Args<T>& a, T* __restric
         FRow<T> cur = jrow(vcur, vdn, k, g.y0, true);
         vcur = vdn;
         vdn = finish_vrow<T, false, false>(raw_vrow<T, false, false>(a, g, g.y0 + 2));
-        // apply carries from the row above: J(up->cur) and J(cur->up) with its angle term
-        T in_up_x, in_up_y, my_x, my_y, thm, ax, ay;
-        jedge(up.px(), up.py(), up.pt(), up.c, up.s, up.ux, up.uy, cur.px(), cur.py(), cur.ux, cur.uy,
-              up.act && cur.act, wr, in_up_x, in_up_y, ax, ay);
-        jedge(cur.px(), cur.py(), cur.pt(), cur.c, cur.s, cur.ux, cur.uy, up.px(), up.py(), up.ux, up.uy,
-              up.act && cur.act, wr, my_x, my_y, ax, ay);
-        thm = -wr * (ax * my_x + ay * my_y);
+        // apply carries from the row above (apply_ap2's recursion, the body iw_pcg recomputes
+        // Ap_0 with: both act on the same rounded p_0 and agree bitwise)
+        ACarry<T> k2 = acarry_init(up.p(), up.pt(), up.c, up.s, up.u(), up.act, cur.p(), cur.pt(), cur.c, cur.s,
+                                   cur.u(), cur.act, wr);
         for (int y = g.y0; y < g.y1; ++y) {
             // J^T F needs rows up to y1 + 1; the last trip re-reads that row (an L2 hit)
             // instead of fetching row y1 + 2
             const VRaw<T> nx = raw_vrow<T, false, false>(a, g, min(y + 3, g.y1 + 1));
             const FRow<T> dn = jrow(vcur, vdn, k, y + 1, y + 1 < g.y1);
-            const T cpx = cur.px(), cpy = cur.py(), cpt = cur.pt(), dpx = dn.px(), dpy = dn.py(), dpt = dn.pt();
-            // iw_apply's row body; lanes 0, 1, 62, 63 are not outputs, so no edge operand
-            const T lpx = from_left(cpx, (T)0), lpy = from_left(cpy, (T)0);
-            const T rpx = from_right(cpx, (T)0), rpy = from_right(cpy, (T)0);
-            const float lux = from_left(cur.ux, 0.f), luy = from_left(cur.uy, 0.f);
-            const float rux = from_right(cur.ux, 0.f), ruy = from_right(cur.uy, 0.f);
-            const int lact = from_left_i(cur.act, 0), ract = from_right_i(cur.act, 0);
-            T jpx_x, jpx_y, apx_x, apx_y, jmx_x, jmx_y, amx_x, amx_y;
-            T jpy_x, jpy_y, apy_x, apy_y, jdn_x, jdn_y, adn_x, adn_y;
-            jedge(cpx, cpy, cpt, cur.c, cur.s, cur.ux, cur.uy, rpx, rpy, rux, ruy,
-                  cur.act && ract, wr, jpx_x, jpx_y, apx_x, apx_y);
-            jedge(cpx, cpy, cpt, cur.c, cur.s, cur.ux, cur.uy, lpx, lpy, lux, luy,
-                  cur.act && lact, wr, jmx_x, jmx_y, amx_x, amx_y);
-            jedge(cpx, cpy, cpt, cur.c, cur.s, cur.ux, cur.uy, dpx, dpy, dn.ux, dn.uy,
-                  cur.act && dn.act, wr, jpy_x, jpy_y, apy_x, apy_y);
-            jedge(dpx, dpy, dpt, dn.c, dn.s, dn.ux, dn.uy, cpx, cpy, cur.ux, cur.uy,
-                  cur.act && dn.act, wr, jdn_x, jdn_y, adn_x, adn_y);
-            const T inpx_x = from_right(jmx_x, (T)0), inpx_y = from_right(jmx_y, (T)0);
-            const T inmx_x = from_left(jpx_x, (T)0), inmx_y = from_left(jpx_y, (T)0);
-            T aox = wr * ((jpx_x + jmx_x + jpy_x + my_x) - (inpx_x + inmx_x + jdn_x + in_up_x));
-            T aoy = wr * ((jpx_y + jmx_y + jpy_y + my_y) - (inpx_y + inmx_y + jdn_y + in_up_y));
-            if (cur.fit) { aox += wf2 * cpx; aoy += wf2 * cpy; }
-            T aot = thm - wr * ((apx_x * jpx_x + apx_y * jpx_y) + (amx_x * jmx_x + amx_y * jmx_y) +
-                                (apy_x * jpy_x + apy_y * jpy_y));
-            if (!cur.act) { aox = 0; aoy = 0; aot = 0; }
+            const vec2_t<T> cp = cur.p();
+            const T cpt = cur.pt();
+            vec2_t<T> ao;
+            T aot;
+            apply_ap2(cp, cpt, cur.c, cur.s, cur.u(), cur.act, cur.fit, dn.p(), dn.pt(), dn.c, dn.s, dn.u(), dn.act,
+                      wr, wf2, k2, ao, aot);
             if (g.out_lane) {
                 const POff<T> off((unsigned)a.dom.off(g.x, y), tb);
-                if (Ap) {   // null when lIterations == 1: nothing reads that Ap
-                    vec2_t<T> v; v.x = aox; v.y = aoy;
-                    stb<(NT & 2) != 0>(Ap, off.xy, v); stb<(NT & 2) != 0>(Ap, off.t, aot);
+                if (Ap) {   // null when lIterations == 1 or when iw_pcg recomputes Ap_0
+                    stb<(NT & 2) != 0>(Ap, off.xy, ao); stb<(NT & 2) != 0>(Ap, off.t, aot);
                 }
                 if (pout) {   // null when the loop forms p_0 from r_0 itself (lIterations >= 3)
-                    vec2_t<T> pv; pv.x = cpx; pv.y = cpy;
-                    stb<(NT & 2) != 0>(pout, off.xy, pv); stb<(NT & 2) != 0>(pout, off.t, cpt);
+                    stb<(NT & 2) != 0>(pout, off.xy, cp); stb<(NT & 2) != 0>(pout, off.t, cpt);
                 }
-                papdot += dot3(cpx, aox, cpy, aoy, cpt, aot);
+                papdot += dot3(cp.x, ao.x, cp.y, ao.y, cpt, aot);
                 // PCGStep2's weights: pre, or 1 without a preconditioner
                 const T w0 = a.use_pre ? cur.wo : (T)1, w2 = a.use_pre ? cur.wt : (T)1;
-                rapd += wdot3(w0, cur.rx, aox, w0, cur.ry, aoy, w2, cur.rt, aot);
-                apapd += wdot3(w0, aox, aox, w0, aoy, aoy, w2, aot, aot);
+                rapd += wdot3(w0, cur.rx, ao.x, w0, cur.ry, ao.y, w2, cur.rt, aot);
+                apapd += wdot3(w0, ao.x, ao.x, w0, ao.y, ao.y, w2, aot, aot);
             }
-            in_up_x = jpy_x; in_up_y = jpy_y;
-            my_x = jdn_x; my_y = jdn_y;
-            thm = -wr * (adn_x * jdn_x + adn_y * jdn_y);
             cur = dn;
             vcur = vdn;
             vdn = finish_vrow<T, false, false>(nx);
@@ -2047,7 +2148,11 @@ private:
         side_ = env_int("OPT_AMD_IW_SIDE", 0) != 0;
         apfree_ = env_int("OPT_AMD_IW_APFREE", 1) != 0;
         pcg_nt_ = env_int("OPT_AMD_IW_PCG_NT", 0) != 0;
-        jtf_nt_ = env_int("OPT_AMD_IW_JTF_NT", 1) != 0;
+        pcg_u2_ = env_int("OPT_AMD_IW_PCG_U2", 0);
+        // iw_jtf_apply's 60-column strips store 240-B row segments that share cache lines
+        // with the neighbouring strips: plain stores (merged in the L2) measured 217-220 us
+        // against 233-245 with streaming ones (round 5, same box, interleaved)
+        jtf_nt_ = env_int("OPT_AMD_IW_JTF_NT", 0) != 0;
     }
     // A zeroed plan vector with kSlack spare bytes: place() may move each vector's base
     // within them between Steps (every vector is rewritten before it is read in a Step).
@@ -2248,20 +2353,24 @@ private:
             launch_timed("iw_pcg", kern, nb, a, pin, rin, (const T*)pre_, pout, rout, delta_, red_.scalars, rz(i - 1),
                          base_scale, rs, pin2);
         };
-        auto pick = [&](auto nt) {
-            constexpr bool SNT = decltype(nt)::value;
+        auto pick = [&](auto nt, auto u2, auto pf2) {
+            constexpr bool SNT = decltype(nt)::value, U2 = decltype(u2)::value, PF2 = decltype(pf2)::value;
             if (pin2 || (defer_ && i == 1)) {
-                if (i == 1 && p0) go(iw::iw_pcg<T, 0, 0, true, SNT>);
-                else if (i % 2 == 1) go(iw::iw_pcg<T, 0, 0, false, SNT>);
-                else if (i == 2 && p0) go(iw::iw_pcg<T, 1, 1, true, SNT>);
-                else if (i == 2) go(iw::iw_pcg<T, 1, 1, false, SNT>);
-                else go(iw::iw_pcg<T, 2, 1, false, SNT>);
-            } else if (i == 1 && p0) go(iw::iw_pcg<T, 1, 0, true, SNT>);
-            else if (i == 1) go(iw::iw_pcg<T, 1, 0, false, SNT>);
-            else go(iw::iw_pcg<T, 2, 0, false, SNT>);
+                if (i == 1 && p0) go(iw::iw_pcg<T, 0, 0, true, SNT, U2, PF2>);
+                else if (i % 2 == 1) go(iw::iw_pcg<T, 0, 0, false, SNT, U2, PF2>);
+                else if (i == 2 && p0) go(iw::iw_pcg<T, 1, 1, true, SNT, U2, PF2>);
+                else if (i == 2) go(iw::iw_pcg<T, 1, 1, false, SNT, U2, PF2>);
+                else go(iw::iw_pcg<T, 2, 1, false, SNT, U2, PF2>);
+            } else if (i == 1 && p0) go(iw::iw_pcg<T, 1, 0, true, SNT, U2, PF2>);
+            else if (i == 1) go(iw::iw_pcg<T, 1, 0, false, SNT, U2, PF2>);
+            else go(iw::iw_pcg<T, 2, 0, false, SNT, U2, PF2>);
         };
-        if (pcg_nt_) pick(std::true_type{});
-        else pick(std::false_type{});
+        using F = std::false_type;
+        using Tt = std::true_type;
+        if (pcg_u2_ == 2) pick(F{}, Tt{}, Tt{});
+        else if (pcg_u2_) pick(F{}, Tt{}, F{});
+        else if (pcg_nt_) pick(Tt{}, F{}, F{});
+        else pick(F{}, F{}, F{});
     }
     // part 0: every row block; 1: the interior row blocks [1, nrb - 1); 2: the first and
     // last row blocks (the only ones whose stencil reads halo rows)
@@ -2373,7 +2482,8 @@ private:
     bool side_ = false;                 // OPT_AMD_IW_SIDE=1: iw_apply_res with side-by-side waves (Args::side)
     bool apfree_ = true;                // OPT_AMD_IW_APFREE=0: iw_apply_res (stored Ap) instead of iw_pcg
     bool pcg_nt_ = false;               // OPT_AMD_IW_PCG_NT=1: iw_pcg with streaming stores
-    bool jtf_nt_ = true;                // OPT_AMD_IW_JTF_NT=0: iw_jtf_apply with plain stores
+    int pcg_u2_ = 0;                    // OPT_AMD_IW_PCG_U2=1: iw_pcg two rows per trip (U2); 2: and two rows in flight (PF2)
+    bool jtf_nt_ = false;               // OPT_AMD_IW_JTF_NT=1: iw_jtf_apply with streaming stores
     bool offsets32_ = true;             // iw_apply_res's 32-bit byte offsets cover every plan vector
     int rows_ = 0, nstrips_ = 0, nrowblocks_ = 0;
     bool rows_auto_ = true;
