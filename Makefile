@@ -14,8 +14,9 @@ OBJS = $(patsubst $(SRC_DIR)/%.hip,$(OBJ_DIR)/%.o,$(HIP_SRCS)) $(patsubst $(SRC_
 GEN_DIR ?= build/gen
 REDUCE_SRC = $(GEN_DIR)/reduce_dev_src.h
 LIB ?= opt_amd/libopt_amd.so
+RCCL_STUB = tests/rccl_stub/librccl_stub.so
 
-all: $(LIB) oracle
+all: $(LIB) oracle $(RCCL_STUB)
 
 $(OBJ_DIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
 	@mkdir -p $(OBJ_DIR)
@@ -52,8 +53,13 @@ $(LIB): $(OBJS)
 oracle:
 	$(MAKE) -C oracle
 
+# test infrastructure: the multi-process RCCL stand-in (tests/rccl_stub/rccl_stub.cpp)
+$(RCCL_STUB): tests/rccl_stub/rccl_stub.cpp
+	$(HIPCC) -O2 -std=c++17 -fPIC -shared -Wl,-Bsymbolic -Wl,-soname,librccl_stub.so -o $@ $< -lrt
+rccl_stub: $(RCCL_STUB)
+
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(RCCL_STUB)
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean rccl_stub

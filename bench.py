@@ -214,6 +214,26 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+def visible_gpus():
+    """GPUs this process could open, counted without any GPU runtime: the visibility
+    variables if one is set, else the KFD topology's GPU nodes (simd_count > 0); None when
+    neither can be read (each rank then checks its own device, main())."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([d for d in v.split(",") if d.strip() != ""])
+    try:
+        import glob
+        n = 0
+        for f in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+            for line in open(f):
+                if line.startswith("simd_count") and int(line.split()[1]) > 0:
+                    n += 1
+        return n
+    except (OSError, ValueError):
+        return None
+
+
 def spawn_ranks(args) -> int:
     """--gpus N > 1 without a launcher: start N copies of this script, one per GPU, with
     RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set (what
@@ -224,10 +244,8 @@ def spawn_ranks(args) -> int:
 
     n = args.gpus
     if not args.dry_run:
-        import torch   # device_count() does not initialise the GPU on this image
-
-        have = torch.cuda.device_count()
-        if have < n:
+        have = visible_gpus()   # counted without torch / HIP: this process never opens the GPU
+        if have is not None and have < n:
             print(f"bench.py: --gpus {n} but only {have} GPU(s) visible", file=sys.stderr, flush=True)
             return 2
     port = os.environ.get("MASTER_PORT") or str(free_port())
@@ -371,6 +389,10 @@ def main():
         return 0
     import torch
 
+    if local >= torch.cuda.device_count():
+        print(f"bench.py: rank {rank} needs device {local}, {torch.cuda.device_count()} visible", file=sys.stderr,
+              flush=True)
+        return 2
     torch.cuda.set_device(local)
     dist = None
     if world > 1:

@@ -106,6 +106,9 @@ void OptAMD_CommDestroy(OptAMD_Comm* comm);
  * world size the solver actually runs on from here, not from the launcher's env. */
 int OptAMD_CommSize(OptAMD_Comm* comm);
 int OptAMD_CommRank(OptAMD_Comm* comm);
+/* The transport behind a communicator, "rccl" or "local", copied into buf (at most
+ * buflen bytes incl. the terminator); returns its length, -1 for NULL. */
+int OptAMD_CommKind(OptAMD_Comm* comm, char* buf, int buflen);
 /* All ranks as threads of one process (shared device or peer devices): for testing
  * the decomposition on one GPU. The rank handles belong to the group. */
 OptAMD_LocalGroup* OptAMD_LocalGroupCreate(int nranks);

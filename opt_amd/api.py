@@ -72,6 +72,7 @@ _SIGNATURES = [
     ("OptAMD_CommDestroy", None, [_VP]),
     ("OptAMD_CommSize", ctypes.c_int, [_VP]),
     ("OptAMD_CommRank", ctypes.c_int, [_VP]),
+    ("OptAMD_CommKind", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int]),
     ("OptAMD_LocalGroupCreate", _VP, [ctypes.c_int]),
     ("OptAMD_LocalGroupRank", _VP, [_VP, ctypes.c_int]),
     ("OptAMD_LocalGroupDestroy", None, [_VP]),

@@ -2,6 +2,7 @@
 #include "comm.h"
 #include <dlfcn.h>
 #include <rccl/rccl.h>
+#include <cstdlib>
 #include <cstring>
 
 namespace optamd {
@@ -38,7 +39,13 @@ struct RcclApi {
     ncclResult_t (*commSplit)(ncclComm_t, int, int, ncclComm_t*, void*) = nullptr;
     bool load(std::string* err) {
         if (h) return true;
-        for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+        // OPT_AMD_RCCL_LIB: an explicit library (the tests' multi-process stand-in,
+        // tests/rccl_stub), loaded privately so a process's own RCCL (PyTorch's) is untouched
+        if (const char* lib = getenv("OPT_AMD_RCCL_LIB"); lib && *lib) {
+            h = dlopen(lib, RTLD_NOW | RTLD_LOCAL);
+            if (!h) { *err = std::string("cannot load OPT_AMD_RCCL_LIB=") + lib + ": " + dlerror(); return false; }
+        }
+        if (!h) for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
             h = dlopen(n, RTLD_NOW | RTLD_NOLOAD | RTLD_GLOBAL);
             if (!h) h = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
             if (h) break;

@@ -292,6 +292,7 @@ void OptAMD_CommDestroy(OptAMD_Comm* comm) {
 }
 int OptAMD_CommSize(OptAMD_Comm* comm) { return comm ? comm->impl->size() : -1; }
 int OptAMD_CommRank(OptAMD_Comm* comm) { return comm ? comm->impl->rank() : -1; }
+int OptAMD_CommKind(OptAMD_Comm* comm, char* buf, int n) { return comm ? copy_name(comm->impl->kind(), buf, n) : -1; }
 OptAMD_LocalGroup* OptAMD_LocalGroupCreate(int nranks) {
     if (nranks < 1) return nullptr;
     auto* g = new OptAMD_LocalGroup();
