@@ -196,7 +196,7 @@ def parse():
 
 # stencil radius (halo rows) of each workload's energy; checked against the plan's
 # OptAMD_PlanHalo in the real run
-HALO = {"image_warping": 1, "shape_from_shading": 2}
+HALO = {"image_warping": 2, "shape_from_shading": 2}
 
 
 def rank_env():

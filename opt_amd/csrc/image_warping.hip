@@ -539,7 +539,8 @@ constexpr int kFStrip = 60;
 template <typename T>
 __device__ __forceinline__ WaveGeom geom_fused(const Args<T>& a) {
     WaveGeom g;
-    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int lt = xcd_remap(blockIdx.x, gridDim.x);
+    const int t = lt < a.tn0 ? a.tb0 + lt : a.tb1 + (lt - a.tn0);   // the launch's tile ranges (geom)
     g.tile = t;
     const int strip = t % a.nstrips, rb = t / a.nstrips;
     g.lane = threadIdx.x & (kWave - 1);
@@ -1857,7 +1858,10 @@ public:
         release();
     }
 
-    int halo() const override { return 1; }   // radius of the 4-neighbour stencil
+    // rows of neighbour data a slab holds: 2, the reach of iw_jtf_apply (J^T F one row
+    // ahead of the apply) and of iw_pcg (Ap_{i-1} recomputed around p_i's stencil); the
+    // 4-neighbour stencil itself reaches 1
+    int halo() const override { return 2; }
 
     std::string set_decomposition(Comm* comm, int y_lo, int y_hi) override {
         if (opts_.host_buffers) return "row-slab decomposition needs backend_cuda (device arrays)";
@@ -1915,7 +1919,7 @@ public:
         // reference does on every Step (:2001, :2028): problem parameters may be updated
         // in place between Steps (Opt.h:64-65). On one domain it is fused with the first
         // PCG iteration's apply (iw_jtf_apply: the first p = pre r needs no global scalar).
-        const bool fused = fused_init_ && offsets32_ && !distributed() && L >= 1;
+        const bool fused = fused_init_ && offsets32_ && L >= 1;
         // iterations 1.. as iw_apply_res (the residual update folded into the next apply;
         // needs the sums r_0.W Ap_0, Ap_0.W Ap_0 of iteration 0), on one domain and on row
         // slabs: ONE all-reduce of four scalars per PCG iteration instead of two
@@ -1929,10 +1933,20 @@ public:
         // lIterations >= 3 with the fused loop: nothing but passes 1 and 2 reads p_0, and both
         // form it from r_0 (iw_apply_res P0), so PCGInit1 does not store it
         const bool p0 = res && L >= 3;
-        // iterations 1.. as iw_pcg (one domain): Ap_{i-1} recomputed from p_{i-1}, never stored
-        const bool apfree = res && apfree_ && !distributed();
+        // iterations 1.. as iw_pcg: Ap_{i-1} recomputed from p_{i-1}, never stored
+        const bool apfree = res && apfree_;
         if (fused) {
             launch_jtf_apply(p0 ? nullptr : pcur, L == 1 || apfree);
+            allreduce(rz(0), 4);   // rz_0, p.Ap_0, r_0.W Ap_0, Ap_0.W Ap_0
+            if (distributed()) {   // the next pass reads r_0 (and forms p_0) in the halo rows
+                std::vector<HaloPlane> pl;
+                add_vec_planes(pl, r_);
+                pl.push_back({(void*)pre_, sizeof(T) * dom_.W});
+                pl.push_back({(void*)flags_, (size_t)dom_.W});
+                if (!p0) add_vec_planes(pl, pcur);
+                if (!apfree) add_vec_planes(pl, Ap_);
+                exchange(pl);
+            }
         } else {
             tbegin("iw_jtf"); launch_jtf(r_, pre_, rz(0), false, res); tend();
             allreduce(rz(0));
@@ -1949,7 +1963,8 @@ public:
         // launch overhead, so the loop stays as plain stream launches)
         // row slabs with >= 3 row blocks: the halo refresh of r and p_{i-1} runs beside the
         // interior row blocks of the next apply (halo_mark / halo_begin / halo_join)
-        const bool split = distributed() && overlap_ && comm_->concurrent_halo() && nrowblocks_ >= 3;
+        const bool split = distributed() && overlap_ && comm_->concurrent_halo() && nrowblocks_ >= 3 &&
+                           (dom_.y_hi - dom_.y_lo) - (nrowblocks_ - 1) * 4 * rows_ >= 2;
         if (res) {
             // p_i in pb[i % 3] (deferred delta) or pb[i % 2]
             auto pbuf = [&](int i) { return pb[defer ? i % 3 : i % 2]; };
@@ -1963,20 +1978,27 @@ public:
                 T* ab[2] = {Ap_, Ap1_};
                 // pass 2 with P0: p_0 is formed from r_0, still in the r buffer pass 2 writes r_2 to
                 const T* pin2 = (defer && i >= 2) ? ((p0 && i == 2) ? rb[0] : pbuf(i - 2)) : nullptr;
-                if (distributed()) {   // the stencil reads r, Ap and p of iteration i-1 in the halo rows
+                // part 0: every row block; 1: the interior ones; 2: the first and last
+                auto pass = [&](int part) {
+                    if (apfree) launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0, part);
+                    else launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, part, p0);
+                };
+                if (distributed()) {   // the pass reads r and p (and Ap) of iteration i-1 in the halo rows
                     std::vector<HaloPlane> pl;
                     add_vec_planes(pl, rb[(i - 1) & 1]);
-                    add_vec_planes(pl, ab[(i - 1) & 1]);
-                    add_vec_planes(pl, pbuf(i - 1));
-                    if (split) {   // beside the interior row blocks
+                    if (!apfree) add_vec_planes(pl, ab[(i - 1) & 1]);
+                    if (!(p0 && i == 1)) add_vec_planes(pl, pbuf(i - 1));   // P0: pass 1 forms p_0 from r_0
+                    if (fused && i == 1) {   // iw_jtf_apply's exchange carried r_0 (and p_0, Ap_0)
+                        pass(0);
+                    } else if (split) {   // beside the interior row blocks
                         halo_mark();
-                        launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 1, p0);
-                        halo_begin(comm_, pl, dom_, 1);
+                        pass(1);
+                        halo_begin(comm_, pl, dom_, halo());
                         halo_join();
-                        launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 2, p0);
+                        pass(2);
                     } else {
                         exchange(pl);
-                        launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 0, p0);
+                        pass(0);
                     }
                 } else if (apfree) {
                     launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0);
@@ -2331,6 +2353,7 @@ private:
         iw::Args<T> a = args();
         a.nstrips = fused_strips();
         const int nb = fused_blocks();
+        a.tb0 = 0; a.tn0 = nb; a.tb1 = 0;   // every tile (geom_fused)
         if (jtf_nt_)
             launch_timed("iw_jtf_apply", iw::iw_jtf_apply<T, 2>, nb, a, r_, pre_, pout, no_ap ? nullptr : Ap_,
                          red_.slot(nb, rz(0)));
@@ -2340,18 +2363,30 @@ private:
     }
     // PCG iteration i >= 1 without a stored Ap (iw_pcg): reads r_{i-1} and p_{i-1}, writes
     // r_i (unless last) and p_i; the deferred delta and P0 exactly as launch_apply_res
-    void launch_pcg(int i, const T* pin, T* pout, bool last, const T* pin2, bool p0) {
+    // part 0: every row block; 1: the interior row blocks [1, nrb - 1); 2: the first and last
+    // (the only ones that read halo rows: a wave reads rows y0 - 2 .. y1 + 1)
+    void launch_pcg(int i, const T* pin, T* pout, bool last, const T* pin2, bool p0, int part = 0) {
         T* rb[2] = {r_, r1_};
         const T* rin = rb[(i - 1) & 1];
         T* rout = last ? nullptr : rb[i & 1];
         const double base_scale = (i == 1 && !spec_.use_preconditioner) ? 4.0 : 1.0;
         iw::Args<T> a = args();
-        a.nstrips = fused_strips();
-        const int nb = fused_blocks();
+        const int fs = fused_strips();
+        a.nstrips = fs;
+        const int nb = fused_blocks();   // the reduction slot spans every tile
+        a.tb0 = 0; a.tn0 = nb; a.tb1 = 0;
+        int grid = nb;
+        if (part == 1) {
+            a.tb0 = fs; a.tn0 = fs * (nrowblocks_ - 2);
+            grid = a.tn0;
+        } else if (part == 2) {
+            a.tb0 = 0; a.tn0 = fs; a.tb1 = fs * (nrowblocks_ - 1);
+            grid = 2 * fs;
+        }
         const ReduceSlot rs = red_.slot(nb, rz(i));
         auto go = [&](auto kern) {
-            launch_timed("iw_pcg", kern, nb, a, pin, rin, (const T*)pre_, pout, rout, delta_, red_.scalars, rz(i - 1),
-                         base_scale, rs, pin2);
+            launch_timed("iw_pcg", kern, grid, a, pin, rin, (const T*)pre_, pout, rout, delta_, red_.scalars,
+                         rz(i - 1), base_scale, rs, pin2);
         };
         auto pick = [&](auto nt, auto u2, auto pf2) {
             constexpr bool SNT = decltype(nt)::value, U2 = decltype(u2)::value, PF2 = decltype(pf2)::value;

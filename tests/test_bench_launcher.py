@@ -22,9 +22,9 @@ def run(args, env_extra=None, drop=("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_
     return subprocess.run([sys.executable, BENCH] + args, env=env, capture_output=True, text=True, timeout=120)
 
 
-@pytest.mark.parametrize("n,workload,halo", [(2, "image_warping", 1), (4, "image_warping", 1),
-                                             (8, "image_warping", 1), (8, "shape_from_shading", 2),
-                                             (3, "image_warping", 1)])
+@pytest.mark.parametrize("n,workload,halo", [(2, "image_warping", 2), (4, "image_warping", 2),
+                                             (8, "image_warping", 2), (8, "shape_from_shading", 2),
+                                             (3, "image_warping", 2)])
 def test_spawns_n_ranks_with_slabs(n, workload, halo):
     p = run(["--gpus", str(n), "--dry-run", "--workload", workload])
     assert p.returncode == 0, p.stderr

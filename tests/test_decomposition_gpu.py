@@ -25,9 +25,9 @@ def run_decomposed(w, world, nit, lit):
     errors = []
     solvers, params, slabs = [], [], []
     for r in range(world):
-        s = dd.slab(H, r, world, 1)
         sv = solver(W, H)
-        assert sv.halo() == 1
+        assert sv.halo() == 2   # iw_jtf_apply / iw_pcg reach two rows (the stencil itself one)
+        s = dd.slab(H, r, world, sv.halo())
         sv.set_decomposition(lib.OptAMD_LocalGroupRank(group, r), s.y_lo, s.y_hi)
         sv.set_solver_params({"nIterations": nit, "lIterations": lit})
         solvers.append(sv)

@@ -12,6 +12,8 @@
 //   edge64    aligned 64-column strips (rows y0-2 .. y1+1) plus, per row and array, one more
 //             load with lanes 0..3 active for the columns x0-2, x0-1, x0+64, x0+65
 //   pair124   two pixels per lane: 124-column strips, x = 124 s - 2 + 2 lane (+0 / +1)
+//   shiftK    strip64 with every window shifted by K columns (x = 64 s + K + lane): the cost of
+//             a window's byte alignment alone (K = 2: 8 B, 8: 32 B, 16: 64 B, 32: 128 B)
 // Not part of the library.  hipcc --offload-arch=gfx950 -O3 -o tools/pcgbench tools/pcgbench.hip
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -149,6 +151,32 @@ __global__ __launch_bounds__(256) void pair124(Arr A, int W, int H, int rows, in
     }
 }
 
+template <int K>
+__global__ __launch_bounds__(256) void shifted(Arr A, int W, int H, int rows, int nstrips) {
+    const int t = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int strip = t % nstrips, y0 = ((t / nstrips) * 4 + w) * rows;
+    const int x = strip * 64 + K + lane;
+    const bool out = x < W;
+    const int xc = x >= W ? W - 1 : x;
+    const int y1 = min(y0 + rows, H);
+    if (y0 >= y1) return;
+    auto idx = [&](int y) { const int yc = y < 0 ? 0 : (y >= H ? H - 1 : y); return (long long)yc * W + xc; };
+    float acc = 0.f;
+    Row q = ld(A, idx(y0 - 1));
+    for (int y = y0 - 1; y < y1 + 1; ++y) {
+        const Row c = q;
+        q = ld(A, idx(min(y + 1, y1)));
+        const float v = mix(c);
+        acc += v;
+        const int ys = y - 1;
+        if (out && ys >= y0 && ys < y1) {
+            const long long i = idx(ys);
+            A.oxy[i] = make_float2(v, acc); A.ot[i] = v * 2.f;
+            A.qxy[i] = make_float2(acc, v); A.qt[i] = acc;
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void flat(Arr A, long long n) {
     for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
         const Row c = ld(A, i);
@@ -204,6 +232,14 @@ int main() {
         snprintf(nm, 64, "edge64 rows=%d", rows); rep(nm, timeit(edge64, n64 * rb, A, W, H, rows, n64));
         const int n124 = (W + 123) / 124;
         snprintf(nm, 64, "pair124 rows=%d", rows); rep(nm, timeit(pair124, n124 * rb, A, W, H, rows, n124));
+    }
+    {
+        const int rows = 32, n64 = W / 64, rb = (H + 4 * rows - 1) / (4 * rows);
+        rep("shift0 rows=32", timeit(shifted<0>, n64 * rb, A, W, H, rows, n64));
+        rep("shift2 rows=32", timeit(shifted<2>, n64 * rb, A, W, H, rows, n64));
+        rep("shift8 rows=32", timeit(shifted<8>, n64 * rb, A, W, H, rows, n64));
+        rep("shift16 rows=32", timeit(shifted<16>, n64 * rb, A, W, H, rows, n64));
+        rep("shift32 rows=32", timeit(shifted<32>, n64 * rb, A, W, H, rows, n64));
     }
     for (int g : {1024, 2048, 8192}) {
         char nm[64];
