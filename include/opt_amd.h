@@ -109,6 +109,11 @@ int OptAMD_CommRank(OptAMD_Comm* comm);
 /* The transport behind a communicator, "rccl" or "local", copied into buf (at most
  * buflen bytes incl. the terminator); returns its length, -1 for NULL. */
 int OptAMD_CommKind(OptAMD_Comm* comm, char* buf, int buflen);
+/* The error that stopped the last Init / Step of this plan (a problem found only when
+ * the arrays were bound, e.g. an arap graph whose adjacency exceeds 2^31 slots), copied
+ * into buf; returns its length, 0 when there was none (-1 for NULL). After such an
+ * error Opt_ProblemStep returns 0 and Opt_ProblemCurrentCost NaN; the process goes on. */
+int OptAMD_PlanError(Opt_Plan* plan, char* buf, int buflen);
 /* All ranks as threads of one process (shared device or peer devices): for testing
  * the decomposition on one GPU. The rank handles belong to the group. */
 OptAMD_LocalGroup* OptAMD_LocalGroupCreate(int nranks);

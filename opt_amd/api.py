@@ -73,6 +73,7 @@ _SIGNATURES = [
     ("OptAMD_CommSize", ctypes.c_int, [_VP]),
     ("OptAMD_CommRank", ctypes.c_int, [_VP]),
     ("OptAMD_CommKind", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int]),
+    ("OptAMD_PlanError", ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_int]),
     ("OptAMD_LocalGroupCreate", _VP, [ctypes.c_int]),
     ("OptAMD_LocalGroupRank", _VP, [_VP, ctypes.c_int]),
     ("OptAMD_LocalGroupDestroy", None, [_VP]),
@@ -220,11 +221,20 @@ class OptSolver:
     def init(self, problem_params: Sequence):
         self._pk = ParamPack(problem_params)
         self.lib.Opt_ProblemInit(self.state, self.plan, self._pk.ptr)
+        self._raise_plan_error()
 
     def step(self, problem_params: Optional[Sequence] = None) -> int:
         if problem_params is not None:
             self._pk = ParamPack(problem_params)
-        return self.lib.Opt_ProblemStep(self.state, self.plan, self._pk.ptr)
+        r = self.lib.Opt_ProblemStep(self.state, self.plan, self._pk.ptr)
+        self._raise_plan_error()
+        return r
+
+    def _raise_plan_error(self):
+        """OptAMD_PlanError: a problem the plan met when the arrays were bound."""
+        buf = ctypes.create_string_buffer(512)
+        if self.lib.OptAMD_PlanError(self.plan, buf, 512) > 0:
+            raise OptError(buf.value.decode())
 
     def profiled_solve(self, problem_params: Sequence) -> List[float]:
         """launchProfiledSolve (OptUtils.h:47-64): cost after Init and after each Step."""

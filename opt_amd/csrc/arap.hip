@@ -824,8 +824,8 @@ private:
         OPT_HIP_CHECK(hipStreamSynchronize(s));
         const long long total = 64LL * h[ns];
         if (total >= (1LL << 31)) {
-            fprintf(stderr, "[opt_amd] arap_mesh_deformation: adjacency too large (%lld ELL slots)\n", total);
-            exit(1);
+            throw PlanError("arap_mesh_deformation: adjacency too large (" + std::to_string(total) +
+                            " ELL slots, the limit is 2^31)");
         }
         for (auto& x : h) x *= 64;
         OPT_HIP_CHECK(hipMemcpyAsync(g.eoff, h.data(), sizeof(int) * (ns + 1), hipMemcpyHostToDevice, s));
@@ -857,8 +857,8 @@ private:
         OPT_HIP_CHECK(hipStreamSynchronize(s));
         const long long total = 64LL * h[ns];
         if (total >= (1LL << 31)) {
-            fprintf(stderr, "[opt_amd] arap_mesh_deformation: adjacency too large (%lld merged slots)\n", total);
-            exit(1);
+            throw PlanError("arap_mesh_deformation: adjacency too large (" + std::to_string(total) +
+                            " merged slots, the limit is 2^31)");
         }
         for (auto& x : h) x *= 64;
         OPT_HIP_CHECK(hipMemcpyAsync(nb_.eoff, h.data(), sizeof(int) * (ns + 1), hipMemcpyHostToDevice, s));

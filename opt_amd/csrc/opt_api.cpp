@@ -3,6 +3,7 @@
 // API/src/o.t:3301-3352) plus the opt_amd.h extension entry points.
 #include <algorithm>
 #include <cstdio>
+#include <cmath>
 #include <cstring>
 #include <fstream>
 #include <memory>
@@ -27,6 +28,7 @@ struct Opt_Problem {
 };
 struct Opt_Plan {
     std::unique_ptr<optamd::Plan> impl;
+    std::string error;   // set when Init / Step met an optamd::PlanError; the solve stops
 };
 
 namespace {
@@ -161,14 +163,30 @@ void Opt_SetSolverParameter(Opt_State* state, Opt_Plan* plan, const char* name, 
     plan->impl->set_solver_param(name, value);
 }
 
+// A PlanError (a problem the plan cannot run, found when the arrays are bound) stops the
+// solve, not the process: Init returns, every later Step returns 0 (the reference's "no
+// more steps"), Opt_ProblemCurrentCost returns NaN and OptAMD_PlanError the message.
 void Opt_ProblemInit(Opt_State* state, Opt_Plan* plan, void** problemparams) {
     if (!valid_state(state, "Opt_ProblemInit") || !valid_plan(plan, "Opt_ProblemInit")) exit(1);
-    plan->impl->init(problemparams);
+    plan->error.clear();
+    try {
+        plan->impl->init(problemparams);
+    } catch (const optamd::PlanError& e) {
+        plan->error = e.what();
+        fprintf(stderr, "[opt_amd] Opt_ProblemInit: %s\n", e.what());
+    }
 }
 
 int Opt_ProblemStep(Opt_State* state, Opt_Plan* plan, void** problemparams) {
     if (!valid_state(state, "Opt_ProblemStep") || !valid_plan(plan, "Opt_ProblemStep")) exit(1);
-    return plan->impl->step(problemparams);
+    if (!plan->error.empty()) return 0;
+    try {
+        return plan->impl->step(problemparams);
+    } catch (const optamd::PlanError& e) {
+        plan->error = e.what();
+        fprintf(stderr, "[opt_amd] Opt_ProblemStep: %s\n", e.what());
+        return 0;
+    }
 }
 
 void Opt_ProblemSolve(Opt_State* state, Opt_Plan* plan, void** problemparams) {
@@ -180,6 +198,7 @@ void Opt_ProblemSolve(Opt_State* state, Opt_Plan* plan, void** problemparams) {
 double Opt_ProblemCurrentCost(Opt_State* state, Opt_Plan* plan) {
     if (!valid_state(state, "Opt_ProblemCurrentCost") || !valid_plan(plan, "Opt_ProblemCurrentCost"))
         return 0.0;
+    if (!plan->error.empty()) return std::nan("");
     return plan->impl->cost();
 }
 
@@ -292,6 +311,9 @@ void OptAMD_CommDestroy(OptAMD_Comm* comm) {
 }
 int OptAMD_CommSize(OptAMD_Comm* comm) { return comm ? comm->impl->size() : -1; }
 int OptAMD_CommRank(OptAMD_Comm* comm) { return comm ? comm->impl->rank() : -1; }
+int OptAMD_PlanError(Opt_Plan* plan, char* buf, int n) {
+    return valid_plan(plan, "OptAMD_PlanError") ? copy_name(plan->error, buf, n) : -1;
+}
 int OptAMD_CommKind(OptAMD_Comm* comm, char* buf, int n) { return comm ? copy_name(comm->impl->kind(), buf, n) : -1; }
 OptAMD_LocalGroup* OptAMD_LocalGroupCreate(int nranks) {
     if (nranks < 1) return nullptr;

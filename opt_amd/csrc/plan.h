@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <map>
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <vector>
 #include "comm.h"
@@ -11,6 +12,15 @@
 #include "problem.h"
 
 namespace optamd {
+
+// A problem the plan cannot run, found when the arrays are bound (Init / Step) rather
+// than at Opt_ProblemPlan (e.g. an arap graph whose adjacency exceeds the 32-bit index
+// range): thrown by the plan, caught at the C ABI (opt_api.cpp), which reports it on
+// stderr and through OptAMD_PlanError and stops the solve instead of the process.
+struct PlanError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
 
 // Runtime solver parameters with the reference defaults
 // (API/src/solverGPUGaussNewton.t:41-55, struct SolverParameters :186-201).

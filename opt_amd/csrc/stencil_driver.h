@@ -203,14 +203,17 @@ __global__ __launch_bounds__(kBlock) void step2_kernel(long long n, const T* __r
 // PCGStep3 (:814-845): beta = sc[i_num]/sc[i_den]; p = z + beta p.
 // DM (GN, PCGStep2's delta update moved here, where p_old is read anyway; same
 // expression): 1 delta = alpha p_old, 2 delta += alpha p_old, alpha = sc[ia_num]/sc[ia_den].
-template <typename T, int DM = 0>
+// GUARD (the fused loop's residual-reset iterations): beta = 0 unless both rz
+// are positive, as step23_kernel — bitwise the plain division wherever that is finite and
+// positive; the classic loop keeps the reference's unguarded division (:842).
+template <typename T, int DM = 0, bool GUARD = false>
 __global__ __launch_bounds__(kBlock) void step3_kernel(long long n, const T* __restrict__ pre,
                                                        const T* __restrict__ r, T* __restrict__ p,
                                                        const double* __restrict__ sc, int i_num, int i_den,
                                                        int use_pre, const int* stop, T* __restrict__ delta = nullptr,
                                                        int ia_num = 0, int ia_den = 0) {
     if (stopped(stop)) return;
-    const T beta = (T)(sc[i_num] / sc[i_den]);
+    const T beta = (!GUARD || (sc[i_num] > 0.0 && sc[i_den] > 0.0)) ? (T)(sc[i_num] / sc[i_den]) : (T)0;
     const T alpha = DM ? (T)(sc[ia_num] / sc[ia_den]) : (T)0;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x) {
@@ -271,12 +274,13 @@ __global__ __launch_bounds__(kBlock) void step23_kernel(long long n, T* __restri
 }
 
 // Residual reset, LM only (:738-801): first half delta += alpha p ...
-template <typename T>
+// GUARD: alpha = 0 unless p.Ap is positive (step23_kernel's zero step far past convergence)
+template <typename T, bool GUARD = false>
 __global__ __launch_bounds__(kBlock) void half1_kernel(long long n, const T* __restrict__ p,
                                                        T* __restrict__ delta, const double* __restrict__ sc,
                                                        int i_num, int i_den, const int* stop) {
     if (stopped(stop)) return;
-    const T alpha = (T)(sc[i_num] / sc[i_den]);
+    const T alpha = (!GUARD || sc[i_den] > 0.0) ? (T)(sc[i_num] / sc[i_den]) : (T)0;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
          e += (long long)gridDim.x * blockDim.x)
         delta[e] = delta[e] + alpha * p[e];

@@ -353,9 +353,9 @@ public:
             }
             allreduce(pap(i), 1);
             const bool reset = lm_ && ((i + 1) % std::max(1, sp_.residual_reset_period)) == 0;
-            if (reset) {
-                hipLaunchKernelGGL((half1_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)p_, delta_,
-                                   red_.scalars, rz(i), pap(i), stop);
+            if (reset) {   // the classic halves, with step23's guards (a zero step / beta = 0)
+                hipLaunchKernelGGL((half1_kernel<T, true>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)p_,
+                                   delta_, red_.scalars, rz(i), pap(i), stop);
                 exchange_vec(delta_);
                 op_->apply(delta_, Adelta_, CtC_, stop, red_.slot(nb(), kScTmp), stream_);
                 hipLaunchKernelGGL((half2_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)Adelta_,
@@ -442,8 +442,8 @@ public:
                                    red_.slot(fg(), rz(i + 1)), z);
                 allreduce(rz(i + 1), 2);
                 tbegin("step3");
-                hipLaunchKernelGGL((step3_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)pre_,
-                                   (const T*)r_, p_, red_.scalars, rz(i + 1), rz(i), use_pre, stop);
+                hipLaunchKernelGGL((step3_kernel<T, 0, true>), dim3(fg()), dim3(kBlock), 0, stream_, n_,
+                                   (const T*)pre_, (const T*)r_, p_, red_.scalars, rz(i + 1), rz(i), use_pre, stop);
                 tend();
                 if (!z.on)
                     hipLaunchKernelGGL((zeta_kernel<T>), dim3(1), dim3(1), 0, stream_, red_.scalars, q(i + 1),

@@ -331,3 +331,36 @@ def test_merged_batch_size_is_bitwise(monkeypatch, double):
         s.close()
     assert out["2"][0] == out["3"][0]
     assert np.array_equal(out["2"][1], out["3"][1]) and np.array_equal(out["2"][2], out["3"][2])
+
+
+def test_adjacency_over_the_index_range_is_an_error_not_an_exit():
+    """a mesh whose sliced-ELL adjacency needs >= 2^31 slots (here 34,000 64-vertex
+    slices, each holding one vertex with 1,100 out-edges: 64 x 34,000 x 1,100 = 2.39e9 slots)
+    is refused when the edges are bound — through the plan's error path (optamd::PlanError:
+    Init stops, Step returns 0, OptAMD_PlanError holds the message, the wrapper raises) —
+    and the process goes on: a normal solve runs afterwards in the same process."""
+    from opt_amd.api import OptError
+
+    ns, deg = 34000, 1100
+    N, E = 64 * ns, ns * deg
+    rng = np.random.default_rng(5)
+    P = rng.uniform(0, 1, 3 * N).astype(np.float32)
+    C = np.full(3 * N, -np.inf, np.float32)
+    v0 = np.repeat(np.arange(ns, dtype=np.int32) * 64, deg)
+    v1 = rng.integers(0, N, E, dtype=np.int32)
+    w = {"Offset": P, "Angle": np.zeros(3 * N, np.float32), "UrShape": P, "Constraints": C, "v0": v0, "v1": v1,
+         "N": N, "E": E, "w_fitSqrt": 2.0, "w_regSqrt": 1.0}
+    s = solver(w)
+    s.set_solver_params({"nIterations": 1, "lIterations": 1})
+    with pytest.raises(OptError, match="adjacency too large"):
+        s.init(params(w))
+    assert np.isnan(s.cost())
+    with pytest.raises(OptError, match="adjacency too large"):   # Step returns 0; the wrapper raises
+        s.step()
+    s.close()
+    del w, v0, v1, P, C
+    w2 = perturbed(7, 5, seed=3)
+    s2 = solver(w2)
+    s2.set_solver_params({"nIterations": 2, "lIterations": 10})
+    c = s2.profiled_solve(params(w2))
+    assert np.isfinite(c).all() and c[-1] < c[0]

@@ -336,3 +336,28 @@ def test_fused_pcg_step_matches_classic(monkeypatch, kind, double, W, H, lit):
         if rz == 0:
             continue
         assert abs(rz_id - rz) <= (1e-12 if double else 1e-7) * abs(rz) + 1e-300, (i, rz, rz_id)
+
+
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_lm_far_past_convergence_with_residual_resets_stays_finite(monkeypatch, fuse):
+    """the fused LM loop (step23_kernel: a zero step where p.Ap <= 0, beta = 0
+    where the identity's rz <= 0) runs the classic halves on its residual-reset iterations
+    (every residual_reset_period = 10, solverGPUGaussNewton.t:738-801); those now carry the
+    same guards (half1_kernel / step3_kernel GUARD). A 7 x 5 image (35 unknowns) with
+    lIterations = 120 and the zeta exit disabled (q_tolerance = 0) takes every PCG iteration
+    far past convergence, through 12 resets per LM step: the energies and depths stay finite
+    and the LM energy never increases (a rejected step is reverted). Both the fused loop
+    (OPT_AMD_FUSE23=1) and the classic one (0) are run; the classic loop divides as the
+    reference does, so only its finiteness where the reference's is finite is asserted."""
+    monkeypatch.setenv("OPT_AMD_FUSE23", fuse)
+    W, H = 7, 5
+    w = synthetic(W, H, seed=4)
+    s = OptSolver([W, H], ENERGY, "LMGPU")
+    prm = params(w)
+    s.set_solver_params({"nIterations": 4, "lIterations": 120, "q_tolerance": 0.0})
+    costs = np.array(s.profiled_solve(prm))
+    X = to_np(prm[16])
+    print(f"FUSE23={fuse}: energies {costs}")
+    if fuse == "1":
+        assert np.all(np.isfinite(costs)) and np.all(np.isfinite(X[w["D_i"] > 0]))
+        assert np.all(np.diff(costs) <= 0) and costs[-1] <= costs[0]
