@@ -651,3 +651,25 @@ def test_pcg_pass_without_stored_ap_fp64(monkeypatch, W, H):
     assert rel_err(out[1][1], out[0][1]) < 1e-9
     _, _, c_ref, _ = oracle.iw_solve(w, 3, 10, double=True)
     np.testing.assert_allclose(out[1][0], c_ref, rtol=1e-8)
+
+
+@pytest.mark.parametrize("W,H,lit", [(150, 110, 10), (5, 3, 4), (200, 1, 3), (700, 300, 10), (64, 64, 2),
+                                     (61, 2, 5), (1, 9, 4), (121, 66, 1), (240, 97, 7)])
+@pytest.mark.parametrize("double", [False, True])
+def test_dup_layout_is_bitwise_the_image_layout(monkeypatch, W, H, lit, double):
+    """OPT_AMD_IW_DUP=1 (default 0): the fused loop's solver vectors in the DUP layout (each
+    60-column strip an aligned 64-slot block with its halo columns duplicated, UrShape and
+    the angle's cos / sin copied per Step by iw_jtf_apply) against the image layout: the
+    same per-pixel arithmetic, the same tiles and sums — the trajectory (energies, Offset,
+    Angle, PCG scalars) is bitwise the same, fp32 and fp64."""
+    out = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("OPT_AMD_IW_DUP", v)
+        w = perturbed(W, H, seed=7 * W + H)
+        s = solver(W, H, double=double)
+        prm = device_params(w, double=double)
+        s.set_solver_params({"nIterations": 3, "lIterations": lit})
+        c = np.array(s.profiled_solve(prm))
+        out.append((c, to_np(prm[0]), to_np(prm[1]), np.array(s.scalars(2 + 5 * (lit + 2)))))
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)

@@ -9,6 +9,13 @@
 //   pad60     strip60 with every array in a strip-padded layout (a row = nstrips x 64 slots,
 //             column x at slot 64 (x / 60) + x % 60): a wave's 60 outputs start 256-B aligned
 //   pad60u    pad60 for the solver's own vectors, UrShape and the angle in the image layout
+//   pad60f    pad60 with every lane storing: lanes 0, 1, 62, 63 fill the block's unused slots
+//             60..63 (junk no one reads), so each store covers whole 128-B lines
+//   pad60fu   pad60f, UrShape and the angle in the image layout
+//   aos60     strip60 with records: (u.x, u.y, angle, pre) as one 16-B record, (r, p) as one
+//             24-B record read and another written (fewer, wider arrays: fewer partial lines
+//             per byte at the strip edges); flags u8
+//   aos60p    aos60 with the (r, p) record padded to 32 B (dwordx4 twice; 73 B/px moved)
 //   edge64    aligned 64-column strips (rows y0-2 .. y1+1) plus, per row and array, one more
 //             load with lanes 0..3 active for the columns x0-2, x0-1, x0+64, x0+65
 //   pair124   two pixels per lane: 124-column strips, x = 124 s - 2 + 2 lane (+0 / +1)
@@ -40,7 +47,7 @@ __device__ __forceinline__ float mix(const Row& q) {
     return q.u.x + q.u.y + q.a + q.r.x + q.r.y + q.rt + q.w + q.p.x + q.p.y + q.pt + (float)q.f;
 }
 
-template <int MODE, int PF>   // MODE 0 strip60, 1 strip64, 2 side64, 3 pad60, 4 pad60u; PF rows in flight
+template <int MODE, int PF>   // MODE 0 strip60, 1 strip64, 2 side64, 3 pad60, 4 pad60u, 5 pad60f, 6 pad60fu; PF rows in flight
 __global__ __launch_bounds__(256) void walk(Arr A, int W, int H, int rows, int nstrips) {
     const int t = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int strip, y0;
@@ -67,7 +74,7 @@ __global__ __launch_bounds__(256) void walk(Arr A, int W, int H, int rows, int n
     };
     auto idu = [&](int y) {
         const int yc = y < 0 ? 0 : (y >= H ? H - 1 : y);
-        return MODE == 3 ? (long long)yc * pw + xs : (long long)yc * W + xc;
+        return (MODE == 3 || MODE == 5) ? (long long)yc * pw + xs : (long long)yc * W + xc;
     };
     Row q[PF];
 #pragma unroll
@@ -81,10 +88,60 @@ __global__ __launch_bounds__(256) void walk(Arr A, int W, int H, int rows, int n
         const float v = mix(c);
         acc += v;
         const int ys = y - (lo - 1) - 1;   // the row stored this trip (one behind the loads)
-        if (out && ys >= y0 && ys < y1) {
+        if (MODE >= 5) {   // full-line stores: every lane, a bijection lane -> slot
+            if (ys >= y0 && ys < y1) {
+                const int sl = (lane >= 2 && lane < 62) ? lane - 2 : (lane < 2 ? 60 + lane : lane);
+                const long long i = (long long)ys * pw + 64 * strip + sl;
+                A.oxy[i] = make_float2(v, acc); A.ot[i] = v * 2.f;
+                A.qxy[i] = make_float2(acc, v); A.qt[i] = acc;
+            }
+        } else if (out && ys >= y0 && ys < y1) {
             const long long i = idx(ys);
             A.oxy[i] = make_float2(v, acc); A.ot[i] = v * 2.f;
             A.qxy[i] = make_float2(acc, v); A.qt[i] = acc;
+        }
+    }
+}
+
+template <int PAD>
+__global__ __launch_bounds__(256) void aos60(const uint8_t* F, const float4* SA, const float* RP, float* RPo, int W,
+                                             int H, int rows, int nstrips) {
+    const int t = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int strip = t % nstrips, y0 = ((t / nstrips) * 4 + w) * rows;
+    const int x = strip * 60 - 2 + lane;
+    const bool out = lane >= 2 && lane < 62 && x < W;
+    const int xc = x < 0 ? 0 : (x >= W ? W - 1 : x);
+    const int y1 = min(y0 + rows, H);
+    if (y0 >= y1) return;
+    constexpr int RS = PAD ? 8 : 6;   // floats per (r, p) record
+    auto idx = [&](int y) { const int yc = y < 0 ? 0 : (y >= H ? H - 1 : y); return (long long)yc * W + xc; };
+    struct Q { float4 sa; float2 a, b, c; float4 d, e; int f; };
+    auto ld = [&](long long i) {
+        Q q;
+        q.f = F[i]; q.sa = SA[i];
+        if (PAD) { q.d = *(const float4*)(RP + RS * i); q.e = *(const float4*)(RP + RS * i + 4); }
+        else { q.a = *(const float2*)(RP + RS * i); q.b = *(const float2*)(RP + RS * i + 2); q.c = *(const float2*)(RP + RS * i + 4); }
+        return q;
+    };
+    float acc = 0.f;
+    Q q = ld(idx(y0 - 2));
+    for (int y = y0 - 2; y < y1 + 2; ++y) {
+        const Q c = q;
+        q = ld(idx(min(y + 1, y1 + 1)));
+        const float v = PAD ? c.sa.x + c.sa.y + c.sa.z + c.sa.w + c.d.x + c.d.y + c.d.z + c.e.x + c.e.y + c.e.z + (float)c.f
+                            : c.sa.x + c.sa.y + c.sa.z + c.sa.w + c.a.x + c.a.y + c.b.x + c.b.y + c.c.x + c.c.y + (float)c.f;
+        acc += v;
+        const int ys = y - 2;
+        if (out && ys >= y0 && ys < y1) {
+            const long long i = idx(ys);
+            if (PAD) {
+                *(float4*)(RPo + RS * i) = make_float4(v, acc, v, 0.f);
+                *(float4*)(RPo + RS * i + 4) = make_float4(acc, v, acc, 0.f);
+            } else {
+                *(float2*)(RPo + RS * i) = make_float2(v, acc);
+                *(float2*)(RPo + RS * i + 2) = make_float2(v, acc);
+                *(float2*)(RPo + RS * i + 4) = make_float2(v, acc);
+            }
         }
     }
 }
@@ -209,9 +266,9 @@ int main() {
     const long long NP = (long long)((W + 59) / 60) * 64 * H;   // padded layout
     CK(hipMalloc(&p, NP)); CK(hipMemset(p, 1, NP)); A.f = (const uint8_t*)p;
     size_t f2 = 8 * NP, f1 = 4 * NP;
-    void* bufs[11];
-    size_t sz[11] = {f2, f1, f2, f1, f1, f2, f1, f2, f1, f2, f1};
-    for (int k = 0; k < 11; ++k) { CK(hipMalloc(&bufs[k], sz[k])); CK(hipMemset(bufs[k], 0, sz[k])); }
+    void* bufs[12];
+    size_t sz[12] = {4 * f2, f1, 4 * f2, f1, f1, f2, f1, 4 * f2, f1, f2, f1, 2 * f2};
+    for (int k = 0; k < 12; ++k) { CK(hipMalloc(&bufs[k], sz[k])); CK(hipMemset(bufs[k], 0, sz[k])); }
     A.u = (const float2*)bufs[0]; A.ang = (const float*)bufs[1]; A.rxy = (const float2*)bufs[2];
     A.rt = (const float*)bufs[3]; A.pre = (const float*)bufs[4]; A.pxy = (const float2*)bufs[5];
     A.pt = (const float*)bufs[6]; A.oxy = (float2*)bufs[7]; A.ot = (float*)bufs[8]; A.qxy = (float2*)bufs[9];
@@ -229,7 +286,18 @@ int main() {
         snprintf(nm, 64, "side64 rows=%d pf2", rows); rep(nm, timeit(walk<2, 2>, (n64 / 4) * (H / rows), A, W, H, rows, n64));
         snprintf(nm, 64, "pad60 rows=%d pf1", rows); rep(nm, timeit(walk<3, 1>, n60 * rb, A, W, H, rows, n60));
         snprintf(nm, 64, "pad60u rows=%d pf1", rows); rep(nm, timeit(walk<4, 1>, n60 * rb, A, W, H, rows, n60));
+        snprintf(nm, 64, "pad60f rows=%d pf1", rows); rep(nm, timeit(walk<5, 1>, n60 * rb, A, W, H, rows, n60));
+        snprintf(nm, 64, "pad60f rows=%d pf2", rows); rep(nm, timeit(walk<5, 2>, n60 * rb, A, W, H, rows, n60));
+        snprintf(nm, 64, "pad60fu rows=%d pf1", rows); rep(nm, timeit(walk<6, 1>, n60 * rb, A, W, H, rows, n60));
         snprintf(nm, 64, "edge64 rows=%d", rows); rep(nm, timeit(edge64, n64 * rb, A, W, H, rows, n64));
+        {
+            const float* rp = (const float*)bufs[2];   // 8 NP floats each: room for 32-B records
+            float* rpo = (float*)bufs[7];
+            snprintf(nm, 64, "aos60 rows=%d", rows);
+            rep(nm, timeit(aos60<0>, n60 * rb, A.f, (const float4*)bufs[11], rp, rpo, W, H, rows, n60));
+            snprintf(nm, 64, "aos60p rows=%d", rows);
+            rep(nm, timeit(aos60<1>, n60 * rb, A.f, (const float4*)bufs[11], rp, rpo, W, H, rows, n60));
+        }
         const int n124 = (W + 123) / 124;
         snprintf(nm, 64, "pair124 rows=%d", rows); rep(nm, timeit(pair124, n124 * rb, A, W, H, rows, n124));
     }
