@@ -43,8 +43,8 @@ namespace optamd {
 namespace iw {
 // Contraction inside one expression only (a * b + c as written): with the default
 // cross-statement fusion the backend's choice of which product joins an fma depended on
-// the surrounding code, so two instantiations of the same arithmetic (the DUP and image
-// layouts) rounded a few pixels differently
+// the surrounding code, so two instantiations of the same arithmetic (round 5's trial of
+// a strip-blocked layout against the image layout) rounded a few pixels differently
 #pragma clang fp contract(on)
 
 constexpr int kStrip = 64;   // columns per wavefront strip (aligned: x = 64*strip + lane)
@@ -82,18 +82,16 @@ struct Args {
     // side != 0 (geom): the block's four waves walk the SAME rows over four adjacent strips
     // (tile = row chunk x group of 4 strips) instead of four stacked row ranges of one strip
     int side;
-    // DUP layout (round 5; iw_jtf_apply / iw_pcg / iw_update with DUP): every solver vector
-    // and a per-Step copy of UrShape and of the angle's (cos, sin) is held per 60-column
-    // strip of iw_pcg's geometry in an ALIGNED block of 64 slots — slot l of strip s is
-    // column 60 s - 2 + l, so the strip's two halo columns on each side are duplicated in
-    // the neighbouring blocks — and a wave's 64 lanes load exactly its block: one aligned
-    // segment per array and row (the image layout's windows start 8 bytes before a line
-    // and touch one more cache line per load; measured 1.3x the aligned pattern's time,
-    // tools/pcgbench.hip). pitch = 64 x strips slots per row, ndup = pitch x memory rows.
-    int pitch;
-    long long ndup;
-    float* Ud;   // UrShape (2 per slot)
-    T* CSd;      // cos, sin of the angle (2 per slot)
+    // REC layout (round 5; the fused loop's iw_jtf_apply / iw_pcg / iw_update with REC): the
+    // PCG vectors of iteration i as ONE record per pixel, [r.x r.y | p.x p.y | r.t p.t]
+    // (6 T: three aligned pairs), and the per-Step static data as the record
+    // S = [u.x u.y angle pre_t] (4 T), both in the image's pixel order. A wave's row is then
+    // read from 3 wide arrays (flags, S, the record) instead of 8 narrow ones, and each row
+    // segment of a 60-column strip shares a cache line with its neighbours only at its two
+    // ends: the same bytes measured 253 against 299 us in a load/store-only walk
+    // (tools/pcgbench.hip, aos60 vs strip60). The delta stays in the unknown layout (own
+    // pixels only). Off by default: the solver's passes did not gain (ImageWarpingPlan::rec_on_).
+    T* S;
     // Jacobi preconditioner of the two Offset channels: diag(J^T J) there is
     // 2 wr^2 (#valid edges) + wf^2 [fit], so pre = 1/(1+sqrt(diag))^2 takes one of ten
     // values (host-computed once per step; 0.25 everywhere for UsePreconditioner(false)).
@@ -160,7 +158,6 @@ __device__ __forceinline__ T opaque(T v) {
 struct WaveGeom {
     int x, ex, lane, y0, y1, tile;
     bool out_lane, edge_lane;
-    int strip;   // geom_fused: the 60-column strip (the DUP block)
 };
 template <typename T>
 __device__ __forceinline__ WaveGeom geom(const Args<T>& a) {
@@ -564,7 +561,6 @@ __device__ __forceinline__ WaveGeom geom_fused(const Args<T>& a) {
     g.lane = threadIdx.x & (kWave - 1);
     const int w = threadIdx.x / kWave;
     g.x = strip * kFStrip - 2 + g.lane;
-    g.strip = strip;
     g.edge_lane = false;
     g.ex = g.x;
     g.y0 = a.dom.y_lo + (rb * (kBlock / kWave) + w) * a.rows;
@@ -572,20 +568,37 @@ __device__ __forceinline__ WaveGeom geom_fused(const Args<T>& a) {
     g.out_lane = g.lane >= 2 && g.lane < 2 + kFStrip && g.x < a.dom.W;
     return g;
 }
-// DUP slot of (this lane, row y): block `strip`, slot `lane`, in memory row y - y_mem0
+// REC byte offsets of pixel i: the record's pairs r.xy, p.xy, (r.t, p.t) and the S record
 template <typename T>
-__device__ __forceinline__ unsigned dslot(const Args<T>& a, const WaveGeom& g, int y) {
-    return (unsigned)((long long)(y - a.dom.y_mem0) * a.pitch + 64 * g.strip + g.lane);
+struct ROff {
+    unsigned r, p, t, s;
+    __device__ __forceinline__ ROff(unsigned i) : r(i * 6u * (unsigned)sizeof(T)), p(r + 2u * (unsigned)sizeof(T)),
+        t(r + 4u * (unsigned)sizeof(T)), s(i * 4u * (unsigned)sizeof(T)) {}
+};
+// the plan takes the REC layout only when its 32-bit byte offsets fit
+template <typename T>
+constexpr bool offsets_fit_rec(long long npix) {
+    return 6 * npix * (long long)sizeof(T) < (1LL << 32);
 }
-// The second copy of an output column that a neighbouring block holds as a halo column:
-// lanes 2, 3 (columns 60 s, 60 s + 1) are slots 62, 63 of block s - 1 (own slot - 4),
-// lanes 60, 61 (columns 60 s + 58, 60 s + 59) slots 0, 1 of block s + 1 (own slot + 4);
-// -1 for every other lane and at the image's outer strips.
-template <typename T>
-__device__ __forceinline__ int dup_delta(const Args<T>& a, const WaveGeom& g) {
-    if ((g.lane == 2 || g.lane == 3) && g.strip > 0) return -4;
-    if ((g.lane == 60 || g.lane == 61) && g.strip + 1 < a.nstrips) return 4;
-    return 0;
+typedef float vec4f_t __attribute__((ext_vector_type(4)));
+// S = [u.x u.y angle pre_t]: one 16-B load in fp32, two in fp64
+__device__ __forceinline__ void ld_srec(const float* S, unsigned off, vec2_t<float>& u, float& ang, float& pre) {
+    const vec4f_t v = ldb<false, vec4f_t>(S, off);
+    u.x = v.x; u.y = v.y; ang = v.z; pre = v.w;
+}
+__device__ __forceinline__ void ld_srec(const double* S, unsigned off, vec2_t<float>& u, double& ang, double& pre) {
+    const vec2_t<double> a = ldb<false, vec2_t<double>>(S, off), b = ldb<false, vec2_t<double>>(S, off + 16u);
+    u.x = (float)a.x; u.y = (float)a.y; ang = b.x; pre = b.y;
+}
+template <bool NT>
+__device__ __forceinline__ void st_srec(float* S, unsigned off, float ux, float uy, float ang, float pre) {
+    vec4f_t v; v.x = ux; v.y = uy; v.z = ang; v.w = pre;
+    stb<NT>(S, off, v);
+}
+template <bool NT>
+__device__ __forceinline__ void st_srec(double* S, unsigned off, float ux, float uy, double ang, double pre) {
+    vec2_t<double> a, b; a.x = ux; a.y = uy; b.x = ang; b.y = pre;
+    stb<NT>(S, off, a); stb<NT>(S, off + 16u, b);
 }
 
 template <typename T>
@@ -974,48 +987,54 @@ struct GRow {          // a finished row of p_{i-1} with the pixel's static data
 };
 template <typename T>
 struct GRaw {
-    vec2_t<T> p, r, d, q2, cs;
+    vec2_t<T> p, r, d, q2;
     T pt, rt, w2, ang, dt, q2t;
     vec2_t<float> u;
     int f, in;
 };
-// DUP: every array from the DUP layout (the wave's aligned block), (cos, sin) from CSd
-template <typename T, int DM, int E, bool P0, bool DUP>
+// REC: flags, S and the record of iteration i-1 (pin == rin); p_{i-2} (E) from its record,
+// r_0's part when P0 (pass 2 forms p_0 from it). oob: an offset past every buffer.
+template <typename T, int DM, int E, bool P0, bool REC>
 __device__ __forceinline__ GRaw<T> raw_grow(const Args<T>& a, const WaveGeom& g, int y, unsigned tb, const T* pin,
                                             const T* rin, const T* pre, __amdgpu_buffer_rsrc_t rdl,
                                             __amdgpu_buffer_rsrc_t rq2, unsigned oob, bool own) {
     GRaw<T> q;
     q.in = present(a.dom, g.x, y);
-    const unsigned i = q.in ? (DUP ? dslot(a, g, y) : (unsigned)a.dom.off(g.x, y)) : 0u;
+    const unsigned i = q.in ? (unsigned)a.dom.off(g.x, y) : 0u;
     const POff<T> o(i, tb);
     q.f = ldb<false, uint8_t>(a.flags, i);
-    if constexpr (DUP) {
-        q.u = ldb<false, vec2_t<float>>(a.Ud, 8u * i);
-        q.cs = ldb<false, vec2_t<T>>(a.CSd, i * 2u * (unsigned)sizeof(T));
-    } else {
-        q.u = ldb<false, vec2_t<float>>(a.U, 8u * i);
-        q.ang = ldb<false, T>(a.A, o.s);
+    own = own && g.out_lane;
+    const unsigned oxy = own ? o.xy : oob, ot = own ? o.t : oob;
+    if constexpr (REC) {
+        const ROff<T> ro(i);
+        ld_srec(a.S, ro.s, q.u, q.ang, q.w2);
+        q.r = ldb<false, vec2_t<T>>(rin, ro.r);
+        const vec2_t<T> tt = ldb<false, vec2_t<T>>(rin, ro.t);
+        q.rt = tt.x; q.pt = tt.y;
+        if (!(P0 && !E)) q.p = ldb<false, vec2_t<T>>(rin, ro.p);
+        if (DM == 2) { q.d = bld<vec2_t<T>>(rdl, oxy); q.dt = bld<T>(rdl, ot); }
+        if (E) {
+            q.q2 = bld<vec2_t<T>>(rq2, own ? (P0 ? ro.r : ro.p) : oob);
+            const vec2_t<T> t2 = bld<vec2_t<T>>(rq2, own ? ro.t : oob);
+            q.q2t = P0 ? t2.x : t2.y;
+        }
+        return q;
     }
+    q.u = ldb<false, vec2_t<float>>(a.U, 8u * i);
+    q.ang = ldb<false, T>(a.A, o.s);
     q.r = ldb<false, vec2_t<T>>(rin, o.xy); q.rt = ldb<false, T>(rin, o.t);
     q.w2 = ldb<false, T>(pre, o.s);
     if (!(P0 && !E)) { q.p = ldb<false, vec2_t<T>>(pin, o.xy); q.pt = ldb<false, T>(pin, o.t); }
-    own = own && g.out_lane;
-    const unsigned oxy = own ? o.xy : oob, ot = own ? o.t : oob;
     if (DM == 2) { q.d = bld<vec2_t<T>>(rdl, oxy); q.dt = bld<T>(rdl, ot); }
     if (E) { q.q2 = bld<vec2_t<T>>(rq2, oxy); q.q2t = bld<T>(rq2, ot); }
     return q;
 }
-template <typename T, int E, bool P0, bool DUP>
+template <typename T, int E, bool P0>
 __device__ __forceinline__ GRow<T> finish_grow(const Args<T>& a, const GRaw<T>& q) {
     GRow<T> o;
     o.f = q.in ? q.f : 0;
     o.u = q.in ? q.u : (vec2_t<float>)0.f;
-    if constexpr (DUP) {   // iw_jtf_apply's sincos of the same angle (cos 0 = 1 off the image)
-        o.c = q.in ? q.cs.x : (T)1;
-        o.s = q.in ? q.cs.y : (T)0;
-    } else {
-        sc_of(q.in ? q.ang : (T)0, &o.c, &o.s);
-    }
+    sc_of(q.in ? q.ang : (T)0, &o.c, &o.s);
     o.r = q.r; o.rt = q.rt; o.w2 = q.w2;
     o.d = q.d; o.dt = q.dt;
     o.q2 = q.q2; o.q2t = q.q2t;
@@ -1044,14 +1063,13 @@ struct HRow {
 // U2: two rows per loop trip with the row records swapping roles (no register copies, but
 // more VGPRs live: 138-168 against 120-142, 3 waves per SIMD instead of 4 on the odd passes)
 // PF2 (with U2): two raw rows in flight per wave instead of one.
-// DUP: the DUP layout (Args::pitch): aligned loads of the wave's block; r_i and p_i also
-// stored to the neighbour's halo slot (dup_delta), delta own slots only.
-template <typename T, int DM, int E = 0, bool P0 = false, bool SNT = false, bool U2 = false, bool PF2 = false,
-          bool DUP = false>
-__global__ __launch_bounds__(kBlock) void iw_pcg(Args<T> a, const T* __restrict__ pin, const T* __restrict__ rin,
-                                                 const T* __restrict__ pre, T* __restrict__ pout, T* rout,
-                                                 T* __restrict__ delta, double* __restrict__ sc, int prev,
-                                                 double base_scale, ReduceSlot rs, const T* pin2 = nullptr) {
+// REC: the REC layout (Args::S): pin == rin is the record of iteration i-1, pout == rout
+// that of iteration i, both halves stored by stage A; pin2 the record of iteration i-2.
+template <typename T, int DM, int E, bool P0, bool SNT, bool U2, bool PF2, bool REC>
+__device__ __forceinline__ void iw_pcg_body(const Args<T>& a, const T* __restrict__ pin, const T* __restrict__ rin,
+                                            const T* __restrict__ pre, T* __restrict__ pout, T* rout,
+                                            T* __restrict__ delta, double* __restrict__ sc, int prev,
+                                            double base_scale, ReduceSlot rs, const T* pin2) {
     IW_PRE_TABLE(a);
     const WaveGeom g = geom_fused(a);
     // the scalars exactly as iw_apply_res forms them
@@ -1063,19 +1081,20 @@ __global__ __launch_bounds__(kBlock) void iw_pcg(Args<T> a, const T* __restrict_
     const T alpha2 = E ? pcg_alpha<T>(sc[prev - kSlots], sc[prev - kSlots + 1]) : (T)0;
     if (blockIdx.x == 0 && threadIdx.x == 0) sc[prev + kSlots + 4] = rz_id;
     const T wr = a.wr, wf2 = a.wf * a.wf;
-    const long long nplane = DUP ? a.ndup : a.dom.npix_mem();
+    const long long nplane = a.dom.npix_mem();
     const unsigned tb = (unsigned)(2 * nplane * (long long)sizeof(T));
-    // the unknown-layout vectors' byte size: the buffers' range and the drop offset
-    const unsigned oob = (unsigned)(3 * nplane * (long long)sizeof(T));
-    const int dd = DUP ? dup_delta(a, g) : 0;
-    const __amdgpu_buffer_rsrc_t r_out = bres(rout, oob), r_p = bres(pout, oob), r_d = bres(delta, oob),
+    // the unknown-layout vectors' byte size (REC: the records'): the buffers' range and the
+    // drop offset
+    const unsigned vb = (unsigned)(3 * nplane * (long long)sizeof(T));
+    const unsigned oob = REC ? 2u * vb : vb;
+    const __amdgpu_buffer_rsrc_t r_out = bres(rout, oob), r_p = bres(pout, oob), r_d = bres(delta, vb),
                                  r_q2 = bres(pin2, oob);
     acc_t rzd = 0, papd = 0, rapd = 0, apapd = 0;
     if (g.y0 < g.y1) {
         auto raw = [&](int y) {
-            return raw_grow<T, DM, E, P0, DUP>(a, g, y, tb, pin, rin, pre, r_d, r_q2, oob, y >= g.y0 && y < g.y1);
+            return raw_grow<T, DM, E, P0, REC>(a, g, y, tb, pin, rin, pre, r_d, r_q2, oob, y >= g.y0 && y < g.y1);
         };
-        auto fin = [&](const GRaw<T>& q) { return finish_grow<T, E, P0, DUP>(a, q); };
+        auto fin = [&](const GRaw<T>& q) { return finish_grow<T, E, P0>(a, q); };
         // stage A at row y (cur = row y, dn = row y+1, carry from row y-1): Ap_{i-1}, then
         // r_i and p_i (stores r_i and delta on an owned row)
         ACarry<T> ka;
@@ -1099,7 +1118,7 @@ __global__ __launch_bounds__(kBlock) void iw_pcg(Args<T> a, const T* __restrict_
             h.w2 = a.use_pre ? cur.w2 : (T)1;
             const bool mine = y >= g.y0 && y < g.y1 && g.out_lane;
             {
-                const unsigned iy = mine ? (DUP ? dslot(a, g, y) : (unsigned)a.dom.off(g.x, y)) : 0u;
+                const unsigned iy = mine ? (unsigned)a.dom.off(g.x, y) : 0u;
                 const POff<T> off(iy, tb);
                 const unsigned oxy = mine ? off.xy : oob, ot = mine ? off.t : oob;
                 if (DM != 0) {   // iw_apply_res's deferred delta terms, term by term (explicit fmas)
@@ -1117,10 +1136,15 @@ __global__ __launch_bounds__(kBlock) void iw_pcg(Args<T> a, const T* __restrict_
                     if (!h.act) { d = (vec2_t<T>)0; dt = 0; }
                     bst(r_d, oxy, d); bst(r_d, ot, dt);
                 }
-                bst(r_out, oxy, h.r); bst(r_out, ot, h.rt);   // rout null (last pass): dropped
-                if constexpr (DUP) {   // the neighbour block's halo copy (dropped where there is none)
-                    const POff<T> od((unsigned)((int)iy + dd), tb);
-                    bst(r_out, mine && dd ? od.xy : oob, h.r); bst(r_out, mine && dd ? od.t : oob, h.rt);
+                if constexpr (REC) {   // the whole record (p_i zero on inactive pixels, as stage B's)
+                    const ROff<T> ro(iy);
+                    const vec2_t<T> pm = h.act ? h.p : (vec2_t<T>)0;
+                    vec2_t<T> tt;
+                    tt.x = h.rt; tt.y = h.act ? h.pt : (T)0;
+                    bst(r_out, mine ? ro.r : oob, h.r); bst(r_out, mine ? ro.p : oob, pm);
+                    bst(r_out, mine ? ro.t : oob, tt);
+                } else {
+                    bst(r_out, oxy, h.r); bst(r_out, ot, h.rt);   // rout null (last pass): dropped
                 }
                 const acc_t rz = wdot3(h.w0, h.r.x, h.r.x, h.w0, h.r.y, h.r.y, h.w2, h.rt, h.rt);
                 rzd += mine ? rz : 0.0;
@@ -1146,12 +1170,10 @@ __global__ __launch_bounds__(kBlock) void iw_pcg(Args<T> a, const T* __restrict_
             apply_ap2(cur.p, cur.pt, cur.c, cur.s, cur.u, cur.act, cur.fit, dn.p, dn.pt, dn.c, dn.s, dn.u, dn.act, wr,
                       wf2, kb, ao, aot);
             {
-                const unsigned iy = g.out_lane ? (DUP ? dslot(a, g, y) : (unsigned)a.dom.off(g.x, y)) : 0u;
-                const POff<T> off(iy, tb);
-                bst(r_p, g.out_lane ? off.xy : oob, cur.p); bst(r_p, g.out_lane ? off.t : oob, cur.pt);
-                if constexpr (DUP) {
-                    const POff<T> od((unsigned)((int)iy + dd), tb);
-                    bst(r_p, g.out_lane && dd ? od.xy : oob, cur.p); bst(r_p, g.out_lane && dd ? od.t : oob, cur.pt);
+                if constexpr (!REC) {
+                    const unsigned iy = g.out_lane ? (unsigned)a.dom.off(g.x, y) : 0u;
+                    const POff<T> off(iy, tb);
+                    bst(r_p, g.out_lane ? off.xy : oob, cur.p); bst(r_p, g.out_lane ? off.t : oob, cur.pt);
                 }
                 const acc_t s1 = dot3(cur.p.x, ao.x, cur.p.y, ao.y, cur.pt, aot);
                 const acc_t s2 = wdot3(cur.w0, cur.r.x, ao.x, cur.w0, cur.r.y, ao.y, cur.w2, cur.rt, aot);
@@ -1206,6 +1228,14 @@ __global__ __launch_bounds__(kBlock) void iw_pcg(Args<T> a, const T* __restrict_
     }
     double v[4] = {(double)rzd, (double)papd, (double)rapd, (double)apapd};
     block_reduce_publish<4>(v, rs, g.tile);
+}
+template <typename T, int DM, int E = 0, bool P0 = false, bool SNT = false, bool U2 = false, bool PF2 = false,
+          bool REC = false>
+__global__ __launch_bounds__(kBlock) void iw_pcg(Args<T> a, const T* __restrict__ pin, const T* __restrict__ rin,
+                                                 const T* __restrict__ pre, T* __restrict__ pout, T* rout,
+                                                 T* __restrict__ delta, double* __restrict__ sc, int prev,
+                                                 double base_scale, ReduceSlot rs, const T* pin2 = nullptr) {
+    iw_pcg_body<T, DM, E, P0, SNT, U2, PF2, REC>(a, pin, rin, pre, pout, rout, delta, sc, prev, base_scale, rs, pin2);
 }
 
 // ------------------------------------------------------------- value rows
@@ -1495,42 +1525,38 @@ struct FRow {          // a finished row of the fused kernel's apply window
         return v;
     }
 };
-// DUP: r, pre, flags (and p_0) go to the DUP layout (Args::pitch), each output column to
-// its own block and, for the two columns at each strip edge, to the neighbour's halo slot;
-// UrShape and (cos, sin) of the angle are copied to Ud / CSd for every column of the block
-template <typename T, int NT = 2, bool DUP = false>
+// REC: r_0 (and p_0 unless pout is null) go to the record r, UrShape / the angle / pre_t
+// to the S record (Args::S); pre is not written
+template <typename T, int NT = 2, bool REC = false>
 __device__ __forceinline__ void iw_jtf_apply_body(const Args<T>& a, T* __restrict__ r, T* __restrict__ pre,
                                                   T* __restrict__ pout, T* __restrict__ Ap, ReduceSlot rs) {
     IW_PRE_TABLE(a);
     const WaveGeom g = geom_fused(a);
     const T wr = a.wr, wf2 = a.wf * a.wf;
-    const unsigned tb = DUP ? (unsigned)(2 * a.ndup * (long long)sizeof(T))
-                            : (unsigned)(2 * a.dom.npix_mem() * (long long)sizeof(T));
-    const int dd = DUP ? dup_delta(a, g) : 0;
+    const unsigned tb = (unsigned)(2 * a.dom.npix_mem() * (long long)sizeof(T));
     acc_t rzdot = 0, papdot = 0, rapd = 0, apapd = 0;
     // J^T F of row y from the window (cur = row y, dn = row y+1): stores r / pre / flags
     // when the row is this wave's, returns the apply's view of the row (p = pre r)
     auto jrow = [&](const VRow<T>& cur, const VRow<T>& dn, JCarry<T>& k, int y, bool own) {
         const JRow<T> j = jtf_row<T, false>(a, cur, dn, k);
         const JOut<T> o = jtf_out(a, cur, j);
-        if constexpr (DUP) {   // the per-Step copies, every in-image column of the block
-            if (own && g.x >= 0 && g.x < a.dom.W) {
-                const unsigned i = dslot(a, g, y);
-                vec2_t<float> u; u.x = cur.ux; u.y = cur.uy;
-                stb<false>(a.Ud, 8u * i, u);
-                vec2_t<T> cs; cs.x = cur.c; cs.y = cur.s;
-                stb<false>(a.CSd, i * 2u * (unsigned)sizeof(T), cs);
-            }
-        }
         if (own && g.out_lane) {
             // 32-bit byte offsets from uniform bases (the plan takes this kernel only when
             // they fit, offsets_fit_32), the Offset pair as one 8/16-byte store
-            const unsigned i = DUP ? dslot(a, g, y) : (unsigned)a.dom.off(g.x, y);
+            const unsigned i = (unsigned)a.dom.off(g.x, y);
             vec2_t<T> rv; rv.x = o.rx; rv.y = o.ry;
-            for (int c = 0; c < (DUP && dd ? 2 : 1); ++c) {   // DUP: the neighbour's halo copy too
-                const unsigned ic = c ? (unsigned)((int)i + dd) : i;
-                const POff<T> off(ic, tb);
-                stb<false>(a.flags, ic, (uint8_t)o.f);
+            stb<false>(a.flags, i, (uint8_t)o.f);
+            if constexpr (REC) {   // p_0 = pre r_0 as FRow::p / pt form it (whole records: a
+                // record left partly unwritten costs a partial-line write per line)
+                const ROff<T> ro(i);
+                stb<(NT & 2) != 0>(r, ro.r, rv);
+                vec2_t<T> tt;
+                tt.x = o.rt; tt.y = opaque(o.wt * o.rt);
+                stb<(NT & 2) != 0>(r, ro.t, tt);
+                stb<(NT & 2) != 0>(r, ro.p, opaque(o.wo * rv));
+                st_srec<(NT & 2) != 0>(a.S, ro.s, cur.ux, cur.uy, cur.t, o.wt);
+            } else {
+                const POff<T> off(i, tb);
                 stb<(NT & 2) != 0>(r, off.xy, rv); stb<(NT & 2) != 0>(r, off.t, o.rt);
                 stb<(NT & 2) != 0>(pre, off.s, o.wt);
             }
@@ -1568,17 +1594,13 @@ __device__ __forceinline__ void iw_jtf_apply_body(const Args<T>& a, T* __restric
             apply_ap2(cp, cpt, cur.c, cur.s, cur.u(), cur.act, cur.fit, dn.p(), dn.pt(), dn.c, dn.s, dn.u(), dn.act,
                       wr, wf2, k2, ao, aot);
             if (g.out_lane) {
-                const unsigned iy = DUP ? dslot(a, g, y) : (unsigned)a.dom.off(g.x, y);
+                const unsigned iy = (unsigned)a.dom.off(g.x, y);
                 const POff<T> off(iy, tb);
-                if (Ap) {   // null when lIterations == 1 or when iw_pcg recomputes Ap_0 (always with DUP)
+                if (Ap) {   // null when lIterations == 1 or when iw_pcg recomputes Ap_0 (always with REC)
                     stb<(NT & 2) != 0>(Ap, off.xy, ao); stb<(NT & 2) != 0>(Ap, off.t, aot);
                 }
-                if (pout) {   // null when the loop forms p_0 from r_0 itself (lIterations >= 3)
+                if (!REC && pout) {   // null when the loop forms p_0 from r_0 itself (lIterations >= 3)
                     stb<(NT & 2) != 0>(pout, off.xy, cp); stb<(NT & 2) != 0>(pout, off.t, cpt);
-                    if (DUP && dd) {
-                        const POff<T> od((unsigned)((int)iy + dd), tb);
-                        stb<(NT & 2) != 0>(pout, od.xy, cp); stb<(NT & 2) != 0>(pout, od.t, cpt);
-                    }
                 }
                 papdot += dot3(cp.x, ao.x, cp.y, ao.y, cpt, aot);
                 // PCGStep2's weights: pre, or 1 without a preconditioner
@@ -1595,10 +1617,10 @@ __device__ __forceinline__ void iw_jtf_apply_body(const Args<T>& a, T* __restric
     block_reduce_publish<4>(v, rs, g.tile);
 }
 // (the compiler's 112-114 VGPRs give 4 waves per SIMD; forcing 5 spills: 504 vs 373 us)
-template <typename T, int NT = 2, bool DUP = false>
+template <typename T, int NT = 2, bool REC = false>
 __global__ __launch_bounds__(kBlock) void iw_jtf_apply(Args<T> a, T* __restrict__ r, T* __restrict__ pre,
                                                        T* __restrict__ pout, T* __restrict__ Ap, ReduceSlot rs) {
-    iw_jtf_apply_body<T, NT, DUP>(a, r, pre, pout, Ap, rs);
+    iw_jtf_apply_body<T, NT, REC>(a, r, pre, pout, Ap, rs);
 }
 
 // ----------------------------------------------------------------- cost kernel
@@ -1791,8 +1813,8 @@ __device__ __forceinline__ T upd_delta(T alpha, T q, T alpha2, T q2, T d) {
 }
 // X += delta_L on active pixels of the owned rows (PCGLinearUpdate, :854-859), where
 // delta_L = delta_{L-1} + alpha_{L-1} p_{L-1} is the last PCG iteration's delta update
-// (HAS_DELTA = false when lIterations == 1: delta_0 = 0).
-template <typename T, bool HAS_DELTA, bool E2 = false>
+// (HAS_DELTA = false when lIterations == 1: delta_0 = 0). REC: p and p2 are records.
+template <typename T, bool HAS_DELTA, bool E2 = false, bool REC = false>
 __global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O, T* __restrict__ A,
                                                     const T* __restrict__ delta, const T* __restrict__ p,
                                                     const double* __restrict__ sc, int ia_num, int ia_den,
@@ -1806,66 +1828,31 @@ __global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O
          i += (long long)gridDim.x * blockDim.x) {
         const int f = a.flags[i];
         const Vec2<T> o = reinterpret_cast<const Vec2<T>*>(O)[i];
-        const Vec2<T> pp = reinterpret_cast<const Vec2<T>*>(p)[i];
-        const T t = A[i], pt = p[2 * N + i];
-        Vec2<T> d{}, q2{};
-        T dt = 0, q2t = 0;
+        const T t = A[i];
+        // p.xy and p.t of a vector / record (REC: [r.xy | p.xy | r.t p.t])
+        auto pget = [&](const T* v, Vec2<T>& xy, T& pt) {
+            if constexpr (REC) {
+                xy = reinterpret_cast<const Vec2<T>*>(v)[3 * i + 1];
+                pt = reinterpret_cast<const Vec2<T>*>(v)[3 * i + 2].y;
+            } else {
+                xy = reinterpret_cast<const Vec2<T>*>(v)[i];
+                pt = v[2 * N + i];
+            }
+        };
+        Vec2<T> pp, d{}, q2{};
+        T pt, dt = 0, q2t = 0;
+        pget(p, pp, pt);
         if (HAS_DELTA) {
             d = reinterpret_cast<const Vec2<T>*>(delta)[i];
             dt = delta[2 * N + i];
         }
-        if (E2) {
-            q2 = reinterpret_cast<const Vec2<T>*>(p2)[i];
-            q2t = p2[2 * N + i];
-        }
+        if (E2) pget(p2, q2, q2t);
         d.x = upd_delta<T, HAS_DELTA, E2>(alpha, pp.x, alpha2, q2.x, d.x);
         d.y = upd_delta<T, HAS_DELTA, E2>(alpha, pp.y, alpha2, q2.y, d.y);
         dt = upd_delta<T, HAS_DELTA, E2>(alpha, pt, alpha2, q2t, dt);
         if (f & 1) {
             reinterpret_cast<Vec2<T>*>(O)[i] = Vec2<T>{o.x + d.x, o.y + d.y};
             A[i] = t + dt;
-        }
-    }
-}
-
-// The same update reading delta / p / p_{i-2} / flags from the DUP layout (own slots: lanes
-// 2..61 of each block), the unknowns in the caller's image layout
-template <typename T, bool HAS_DELTA, bool E2 = false>
-__global__ __launch_bounds__(kBlock) void iw_update_dup(Args<T> a, T* __restrict__ O, T* __restrict__ A,
-                                                        const T* __restrict__ delta, const T* __restrict__ p,
-                                                        const double* __restrict__ sc, int ia_num, int ia_den,
-                                                        const T* __restrict__ p2 = nullptr, int ia2_num = 0,
-                                                        int ia2_den = 0) {
-    const long long N = a.ndup;
-    const T alpha = pcg_alpha<T>(sc[ia_num], sc[ia_den]);
-    const T alpha2 = E2 ? pcg_alpha<T>(sc[ia2_num], sc[ia2_den]) : (T)0;
-    const long long rows = a.dom.y_hi - a.dom.y_lo, n = rows * a.pitch;
-    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += (long long)gridDim.x * blockDim.x) {
-        const int row = (int)(q / a.pitch), slot = (int)(q - (long long)row * a.pitch);
-        const int l = slot & 63, x = (slot >> 6) * kFStrip - 2 + l;
-        if (l < 2 || l >= 2 + kFStrip || x >= a.dom.W) continue;
-        const int y = a.dom.y_lo + row;
-        const long long i = (long long)(y - a.dom.y_mem0) * a.pitch + slot, iu = a.dom.off(x, y);
-        const int f = a.flags[i];
-        const Vec2<T> o = reinterpret_cast<const Vec2<T>*>(O)[iu];
-        const Vec2<T> pp = reinterpret_cast<const Vec2<T>*>(p)[i];
-        const T t = A[iu], pt = p[2 * N + i];
-        Vec2<T> d{}, q2{};
-        T dt = 0, q2t = 0;
-        if (HAS_DELTA) {
-            d = reinterpret_cast<const Vec2<T>*>(delta)[i];
-            dt = delta[2 * N + i];
-        }
-        if (E2) {
-            q2 = reinterpret_cast<const Vec2<T>*>(p2)[i];
-            q2t = p2[2 * N + i];
-        }
-        d.x = upd_delta<T, HAS_DELTA, E2>(alpha, pp.x, alpha2, q2.x, d.x);
-        d.y = upd_delta<T, HAS_DELTA, E2>(alpha, pp.y, alpha2, q2.y, d.y);
-        dt = upd_delta<T, HAS_DELTA, E2>(alpha, pt, alpha2, q2t, dt);
-        if (f & 1) {
-            reinterpret_cast<Vec2<T>*>(O)[iu] = Vec2<T>{o.x + d.x, o.y + d.y};
-            A[iu] = t + dt;
         }
     }
 }
@@ -2060,22 +2047,24 @@ public:
         const bool p0 = res && L >= 3;
         // iterations 1.. as iw_pcg: Ap_{i-1} recomputed from p_{i-1}, never stored
         const bool apfree = res && apfree_;
-        // the solver vectors in the DUP layout (Args::pitch): iw_jtf_apply, iw_pcg, iw_update
-        const bool dup = dupl_ && fused && apfree;
+        // the PCG vectors as records (Args::S): iw_jtf_apply, iw_pcg, iw_update
+        const bool rec = recl_ && fused && apfree;
+        if (rec) { pcur = rec_[0]; pb[0] = rec_[0]; pb[1] = rec_[1]; pb[2] = rec_[2]; }
         if (fused) {
-            launch_jtf_apply(p0 ? nullptr : pcur, L == 1 || apfree, dup);
+            launch_jtf_apply(p0 ? nullptr : pcur, L == 1 || apfree, rec);
             allreduce(rz(0), 4);   // rz_0, p.Ap_0, r_0.W Ap_0, Ap_0.W Ap_0
             if (distributed()) {   // the next pass reads r_0 (and forms p_0) in the halo rows
                 std::vector<HaloPlane> pl;
-                add_vec_planes(pl, r_, dup);
-                pl.push_back({(void*)pre_, sizeof(T) * rowlen(dup)});
-                pl.push_back({(void*)flags_, (size_t)rowlen(dup)});
-                if (!p0) add_vec_planes(pl, pcur, dup);
-                if (!apfree) add_vec_planes(pl, Ap_);
-                if (dup) {   // the per-Step copies iw_pcg reads in its halo rows
-                    pl.push_back({(void*)Ud_, 2 * sizeof(float) * rowlen(dup)});
-                    pl.push_back({(void*)CSd_, 2 * sizeof(T) * rowlen(dup)});
+                if (rec) {   // r_0 / p_0's record, S, flags
+                    pl.push_back({(void*)rec_[0], 6 * sizeof(T) * dom_.W});
+                    pl.push_back({(void*)srec_, 4 * sizeof(T) * dom_.W});
+                } else {
+                    add_vec_planes(pl, r_);
+                    pl.push_back({(void*)pre_, sizeof(T) * dom_.W});
+                    if (!p0) add_vec_planes(pl, pcur);
+                    if (!apfree) add_vec_planes(pl, Ap_);
                 }
+                pl.push_back({(void*)flags_, (size_t)dom_.W});
                 exchange(pl);
             }
         } else {
@@ -2108,17 +2097,21 @@ public:
                 T* rb[2] = {r_, r1_};
                 T* ab[2] = {Ap_, Ap1_};
                 // pass 2 with P0: p_0 is formed from r_0, still in the r buffer pass 2 writes r_2 to
-                const T* pin2 = (defer && i >= 2) ? ((p0 && i == 2) ? rb[0] : pbuf(i - 2)) : nullptr;
+                const T* pin2 = (defer && i >= 2) ? ((p0 && i == 2 && !rec) ? rb[0] : pbuf(i - 2)) : nullptr;
                 // part 0: every row block; 1: the interior ones; 2: the first and last
                 auto pass = [&](int part) {
-                    if (apfree) launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0, part, dup);
+                    if (apfree) launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0, part, rec);
                     else launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, part, p0);
                 };
                 if (distributed()) {   // the pass reads r and p (and Ap) of iteration i-1 in the halo rows
                     std::vector<HaloPlane> pl;
-                    add_vec_planes(pl, rb[(i - 1) & 1], dup);
-                    if (!apfree) add_vec_planes(pl, ab[(i - 1) & 1]);
-                    if (!(p0 && i == 1)) add_vec_planes(pl, pbuf(i - 1), dup);   // P0: pass 1 forms p_0 from r_0
+                    if (rec) {
+                        pl.push_back({(void*)pbuf(i - 1), 6 * sizeof(T) * dom_.W});
+                    } else {
+                        add_vec_planes(pl, rb[(i - 1) & 1]);
+                        if (!apfree) add_vec_planes(pl, ab[(i - 1) & 1]);
+                        if (!(p0 && i == 1)) add_vec_planes(pl, pbuf(i - 1));   // P0: pass 1 forms p_0 from r_0
+                    }
                     if (fused && i == 1) {   // iw_jtf_apply's exchange carried r_0 (and p_0, Ap_0)
                         pass(0);
                     } else if (split) {   // beside the interior row blocks
@@ -2132,7 +2125,7 @@ public:
                         pass(0);
                     }
                 } else if (apfree) {
-                    launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0, 0, dup);
+                    launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0, 0, rec);
                 } else {
                     launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 0, p0);
                 }
@@ -2178,39 +2171,39 @@ public:
         // PCGLinearUpdate (with the last delta += alpha p) + cost
         if (L > 0 && defer) {
             // pending: p_{L-1}, and p_{L-2} too when L-1 is odd (the even iterations fold pairs)
-            const int ub = dup ? flat_grid((long long)(dom_.y_hi - dom_.y_lo) * pitch_, 1) : flat_grid(dom_.npix_mem(), 1);
+            const int ub = flat_grid(dom_.npix_mem(), 1);
             const T* pl = pb[(L - 1) % 3];
             const T* pl2 = L >= 2 ? pb[(L - 2) % 3] : nullptr;
             const bool e2 = L % 2 == 0, has = L >= 3;
             tbegin("iw_update");
             if (e2 && has)
-                hipLaunchKernelGGL((dup ? iw::iw_update_dup<T, true, true> : iw::iw_update<T, true, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
+                hipLaunchKernelGGL((rec ? iw::iw_update<T, true, true, true> : iw::iw_update<T, true, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
                                    cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1), pl2, rz(L - 2),
                                    pap(L - 2));
             else if (e2)
-                hipLaunchKernelGGL((dup ? iw::iw_update_dup<T, false, true> : iw::iw_update<T, false, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
+                hipLaunchKernelGGL((rec ? iw::iw_update<T, false, true, true> : iw::iw_update<T, false, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
                                    cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1), pl2, rz(L - 2),
                                    pap(L - 2));
             else if (has)
-                hipLaunchKernelGGL((dup ? iw::iw_update_dup<T, true> : iw::iw_update<T, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
+                hipLaunchKernelGGL((rec ? iw::iw_update<T, true, false, true> : iw::iw_update<T, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
                                    cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1),
                                    (const T*)nullptr, 0, 0);
             else
-                hipLaunchKernelGGL((dup ? iw::iw_update_dup<T, false> : iw::iw_update<T, false>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
+                hipLaunchKernelGGL((rec ? iw::iw_update<T, false, false, true> : iw::iw_update<T, false>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
                                    cur_A_, (const T*)delta_, pl, red_.scalars, rz(L - 1), pap(L - 1),
                                    (const T*)nullptr, 0, 0);
             OPT_HIP_CHECK(hipGetLastError());
             tend();
             exchange_unknowns();
         } else if (L > 0) {
-            const int ub = dup ? flat_grid((long long)(dom_.y_hi - dom_.y_lo) * pitch_, 1) : flat_grid(dom_.npix_mem(), 1);
+            const int ub = flat_grid(dom_.npix_mem(), 1);
             tbegin("iw_update");
             if (L >= 2)
-                hipLaunchKernelGGL((dup ? iw::iw_update_dup<T, true> : iw::iw_update<T, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
+                hipLaunchKernelGGL((rec ? iw::iw_update<T, true, false, true> : iw::iw_update<T, true>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
                                    cur_A_, (const T*)delta_, (const T*)pcur, red_.scalars, rz(L - 1), pap(L - 1),
                                    (const T*)nullptr, 0, 0);
             else
-                hipLaunchKernelGGL((dup ? iw::iw_update_dup<T, false> : iw::iw_update<T, false>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
+                hipLaunchKernelGGL((rec ? iw::iw_update<T, false, false, true> : iw::iw_update<T, false>), dim3(ub), dim3(kBlock), 0, stream_, args(), cur_O_,
                                    cur_A_, (const T*)delta_, (const T*)pcur, red_.scalars, rz(L - 1), pap(L - 1),
                                    (const T*)nullptr, 0, 0);
             OPT_HIP_CHECK(hipGetLastError());
@@ -2300,7 +2293,7 @@ private:
         defer_ = env_int("OPT_AMD_IW_DEFER", 1) != 0;
         side_ = env_int("OPT_AMD_IW_SIDE", 0) != 0;
         apfree_ = env_int("OPT_AMD_IW_APFREE", 1) != 0;
-        dup_ = env_int("OPT_AMD_IW_DUP", 0) != 0;
+        rec_on_ = env_int("OPT_AMD_IW_REC", 0) != 0;
         pcg_nt_ = env_int("OPT_AMD_IW_PCG_NT", 0) != 0;
         pcg_u2_ = env_int("OPT_AMD_IW_PCG_U2", 0);
         // iw_jtf_apply's 60-column strips store 240-B row segments that share cache lines
@@ -2329,24 +2322,25 @@ private:
         for (int k = 0; k < 8; ++k) *vs[k] = (T*)(raw_[k] + ((size_t)stagger_ * k) % kSlack);
         flags_ = (uint8_t*)(raw_[8] + ((size_t)stagger_ * 8) % kSlack);
         p2_ = (T*)(raw_[9] + ((size_t)stagger_ * 9) % kSlack);
+        if (recl_ && raw_.size() >= 14) {
+            for (int k = 0; k < 3; ++k) rec_[k] = (T*)(raw_[10 + k] + ((size_t)stagger_ * (10 + k)) % kSlack);
+            srec_ = (T*)(raw_[13] + ((size_t)stagger_ * 13) % kSlack);
+        }
     }
     void allocate() {
         const long long N = dom_.npix_mem();
         nvec_ = 3 * N;
         offsets32_ = iw::offsets_fit_32<T>(N);
-        // the DUP layout (Args::pitch) for the fused loop: 64 slots per 60-column strip
-        pitch_ = 64 * fused_strips();
-        ndup_ = (long long)pitch_ * dom_.mem_rows;
-        dupl_ = dup_ && fused_init_ && fused_res_ && apfree_ && iw::offsets_fit_32<T>(ndup_ + 1);
-        const long long nv = dupl_ ? std::max(N, ndup_) : N;   // slots per plane of the vectors
         for (T** v : {&r_, &p0_, &p1_, &Ap_, &delta_, &r1_, &Ap1_})
-            *v = (T*)vec_alloc(sizeof(T) * 3 * nv);
-        pre_ = (T*)vec_alloc(sizeof(T) * nv);   // angle channel only (Args::preO)
-        flags_ = (uint8_t*)vec_alloc(nv);
-        p2_ = (T*)vec_alloc(sizeof(T) * 3 * nv);   // third p buffer (deferred delta)
-        if (dupl_) {
-            Ud_ = (float*)vec_alloc(sizeof(float) * 2 * ndup_);
-            CSd_ = (T*)vec_alloc(sizeof(T) * 2 * ndup_);
+            *v = (T*)vec_alloc(sizeof(T) * 3 * N);
+        pre_ = (T*)vec_alloc(sizeof(T) * N);   // angle channel only (Args::preO)
+        flags_ = (uint8_t*)vec_alloc(N);
+        p2_ = (T*)vec_alloc(sizeof(T) * 3 * N);   // third p buffer (deferred delta)
+        // the REC layout (Args::S) for the fused loop
+        recl_ = rec_on_ && fused_init_ && fused_res_ && apfree_ && iw::offsets_fit_rec<T>(N);
+        if (recl_) {
+            for (T*& v : rec_) v = (T*)vec_alloc(sizeof(T) * 6 * N);
+            srec_ = (T*)vec_alloc(sizeof(T) * 4 * N);
         }
         place();
         nstrips_ = (dom_.W + iw::kStrip - 1) / iw::kStrip;
@@ -2366,8 +2360,8 @@ private:
         raw_.clear();
         for (T** v : {&r_, &pre_, &p0_, &p1_, &Ap_, &delta_, &r1_, &Ap1_, &p2_}) *v = nullptr;
         flags_ = nullptr;
-        Ud_ = nullptr;
-        CSd_ = nullptr;
+        for (T*& v : rec_) v = nullptr;
+        srec_ = nullptr;
         for (T** v : {&dO_, &dA_}) { dfree(*v); *v = nullptr; }
         for (float** v : {&dU_, &dC_, &dM_}) { dfree(*v); *v = nullptr; }
     }
@@ -2377,13 +2371,11 @@ private:
     void allreduce(int idx, int n = 1) {
         if (distributed()) comm_->allreduce_sum(red_.scalars + idx, n, stream_);
     }
-    // elements per row of the solver vectors in the image or the DUP layout
-    long long rowlen(bool dup = false) const { return dup ? pitch_ : dom_.W; }
-    // halo planes of an unknown-layout vector [Offset.xy | Angle] (image or DUP layout)
-    void add_vec_planes(std::vector<HaloPlane>& v, const T* x, bool dup = false) const {
-        const long long plane = dup ? ndup_ : dom_.npix_mem();
-        v.push_back({(void*)x, sizeof(T) * 2 * rowlen(dup)});
-        v.push_back({(void*)(x + 2 * plane), sizeof(T) * rowlen(dup)});
+    // halo planes of an unknown-layout vector [Offset.xy | Angle]
+    void add_vec_planes(std::vector<HaloPlane>& v, const T* x) const {
+        const long long plane = dom_.npix_mem();
+        v.push_back({(void*)x, sizeof(T) * 2 * dom_.W});
+        v.push_back({(void*)(x + 2 * plane), sizeof(T) * dom_.W});
     }
     void exchange(const std::vector<HaloPlane>& planes) {
         if (!distributed()) return;
@@ -2421,7 +2413,7 @@ private:
         a.nstrips = nstrips_; a.nrowblocks = nrowblocks_; a.rows = rows_;
         a.tb0 = 0; a.tn0 = nstrips_ * nrowblocks_; a.tb1 = 0;
         a.side = 0;
-        a.pitch = pitch_; a.ndup = ndup_; a.Ud = Ud_; a.CSd = CSd_;
+        a.S = srec_;
         // same float expression the reference's evalJTF + guardedInvert evaluate
         const T wr2 = (T)wr_ * (T)wr_, wf2 = (T)wf_ * (T)wf_;
         for (int fit = 0; fit < 2; ++fit)
@@ -2496,23 +2488,30 @@ private:
     }
     // PCGInit1 + the first apply: r, pre, flags, p_0 = pre r (into pout), Ap_0 (unless
     // lIterations == 1: nothing reads that Ap), the four sums from sc[rz(0)].
-    void launch_jtf_apply(T* pout, bool no_ap, bool dup = false) {
+    // REC: r_0 (and p_0 when pout, the same record rec_[0]) and the S record; no Ap
+    void launch_jtf_apply(T* pout, bool no_ap, bool rec = false) {
         iw::Args<T> a = args();
         a.nstrips = fused_strips();
         const int nb = fused_blocks();
         a.tb0 = 0; a.tn0 = nb; a.tb1 = 0;   // every tile (geom_fused)
-        auto k = dup ? (jtf_nt_ ? iw::iw_jtf_apply<T, 2, true> : iw::iw_jtf_apply<T, 0, true>)
-                     : (jtf_nt_ ? iw::iw_jtf_apply<T, 2> : iw::iw_jtf_apply<T, 0>);
-        launch_timed("iw_jtf_apply", k, nb, a, r_, pre_, pout, no_ap ? nullptr : Ap_, red_.slot(nb, rz(0)));
+        if (rec) {
+            if (!no_ap || (pout && pout != rec_[0])) throw std::logic_error("iw_jtf_apply<REC>: record 0 only, no Ap");
+            launch_timed("iw_jtf_apply", jtf_nt_ ? iw::iw_jtf_apply<T, 2, true> : iw::iw_jtf_apply<T, 0, true>, nb, a,
+                         rec_[0], (T*)nullptr, pout, (T*)nullptr, red_.slot(nb, rz(0)));
+            return;
+        }
+        launch_timed("iw_jtf_apply", jtf_nt_ ? iw::iw_jtf_apply<T, 2> : iw::iw_jtf_apply<T, 0>, nb, a, r_, pre_, pout,
+                     no_ap ? nullptr : Ap_, red_.slot(nb, rz(0)));
     }
     // PCG iteration i >= 1 without a stored Ap (iw_pcg): reads r_{i-1} and p_{i-1}, writes
     // r_i (unless last) and p_i; the deferred delta and P0 exactly as launch_apply_res
     // part 0: every row block; 1: the interior row blocks [1, nrb - 1); 2: the first and last
     // (the only ones that read halo rows: a wave reads rows y0 - 2 .. y1 + 1)
-    void launch_pcg(int i, const T* pin, T* pout, bool last, const T* pin2, bool p0, int part = 0, bool dup = false) {
+    // REC: pin / pout / pin2 are the records of iterations i-1, i, i-2 (r and p together)
+    void launch_pcg(int i, const T* pin, T* pout, bool last, const T* pin2, bool p0, int part = 0, bool rec = false) {
         T* rb[2] = {r_, r1_};
-        const T* rin = rb[(i - 1) & 1];
-        T* rout = last ? nullptr : rb[i & 1];
+        const T* rin = rec ? pin : rb[(i - 1) & 1];
+        T* rout = rec ? pout : (last ? nullptr : rb[i & 1]);
         const double base_scale = (i == 1 && !spec_.use_preconditioner) ? 4.0 : 1.0;
         iw::Args<T> a = args();
         const int fs = fused_strips();
@@ -2547,7 +2546,7 @@ private:
         };
         using F = std::false_type;
         using Tt = std::true_type;
-        if (dup) {
+        if (rec) {
             if (pcg_u2_ == 2) pick(F{}, Tt{}, Tt{}, Tt{});
             else pick(F{}, F{}, F{}, Tt{});
         } else if (pcg_u2_ == 2) pick(F{}, Tt{}, Tt{}, F{});
@@ -2664,12 +2663,14 @@ private:
     bool defer_ = true;                 // OPT_AMD_IW_DEFER=0: iw_apply_res updates delta in every iteration
     bool side_ = false;                 // OPT_AMD_IW_SIDE=1: iw_apply_res with side-by-side waves (Args::side)
     bool apfree_ = true;                // OPT_AMD_IW_APFREE=0: iw_apply_res (stored Ap) instead of iw_pcg
-    bool dup_ = false;                  // OPT_AMD_IW_DUP=1: the fused loop in the DUP layout (slower: 4.43 vs 3.72 ms per GN step)
-    bool dupl_ = false;                 // the plan holds the DUP layout (dup_ and the fused loop's knobs)
-    int pitch_ = 0;                     // DUP slots per row (64 x fused strips)
-    long long ndup_ = 0;                // DUP slots per plane (pitch_ x memory rows)
-    float* Ud_ = nullptr;               // per-Step copies in the DUP layout (iw_jtf_apply<DUP>)
-    T* CSd_ = nullptr;
+    // OPT_AMD_IW_REC=1: the fused loop's vectors as records (Args::S). Measured slower (round 5,
+    // interleaved A/B, 4096^2 fp32 GN step 3.99 against 3.75 ms: iw_jtf_apply writes 41 B/px
+    // instead of 17, 318 against 218 us; iw_pcg 354 against 347 us — the pass is bound by its
+    // VALU work and latency, not by the strip edges' partial lines)
+    bool rec_on_ = false;
+    bool recl_ = false;                 // the plan holds the REC layout (rec_on_ and the fused loop's knobs)
+    T* rec_[3] = {nullptr, nullptr, nullptr};   // REC: iteration i's record in rec_[i % 3] (i % 2 undeferred)
+    T* srec_ = nullptr;                 // REC: the S record [u.x u.y angle pre_t], written by iw_jtf_apply
     bool pcg_nt_ = false;               // OPT_AMD_IW_PCG_NT=1: iw_pcg with streaming stores
     int pcg_u2_ = 0;                    // OPT_AMD_IW_PCG_U2=1: iw_pcg two rows per trip (U2); 2: and two rows in flight (PF2)
     bool jtf_nt_ = false;               // OPT_AMD_IW_JTF_NT=1: iw_jtf_apply with streaming stores

@@ -656,15 +656,15 @@ def test_pcg_pass_without_stored_ap_fp64(monkeypatch, W, H):
 @pytest.mark.parametrize("W,H,lit", [(150, 110, 10), (5, 3, 4), (200, 1, 3), (700, 300, 10), (64, 64, 2),
                                      (61, 2, 5), (1, 9, 4), (121, 66, 1), (240, 97, 7)])
 @pytest.mark.parametrize("double", [False, True])
-def test_dup_layout_is_bitwise_the_image_layout(monkeypatch, W, H, lit, double):
-    """OPT_AMD_IW_DUP=1 (default 0): the fused loop's solver vectors in the DUP layout (each
-    60-column strip an aligned 64-slot block with its halo columns duplicated, UrShape and
-    the angle's cos / sin copied per Step by iw_jtf_apply) against the image layout: the
-    same per-pixel arithmetic, the same tiles and sums — the trajectory (energies, Offset,
+def test_rec_layout_is_bitwise_the_image_layout(monkeypatch, W, H, lit, double):
+    """OPT_AMD_IW_REC=1 (default 0): the fused loop's PCG vectors as one record per pixel
+    ([r.xy | p.xy | r.t p.t]) and the per-Step S record ([u.x u.y angle pre_t]) against the
+    unknown layout: the same per-pixel arithmetic (one-expression contraction, so every
+    instantiation rounds alike), the same tiles and sums — the trajectory (energies, Offset,
     Angle, PCG scalars) is bitwise the same, fp32 and fp64."""
     out = []
     for v in ("0", "1"):
-        monkeypatch.setenv("OPT_AMD_IW_DUP", v)
+        monkeypatch.setenv("OPT_AMD_IW_REC", v)
         w = perturbed(W, H, seed=7 * W + H)
         s = solver(W, H, double=double)
         prm = device_params(w, double=double)

@@ -1,7 +1,7 @@
-"""Where do OPT_AMD_IW_DUP=0 and =1 first part? Runs W x H (fp32) for 1..n GN steps with
+"""Where do OPT_AMD_IW_REC=0 and =1 first part? Runs W x H (fp32) for 1..n GN steps with
 lIterations `lit` in both layouts and prints the first step whose energies, Offset, Angle
 or PCG scalars differ, with the differing pixels.
-Usage: python tools/dup_diag.py W H lit [steps]"""
+Usage: python tools/layout_diag.py W H lit [steps]"""
 import os
 import sys
 
@@ -14,7 +14,7 @@ from tests.iw_helpers import device_params, perturbed, solver  # noqa: E402
 
 
 def run(W, H, lit, n, dup):
-    os.environ["OPT_AMD_IW_DUP"] = dup
+    os.environ["OPT_AMD_IW_REC"] = dup
     w = perturbed(W, H, seed=7 * W + H)
     s = solver(W, H)
     prm = device_params(w)
