@@ -146,6 +146,20 @@ def init_bytes_per_px(liter: int = 10, ap: bool = True) -> int:
     return 8 + 4 + 8 + 8 + 4 + 12 + 4 + 1 + (12 if ap else 0) + (12 if liter <= 2 else 0)
 
 
+# The step's two other kernels (HIP-event timed like the passes): iw_update reads the flag 1,
+# Offset 8, Angle 4, delta 12, p_{L-1} 12 (+ p_{L-2} 12 when the deferred pair is pending,
+# lIterations even) and writes Offset + Angle 12; iw_cost reads Offset 8, Angle 4, UrShape 8,
+# Constraints 8, Mask 4.
+STEP_KERNELS = ("iw_jtf_apply", "iw_pcg", "iw_update", "iw_cost")
+
+
+def update_bytes_per_px(liter: int = 10) -> int:
+    return 1 + 8 + 4 + (12 if liter >= 2 else 0) + 12 + (12 if liter % 2 == 0 else 0) + 12
+
+
+COST_BYTES_PER_PX = 32
+
+
 def pmc_traffic(liter: int, first: int = 0, res=False):
     try:
         with open(PMC_FILE) as f:
@@ -477,6 +491,7 @@ def main():
             kname, n_apply, apply_ms, res = PCG_KERNEL, n_pcg, pcg_ms, "pcg"
         elif n_res:   # as iw_apply_res passes (row slabs, OPT_AMD_IW_APFREE=0)
             kname, n_apply, apply_ms, res = RES_KERNEL, n_res, res_ms, True
+    kstats = {k: s.kernel_stat(k) for k in STEP_KERNELS}
     s.set_kernel_timing(0)
     # the in-loop applies of one step: PCG iterations first..liter-1 (first = 1 when the
     # first iteration's apply ran inside iw_jtf_apply)
@@ -544,6 +559,17 @@ def main():
         ach = ibpp * npx / init_s / 1e9
         result["init_kernel"] = {"kernel": INIT_KERNEL, "avg_us": init_s * 1e6, "launches": n_init,
                                  "bytes_per_px": ibpp, "achieved": ach, "frac": ach / PEAK_HBM_GBS}
+    if not sfs:   # every kernel of the step: launches per step, average duration, HBM rate
+        per_px = {"iw_jtf_apply": init_bytes_per_px(args.liter, ap=res != "pcg"), "iw_pcg": bpp,
+                  "iw_update": update_bytes_per_px(args.liter), "iw_cost": COST_BYTES_PER_PX}
+        ks = {}
+        for k in STEP_KERNELS:
+            n, ms = kstats[k]
+            if n:
+                us = 1e3 * ms / n
+                ks[k] = {"per_step": n / args.steps, "avg_us": us, "bytes_per_px": per_px[k],
+                         "frac": per_px[k] * npx / (us * 1e-6) / 1e9 / PEAK_HBM_GBS}
+        result["step_kernels"] = ks
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = (cpu_baseline_sfs(w, W, H, args.liter) if sfs
                                   else cpu_baseline(w, n_unknowns, args.liter))

@@ -1109,13 +1109,13 @@ __device__ __forceinline__ void iw_pcg_body(const Args<T>& a, const T* __restric
             const T w0 = pre_offset(a, cur.f);
             h.r = cur.r - alpha * ap;
             h.rt = cur.rt - alpha * at;
-            vec2_t<T> z = h.r;
-            T zt = h.rt;
-            if (a.use_pre) { z = w0 * h.r; zt = cur.w2 * h.rt; }
-            h.p = z + beta * cur.p;
-            h.pt = zt + beta * cur.pt;
+            // (z = 1 r = r exactly without a preconditioner: one select per weight, not per channel)
             h.w0 = a.use_pre ? w0 : (T)1;
             h.w2 = a.use_pre ? cur.w2 : (T)1;
+            const vec2_t<T> z = h.w0 * h.r;
+            const T zt = h.w2 * h.rt;
+            h.p = z + beta * cur.p;
+            h.pt = zt + beta * cur.pt;
             const bool mine = y >= g.y0 && y < g.y1 && g.out_lane;
             {
                 const unsigned iy = mine ? (unsigned)a.dom.off(g.x, y) : 0u;
@@ -1667,6 +1667,53 @@ __global__ __launch_bounds__(kBlock) void iw_cost(Args<T> a, ReduceSlot rs) {
     block_reduce_publish<1>(v, rs, blockIdx.x);
 }
 
+// The same cost on iw_jtf_apply's 60-column strips (geom_fused, x = 60 strip - 2 + lane):
+// every horizontal neighbour of an output lane (2..61) is a lane neighbour, so there is no
+// edge record — round 4's 64-column form above fetched the strip's two outside columns per
+// row with separate 2-lane loads (141 us at 4096^2, 0.48 of 8 TB/s). Per pixel the same
+// eedge calls in the same order; the sums group by 60-column strips instead.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void iw_cost60(Args<T> a, ReduceSlot rs) {
+    const WaveGeom g = geom_fused(a);
+    const T wr = a.wr, wf = a.wf;
+    T acc = 0;
+    if (g.y0 < g.y1) {
+        auto row = [&](const VRaw<T>& q) { return finish_vrow<T, false, false>(q); };
+        VRow<T> up = row(raw_vrow<T, false, false>(a, g, g.y0 - 1)), cur = row(raw_vrow<T, false, false>(a, g, g.y0)),
+                dn = row(raw_vrow<T, false, false>(a, g, g.y0 + 1));
+        for (int y = g.y0; y < g.y1; ++y) {
+            const VRaw<T> nx = raw_vrow<T, false, false>(a, g, min(y + 2, g.y1));
+            const T lox = from_left(cur.ox, (T)0), loy = from_left(cur.oy, (T)0);
+            const T rox = from_right(cur.ox, (T)0), roy = from_right(cur.oy, (T)0);
+            const float lux = from_left(cur.ux, 0.f), luy = from_left(cur.uy, 0.f);
+            const float rux = from_right(cur.ux, 0.f), ruy = from_right(cur.uy, 0.f);
+            const int lact = from_left_i(cur.act, 0), ract = from_right_i(cur.act, 0);
+            T ex, ey, ax, ay, sum = 0;
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, rox, roy, rux, ruy,
+                  cur.act && ract, wr, ex, ey, ax, ay);
+            sum += ex * ex + ey * ey;
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, lox, loy, lux, luy,
+                  cur.act && lact, wr, ex, ey, ax, ay);
+            sum += ex * ex + ey * ey;
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, dn.ox, dn.oy, dn.ux, dn.uy,
+                  cur.act && dn.act, wr, ex, ey, ax, ay);
+            sum += ex * ex + ey * ey;
+            eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, up.ox, up.oy, up.ux, up.uy,
+                  cur.act && up.act, wr, ex, ey, ax, ay);
+            sum += ex * ex + ey * ey;
+            if (cur.fit) {
+                const T fx = wf * (cur.ox - (T)cur.cx), fy = wf * (cur.oy - (T)cur.cy);
+                sum += fx * fx + fy * fy;
+            }
+            if (g.out_lane && cur.act) acc += (T)0.5 * sum;
+            up = cur; cur = dn;
+            dn = row(nx);
+        }
+    }
+    double v[1] = {(double)acc};
+    block_reduce_publish<1>(v, rs, g.tile);
+}
+
 // ----------------------------------------------------------- model cost kernel
 // LM only, once per step: sc[rs.out] = sum over active pixels of
 // 1/2 (sum_s |e_reg(k,s) + J_reg(k,s) delta|^2 + |e_fit(k) + wf delta_O(k)|^2)
@@ -1962,7 +2009,7 @@ public:
         // against the canonical energy's (fit weight declared first), so names play no part
         read_knobs();
         timer_.apply_name = apply_kernel_name();
-        timer_.aux_names = {"iw_jtf_apply", "iw_apply_res", "iw_pcg"};
+        timer_.aux_names = {"iw_jtf_apply", "iw_apply_res", "iw_pcg", "iw_update", "iw_cost"};
         allocate();
     }
     ~ImageWarpingPlan() override {
@@ -2294,6 +2341,7 @@ private:
         side_ = env_int("OPT_AMD_IW_SIDE", 0) != 0;
         apfree_ = env_int("OPT_AMD_IW_APFREE", 1) != 0;
         rec_on_ = env_int("OPT_AMD_IW_REC", 0) != 0;
+        cost60_ = env_int("OPT_AMD_IW_COST60", 1) != 0;
         pcg_nt_ = env_int("OPT_AMD_IW_PCG_NT", 0) != 0;
         pcg_u2_ = env_int("OPT_AMD_IW_PCG_U2", 0);
         // iw_jtf_apply's 60-column strips store 240-B row segments that share cache lines
@@ -2346,7 +2394,7 @@ private:
         nstrips_ = (dom_.W + iw::kStrip - 1) / iw::kStrip;
         if (rows_ <= 0 || rows_auto_) { rows_auto_ = true; rows_ = iw::rows_for(nstrips_, dom_.y_hi - dom_.y_lo); }
         nrowblocks_ = (dom_.y_hi - dom_.y_lo + rows_ * 4 - 1) / (rows_ * 4);
-        red_.ensure(std::max(stencil_blocks(), 2048), 1, 64);
+        red_.ensure(std::max({stencil_blocks(), fused_blocks(), 2048}), 1, 64);
         if (opts_.host_buffers) {
             dO_ = (T*)dmalloc(sizeof(T) * 2 * N);
             dA_ = (T*)dmalloc(sizeof(T) * N);
@@ -2637,9 +2685,18 @@ private:
                            (const T*)pre_, r_, red_.scalars, i_num, i_den, red_.slot(nb, sc_out));
         OPT_HIP_CHECK(hipGetLastError());
     }
+    // iw_cost60 on the fused strips when its 32-bit offsets fit (offsets32_), else iw_cost
     void launch_cost(int sc_out) {
-        const int nb = stencil_blocks();
-        hipLaunchKernelGGL(iw::iw_cost<T>, dim3(nb), dim3(kBlock), 0, stream_, args(), red_.slot(nb, sc_out));
+        if (offsets32_ && cost60_) {
+            iw::Args<T> a = args();
+            a.nstrips = fused_strips();
+            const int nb = fused_blocks();
+            a.tb0 = 0; a.tn0 = nb; a.tb1 = 0;
+            hipLaunchKernelGGL(iw::iw_cost60<T>, dim3(nb), dim3(kBlock), 0, stream_, a, red_.slot(nb, sc_out));
+        } else {
+            const int nb = stencil_blocks();
+            hipLaunchKernelGGL(iw::iw_cost<T>, dim3(nb), dim3(kBlock), 0, stream_, args(), red_.slot(nb, sc_out));
+        }
         OPT_HIP_CHECK(hipGetLastError());
     }
     void launch_flags() {
@@ -2668,6 +2725,12 @@ private:
     // instead of 17, 318 against 218 us; iw_pcg 354 against 347 us — the pass is bound by its
     // VALU work and latency, not by the strip edges' partial lines)
     bool rec_on_ = false;
+    // OPT_AMD_IW_COST60=0: the cost on 64-column strips with edge loads (iw_cost; 147 against
+    // 141 us at 4096^2 fp32). A flat one-pixel-per-thread form with direct neighbour loads
+    // measured 297 us, a bitwise copy of sincosf's small-argument path no change (the device
+    // library already branches around its large-argument reduction): the strip kernels are
+    // bound by their VALU work and load latency, not by the sine
+    bool cost60_ = true;
     bool recl_ = false;                 // the plan holds the REC layout (rec_on_ and the fused loop's knobs)
     T* rec_[3] = {nullptr, nullptr, nullptr};   // REC: iteration i's record in rec_[i % 3] (i % 2 undeferred)
     T* srec_ = nullptr;                 // REC: the S record [u.x u.y angle pre_t], written by iw_jtf_apply
