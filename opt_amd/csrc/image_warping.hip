@@ -166,7 +166,9 @@ __device__ __forceinline__ WaveGeom geom(const Args<T>& a) {
     const int t = lt < a.tn0 ? a.tb0 + lt : a.tb1 + (lt - a.tn0);
     g.tile = t;
     g.lane = threadIdx.x & (kWave - 1);
-    const int w = threadIdx.x / kWave;
+    // the wave index as a wave-uniform (SGPR) value: every row index, bound and row base
+    // derived from it is then scalar arithmetic, not per-lane VALU work
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     int strip, ychunk;
     if (a.side) {
         const int ng = (a.nstrips + kBlock / kWave - 1) / (kBlock / kWave);
@@ -559,7 +561,9 @@ __device__ __forceinline__ WaveGeom geom_fused(const Args<T>& a) {
     g.tile = t;
     const int strip = t % a.nstrips, rb = t / a.nstrips;
     g.lane = threadIdx.x & (kWave - 1);
-    const int w = threadIdx.x / kWave;
+    // the wave index as a wave-uniform (SGPR) value: every row index, bound and row base
+    // derived from it is then scalar arithmetic, not per-lane VALU work
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
     g.x = strip * kFStrip - 2 + g.lane;
     g.edge_lane = false;
     g.ex = g.x;
