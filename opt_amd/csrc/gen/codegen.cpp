@@ -74,6 +74,13 @@ const GraphCache* g_gcache = nullptr;
 // saddr form of global_load, one 32-bit multiply per neighbour instead of a 64-bit address
 // per gathered array
 bool g_off32 = false;
+// the register-strip kernels' row loads / stores through 32-bit offsets (with off32):
+// OPT_AMD_GEN_STRIP32=0 64-bit element indices, 1 32-bit, 2 32-bit kept opaque (opt_o32),
+// 3 opaque for single-element reads only
+int g_strip32 = 2;
+// OPT_AMD_GEN_WIDU=1: the strip kernels' wave index through readfirstlane (row indices and
+// bounds in SGPRs)
+bool g_widu = true;
 
 bool transcendental(const Node& n) {
     return n.op == Op::Sin || n.op == Op::Cos || n.op == Op::Exp || n.op == Op::Log || n.op == Op::Sqrt;
@@ -309,6 +316,13 @@ struct Instance {   // a centred residual shifted so that it contains unknown (i
 GenSource generate(GModel& m, bool dbl, bool off32) {
     GenSource gs;
     g_off32 = off32;
+    {
+        const char* sv = getenv("OPT_AMD_GEN_STRIP32");
+        g_strip32 = sv ? atoi(sv) : 2;
+        const char* wv = getenv("OPT_AMD_GEN_WIDU");
+        g_widu = !wv || atoi(wv) != 0;
+    }
+    const bool s32 = off32 && g_strip32 != 0;
     Pool& P = m.pool;
     const int nd = m.unknown_dims();
     const std::vector<int> unk = m.unknown_images();
@@ -370,6 +384,30 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
     // the 32-bit sum cannot: the compiler must allow for its wrap-around)
     o << "template <typename E> __device__ __forceinline__ E opt_g32(const E* b, int v, unsigned stride, unsigned c) {\n"
          "    return ((const E*)((const char*)b + (unsigned)v * (stride * (unsigned)sizeof(E))))[c];\n}\n";
+    // the same reads and element access through a 32-bit byte offset from a uniform base
+    // (generate's off32: every array below 2 GiB): global_load / global_store with an SGPR
+    // base and one VGPR offset, no 64-bit address arithmetic per access
+    // (the byte offset passes through an empty asm: left visible, the compiler shares one
+    // 64-bit extension of it between arrays and adds each base in 64 bits per access)
+    o << (g_strip32 >= 2 ? "__device__ __forceinline__ unsigned opt_o32(unsigned o) { asm(\"\" : \"+v\"(o)); return o; }\n"
+                         : "__device__ __forceinline__ unsigned opt_o32(unsigned o) { return o; }\n");
+    // (3: the pair reads' offsets left visible)
+    o << (g_strip32 == 3 ? "__device__ __forceinline__ unsigned opt_p32(unsigned o) { return o; }\n"
+                         : "__device__ __forceinline__ unsigned opt_p32(unsigned o) { return opt_o32(o); }\n");
+    o << "template <typename E> __device__ __forceinline__ const E& opt_at32(const E* b, unsigned i) {\n"
+         "    return *(const E*)((const char*)b + opt_o32(i * (unsigned)sizeof(E)));\n}\n"
+         "template <typename E> __device__ __forceinline__ E& opt_at32(E* b, unsigned i) {\n"
+         "    return *(E*)((char*)b + opt_o32(i * (unsigned)sizeof(E)));\n}\n"
+         "template <typename E> __device__ __forceinline__ T opt_ldm32(const E* b, unsigned i, bool c) {\n"
+         "    const E v = opt_at32(b, c ? i : 0u); return c ? (T)v : (T)0;\n}\n"
+         "template <typename E> __device__ __forceinline__ void opt_ldm2_32(const E* b, unsigned i, bool c, T& v0, T& v1) {\n"
+         "    const unsigned j = c ? i : 0u;\n"
+         "    E x, y;\n"
+         "    if ((((unsigned long long)b) & (2 * sizeof(E) - 1)) == 0) {\n"
+         "        struct alignas(2 * sizeof(E)) P2 { E x, y; };\n"
+         "        const P2 v = *(const P2*)((const char*)b + opt_p32(j * (unsigned)sizeof(E))); x = v.x; y = v.y;\n"
+         "    } else { x = opt_at32(b, j); y = opt_at32(b, j + 1); }\n"
+         "    v0 = c ? (T)x : (T)0; v1 = c ? (T)y : (T)0;\n}\n";
     o << "template <typename E> __device__ __forceinline__ T opt_ldm(const E* b, long long i, bool c) {\n"
          "    const E v = b[c ? i : 0]; return c ? (T)v : (T)0;\n}\n"
          // both channels of a 2-channel element (i = its first channel) in one access when
@@ -916,7 +954,8 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         o << "    const int lane = threadIdx.x & 63, z = 0; (void)z;\n"
              "    const int nsx = (W + " << nout - 1 << ") / " << nout << ", G = gridDim.x * 4;\n"
              "    const int RB = max(8, (int)(((long long)H * nsx + G - 1) / G)), nby = (H + RB - 1) / RB;\n"
-             "    for (int wid = (int)opt_xcd_block() * 4 + (threadIdx.x >> 6); wid < nsx * nby; wid += G) {\n"
+             "    for (int wid = " << (g_widu ? "__builtin_amdgcn_readfirstlane((int)opt_xcd_block() * 4 + (threadIdx.x >> 6))"
+                                      : "(int)opt_xcd_block() * 4 + (threadIdx.x >> 6)") << "; wid < nsx * nby; wid += G) {\n"
              "        const int x = (wid % nsx) * " << nout << " + lane - " << loff << ";\n"
              "        const int y0 = (wid / nsx) * RB, y1 = min(H, y0 + RB);\n"
              "        const bool xin = x >= 0 && x < W, xout = xin && lane >= " << loff << " && lane < " << loff + nout << ";\n";
@@ -940,15 +979,17 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         auto load = [&](const std::tuple<int, int, int>& k, const std::string& yy, int dy, const char* sfx) {
             const int i = std::get<1>(k), c = std::get<2>(k), ch = m.images[i].channels;
             const std::string cond = "xin && " + yy + " >= 0 && " + yy + " < H";
-            const std::string pix = "(long long)(" + yy + " * W + x) * " + std::to_string(ch);
+            const std::string pix = s32 ? "(unsigned)(" + yy + " * W + x) * " + std::to_string(ch) + "u"
+                                            : "(long long)(" + yy + " * W + x) * " + std::to_string(ch);
+            const std::string sf = s32 ? "_32(" : "(";
             if (partner(k)) {
                 if (c == 1) return std::string();
                 const auto k1 = std::make_tuple(std::get<0>(k), i, 1);
-                return "opt_ldm2(" + base_of(k) + ", " + pix + ", " + cond + ", " + wname(k, dy) + sfx + ", " +
+                return "opt_ldm2" + sf + base_of(k) + ", " + pix + ", " + cond + ", " + wname(k, dy) + sfx + ", " +
                        wname(k1, dy) + sfx + ");";
             }
-            return wname(k, dy) + sfx + " = opt_ldm(" + base_of(k) + ", " + pix + " + " + std::to_string(c) +
-                   ", " + cond + ");";
+            return wname(k, dy) + sfx + " = opt_ldm" + (s32 ? std::string("32(") : std::string("(")) + base_of(k) +
+                   ", " + pix + " + " + std::to_string(c) + ", " + cond + ");";
         };
         const std::string qy0 = "(y0 - " + std::to_string(maxy) + ")";
         // each window's next top row is loaded one row ahead (<window>_n): its loads are
@@ -985,28 +1026,35 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         }
         o << "        const bool qin = xin && y >= 0 && y < H;\n" << body.str();
         // output row y + miny has all its centres
+        // (off32: the element index as a 32-bit byte offset from the array's base, opt_at32)
+        const std::string ity = s32 ? "unsigned" : "long long";
+        auto at = [&](const std::string& arr, const std::string& e) {
+            return s32 ? "opt_at32(" + arr + ", " + e + ")" : arr + "[" + e + "]";
+        };
         o << "        const int yo = y + " << miny << ";\n"
              "        if (xout && yo >= y0 && yo < y1) {\n"
-             "        const long long lin = (long long)yo * W + x;\n";
-        if (jtf) o << fin.str() << "        a.flags[lin] = act ? 1 : 0;\n";
-        else o << "        const bool act = (a.flags[lin] & 1) != 0;\n";
+             "        const " << ity << " lin = (" << ity << ")yo * W + x;\n";
+        if (jtf) o << fin.str() << "        " << at("a.flags", "lin") << " = act ? 1 : 0;\n";
+        else o << "        const bool act = (" << at("a.flags", "lin") << " & 1) != 0;\n";
         for (int k : unk)
             for (int c = 0; c < m.images[k].channels; ++c) {
-                const std::string el = "a.uoff[" + std::to_string(uslot[k]) + "] + lin * " + std::to_string(m.images[k].channels) +
-                                       " + " + std::to_string(c);
+                const std::string el = "(" + ity + ")a.uoff[" + std::to_string(uslot[k]) + "] + lin * " +
+                                       std::to_string(m.images[k].channels) + " + " + std::to_string(c);
                 const std::string sfx = std::to_string(uslot[k]) + "_" + std::to_string(c) + "_0";
                 if (jtf) {
-                    o << "        { const long long e = " << el << "; r[e] = act ? -ac" << sfx << " : (T)0; diag[e] = dq" << sfx << "; }\n";
+                    o << "        { const " << ity << " e = " << el << "; " << at("r", "e") << " = act ? -ac" << sfx
+                      << " : (T)0; " << at("diag", "e") << " = dq" << sfx << "; }\n";
                     continue;
                 }
                 // p at the output pixel: its row window when one holds row yo (same load)
-                std::string pe = "p[e]";
+                std::string pe = at("p", "e");
                 auto wi = win.find(std::make_tuple(1, k, c));
                 if (wi != win.end() && wi->second.first <= miny && miny <= wi->second.second)
                     pe = wname(wi->first, miny);
-                o << "        { const long long e = " << el << "; const T acc = ac" << sfx << ";\n"
-                     "          if (finish) { const T pe = " << pe << "; const T o = act ? acc + (dadd ? dadd[e] * pe : (T)0) : (T)0; Ap[e] = o; dot += pe * o; }\n"
-                     "          else Ap[e] = acc; }\n";
+                o << "        { const " << ity << " e = " << el << "; const T acc = ac" << sfx << ";\n"
+                     "          if (finish) { const T pe = " << pe << "; const T o = act ? acc + (dadd ? " << at("dadd", "e")
+                  << " * pe : (T)0) : (T)0; " << at("Ap", "e") << " = o; dot += pe * o; }\n"
+                     "          else " << at("Ap", "e") << " = acc; }\n";
             }
         o << "        }\n";
         for (int k : unk)
@@ -1097,7 +1145,8 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
              "    const int lane = threadIdx.x & 63, z = 0; (void)z;\n"
              "    const int nsx = (W + " << nout - 1 << ") / " << nout << ", G = gridDim.x * 4;\n"
              "    const int RB = max(8, (int)(((long long)H * nsx + G - 1) / G)), nby = (H + RB - 1) / RB;\n"
-             "    for (int wid = (int)opt_xcd_block() * 4 + (threadIdx.x >> 6); wid < nsx * nby; wid += G) {\n"
+             "    for (int wid = " << (g_widu ? "__builtin_amdgcn_readfirstlane((int)opt_xcd_block() * 4 + (threadIdx.x >> 6))"
+                                      : "(int)opt_xcd_block() * 4 + (threadIdx.x >> 6)") << "; wid < nsx * nby; wid += G) {\n"
              "        const int x = (wid % nsx) * " << nout << " + lane - " << loff << ";\n"
              "        const int y0 = (wid / nsx) * RB, y1 = min(H, y0 + RB);\n"
              "        const bool xin = x >= 0 && x < W, xout = xin && lane >= " << loff << " && lane < " << loff + nout << ";\n";
@@ -1118,15 +1167,17 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         auto load = [&](const std::tuple<int, int, int>& k, const std::string& yy, int dy, const char* sfx) {
             const int i = std::get<1>(k), c = std::get<2>(k), ch = m.images[i].channels;
             const std::string cond = "xin && " + yy + " >= 0 && " + yy + " < H" + (std::get<0>(k) ? " && delta" : "");
-            const std::string pix = "(long long)(" + yy + " * W + x) * " + std::to_string(ch);
+            const std::string pix = s32 ? "(unsigned)(" + yy + " * W + x) * " + std::to_string(ch) + "u"
+                                            : "(long long)(" + yy + " * W + x) * " + std::to_string(ch);
+            const std::string sf = s32 ? "_32(" : "(";
             if (partner(k)) {
                 if (c == 1) return std::string();
                 const auto k1 = std::make_tuple(std::get<0>(k), i, 1);
-                return "opt_ldm2(" + base_of(k) + ", " + pix + ", " + cond + ", " + wname(k, dy) + sfx + ", " +
+                return "opt_ldm2" + sf + base_of(k) + ", " + pix + ", " + cond + ", " + wname(k, dy) + sfx + ", " +
                        wname(k1, dy) + sfx + ");";
             }
-            return wname(k, dy) + sfx + " = opt_ldm(" + base_of(k) + ", " + pix + " + " + std::to_string(c) +
-                   ", " + cond + ");";
+            return wname(k, dy) + sfx + " = opt_ldm" + (s32 ? std::string("32(") : std::string("(")) + base_of(k) +
+                   ", " + pix + " + " + std::to_string(c) + ", " + cond + ");";
         };
         for (auto& w : win) {
             o << "        T " << wname(w.first, w.second.second) << "_n = 0";
