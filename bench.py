@@ -64,7 +64,7 @@ def apply_bytes_per_px(i: int, liter: int = 10) -> int:
 # bench). FETCH_SIZE reads exactly 1/2 of the bytes on gfx950 for 1/4/8/16-B-per-lane
 # streaming reads and WRITE_SIZE is exact (profiles/r01_fetchcal.json, 1 GiB arrays), so
 # traffic = 2 FETCH_SIZE + WRITE_SIZE, averaged over the lIterations in-loop launches.
-PMC_FILE = os.path.join(ROOT, "profiles", "r04_final2_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r05_pmc.json")
 APPLY_VARIANT = {0: "iw_apply<float, 1, 0,", 1: "iw_apply<float, 2, 1,", 2: "iw_apply<float, 2, 2,"}
 
 
@@ -125,13 +125,13 @@ def pcg_bytes_per_px(i: int, liter: int = 10, defer: bool = IW_DEFER) -> int:
 
 
 def pcg_variant(i: int, defer: bool = IW_DEFER, liter: int = 10) -> str:
-    """The iw_pcg instantiation PCG iteration i >= 1 runs (<T, DM, E, P0, SNT>)."""
+    """The iw_pcg instantiation PCG iteration i >= 1 runs (<T, DM, E, P0, SNT, U2, PF2, REC>)."""
     if defer:
         dm, e = (0, 0) if i % 2 == 1 else ((1, 1) if i == 2 else (2, 1))
     else:
         dm, e = (1 if i == 1 else 2), 0
     p0 = "true" if liter >= 3 and (i == 1 or (defer and i == 2)) else "false"
-    return f"iw_pcg<float, {dm}, {e}, {p0}, false, false>"
+    return f"iw_pcg<float, {dm}, {e}, {p0}, false, false, false, false>"
 
 
 # PCGInit1 fused with the first apply (iw_jtf_apply, one strip pass): Offset 8 + Angle 4 +

@@ -175,6 +175,13 @@ public:
             }
         }
         std::string e;
+        if (n.op != Op::Const && is_bool(id)) {   // a 0 / 1 value: its bool, as a number
+            e = "(T)(" + bv(id) + ")";
+            const std::string name = "t" + std::to_string(id);
+            out(id) << "        const T " << name << " = " << e << ";\n";
+            done_[id] = name;
+            return name;
+        }
         switch (n.op) {
             case Op::Const: done_[id] = lit(n.c); return done_[id];
             case Op::Param: e = "(T)a.prm[" + std::to_string(n.i) + "]"; break;
@@ -201,7 +208,7 @@ public:
             case Op::Log: e = "log(" + v(n.a) + ")"; break;
             case Op::Abs: e = "fabs(" + v(n.a) + ")"; break;
             case Op::Pow: e = "pow(" + v(n.a) + ", " + v(n.b) + ")"; break;
-            case Op::Select: e = "(" + v(n.a) + " != (T)0) ? " + v(n.b) + " : " + v(n.d); break;
+            case Op::Select: e = cond(n.a) + " ? " + v(n.b) + " : " + v(n.d); break;
             case Op::Sample:
                 e = "opt_sample(" + img_ptr(n.i) + ", " + std::to_string(M_.images[n.i].channels) + ", " +
                     std::to_string(n.ch) + ", " + v(n.a) + ", " + v(n.b) + ", W, H)";
@@ -219,6 +226,53 @@ public:
         const std::string name = "t" + std::to_string(id);
         out(id) << "        const T " << name << " = " << e << ";\n";
         done_[id] = name;
+        return name;
+    }
+    // Boolean-valued nodes — comparisons, And / Or / Not, InBox, products of booleans, the
+    // constants 0 and 1 — are emitted as `bool` and turned into T only where a number is
+    // needed: the energies' validity masks (inside * (Mask == 0) * ...) become one && chain
+    // instead of float compares, conversions and multiplies, and a Select reads them directly
+    // (the same 0 / 1 values: a product of 0 / 1 numbers is their logical and).
+    bool is_bool(int id) {
+        auto it = isb_.find(id);
+        if (it != isb_.end()) return it->second;
+        const Node n = P_.at(id);
+        bool r = false;
+        switch (n.op) {
+            case Op::Lt: case Op::Le: case Op::Gt: case Op::Ge: case Op::Eq: case Op::Ne:
+            case Op::And: case Op::Or: case Op::Not: case Op::InBox: r = true; break;
+            case Op::Const: r = n.c == 0.0 || n.c == 1.0; break;
+            case Op::Mul: r = is_bool(n.a) && is_bool(n.b); break;
+            default: r = false;
+        }
+        isb_[id] = r;
+        return r;
+    }
+    // node `id` as a C++ condition (nonzero)
+    std::string cond(int id) { return is_bool(id) ? bv(id) : "(" + v(id) + " != (T)0)"; }
+    // the bool value of boolean node `id`
+    std::string bv(int id) {
+        auto it = bdone_.find(id);
+        if (it != bdone_.end()) return it->second;
+        const Node n = P_.at(id);
+        std::string e;
+        switch (n.op) {
+            case Op::Const: bdone_[id] = n.c != 0.0 ? "true" : "false"; return bdone_[id];
+            case Op::Lt: e = v(n.a) + " < " + v(n.b); break;
+            case Op::Le: e = v(n.a) + " <= " + v(n.b); break;
+            case Op::Gt: e = v(n.a) + " > " + v(n.b); break;
+            case Op::Ge: e = v(n.a) + " >= " + v(n.b); break;
+            case Op::Eq: e = v(n.a) + " == " + v(n.b); break;
+            case Op::Ne: e = v(n.a) + " != " + v(n.b); break;
+            case Op::And: case Op::Mul: e = cond(n.a) + " && " + cond(n.b); break;
+            case Op::Or: e = cond(n.a) + " || " + cond(n.b); break;
+            case Op::Not: e = "!" + cond(n.a); break;
+            case Op::InBox: e = inbox(n.off, n.off2); break;
+            default: e = "false";
+        }
+        const std::string name = "b" + std::to_string(id);
+        out(id) << "        const bool " << name << " = " << e << ";\n";
+        bdone_[id] = name;
         return name;
     }
     // the search direction / step vector at unknown access `u` (a Read of an unknown)
@@ -297,7 +351,8 @@ private:
     std::ostringstream& o_;
     int nd_;
     const std::vector<int>& uslot_;
-    std::map<int, std::string> done_;
+    std::map<int, std::string> done_, bdone_;
+    std::map<int, bool> isb_;
     std::set<int> sincos_, rec_;
     std::map<std::string, std::string> vdone_;
     std::ostringstream* pre_ = nullptr;
