@@ -76,8 +76,8 @@ const GraphCache* g_gcache = nullptr;
 bool g_off32 = false;
 // the register-strip kernels' row loads / stores through 32-bit offsets (with off32):
 // OPT_AMD_GEN_STRIP32=0 64-bit element indices, 1 32-bit, 2 32-bit kept opaque (opt_o32),
-// 3 opaque for single-element reads only
-int g_strip32 = 2;
+// 4 (default) opaque in the kernels without two-channel pair reads
+int g_strip32 = 4;
 // OPT_AMD_GEN_WIDU=1: the strip kernels' wave index through readfirstlane (row indices and
 // bounds in SGPRs)
 bool g_widu = true;
@@ -373,7 +373,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
     g_off32 = off32;
     {
         const char* sv = getenv("OPT_AMD_GEN_STRIP32");
-        g_strip32 = sv ? atoi(sv) : 2;
+        g_strip32 = sv ? atoi(sv) : 4;
         const char* wv = getenv("OPT_AMD_GEN_WIDU");
         g_widu = !wv || atoi(wv) != 0;
     }
@@ -442,26 +442,27 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
     // the same reads and element access through a 32-bit byte offset from a uniform base
     // (generate's off32: every array below 2 GiB): global_load / global_store with an SGPR
     // base and one VGPR offset, no 64-bit address arithmetic per access
-    // (the byte offset passes through an empty asm: left visible, the compiler shares one
-    // 64-bit extension of it between arrays and adds each base in 64 bits per access)
-    o << (g_strip32 >= 2 ? "__device__ __forceinline__ unsigned opt_o32(unsigned o) { asm(\"\" : \"+v\"(o)); return o; }\n"
-                         : "__device__ __forceinline__ unsigned opt_o32(unsigned o) { return o; }\n");
-    // (3: the pair reads' offsets left visible)
-    o << (g_strip32 == 3 ? "__device__ __forceinline__ unsigned opt_p32(unsigned o) { return o; }\n"
-                         : "__device__ __forceinline__ unsigned opt_p32(unsigned o) { return opt_o32(o); }\n");
-    o << "template <typename E> __device__ __forceinline__ const E& opt_at32(const E* b, unsigned i) {\n"
-         "    return *(const E*)((const char*)b + opt_o32(i * (unsigned)sizeof(E)));\n}\n"
-         "template <typename E> __device__ __forceinline__ E& opt_at32(E* b, unsigned i) {\n"
-         "    return *(E*)((char*)b + opt_o32(i * (unsigned)sizeof(E)));\n}\n"
-         "template <typename E> __device__ __forceinline__ T opt_ldm32(const E* b, unsigned i, bool c) {\n"
-         "    const E v = opt_at32(b, c ? i : 0u); return c ? (T)v : (T)0;\n}\n"
-         "template <typename E> __device__ __forceinline__ void opt_ldm2_32(const E* b, unsigned i, bool c, T& v0, T& v1) {\n"
+    // O: the byte offset passes through an empty asm (opt_o32). Left visible, the compiler
+    // shares one 64-bit extension of it between arrays and adds each base in 64 bits per
+    // access; kept opaque, every access takes the SGPR-base form — which measured faster for
+    // kernels whose windows are all single-channel (generated shape_from_shading 161 ->
+    // 150 us) and slower where two-channel pair reads share the offsets (image_warping 192 ->
+    // 205 us), so the strip kernels choose per kernel (OPT_AMD_GEN_STRIP32)
+    o << "__device__ __forceinline__ unsigned opt_o32(unsigned o) { asm(\"\" : \"+v\"(o)); return o; }\n"
+         "template <bool O, typename E> __device__ __forceinline__ const E& opt_at32(const E* b, unsigned i) {\n"
+         "    const unsigned o = i * (unsigned)sizeof(E); return *(const E*)((const char*)b + (O ? opt_o32(o) : o));\n}\n"
+         "template <bool O, typename E> __device__ __forceinline__ E& opt_at32(E* b, unsigned i) {\n"
+         "    const unsigned o = i * (unsigned)sizeof(E); return *(E*)((char*)b + (O ? opt_o32(o) : o));\n}\n"
+         "template <bool O, typename E> __device__ __forceinline__ T opt_ldm32(const E* b, unsigned i, bool c) {\n"
+         "    const E v = opt_at32<O>(b, c ? i : 0u); return c ? (T)v : (T)0;\n}\n"
+         "template <bool O, typename E> __device__ __forceinline__ void opt_ldm2_32(const E* b, unsigned i, bool c, T& v0, T& v1) {\n"
          "    const unsigned j = c ? i : 0u;\n"
          "    E x, y;\n"
          "    if ((((unsigned long long)b) & (2 * sizeof(E) - 1)) == 0) {\n"
          "        struct alignas(2 * sizeof(E)) P2 { E x, y; };\n"
-         "        const P2 v = *(const P2*)((const char*)b + opt_p32(j * (unsigned)sizeof(E))); x = v.x; y = v.y;\n"
-         "    } else { x = opt_at32(b, j); y = opt_at32(b, j + 1); }\n"
+         "        const unsigned o = j * (unsigned)sizeof(E);\n"
+         "        const P2 v = *(const P2*)((const char*)b + (O ? opt_o32(o) : o)); x = v.x; y = v.y;\n"
+         "    } else { x = opt_at32<O>(b, j); y = opt_at32<O>(b, j + 1); }\n"
          "    v0 = c ? (T)x : (T)0; v1 = c ? (T)y : (T)0;\n}\n";
     o << "template <typename E> __device__ __forceinline__ T opt_ldm(const E* b, long long i, bool c) {\n"
          "    const E v = b[c ? i : 0]; return c ? (T)v : (T)0;\n}\n"
@@ -1030,20 +1031,23 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
             if (a0 == win.end() || a1 == win.end() || a0->second != a1->second) return nullptr;
             return &a1->second;
         };
+        bool pairs = false;
+        for (auto& w : win) pairs = pairs || (std::get<2>(w.first) == 0 && partner(w.first));
+        const bool opq = g_strip32 == 2 || (g_strip32 == 4 && !pairs);   // opt_at32<O>
         // statement loading row yy of window k into `dst` (and of its partner channel)
         auto load = [&](const std::tuple<int, int, int>& k, const std::string& yy, int dy, const char* sfx) {
             const int i = std::get<1>(k), c = std::get<2>(k), ch = m.images[i].channels;
             const std::string cond = "xin && " + yy + " >= 0 && " + yy + " < H";
             const std::string pix = s32 ? "(unsigned)(" + yy + " * W + x) * " + std::to_string(ch) + "u"
                                             : "(long long)(" + yy + " * W + x) * " + std::to_string(ch);
-            const std::string sf = s32 ? "_32(" : "(";
+            const std::string sf = s32 ? (opq ? "_32<true>(" : "_32<false>(") : "(";
             if (partner(k)) {
                 if (c == 1) return std::string();
                 const auto k1 = std::make_tuple(std::get<0>(k), i, 1);
                 return "opt_ldm2" + sf + base_of(k) + ", " + pix + ", " + cond + ", " + wname(k, dy) + sfx + ", " +
                        wname(k1, dy) + sfx + ");";
             }
-            return wname(k, dy) + sfx + " = opt_ldm" + (s32 ? std::string("32(") : std::string("(")) + base_of(k) +
+            return wname(k, dy) + sfx + " = opt_ldm" + (s32 ? std::string(opq ? "32<true>(" : "32<false>(") : std::string("(")) + base_of(k) +
                    ", " + pix + " + " + std::to_string(c) + ", " + cond + ");";
         };
         const std::string qy0 = "(y0 - " + std::to_string(maxy) + ")";
@@ -1084,7 +1088,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         // (off32: the element index as a 32-bit byte offset from the array's base, opt_at32)
         const std::string ity = s32 ? "unsigned" : "long long";
         auto at = [&](const std::string& arr, const std::string& e) {
-            return s32 ? "opt_at32(" + arr + ", " + e + ")" : arr + "[" + e + "]";
+            return s32 ? std::string(opq ? "opt_at32<true>(" : "opt_at32<false>(") + arr + ", " + e + ")" : arr + "[" + e + "]";
         };
         o << "        const int yo = y + " << miny << ";\n"
              "        if (xout && yo >= y0 && yo < y1) {\n"
@@ -1219,19 +1223,22 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
             auto a1 = win.find(std::make_tuple(std::get<0>(k), i, 1));
             return a0 != win.end() && a1 != win.end() && a0->second == a1->second;
         };
+        bool pairs = false;
+        for (auto& w : win) pairs = pairs || (std::get<2>(w.first) == 0 && partner(w.first));
+        const bool opq = g_strip32 == 2 || (g_strip32 == 4 && !pairs);   // opt_at32<O>
         auto load = [&](const std::tuple<int, int, int>& k, const std::string& yy, int dy, const char* sfx) {
             const int i = std::get<1>(k), c = std::get<2>(k), ch = m.images[i].channels;
             const std::string cond = "xin && " + yy + " >= 0 && " + yy + " < H" + (std::get<0>(k) ? " && delta" : "");
             const std::string pix = s32 ? "(unsigned)(" + yy + " * W + x) * " + std::to_string(ch) + "u"
                                             : "(long long)(" + yy + " * W + x) * " + std::to_string(ch);
-            const std::string sf = s32 ? "_32(" : "(";
+            const std::string sf = s32 ? (opq ? "_32<true>(" : "_32<false>(") : "(";
             if (partner(k)) {
                 if (c == 1) return std::string();
                 const auto k1 = std::make_tuple(std::get<0>(k), i, 1);
                 return "opt_ldm2" + sf + base_of(k) + ", " + pix + ", " + cond + ", " + wname(k, dy) + sfx + ", " +
                        wname(k1, dy) + sfx + ");";
             }
-            return wname(k, dy) + sfx + " = opt_ldm" + (s32 ? std::string("32(") : std::string("(")) + base_of(k) +
+            return wname(k, dy) + sfx + " = opt_ldm" + (s32 ? std::string(opq ? "32<true>(" : "32<false>(") : std::string("(")) + base_of(k) +
                    ", " + pix + " + " + std::to_string(c) + ", " + cond + ");";
         };
         for (auto& w : win) {
