@@ -1685,8 +1685,11 @@ __global__ __launch_bounds__(kBlock) void iw_cost60(Args<T> a, ReduceSlot rs) {
         auto row = [&](const VRaw<T>& q) { return finish_vrow<T, false, false>(q); };
         VRow<T> up = row(raw_vrow<T, false, false>(a, g, g.y0 - 1)), cur = row(raw_vrow<T, false, false>(a, g, g.y0)),
                 dn = row(raw_vrow<T, false, false>(a, g, g.y0 + 1));
+        // two raw rows in flight (the walk waits on memory, not on issue: SQ_WAIT_ANY 0.49)
+        VRaw<T> n1 = raw_vrow<T, false, false>(a, g, min(g.y0 + 2, g.y1));
         for (int y = g.y0; y < g.y1; ++y) {
-            const VRaw<T> nx = raw_vrow<T, false, false>(a, g, min(y + 2, g.y1));
+            const VRaw<T> nx = n1;
+            n1 = raw_vrow<T, false, false>(a, g, min(y + 3, g.y1));
             const T lox = from_left(cur.ox, (T)0), loy = from_left(cur.oy, (T)0);
             const T rox = from_right(cur.ox, (T)0), roy = from_right(cur.oy, (T)0);
             const float lux = from_left(cur.ux, 0.f), luy = from_left(cur.uy, 0.f);
