@@ -1911,6 +1911,46 @@ __global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O
     }
 }
 
+// PCGLinearUpdate with every p_i kept (ALLP, lIterations <= kAllPMax): the passes carry no
+// delta terms at all, and this kernel forms delta_L = sum_i alpha_i p_i per pixel in
+// PCGStep2's order — alpha_0 p_0, then one fma per iteration — so it is bitwise the
+// per-iteration (and the deferred) update. p_i = pall + i * pstride.
+constexpr int kAllPMax = 16;
+// (L a template parameter: the loop unrolls with every load of a pixel issued back to back)
+template <typename T, int L>
+__global__ __launch_bounds__(kBlock) void iw_update_all(Args<T> a, T* __restrict__ O, T* __restrict__ A,
+                                                        const T* __restrict__ pall, long long pstride,
+                                                        const double* __restrict__ sc, int sc0) {
+    const long long N = a.dom.npix_mem();
+    T al[L];
+#pragma unroll
+    for (int i = 0; i < L; ++i) al[i] = pcg_alpha<T>(sc[sc0 + kSlots * i], sc[sc0 + kSlots * i + 1]);
+    const long long b = a.dom.off(0, a.dom.y_lo), e = a.dom.off(0, a.dom.y_hi);
+    for (long long k = b + (long long)blockIdx.x * blockDim.x + threadIdx.x; k < e;
+         k += (long long)gridDim.x * blockDim.x) {
+        const int f = a.flags[k];
+        Vec2<T> q[L];
+        T qt[L];
+#pragma unroll
+        for (int i = 0; i < L; ++i) {
+            q[i] = reinterpret_cast<const Vec2<T>*>(pall + i * pstride)[k];
+            qt[i] = pall[i * pstride + 2 * N + k];
+        }
+        T dx = al[0] * q[0].x, dy = al[0] * q[0].y, dt = al[0] * qt[0];
+#pragma unroll
+        for (int i = 1; i < L; ++i) {
+            dx = fmad(al[i], q[i].x, dx);
+            dy = fmad(al[i], q[i].y, dy);
+            dt = fmad(al[i], qt[i], dt);
+        }
+        if (f & 1) {
+            const Vec2<T> o = reinterpret_cast<const Vec2<T>*>(O)[k];
+            reinterpret_cast<Vec2<T>*>(O)[k] = Vec2<T>{o.x + dx, o.y + dy};
+            A[k] = A[k] + dt;
+        }
+    }
+}
+
 // ---------------------------------------------------- materialized Jacobian
 // saveJToCRS (solverGPUGaussNewton.t:1004-1022) with generateDumpJ (:385-442): every
 // pixel (excluded ones included, as the reference) writes its 10 residual rows — for s
@@ -2094,8 +2134,16 @@ public:
         const bool res = fused_res_ && offsets32_ && L >= 1;
         // res with defer_: p_i in pb[i % 3]; the delta terms of odd iterations are folded
         // in pairs by the next even iteration (or the update), which reads p_{i-2} again
-        const bool defer = res && defer_;
+        // every p_i kept (OPT_AMD_IW_ALLP, lIterations <= kAllPMax): no pass carries a delta
+        // term, iw_update_all forms delta once at the end
+        const bool allp = allp_ && fused_init_ && offsets32_ && res && apfree_ && !recl_ && L >= 2 &&
+                          L <= iw::kAllPMax;
+        const bool defer = res && defer_ && !allp;
         T* pb[3] = {p0_, p1_, p2_};
+        if (allp) {
+            ensure_pall(L);
+            pcur = pall_;
+        }
         // lIterations >= 3 with the fused loop: nothing but passes 1 and 2 reads p_0, and both
         // form it from r_0 (iw_apply_res P0), so PCGInit1 does not store it
         const bool p0 = res && L >= 3;
@@ -2105,7 +2153,7 @@ public:
         const bool rec = recl_ && fused && apfree;
         if (rec) { pcur = rec_[0]; pb[0] = rec_[0]; pb[1] = rec_[1]; pb[2] = rec_[2]; }
         if (fused) {
-            launch_jtf_apply(p0 ? nullptr : pcur, L == 1 || apfree, rec);
+            launch_jtf_apply(p0 && !allp ? nullptr : pcur, L == 1 || apfree, rec);   // allp: p_0 for the update
             allreduce(rz(0), 4);   // rz_0, p.Ap_0, r_0.W Ap_0, Ap_0.W Ap_0
             if (distributed()) {   // the next pass reads r_0 (and forms p_0) in the halo rows
                 std::vector<HaloPlane> pl;
@@ -2141,7 +2189,7 @@ public:
                            (dom_.y_hi - dom_.y_lo) - (nrowblocks_ - 1) * 4 * rows_ >= 2;
         if (res) {
             // p_i in pb[i % 3] (deferred delta) or pb[i % 2]
-            auto pbuf = [&](int i) { return pb[defer ? i % 3 : i % 2]; };
+            auto pbuf = [&](int i) { return allp ? pall_ + (size_t)i * 3 * dom_.npix_mem() : pb[defer ? i % 3 : i % 2]; };
             if (!fused) {   // iteration 0 with the two extra sums (PCGInit1 ran as iw_jtf)
                 launch_apply<1, 0>(nullptr, pbuf(0), pap(0), 0, 0, 0, 0, nullptr, L == 1, 0, true);
                 allreduce(pap(0), 3);
@@ -2154,7 +2202,7 @@ public:
                 const T* pin2 = (defer && i >= 2) ? ((p0 && i == 2 && !rec) ? rb[0] : pbuf(i - 2)) : nullptr;
                 // part 0: every row block; 1: the interior ones; 2: the first and last
                 auto pass = [&](int part) {
-                    if (apfree) launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0, part, rec);
+                    if (apfree) launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0, part, rec, allp);
                     else launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, part, p0);
                 };
                 if (distributed()) {   // the pass reads r and p (and Ap) of iteration i-1 in the halo rows
@@ -2179,7 +2227,7 @@ public:
                         pass(0);
                     }
                 } else if (apfree) {
-                    launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0, 0, rec);
+                    launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0, 0, rec, allp);
                 } else {
                     launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 0, p0);
                 }
@@ -2223,7 +2271,12 @@ public:
             }
         }
         // PCGLinearUpdate (with the last delta += alpha p) + cost
-        if (L > 0 && defer) {
+        if (allp) {
+            tbegin("iw_update");
+            launch_update_all(L);
+            tend();
+            exchange_unknowns();
+        } else if (L > 0 && defer) {
             // pending: p_{L-1}, and p_{L-2} too when L-1 is odd (the even iterations fold pairs)
             const int ub = flat_grid(dom_.npix_mem(), 1);
             const T* pl = pb[(L - 1) % 3];
@@ -2349,6 +2402,7 @@ private:
         apfree_ = env_int("OPT_AMD_IW_APFREE", 1) != 0;
         rec_on_ = env_int("OPT_AMD_IW_REC", 0) != 0;
         cost60_ = env_int("OPT_AMD_IW_COST60", 1) != 0;
+        allp_ = env_int("OPT_AMD_IW_ALLP", 1) != 0;
         pcg_nt_ = env_int("OPT_AMD_IW_PCG_NT", 0) != 0;
         pcg_u2_ = env_int("OPT_AMD_IW_PCG_U2", 0);
         // iw_jtf_apply's 60-column strips store 240-B row segments that share cache lines
@@ -2410,9 +2464,35 @@ private:
             dM_ = (float*)dmalloc(sizeof(float) * N);
         }
     }
+    template <int K>
+    void launch_update_all_k(int L) {
+        if constexpr (K <= iw::kAllPMax) {
+            if (L != K) { launch_update_all_k<K + 1>(L); return; }
+            hipLaunchKernelGGL((iw::iw_update_all<T, K>), dim3(flat_grid(dom_.npix_mem(), 1)), dim3(kBlock), 0, stream_,
+                               args(), cur_O_, cur_A_, (const T*)pall_, 3 * dom_.npix_mem(),
+                               (const double*)red_.scalars, rz(0));
+            OPT_HIP_CHECK(hipGetLastError());
+        } else {
+            throw std::logic_error("iw_update_all: lIterations above kAllPMax");
+        }
+    }
+    void launch_update_all(int L) { launch_update_all_k<2>(L); }
+    // allp's p vectors, grown to L (lIterations may rise between Steps)
+    void ensure_pall(int L) {
+        if (L <= pall_cap_) return;
+        OPT_HIP_CHECK(hipStreamSynchronize(stream_));
+        dfree(pall_);
+        pall_ = (T*)dmalloc(sizeof(T) * 3 * (size_t)dom_.npix_mem() * L);
+        // (ordered on the plan's stream: a null-stream memset is not ordered against it)
+        OPT_HIP_CHECK(hipMemsetAsync(pall_, 0, sizeof(T) * 3 * (size_t)dom_.npix_mem() * L, stream_));
+        pall_cap_ = L;
+    }
     void release() {
         for (char* p : raw_) dfree(p);
         raw_.clear();
+        dfree(pall_);
+        pall_ = nullptr;
+        pall_cap_ = 0;
         for (T** v : {&r_, &pre_, &p0_, &p1_, &Ap_, &delta_, &r1_, &Ap1_, &p2_}) *v = nullptr;
         flags_ = nullptr;
         for (T*& v : rec_) v = nullptr;
@@ -2563,7 +2643,9 @@ private:
     // part 0: every row block; 1: the interior row blocks [1, nrb - 1); 2: the first and last
     // (the only ones that read halo rows: a wave reads rows y0 - 2 .. y1 + 1)
     // REC: pin / pout / pin2 are the records of iterations i-1, i, i-2 (r and p together)
-    void launch_pcg(int i, const T* pin, T* pout, bool last, const T* pin2, bool p0, int part = 0, bool rec = false) {
+    // nodelta (allp): no delta term in any pass (iw_update_all forms delta)
+    void launch_pcg(int i, const T* pin, T* pout, bool last, const T* pin2, bool p0, int part = 0, bool rec = false,
+                    bool nodelta = false) {
         T* rb[2] = {r_, r1_};
         const T* rin = rec ? pin : rb[(i - 1) & 1];
         T* rout = rec ? pout : (last ? nullptr : rb[i & 1]);
@@ -2589,7 +2671,10 @@ private:
         auto pick = [&](auto nt, auto u2, auto pf2, auto dp) {
             constexpr bool SNT = decltype(nt)::value, U2 = decltype(u2)::value, PF2 = decltype(pf2)::value,
                            DP = decltype(dp)::value;
-            if (pin2 || (defer_ && i == 1)) {
+            if (nodelta) {
+                if (i == 1 && p0) go(iw::iw_pcg<T, 0, 0, true, SNT, U2, PF2, DP>);
+                else go(iw::iw_pcg<T, 0, 0, false, SNT, U2, PF2, DP>);
+            } else if (pin2 || (defer_ && i == 1)) {
                 if (i == 1 && p0) go(iw::iw_pcg<T, 0, 0, true, SNT, U2, PF2, DP>);
                 else if (i % 2 == 1) go(iw::iw_pcg<T, 0, 0, false, SNT, U2, PF2, DP>);
                 else if (i == 2 && p0) go(iw::iw_pcg<T, 1, 1, true, SNT, U2, PF2, DP>);
@@ -2738,6 +2823,11 @@ private:
     // library already branches around its large-argument reduction): the strip kernels are
     // bound by their VALU work and load latency, not by the sine
     bool cost60_ = true;
+    // OPT_AMD_IW_ALLP=0: the deferred delta (pairs folded by the even passes) instead of every
+    // p_i kept for iw_update_all
+    bool allp_ = true;
+    T* pall_ = nullptr;                 // allp: lIterations p vectors of 3 N, p_i = pall_ + 3 N i
+    int pall_cap_ = 0;
     bool recl_ = false;                 // the plan holds the REC layout (rec_on_ and the fused loop's knobs)
     T* rec_[3] = {nullptr, nullptr, nullptr};   // REC: iteration i's record in rec_[i % 3] (i % 2 undeferred)
     T* srec_ = nullptr;                 // REC: the S record [u.x u.y angle pre_t], written by iw_jtf_apply

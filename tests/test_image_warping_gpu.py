@@ -654,6 +654,27 @@ def test_pcg_pass_without_stored_ap_fp64(monkeypatch, W, H):
 
 
 @pytest.mark.parametrize("W,H,lit", [(150, 110, 10), (5, 3, 4), (200, 1, 3), (700, 300, 10), (64, 64, 2),
+                                     (61, 2, 5), (1, 9, 4), (121, 66, 1), (240, 97, 7), (90, 70, 16), (90, 70, 17)])
+@pytest.mark.parametrize("double", [False, True])
+def test_kept_p_update_is_bitwise_the_deferred_delta(monkeypatch, W, H, lit, double):
+    """OPT_AMD_IW_ALLP (default 1, lIterations 2..16): every p_i kept and delta formed once
+    by iw_update_all (alpha_0 p_0, then one fma per iteration) against the deferred delta
+    (pairs folded by the even passes): the trajectory is bitwise the same, fp32 and fp64
+    (lIterations 1 and 17 take the deferred path either way)."""
+    out = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("OPT_AMD_IW_ALLP", v)
+        w = perturbed(W, H, seed=5 * W + H)
+        s = solver(W, H, double=double)
+        prm = device_params(w, double=double)
+        s.set_solver_params({"nIterations": 3, "lIterations": lit})
+        c = np.array(s.profiled_solve(prm))
+        out.append((c, to_np(prm[0]), to_np(prm[1]), np.array(s.scalars(2 + 5 * (lit + 2)))))
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("W,H,lit", [(150, 110, 10), (5, 3, 4), (200, 1, 3), (700, 300, 10), (64, 64, 2),
                                      (61, 2, 5), (1, 9, 4), (121, 66, 1), (240, 97, 7)])
 @pytest.mark.parametrize("double", [False, True])
 def test_rec_layout_is_bitwise_the_image_layout(monkeypatch, W, H, lit, double):
