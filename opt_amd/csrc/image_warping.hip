@@ -1917,10 +1917,13 @@ __global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O
 // per-iteration (and the deferred) update. p_i = pall + i * pstride.
 constexpr int kAllPMax = 16;
 // (L a template parameter: the loop unrolls with every load of a pixel issued back to back)
-template <typename T, int L>
+// P0R: p_0 = pre r_0 formed here from r0 / pre (FRow::p's rounded products), not read
+template <typename T, int L, bool P0R>
 __global__ __launch_bounds__(kBlock) void iw_update_all(Args<T> a, T* __restrict__ O, T* __restrict__ A,
                                                         const T* __restrict__ pall, long long pstride,
-                                                        const double* __restrict__ sc, int sc0) {
+                                                        const double* __restrict__ sc, int sc0,
+                                                        const T* __restrict__ r0, const T* __restrict__ pre) {
+    IW_PRE_TABLE(a);
     const long long N = a.dom.npix_mem();
     T al[L];
 #pragma unroll
@@ -1932,9 +1935,18 @@ __global__ __launch_bounds__(kBlock) void iw_update_all(Args<T> a, T* __restrict
         Vec2<T> q[L];
         T qt[L];
 #pragma unroll
-        for (int i = 0; i < L; ++i) {
+        for (int i = P0R ? 1 : 0; i < L; ++i) {
             q[i] = reinterpret_cast<const Vec2<T>*>(pall + i * pstride)[k];
             qt[i] = pall[i * pstride + 2 * N + k];
+        }
+        if constexpr (P0R) {
+            const T w0 = pre_offset(a, f);
+            const Vec2<T> r = reinterpret_cast<const Vec2<T>*>(r0)[k];
+            vec2_t<T> rv;
+            rv.x = r.x; rv.y = r.y;
+            const vec2_t<T> pv = opaque(w0 * rv);
+            q[0] = Vec2<T>{pv.x, pv.y};
+            qt[0] = opaque(pre[k] * r0[2 * N + k]);
         }
         T dx = al[0] * q[0].x, dy = al[0] * q[0].y, dt = al[0] * qt[0];
 #pragma unroll
@@ -2140,6 +2152,9 @@ public:
                           L <= iw::kAllPMax;
         const bool defer = res && defer_ && !allp;
         T* pb[3] = {p0_, p1_, p2_};
+        // allp with P0: r_0 stays in r_ for the update (the passes ping-pong r over r1_ and the
+        // unused Ap_), which forms p_0 = pre r_0 itself, so PCGInit1 does not store it
+        const bool keep0 = allp && res && L >= 3;
         if (allp) {
             ensure_pall(L);
             pcur = pall_;
@@ -2153,7 +2168,7 @@ public:
         const bool rec = recl_ && fused && apfree;
         if (rec) { pcur = rec_[0]; pb[0] = rec_[0]; pb[1] = rec_[1]; pb[2] = rec_[2]; }
         if (fused) {
-            launch_jtf_apply(p0 && !allp ? nullptr : pcur, L == 1 || apfree, rec);   // allp: p_0 for the update
+            launch_jtf_apply(p0 ? nullptr : pcur, L == 1 || apfree, rec);
             allreduce(rz(0), 4);   // rz_0, p.Ap_0, r_0.W Ap_0, Ap_0.W Ap_0
             if (distributed()) {   // the next pass reads r_0 (and forms p_0) in the halo rows
                 std::vector<HaloPlane> pl;
@@ -2202,7 +2217,7 @@ public:
                 const T* pin2 = (defer && i >= 2) ? ((p0 && i == 2 && !rec) ? rb[0] : pbuf(i - 2)) : nullptr;
                 // part 0: every row block; 1: the interior ones; 2: the first and last
                 auto pass = [&](int part) {
-                    if (apfree) launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0, part, rec, allp);
+                    if (apfree) launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0, part, rec, allp, keep0);
                     else launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, part, p0);
                 };
                 if (distributed()) {   // the pass reads r and p (and Ap) of iteration i-1 in the halo rows
@@ -2210,7 +2225,7 @@ public:
                     if (rec) {
                         pl.push_back({(void*)pbuf(i - 1), 6 * sizeof(T) * dom_.W});
                     } else {
-                        add_vec_planes(pl, rb[(i - 1) & 1]);
+                        add_vec_planes(pl, rvec(i - 1, keep0));
                         if (!apfree) add_vec_planes(pl, ab[(i - 1) & 1]);
                         if (!(p0 && i == 1)) add_vec_planes(pl, pbuf(i - 1));   // P0: pass 1 forms p_0 from r_0
                     }
@@ -2227,7 +2242,7 @@ public:
                         pass(0);
                     }
                 } else if (apfree) {
-                    launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0, 0, rec, allp);
+                    launch_pcg(i, pbuf(i - 1), pbuf(i), last, pin2, p0, 0, rec, allp, keep0);
                 } else {
                     launch_apply_res(i, pbuf(i - 1), pbuf(i), last, pin2, 0, p0);
                 }
@@ -2273,7 +2288,7 @@ public:
         // PCGLinearUpdate (with the last delta += alpha p) + cost
         if (allp) {
             tbegin("iw_update");
-            launch_update_all(L);
+            launch_update_all(L, keep0);
             tend();
             exchange_unknowns();
         } else if (L > 0 && defer) {
@@ -2465,18 +2480,27 @@ private:
         }
     }
     template <int K>
-    void launch_update_all_k(int L) {
+    void launch_update_all_k(int L, bool p0r) {
         if constexpr (K <= iw::kAllPMax) {
-            if (L != K) { launch_update_all_k<K + 1>(L); return; }
-            hipLaunchKernelGGL((iw::iw_update_all<T, K>), dim3(flat_grid(dom_.npix_mem(), 1)), dim3(kBlock), 0, stream_,
-                               args(), cur_O_, cur_A_, (const T*)pall_, 3 * dom_.npix_mem(),
-                               (const double*)red_.scalars, rz(0));
+            if (L != K) { launch_update_all_k<K + 1>(L, p0r); return; }
+            auto k = p0r ? iw::iw_update_all<T, K, true> : iw::iw_update_all<T, K, false>;
+            hipLaunchKernelGGL(k, dim3(flat_grid(dom_.npix_mem(), 1)), dim3(kBlock), 0, stream_, args(), cur_O_, cur_A_,
+                               (const T*)pall_, 3 * dom_.npix_mem(), (const double*)red_.scalars, rz(0),
+                               (const T*)r_, (const T*)pre_);
             OPT_HIP_CHECK(hipGetLastError());
         } else {
             throw std::logic_error("iw_update_all: lIterations above kAllPMax");
         }
     }
-    void launch_update_all(int L) { launch_update_all_k<2>(L); }
+    // p0r: p_0 formed from r_0 (r_, pre_) as iw_jtf_apply forms it, instead of read
+    void launch_update_all(int L, bool p0r) { launch_update_all_k<2>(L, p0r); }
+    // r_i of the fused loop: r_ / r1_ alternating, or with keep0 (r_0 kept for
+    // iw_update_all) r_0 in r_ and r_1, r_2, ... alternating over r1_ and Ap_ (Ap-free passes
+    // never use Ap_)
+    T* rvec(int i, bool keep0) const {
+        if (!keep0) return (i & 1) ? r1_ : r_;
+        return i == 0 ? r_ : (i & 1) ? r1_ : Ap_;
+    }
     // allp's p vectors, grown to L (lIterations may rise between Steps)
     void ensure_pall(int L) {
         if (L <= pall_cap_) return;
@@ -2645,10 +2669,9 @@ private:
     // REC: pin / pout / pin2 are the records of iterations i-1, i, i-2 (r and p together)
     // nodelta (allp): no delta term in any pass (iw_update_all forms delta)
     void launch_pcg(int i, const T* pin, T* pout, bool last, const T* pin2, bool p0, int part = 0, bool rec = false,
-                    bool nodelta = false) {
-        T* rb[2] = {r_, r1_};
-        const T* rin = rec ? pin : rb[(i - 1) & 1];
-        T* rout = rec ? pout : (last ? nullptr : rb[i & 1]);
+                    bool nodelta = false, bool keep0 = false) {
+        const T* rin = rec ? pin : rvec(i - 1, keep0);
+        T* rout = rec ? pout : (last ? nullptr : rvec(i, keep0));
         const double base_scale = (i == 1 && !spec_.use_preconditioner) ? 4.0 : 1.0;
         iw::Args<T> a = args();
         const int fs = fused_strips();
