@@ -1918,7 +1918,7 @@ __global__ __launch_bounds__(kBlock) void iw_update(Args<T> a, T* __restrict__ O
 constexpr int kAllPMax = 16;
 // (L a template parameter: the loop unrolls with every load of a pixel issued back to back)
 // P0R: p_0 = pre r_0 formed here from r0 / pre (FRow::p's rounded products), not read
-template <typename T, int L, bool P0R>
+template <typename T, int L, bool P0R, bool NT = false>
 __global__ __launch_bounds__(kBlock) void iw_update_all(Args<T> a, T* __restrict__ O, T* __restrict__ A,
                                                         const T* __restrict__ pall, long long pstride,
                                                         const double* __restrict__ sc, int sc0,
@@ -1936,8 +1936,14 @@ __global__ __launch_bounds__(kBlock) void iw_update_all(Args<T> a, T* __restrict
         T qt[L];
 #pragma unroll
         for (int i = P0R ? 1 : 0; i < L; ++i) {
-            q[i] = reinterpret_cast<const Vec2<T>*>(pall + i * pstride)[k];
-            qt[i] = pall[i * pstride + 2 * N + k];
+            if constexpr (NT) {   // streaming: every p element is read once
+                const T* pi = pall + i * pstride;
+                q[i] = Vec2<T>{ld_v<true>(pi + 2 * k), ld_v<true>(pi + 2 * k + 1)};
+                qt[i] = ld_v<true>(pi + 2 * N + k);
+            } else {
+                q[i] = reinterpret_cast<const Vec2<T>*>(pall + i * pstride)[k];
+                qt[i] = pall[i * pstride + 2 * N + k];
+            }
         }
         if constexpr (P0R) {
             const T w0 = pre_offset(a, f);
@@ -2418,6 +2424,7 @@ private:
         rec_on_ = env_int("OPT_AMD_IW_REC", 0) != 0;
         cost60_ = env_int("OPT_AMD_IW_COST60", 1) != 0;
         allp_ = env_int("OPT_AMD_IW_ALLP", 1) != 0;
+        upd_nt_ = env_int("OPT_AMD_IW_UPD_NT", 1) != 0;
         pcg_nt_ = env_int("OPT_AMD_IW_PCG_NT", 0) != 0;
         pcg_u2_ = env_int("OPT_AMD_IW_PCG_U2", 0);
         // iw_jtf_apply's 60-column strips store 240-B row segments that share cache lines
@@ -2483,7 +2490,8 @@ private:
     void launch_update_all_k(int L, bool p0r) {
         if constexpr (K <= iw::kAllPMax) {
             if (L != K) { launch_update_all_k<K + 1>(L, p0r); return; }
-            auto k = p0r ? iw::iw_update_all<T, K, true> : iw::iw_update_all<T, K, false>;
+            auto k = upd_nt_ ? (p0r ? iw::iw_update_all<T, K, true, true> : iw::iw_update_all<T, K, false, true>)
+                             : (p0r ? iw::iw_update_all<T, K, true> : iw::iw_update_all<T, K, false>);
             hipLaunchKernelGGL(k, dim3(flat_grid(dom_.npix_mem(), 1)), dim3(kBlock), 0, stream_, args(), cur_O_, cur_A_,
                                (const T*)pall_, 3 * dom_.npix_mem(), (const double*)red_.scalars, rz(0),
                                (const T*)r_, (const T*)pre_);
@@ -2849,6 +2857,9 @@ private:
     // OPT_AMD_IW_ALLP=0: the deferred delta (pairs folded by the even passes) instead of every
     // p_i kept for iw_update_all
     bool allp_ = true;
+    // OPT_AMD_IW_UPD_NT=0: iw_update_all with plain loads of the p vectors (streaming: update
+    // 510-518 -> 474 us, the following cost 116 -> 135 us, GN step 3.39-3.40 -> 3.34-3.37 ms)
+    bool upd_nt_ = true;
     T* pall_ = nullptr;                 // allp: lIterations p vectors of 3 N, p_i = pall_ + 3 N i
     int pall_cap_ = 0;
     bool recl_ = false;                 // the plan holds the REC layout (rec_on_ and the fused loop's knobs)
