@@ -107,8 +107,15 @@ def res_variant(i: int, defer: bool = IW_DEFER, liter: int = 10) -> str:
 # PCG iteration i >= 1 as iw_pcg (the default on one GPU, round 5): iw_apply_res with
 # Ap_{i-1} recomputed from p_{i-1} instead of read back, and Ap_i never stored: Angle 4 +
 # UrShape 8 + flag 1 + angle pre 4 + r_{i-1} 12 + p_{i-1} 12 read, p_i 12 written, r_i 12
-# written except in the last iteration; P0 and the deferred delta as iw_apply_res.
+# written except in the last iteration; P0 and the deferred delta as iw_apply_res. With every
+# p_i kept (OPT_AMD_IW_ALLP, the default for lIterations 2..16) no pass carries a delta term:
+# iw_update_all reads the L p vectors once at the end.
 PCG_KERNEL = "iw_pcg"
+IW_ALLP = os.environ.get("OPT_AMD_IW_ALLP", "1") != "0"
+
+
+def allp_on(liter: int) -> bool:
+    return IW_ALLP and 2 <= liter <= 16
 
 
 def pcg_bytes_per_px(i: int, liter: int = 10, defer: bool = IW_DEFER) -> int:
@@ -117,6 +124,8 @@ def pcg_bytes_per_px(i: int, liter: int = 10, defer: bool = IW_DEFER) -> int:
         b -= 12   # P0: p_0 = pre r_0 from the r_0 the pass reads
     if i < liter - 1:
         b += 12
+    if allp_on(liter):
+        return b
     if defer:
         b += 0 if i % 2 == 1 else (24 if i == 2 else 36)
     else:
@@ -126,7 +135,9 @@ def pcg_bytes_per_px(i: int, liter: int = 10, defer: bool = IW_DEFER) -> int:
 
 def pcg_variant(i: int, defer: bool = IW_DEFER, liter: int = 10) -> str:
     """The iw_pcg instantiation PCG iteration i >= 1 runs (<T, DM, E, P0, SNT, U2, PF2, REC>)."""
-    if defer:
+    if allp_on(liter):
+        dm, e, defer = 0, 0, False
+    elif defer:
         dm, e = (0, 0) if i % 2 == 1 else ((1, 1) if i == 2 else (2, 1))
     else:
         dm, e = (1 if i == 1 else 2), 0
@@ -150,10 +161,12 @@ def init_bytes_per_px(liter: int = 10, ap: bool = True) -> int:
 # Offset 8, Angle 4, delta 12, p_{L-1} 12 (+ p_{L-2} 12 when the deferred pair is pending,
 # lIterations even) and writes Offset + Angle 12; iw_cost reads Offset 8, Angle 4, UrShape 8,
 # Constraints 8, Mask 4.
-STEP_KERNELS = ("iw_jtf_apply", "iw_pcg", "iw_update", "iw_cost")
+STEP_KERNELS = ("iw_jtf_apply", "iw_pcg", "iw_update", "iw_cost")   # iw_update: iw_update_all with allp
 
 
 def update_bytes_per_px(liter: int = 10) -> int:
+    if allp_on(liter):   # iw_update_all: flag, Offset, Angle, r_0 + angle pre (p_0 formed), p_1..p_{L-1}
+        return 1 + 8 + 4 + (16 if liter >= 3 else 12) + 12 * (liter - 1) + 12
     return 1 + 8 + 4 + (12 if liter >= 2 else 0) + 12 + (12 if liter % 2 == 0 else 0) + 12
 
 
@@ -175,6 +188,27 @@ def pmc_traffic(liter: int, first: int = 0, res=False):
             return None
         total += (2.0 * hit[0]["FETCH_SIZE"] + hit[0]["WRITE_SIZE"]) * 1024.0
     return total / (liter - first)
+
+
+def pmc_limiter(liter: int, first: int = 0):
+    """What the in-loop iw_pcg passes wait on, from the same PMC summary's SQ pass: the
+    launch-weighted fractions of wave cycles parked on memory / barriers (SQ_WAIT_ANY),
+    stalled at issue (SQ_WAIT_INST_ANY) and issuing VALU (SQ_ACTIVE_INST_VALU)."""
+    try:
+        with open(PMC_FILE) as f:
+            ks = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    acc = {"SQ_WAIT_ANY": 0.0, "SQ_WAIT_INST_ANY": 0.0, "SQ_ACTIVE_INST_VALU": 0.0}
+    for i in range(first, liter):
+        hit = [v for k, v in ks.items() if pcg_variant(i, liter=liter) in k]
+        if not hit or not hit[0].get("SQ_WAVE_CYCLES") or any(c not in hit[0] for c in acc):
+            return None
+        for c in acc:
+            acc[c] += hit[0][c] / hit[0]["SQ_WAVE_CYCLES"] / (liter - first)
+    return {"wait_memory": round(acc["SQ_WAIT_ANY"], 3), "wait_issue": round(acc["SQ_WAIT_INST_ANY"], 3),
+            "valu_active": round(acc["SQ_ACTIVE_INST_VALU"], 3),
+            "source": os.path.relpath(PMC_FILE, ROOT) + " (fractions of SQ_WAVE_CYCLES)"}
 
 
 PMC_FILE_SFS = os.path.join(ROOT, "profiles", "r05_final_pmc_sfs.json")
@@ -551,6 +585,9 @@ def main():
             "avg_us": avg_apply_s * 1e6,
             "launches": n_apply,
             "bytes_per_px": bpp,
+            # the pass is bound by VALU issue, not HBM, when wait_issue dominates
+            "limiter": (pmc_limiter(args.liter, first) if res == "pcg" and world == 1 and args.size == 4096
+                        else None),
         },
     }
     if n_init:
