@@ -2426,7 +2426,7 @@ private:
         allp_ = env_int("OPT_AMD_IW_ALLP", 1) != 0;
         upd_nt_ = env_int("OPT_AMD_IW_UPD_NT", 1) != 0;
         pcg_nt_ = env_int("OPT_AMD_IW_PCG_NT", 0) != 0;
-        pcg_u2_ = env_int("OPT_AMD_IW_PCG_U2", 0);
+        pcg_u2_ = env_int("OPT_AMD_IW_PCG_U2", 1);
         // iw_jtf_apply's 60-column strips store 240-B row segments that share cache lines
         // with the neighbouring strips: plain stores (merged in the L2) measured 217-220 us
         // against 233-245 with streaming ones (round 5, same box, interleaved)
@@ -2866,7 +2866,10 @@ private:
     T* rec_[3] = {nullptr, nullptr, nullptr};   // REC: iteration i's record in rec_[i % 3] (i % 2 undeferred)
     T* srec_ = nullptr;                 // REC: the S record [u.x u.y angle pre_t], written by iw_jtf_apply
     bool pcg_nt_ = false;               // OPT_AMD_IW_PCG_NT=1: iw_pcg with streaming stores
-    int pcg_u2_ = 0;                    // OPT_AMD_IW_PCG_U2=1: iw_pcg two rows per trip (U2); 2: and two rows in flight (PF2)
+    // OPT_AMD_IW_PCG_U2: 0 one row per loop trip, 1 (default since the kept-p loop: 275 ->
+    // 270 us per pass, GN step 3.35 -> 3.30 ms) two rows with the records swapping roles,
+    // 2 the same with two raw rows in flight
+    int pcg_u2_ = 1;
     bool jtf_nt_ = false;               // OPT_AMD_IW_JTF_NT=1: iw_jtf_apply with streaming stores
     bool offsets32_ = true;             // iw_apply_res's 32-bit byte offsets cover every plan vector
     int rows_ = 0, nstrips_ = 0, nrowblocks_ = 0;

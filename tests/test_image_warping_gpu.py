@@ -653,6 +653,28 @@ def test_pcg_pass_without_stored_ap_fp64(monkeypatch, W, H):
     np.testing.assert_allclose(out[1][0], c_ref, rtol=1e-8)
 
 
+@pytest.mark.parametrize("W,H,lit", [(150, 110, 10), (5, 3, 4), (200, 1, 3), (700, 300, 10), (61, 2, 5),
+                                     (1, 9, 4), (240, 97, 7), (333, 131, 17)])
+@pytest.mark.parametrize("double", [False, True])
+def test_pcg_row_pairs_are_bitwise_one_row_per_trip(monkeypatch, W, H, lit, double):
+    """OPT_AMD_IW_PCG_U2 (default 1): iw_pcg walking two rows per loop trip with the row
+    records swapping roles (1), and with two raw rows in flight (2), against one row per
+    trip (0): the same arithmetic in the same order — the trajectory is bitwise the same
+    (odd and even row counts per wave, one-row images, the deferred-delta loop at 17)."""
+    out = []
+    for v in ("0", "1", "2"):
+        monkeypatch.setenv("OPT_AMD_IW_PCG_U2", v)
+        w = perturbed(W, H, seed=3 * W + H)
+        s = solver(W, H, double=double)
+        prm = device_params(w, double=double)
+        s.set_solver_params({"nIterations": 3, "lIterations": lit})
+        c = np.array(s.profiled_solve(prm))
+        out.append((c, to_np(prm[0]), to_np(prm[1]), np.array(s.scalars(2 + 5 * (lit + 2)))))
+    for o in out[1:]:
+        for a, b in zip(out[0], o):
+            np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("W,H,lit", [(150, 110, 10), (5, 3, 4), (200, 1, 3), (700, 300, 10), (64, 64, 2),
                                      (61, 2, 5), (1, 9, 4), (121, 66, 1), (240, 97, 7), (90, 70, 16), (90, 70, 17)])
 @pytest.mark.parametrize("double", [False, True])
