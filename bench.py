@@ -142,7 +142,9 @@ def pcg_variant(i: int, defer: bool = IW_DEFER, liter: int = 10) -> str:
     else:
         dm, e = (1 if i == 1 else 2), 0
     p0 = "true" if liter >= 3 and (i == 1 or (defer and i == 2)) else "false"
-    return f"iw_pcg<float, {dm}, {e}, {p0}, false, false, false, false>"
+    u2 = int(os.environ.get("OPT_AMD_IW_PCG_U2", "1"))   # the plan's default: two rows per trip
+    return (f"iw_pcg<float, {dm}, {e}, {p0}, false, {'true' if u2 >= 1 else 'false'}, "
+            f"{'true' if u2 == 2 else 'false'}, false>")
 
 
 # PCGInit1 fused with the first apply (iw_jtf_apply, one strip pass): Offset 8 + Angle 4 +

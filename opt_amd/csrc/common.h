@@ -104,6 +104,31 @@ __device__ __forceinline__ double from_right(double v, double e) {
     return *reinterpret_cast<double*>(&r);
 }
 
+// The same shifts with 0 shifted into the end lane by the hardware (bound_ctrl): no
+// register has to be set to the edge value first (one instruction per shift, not two)
+__device__ __forceinline__ float from_left0(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float from_right0(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true));
+}
+__device__ __forceinline__ int from_left0_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, true); }
+__device__ __forceinline__ int from_right0_i(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, true); }
+__device__ __forceinline__ double from_left0(double v) {
+    int2 vi = *reinterpret_cast<int2*>(&v);
+    int2 r;
+    r.x = __builtin_amdgcn_update_dpp(0, vi.x, 0x138, 0xf, 0xf, true);
+    r.y = __builtin_amdgcn_update_dpp(0, vi.y, 0x138, 0xf, 0xf, true);
+    return *reinterpret_cast<double*>(&r);
+}
+__device__ __forceinline__ double from_right0(double v) {
+    int2 vi = *reinterpret_cast<int2*>(&v);
+    int2 r;
+    r.x = __builtin_amdgcn_update_dpp(0, vi.x, 0x130, 0xf, 0xf, true);
+    r.y = __builtin_amdgcn_update_dpp(0, vi.y, 0x130, 0xf, 0xf, true);
+    return *reinterpret_cast<double*>(&r);
+}
+
 #include "reduce_dev.h"   // ReduceSlot, wave_sum, block_reduce_publish (also pasted into generated kernels)
 
 // XCD-aware bijective remap of a linear block id (cdna_hip_programming.md §5.5 T1):

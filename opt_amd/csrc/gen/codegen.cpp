@@ -410,12 +410,13 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
          "__device__ __forceinline__ void opt_sincos(double x, double* s, double* c) { sincos(x, s, c); }\n";
     // whole-wave DPP lane shifts (wave_shl:1 / wave_shr:1): opt_sh(v, d) is v of lane l + d
     // (0 past the wave's ends); d is a literal at every use, so the loops unroll away
-    o << "__device__ __forceinline__ float opt_lr(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false)); }\n"
-         "__device__ __forceinline__ float opt_ll(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false)); }\n"
+    // (bound_ctrl: the hardware shifts 0 into the end lane, no register set to 0 first)
+    o << "__device__ __forceinline__ float opt_lr(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true)); }\n"
+         "__device__ __forceinline__ float opt_ll(float v) { return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true)); }\n"
          "__device__ __forceinline__ double opt_dd(double v, bool r) {\n"
          "    const long long b = __double_as_longlong(v);\n"
-         "    const int lo = r ? __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xf, 0xf, false) : __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xf, 0xf, false);\n"
-         "    const int hi = r ? __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, false) : __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, false);\n"
+         "    const int lo = r ? __builtin_amdgcn_update_dpp(0, (int)b, 0x130, 0xf, 0xf, true) : __builtin_amdgcn_update_dpp(0, (int)b, 0x138, 0xf, 0xf, true);\n"
+         "    const int hi = r ? __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x130, 0xf, 0xf, true) : __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x138, 0xf, 0xf, true);\n"
          "    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);\n}\n"
          "__device__ __forceinline__ double opt_lr(double v) { return opt_dd(v, true); }\n"
          "__device__ __forceinline__ double opt_ll(double v) { return opt_dd(v, false); }\n"

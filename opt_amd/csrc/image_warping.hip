@@ -873,13 +873,13 @@ __global__ __launch_bounds__(kBlock) void iw_apply_res(Args<T> a, const T* __res
 template <typename T>
 __device__ __forceinline__ vec2_t<T> shl2(vec2_t<T> v) {   // lane l gets lane l-1's (0 at lane 0)
     vec2_t<T> o;
-    o.x = from_left(v.x, (T)0); o.y = from_left(v.y, (T)0);
+    o.x = from_left0(v.x); o.y = from_left0(v.y);
     return o;
 }
 template <typename T>
 __device__ __forceinline__ vec2_t<T> shr2(vec2_t<T> v) {   // lane l gets lane l+1's (0 at lane 63)
     vec2_t<T> o;
-    o.x = from_right(v.x, (T)0); o.y = from_right(v.y, (T)0);
+    o.x = from_right0(v.x); o.y = from_right0(v.y);
     return o;
 }
 // jedge in pairs: the residual pair J(j -> t) applied to p, and a = dR(t_j)/dt (U_j - U_t)
@@ -920,7 +920,7 @@ __device__ __forceinline__ void apply_ap2(vec2_t<T> cp, T cpt, T cc, T cs, vec2_
                                           ACarry<T>& k, vec2_t<T>& ao, T& aot) {
     const vec2_t<T> lp = shl2(cp), rp = shr2(cp);
     const vec2_t<float> lu = shl2(cu), ru = shr2(cu);
-    const int lact = from_left_i((int)cact, 0), ract = from_right_i((int)cact, 0);
+    const int lact = from_left0_i((int)cact), ract = from_right0_i((int)cact);
     vec2_t<T> jpx, apx, jmx, amx, jpy, apy, jdn, adn;
     jedge2(cp, cpt, cc, cs, cu, rp, ru, cact && ract, wr, jpx, apx);
     jedge2(cp, cpt, cc, cs, cu, lp, lu, cact && lact, wr, jmx, amx);
@@ -1362,11 +1362,17 @@ __device__ __forceinline__ JRow<T> jtf_row(const Args<T>& a, const VRow<T>& cur,
     const T wr = a.wr, wf = a.wf, wr2 = a.wr * a.wr;
     JRow<T> o;
     T ax, ay;
-    const T lox = from_left(cur.ox, cur.eox), loy = from_left(cur.oy, cur.eoy);
-    const T rox = from_right(cur.ox, cur.eox), roy = from_right(cur.oy, cur.eoy);
-    const float lux = from_left(cur.ux, cur.eux), luy = from_left(cur.uy, cur.euy);
-    const float rux = from_right(cur.ux, cur.eux), ruy = from_right(cur.uy, cur.euy);
-    const int lact = from_left_i(cur.act, cur.eact), ract = from_right_i(cur.act, cur.eact);
+    // (EDGE = false: zero-fill shifts, the end lanes' values are unused)
+    const T lox = EDGE ? from_left(cur.ox, cur.eox) : from_left0(cur.ox);
+    const T loy = EDGE ? from_left(cur.oy, cur.eoy) : from_left0(cur.oy);
+    const T rox = EDGE ? from_right(cur.ox, cur.eox) : from_right0(cur.ox);
+    const T roy = EDGE ? from_right(cur.oy, cur.eoy) : from_right0(cur.oy);
+    const float lux = EDGE ? from_left(cur.ux, cur.eux) : from_left0(cur.ux);
+    const float luy = EDGE ? from_left(cur.uy, cur.euy) : from_left0(cur.uy);
+    const float rux = EDGE ? from_right(cur.ux, cur.eux) : from_right0(cur.ux);
+    const float ruy = EDGE ? from_right(cur.uy, cur.euy) : from_right0(cur.uy);
+    const int lact = EDGE ? from_left_i(cur.act, cur.eact) : from_left0_i(cur.act);
+    const int ract = EDGE ? from_right_i(cur.act, cur.eact) : from_right0_i(cur.act);
     const bool vpx = cur.act && ract, vmx = cur.act && lact, vpy = cur.act && dn.act;
     T epx_x, epx_y, apx_x, apx_y, emx_x, emx_y, amx_x, amx_y;
     T epy_x, epy_y, apy_x, apy_y, edn_x, edn_y, adn_x, adn_y, ee_x, ee_y;
@@ -1385,8 +1391,10 @@ __device__ __forceinline__ JRow<T> jtf_row(const Args<T>& a, const VRow<T>& cur,
     } else {
         ee_x = 0; ee_y = 0;
     }
-    const T inpx_x = from_right(emx_x, ee_x), inpx_y = from_right(emx_y, ee_y);
-    const T inmx_x = from_left(epx_x, ee_x), inmx_y = from_left(epx_y, ee_y);
+    const T inpx_x = EDGE ? from_right(emx_x, ee_x) : from_right0(emx_x);
+    const T inpx_y = EDGE ? from_right(emx_y, ee_y) : from_right0(emx_y);
+    const T inmx_x = EDGE ? from_left(epx_x, ee_x) : from_left0(epx_x);
+    const T inmx_y = EDGE ? from_left(epx_y, ee_y) : from_left0(epx_y);
     o.fx = wr * ((epx_x + emx_x + epy_x + k.my_x) - (inpx_x + inmx_x + edn_x + k.inup_x));
     o.fy = wr * ((epx_y + emx_y + epy_y + k.my_y) - (inpx_y + inmx_y + edn_y + k.inup_y));
     o.ft = k.thm - wr * ((apx_x * epx_x + apx_y * epx_y) + (amx_x * emx_x + amx_y * emx_y) +
@@ -1690,11 +1698,11 @@ __global__ __launch_bounds__(kBlock) void iw_cost60(Args<T> a, ReduceSlot rs) {
         for (int y = g.y0; y < g.y1; ++y) {
             const VRaw<T> nx = n1;
             n1 = raw_vrow<T, false, false>(a, g, min(y + 3, g.y1));
-            const T lox = from_left(cur.ox, (T)0), loy = from_left(cur.oy, (T)0);
-            const T rox = from_right(cur.ox, (T)0), roy = from_right(cur.oy, (T)0);
-            const float lux = from_left(cur.ux, 0.f), luy = from_left(cur.uy, 0.f);
-            const float rux = from_right(cur.ux, 0.f), ruy = from_right(cur.uy, 0.f);
-            const int lact = from_left_i(cur.act, 0), ract = from_right_i(cur.act, 0);
+            const T lox = from_left0(cur.ox), loy = from_left0(cur.oy);
+            const T rox = from_right0(cur.ox), roy = from_right0(cur.oy);
+            const float lux = from_left0(cur.ux), luy = from_left0(cur.uy);
+            const float rux = from_right0(cur.ux), ruy = from_right0(cur.uy);
+            const int lact = from_left0_i(cur.act), ract = from_right0_i(cur.act);
             T ex, ey, ax, ay, sum = 0;
             eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, rox, roy, rux, ruy,
                   cur.act && ract, wr, ex, ey, ax, ay);
