@@ -2433,6 +2433,7 @@ private:
         cost60_ = env_int("OPT_AMD_IW_COST60", 1) != 0;
         allp_ = env_int("OPT_AMD_IW_ALLP", 1) != 0;
         upd_nt_ = env_int("OPT_AMD_IW_UPD_NT", 1) != 0;
+        upd_blocks_ = std::max(1, env_int("OPT_AMD_IW_UPD_BLOCKS", 2048));
         pcg_nt_ = env_int("OPT_AMD_IW_PCG_NT", 0) != 0;
         pcg_u2_ = env_int("OPT_AMD_IW_PCG_U2", 1);
         // iw_jtf_apply's 60-column strips store 240-B row segments that share cache lines
@@ -2500,7 +2501,9 @@ private:
             if (L != K) { launch_update_all_k<K + 1>(L, p0r); return; }
             auto k = upd_nt_ ? (p0r ? iw::iw_update_all<T, K, true, true> : iw::iw_update_all<T, K, false, true>)
                              : (p0r ? iw::iw_update_all<T, K, true> : iw::iw_update_all<T, K, false>);
-            hipLaunchKernelGGL(k, dim3(flat_grid(dom_.npix_mem(), 1)), dim3(kBlock), 0, stream_, args(), cur_O_, cur_A_,
+            const long long need = (dom_.npix_mem() + kBlock - 1) / kBlock;
+            const int grid = (int)std::max(1LL, std::min<long long>(need, upd_blocks_));
+            hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, stream_, args(), cur_O_, cur_A_,
                                (const T*)pall_, 3 * dom_.npix_mem(), (const double*)red_.scalars, rz(0),
                                (const T*)r_, (const T*)pre_);
             OPT_HIP_CHECK(hipGetLastError());
@@ -2868,6 +2871,7 @@ private:
     // OPT_AMD_IW_UPD_NT=0: iw_update_all with plain loads of the p vectors (streaming: update
     // 510-518 -> 474 us, the following cost 116 -> 135 us, GN step 3.39-3.40 -> 3.34-3.37 ms)
     bool upd_nt_ = true;
+    int upd_blocks_ = 2048;             // OPT_AMD_IW_UPD_BLOCKS: iw_update_all's grid cap (grid-stride beyond)
     T* pall_ = nullptr;                 // allp: lIterations p vectors of 3 N, p_i = pall_ + 3 N i
     int pall_cap_ = 0;
     bool recl_ = false;                 // the plan holds the REC layout (rec_on_ and the fused loop's knobs)
