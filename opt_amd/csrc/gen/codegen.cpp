@@ -61,6 +61,33 @@ const char* elem_type(const std::string& e, bool unknown) {
 // the cached values are the bits the kernels would compute.
 using CacheMap = std::map<std::tuple<int, int, int>, int>;
 const CacheMap* g_cache = nullptr;
+// Per-step predicate cache (the register strips): comparisons of a centred read of a user
+// array with a constant (Mask == 0, Constraints >= 0, ...) packed as bits of one uint8
+// image, filled by a precompute kernel once per Step — a strip reads one byte per pixel
+// instead of the arrays the masks test. Bit k holds pred_k(v) XOR pred_k(0), so the 0 a
+// window reads outside the image decodes to pred_k(0), the value the uncached expression
+// gives there. Key: (op, image, channel, constant, read on the left).
+struct PredCache {
+    int img = -1;
+    std::vector<std::tuple<int, int, int, double, bool>> keys;
+    std::vector<bool> at0;   // pred_k(0)
+};
+const PredCache* g_pred = nullptr;
+// bit index of predicate node n (and its Read child), -1 when n is not a cached predicate
+int pred_bit(const Pool& P, const Node& n, int* rd) {
+    if (!g_pred) return -1;
+    if (n.op != Op::Lt && n.op != Op::Le && n.op != Op::Gt && n.op != Op::Ge && n.op != Op::Eq && n.op != Op::Ne) return -1;
+    double c;
+    bool left;
+    if (P.is_const(n.b, &c) && P.at(n.a).op == Op::Read) { left = true; *rd = n.a; }
+    else if (P.is_const(n.a, &c) && P.at(n.b).op == Op::Read) { left = false; *rd = n.b; }
+    else return -1;
+    const Node& r = P.at(*rd);
+    if (r.slot >= 0) return -1;
+    for (size_t k = 0; k < g_pred->keys.size(); ++k)
+        if (g_pred->keys[k] == std::make_tuple((int)n.op, r.i, r.ch, c, left)) return (int)k;
+    return -1;
+}
 // Graph energies: the same values for slot reads, packed per vertex into one record image
 // (channel k of the record = key k) — a gather pass evaluates every incident edge, so the
 // other slot's sin / cos would be re-evaluated once per edge (ARAP's angles: three
@@ -81,6 +108,9 @@ int g_strip32 = 4;
 // OPT_AMD_GEN_WIDU=1: the strip kernels' wave index through readfirstlane (row indices and
 // bounds in SGPRs)
 bool g_widu = true;
+// OPT_AMD_GEN_FACTOR=0: the strip apply masks every partial of a masked residual (else the
+// residual's mask once, on Jp)
+bool g_factor = true;
 
 bool transcendental(const Node& n) {
     return n.op == Op::Sin || n.op == Op::Cos || n.op == Op::Exp || n.op == Op::Log || n.op == Op::Sqrt;
@@ -250,12 +280,25 @@ public:
     }
     // node `id` as a C++ condition (nonzero)
     std::string cond(int id) { return is_bool(id) ? bv(id) : "(" + v(id) + " != (T)0)"; }
+    // the strip kernels read cached predicates (g_pred) from the bit image's row windows
+    void use_pred(bool on) { use_pred_ = on; }
     // the bool value of boolean node `id`
     std::string bv(int id) {
         auto it = bdone_.find(id);
         if (it != bdone_.end()) return it->second;
         const Node n = P_.at(id);
         std::string e;
+        int rd = -1;
+        const int k = use_pred_ ? pred_bit(P_, n, &rd) : -1;
+        if (k >= 0) {
+            const int pr = P_.read(g_pred->img, 0, P_.at(rd).off);
+            const std::string w = read(P_.at(pr), nullptr);
+            e = "((((int)(" + w + ")) >> " + std::to_string(k) + ") & 1) " + (g_pred->at0[k] ? "== 0" : "!= 0");
+            const std::string name = "b" + std::to_string(id);
+            out(id) << "        const bool " << name << " = " << e << ";\n";
+            bdone_[id] = name;
+            return name;
+        }
         switch (n.op) {
             case Op::Const: bdone_[id] = n.c != 0.0 ? "true" : "false"; return bdone_[id];
             case Op::Lt: e = v(n.a) + " < " + v(n.b); break;
@@ -353,6 +396,7 @@ private:
     const std::vector<int>& uslot_;
     std::map<int, std::string> done_, bdone_;
     std::map<int, bool> isb_;
+    bool use_pred_ = false;
     std::set<int> sincos_, rec_;
     std::map<std::string, std::string> vdone_;
     std::ostringstream* pre_ = nullptr;
@@ -376,6 +420,8 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         g_strip32 = sv ? atoi(sv) : 4;
         const char* wv = getenv("OPT_AMD_GEN_WIDU");
         g_widu = !wv || atoi(wv) != 0;
+        const char* fv = getenv("OPT_AMD_GEN_FACTOR");
+        g_factor = !fv || atoi(fv) != 0;
     }
     const bool s32 = off32 && g_strip32 != 0;
     Pool& P = m.pool;
@@ -588,6 +634,83 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         }
     }
     g_cache = cache.empty() ? nullptr : &cache;
+
+    // predicate cache (see g_pred): up to 8 comparisons of a user array on the unknowns'
+    // domain with a constant, from the centred residuals and the Exclude expression
+    PredCache pcache;
+    {
+        const char* pv = getenv("OPT_AMD_GEN_PRED");
+        const bool on = !pv || atoi(pv) != 0;
+        const int uimg = unk.empty() ? -1 : unk[0];
+        auto cmp0 = [](Op op, double l, double r) {
+            switch (op) {
+                case Op::Lt: return l < r;
+                case Op::Le: return l <= r;
+                case Op::Gt: return l > r;
+                case Op::Ge: return l >= r;
+                case Op::Eq: return l == r;
+                default: return l != r;
+            }
+        };
+        auto consider = [&](int root) {
+            P.visit(root, [&](int, const Node& n) {
+                if (n.op != Op::Lt && n.op != Op::Le && n.op != Op::Gt && n.op != Op::Ge && n.op != Op::Eq &&
+                    n.op != Op::Ne)
+                    return;
+                double c;
+                bool left;
+                int rd;
+                if (P.is_const(n.b, &c) && P.at(n.a).op == Op::Read) { left = true; rd = n.a; }
+                else if (P.is_const(n.a, &c) && P.at(n.b).op == Op::Read) { left = false; rd = n.b; }
+                else return;
+                const Node r = P.at(rd);
+                if (r.slot >= 0) return;
+                const GImage& im = m.images[r.i];
+                if (im.unknown || im.internal || im.dims != m.images[uimg].dims) return;
+                const auto key = std::make_tuple((int)n.op, r.i, r.ch, c, left);
+                for (auto& k : pcache.keys)
+                    if (k == key) return;
+                if (pcache.keys.size() >= 8) return;
+                pcache.keys.push_back(key);
+                pcache.at0.push_back(left ? cmp0(n.op, 0.0, c) : cmp0(n.op, c, 0.0));
+            });
+        };
+        if (on && uimg >= 0 && m.images.size() < 16 && nd == 2) {
+            for (auto& r : m.residuals)
+                if (r.graph < 0) consider(r.expr);
+            if (m.exclude >= 0) consider(m.exclude);
+        }
+        if (!pcache.keys.empty()) {
+            GImage pi;
+            pi.name = "pred_bits";
+            pi.dims = m.images[uimg].dims;
+            pi.internal = true;
+            pi.tvalued = false;
+            pi.elem = "uint8";
+            pi.channels = 1;
+            m.images.push_back(pi);
+            pcache.img = (int)m.images.size() - 1;
+            o << "extern \"C\" __global__ __launch_bounds__(256) void gen_precompute_" << gs.n_precompute << "(GenArgs a) {\n"
+                 "    OPT_COORDS\n"
+                 "    for (long long lin = a.own_lo + (long long)blockIdx.x * 256 + threadIdx.x; lin < a.own_hi; lin += (long long)gridDim.x * 256) {\n"
+              << coords;
+            Body b(m, o, nd, uslot);
+            b.line("unsigned bits = 0;");
+            const int z0[3] = {0, 0, 0};
+            for (size_t k = 0; k < pcache.keys.size(); ++k) {
+                const auto& key = pcache.keys[k];
+                const Op op = (Op)std::get<0>(key);
+                const int rd0 = P.read(std::get<1>(key), std::get<2>(key), z0), cn = P.cnst(std::get<3>(key));
+                const int pn = std::get<4>(key) ? P.bin(op, rd0, cn) : P.bin(op, cn, rd0);
+                b.line("bits |= (" + b.cond(pn) + (pcache.at0[k] ? " ? 0u : 1u" : " ? 1u : 0u") + ") << " +
+                       std::to_string(k) + ";");
+            }
+            b.line("((unsigned char*)a.img[" + std::to_string(pcache.img) + "])[lin] = (unsigned char)bits;");
+            o << "    }\n}\n";
+            ++gs.n_precompute;
+        }
+    }
+    g_pred = pcache.keys.empty() ? nullptr : &pcache;
 
     // graph record cache (see g_gcache): transcendentals of slot reads of arrays on the
     // unknowns' domain, one record per vertex, filled by one more precompute kernel
@@ -915,6 +1038,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         g_cache = nullptr;   // sin / cos of a window value: no cache images
         {
             Body b(m, body, nd, uslot);
+            b.use_pred(true);
             b.centred_reads([&](const Node& n, const char* vname) {
                 const auto key = std::make_tuple(vname ? 1 : 0, n.i, n.ch);
                 auto it = win.find(key);
@@ -927,6 +1051,57 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
             });
             std::vector<std::string> dname(ents.size());
             for (size_t ci = 0; ci < cres.size(); ++ci) {
+                // A residual Select(c1, Select(c2, e, 0), 0) has partials Select(c1, Select(c2,
+                // de, 0), 0): its mask is evaluated once (m<ci>) and applied to Jp alone — each
+                // partial's contribution d * Jp is then 0 with it — instead of a select per
+                // partial; only when every partial is free of operations that can be non-finite
+                // where the mask is off (division, sqrt, log, pow, exp), where 0 * d could be NaN.
+                std::vector<int> conds;
+                std::vector<int> de(ents.size(), -1);
+                bool factor = !jtf && g_factor;
+                if (factor) {
+                    int core = m.residuals[cres[ci]].expr;
+                    double z;
+                    while (P.at(core).op == Op::Select && P.is_const(P.at(core).d, &z) && z == 0.0) {
+                        conds.push_back(P.at(core).a);
+                        core = P.at(core).b;
+                    }
+                    factor = !conds.empty();
+                    for (size_t ei = 0; ei < ents.size() && factor; ++ei) {
+                        if (ents[ei].r != (int)ci || ents[ei].slot < 0) continue;
+                        int x = ents[ei].dnode;
+                        for (int c : conds) {
+                            const Node& n = P.at(x);
+                            if (n.op == Op::Select && n.a == c && P.is_const(n.d, &z) && z == 0.0) x = n.b;
+                            else { factor = false; break; }
+                        }
+                        P.visit(x, [&](int, const Node& n) {
+                            factor = factor && n.op != Op::Div && n.op != Op::Sqrt && n.op != Op::Log &&
+                                     n.op != Op::Pow && n.op != Op::Exp && n.op != Op::Sample;
+                        });
+                        de[ei] = x;
+                    }
+                }
+                if (factor) {
+                    std::string mc = "qin";
+                    for (int c : conds) mc += " && " + b.cond(c);
+                    b.line("const bool m" + std::to_string(ci) + " = " + mc + ";");
+                    std::string fsum = "(T)0";
+                    for (size_t ei = 0; ei < ents.size(); ++ei) {
+                        if (ents[ei].r != (int)ci) continue;
+                        if (ents[ei].slot >= 0) {
+                            dname[ei] = "d" + std::to_string(ei);
+                            b.line("const T " + dname[ei] + " = " + b.v(de[ei]) + ";");
+                        } else {
+                            double cv;
+                            P.is_const(ents[ei].dnode, &cv);
+                            dname[ei] = lit(cv);
+                        }
+                        fsum += " + " + dname[ei] + " * " + b.vec(ents[ei].u, "p");
+                    }
+                    b.line("const T jp" + std::to_string(ci) + " = m" + std::to_string(ci) + " ? " + fsum + " : (T)0;");
+                    continue;
+                }
                 std::string sum = "(T)0";
                 for (size_t ei = 0; ei < ents.size(); ++ei) {
                     if (ents[ei].r != (int)ci) continue;
@@ -970,6 +1145,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
             if (jtf) {
                 // the output row's Exclude, read from the same windows
                 Body bf(m, fin, nd, uslot);
+                bf.use_pred(true);
                 bf.centred_reads([&](const Node& n, const char* vname) {
                     const auto key = std::make_tuple(vname ? 1 : 0, n.i, n.ch);
                     auto it = win.find(key);
@@ -1154,6 +1330,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         g_cache = nullptr;
         {
             Body b(m, body, nd, uslot);
+            b.use_pred(true);
             b.centred_reads([&](const Node& n, const char* vname) {
                 const auto key = std::make_tuple(vname ? 2 : 0, n.i, n.ch);
                 auto it = win.find(key);
@@ -1589,6 +1766,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
     (void)zero3;
     g_cache = nullptr;
     g_gcache = nullptr;
+    g_pred = nullptr;
     char note[128];
     snprintf(note, sizeof(note), "// apply: %s (%.2f residual instances per centred residual)\n",
              gs.has_strip ? "gen_apply_strip" : gs.prefer_tiled ? "gen_apply_tiled" : "gen_apply",

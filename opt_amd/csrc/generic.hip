@@ -389,7 +389,8 @@ public:
     void computed_planes(std::vector<HaloPlane>& v) const {
         for (size_t i = 0; i < m_.images.size(); ++i)
             if (m_.images[i].internal)
-                v.push_back({dimg_[i], sizeof(T) * m_.images[i].channels * (size_t)dims_[0]});
+                v.push_back({dimg_[i], (size_t)elem_size(m_.images[i], sizeof(T) == 8) * m_.images[i].channels *
+                                           (size_t)dims_[0]});
     }
 
     void jtf(T* r, T* diag, uint8_t* flags, hipStream_t s) {

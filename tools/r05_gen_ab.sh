@@ -10,7 +10,7 @@ for round in 1 2; do
   for v in "$@"; do
     sv=${v% *}; wv=${v#* }
     tag=s${sv}w${wv}
-    OPT_AMD_GEN_STRIP32=$sv OPT_AMD_GEN_WIDU=$wv timeout -k 10 200 python3 tools/bench_families.py \
+    OPT_AMD_GEN_STRIP32=$sv OPT_AMD_GEN_WIDU=$wv OPT_AMD_GEN_FACTOR=${GEN_FACTOR:-1} timeout -k 10 200 python3 tools/bench_families.py \
         --only iw4096_generic,sfs_generic --out $O/gen_$tag.$round.json > $O/gen_$tag.$round.log 2>&1 || exit 1
     python3 -c "
 import json
