@@ -105,9 +105,9 @@ bool g_off32 = false;
 // OPT_AMD_GEN_STRIP32=0 64-bit element indices, 1 32-bit, 2 32-bit kept opaque (opt_o32),
 // 4 (default) opaque in the kernels without two-channel pair reads
 int g_strip32 = 4;
-// OPT_AMD_GEN_WIDU=1: the strip kernels' wave index through readfirstlane (row indices and
-// bounds in SGPRs)
-bool g_widu = true;
+// OPT_AMD_GEN_WIDU: the strip kernels' wave index through readfirstlane (row indices and
+// bounds in SGPRs): 0 never, 1 always, 2 (default) in the kernels without pair windows
+int g_widu = 2;
 // OPT_AMD_GEN_FACTOR=0: the strip apply masks every partial of a masked residual (else the
 // residual's mask once, on Jp)
 bool g_factor = true;
@@ -419,7 +419,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         const char* sv = getenv("OPT_AMD_GEN_STRIP32");
         g_strip32 = sv ? atoi(sv) : 4;
         const char* wv = getenv("OPT_AMD_GEN_WIDU");
-        g_widu = !wv || atoi(wv) != 0;
+        g_widu = wv ? atoi(wv) : 2;
         const char* fv = getenv("OPT_AMD_GEN_FACTOR");
         g_factor = !fv || atoi(fv) != 0;
     }
@@ -1186,12 +1186,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         }
         o << "    const int lane = threadIdx.x & 63, z = 0; (void)z;\n"
              "    const int nsx = (W + " << nout - 1 << ") / " << nout << ", G = gridDim.x * 4;\n"
-             "    const int RB = max(8, (int)(((long long)H * nsx + G - 1) / G)), nby = (H + RB - 1) / RB;\n"
-             "    for (int wid = " << (g_widu ? "__builtin_amdgcn_readfirstlane((int)opt_xcd_block() * 4 + (threadIdx.x >> 6))"
-                                      : "(int)opt_xcd_block() * 4 + (threadIdx.x >> 6)") << "; wid < nsx * nby; wid += G) {\n"
-             "        const int x = (wid % nsx) * " << nout << " + lane - " << loff << ";\n"
-             "        const int y0 = (wid / nsx) * RB, y1 = min(H, y0 + RB);\n"
-             "        const bool xin = x >= 0 && x < W, xout = xin && lane >= " << loff << " && lane < " << loff + nout << ";\n";
+             "    const int RB = max(8, (int)(((long long)H * nsx + G - 1) / G)), nby = (H + RB - 1) / RB;\n";
         auto base_of = [&](const std::tuple<int, int, int>& k) {
             const int i = std::get<1>(k);
             return std::get<0>(k) ? "(p + a.uoff[" + std::to_string(uslot[i]) + "])"
@@ -1211,6 +1206,14 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         bool pairs = false;
         for (auto& w : win) pairs = pairs || (std::get<2>(w.first) == 0 && partner(w.first));
         const bool opq = g_strip32 == 2 || (g_strip32 == 4 && !pairs);   // opt_at32<O>
+        // the wave loop (emitted once pairs is known): the wave index through readfirstlane
+        // in the kernels without pair windows (OPT_AMD_GEN_WIDU=2, the default; 1 always, 0 never)
+        o << "    for (int wid = " << (g_widu == 1 || (g_widu == 2 && !pairs)
+                                          ? "__builtin_amdgcn_readfirstlane((int)opt_xcd_block() * 4 + (threadIdx.x >> 6))"
+                                          : "(int)opt_xcd_block() * 4 + (threadIdx.x >> 6)") << "; wid < nsx * nby; wid += G) {\n"
+             "        const int x = (wid % nsx) * " << nout << " + lane - " << loff << ";\n"
+             "        const int y0 = (wid / nsx) * RB, y1 = min(H, y0 + RB);\n"
+             "        const bool xin = x >= 0 && x < W, xout = xin && lane >= " << loff << " && lane < " << loff + nout << ";\n";
         // statement loading row yy of window k into `dst` (and of its partner channel)
         auto load = [&](const std::tuple<int, int, int>& k, const std::string& yy, int dy, const char* sfx) {
             const int i = std::get<1>(k), c = std::get<2>(k), ch = m.images[i].channels;
@@ -1381,12 +1384,7 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
              "    T acc = 0;\n"
              "    const int lane = threadIdx.x & 63, z = 0; (void)z;\n"
              "    const int nsx = (W + " << nout - 1 << ") / " << nout << ", G = gridDim.x * 4;\n"
-             "    const int RB = max(8, (int)(((long long)H * nsx + G - 1) / G)), nby = (H + RB - 1) / RB;\n"
-             "    for (int wid = " << (g_widu ? "__builtin_amdgcn_readfirstlane((int)opt_xcd_block() * 4 + (threadIdx.x >> 6))"
-                                      : "(int)opt_xcd_block() * 4 + (threadIdx.x >> 6)") << "; wid < nsx * nby; wid += G) {\n"
-             "        const int x = (wid % nsx) * " << nout << " + lane - " << loff << ";\n"
-             "        const int y0 = (wid / nsx) * RB, y1 = min(H, y0 + RB);\n"
-             "        const bool xin = x >= 0 && x < W, xout = xin && lane >= " << loff << " && lane < " << loff + nout << ";\n";
+             "    const int RB = max(8, (int)(((long long)H * nsx + G - 1) / G)), nby = (H + RB - 1) / RB;\n";
         auto base_of = [&](const std::tuple<int, int, int>& k) {
             const int i = std::get<1>(k);
             const std::string own = "((const " + std::string(elem_type(m.images[i].elem, m.images[i].tvalued)) +
@@ -1404,6 +1402,14 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
         bool pairs = false;
         for (auto& w : win) pairs = pairs || (std::get<2>(w.first) == 0 && partner(w.first));
         const bool opq = g_strip32 == 2 || (g_strip32 == 4 && !pairs);   // opt_at32<O>
+        // the wave loop (emitted once pairs is known): the wave index through readfirstlane
+        // in the kernels without pair windows (OPT_AMD_GEN_WIDU=2, the default; 1 always, 0 never)
+        o << "    for (int wid = " << (g_widu == 1 || (g_widu == 2 && !pairs)
+                                          ? "__builtin_amdgcn_readfirstlane((int)opt_xcd_block() * 4 + (threadIdx.x >> 6))"
+                                          : "(int)opt_xcd_block() * 4 + (threadIdx.x >> 6)") << "; wid < nsx * nby; wid += G) {\n"
+             "        const int x = (wid % nsx) * " << nout << " + lane - " << loff << ";\n"
+             "        const int y0 = (wid / nsx) * RB, y1 = min(H, y0 + RB);\n"
+             "        const bool xin = x >= 0 && x < W, xout = xin && lane >= " << loff << " && lane < " << loff + nout << ";\n";
         auto load = [&](const std::tuple<int, int, int>& k, const std::string& yy, int dy, const char* sfx) {
             const int i = std::get<1>(k), c = std::get<2>(k), ch = m.images[i].channels;
             const std::string cond = "xin && " + yy + " >= 0 && " + yy + " < H" + (std::get<0>(k) ? " && delta" : "");
