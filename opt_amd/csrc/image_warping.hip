@@ -2431,6 +2431,7 @@ private:
         apfree_ = env_int("OPT_AMD_IW_APFREE", 1) != 0;
         rec_on_ = env_int("OPT_AMD_IW_REC", 0) != 0;
         cost60_ = env_int("OPT_AMD_IW_COST60", 1) != 0;
+        cost_rows_ = (int)env_int("OPT_AMD_IW_COST_ROWS", 0);
         allp_ = env_int("OPT_AMD_IW_ALLP", 1) != 0;
         upd_nt_ = env_int("OPT_AMD_IW_UPD_NT", 1) != 0;
         upd_blocks_ = std::max(1, env_int("OPT_AMD_IW_UPD_BLOCKS", 2048));
@@ -2486,7 +2487,7 @@ private:
         nstrips_ = (dom_.W + iw::kStrip - 1) / iw::kStrip;
         if (rows_ <= 0 || rows_auto_) { rows_auto_ = true; rows_ = iw::rows_for(nstrips_, dom_.y_hi - dom_.y_lo); }
         nrowblocks_ = (dom_.y_hi - dom_.y_lo + rows_ * 4 - 1) / (rows_ * 4);
-        red_.ensure(std::max({stencil_blocks(), fused_blocks(), 2048}), 1, 64);
+        red_.ensure(std::max({stencil_blocks(), fused_blocks(), cost_blocks(), 2048}), 1, 64);
         if (opts_.host_buffers) {
             dO_ = (T*)dmalloc(sizeof(T) * 2 * N);
             dA_ = (T*)dmalloc(sizeof(T) * N);
@@ -2580,6 +2581,13 @@ private:
     // tiles of iw_jtf_apply: 60-column strips
     int fused_strips() const { return (dom_.W + iw::kFStrip - 1) / iw::kFStrip; }
     int fused_blocks() const { return fused_strips() * nrowblocks_; }
+    // iw_cost60's rows per wave (OPT_AMD_IW_COST_ROWS; 0: the plan's rows, 32 at 4096^2 —
+    // 16 / 24 / 48 / 64 ran 138-146 us against 132-135, tools/r05_cost_rows_ab.sh; held to
+    // 64 VGPRs for 8 waves per SIMD instead of 6 it spilled and ran 141-142)
+    int cost_rows() const { return cost_rows_ > 0 ? cost_rows_ : rows_; }
+    int cost_blocks() const {
+        return fused_strips() * ((dom_.y_hi - dom_.y_lo + cost_rows() * 4 - 1) / (cost_rows() * 4));
+    }
 
     iw::Args<T> args() const {
         iw::Args<T> a;
@@ -2828,7 +2836,9 @@ private:
         if (offsets32_ && cost60_) {
             iw::Args<T> a = args();
             a.nstrips = fused_strips();
-            const int nb = fused_blocks();
+            a.rows = cost_rows();
+            a.nrowblocks = (dom_.y_hi - dom_.y_lo + a.rows * 4 - 1) / (a.rows * 4);
+            const int nb = a.nstrips * a.nrowblocks;
             a.tb0 = 0; a.tn0 = nb; a.tb1 = 0;
             hipLaunchKernelGGL(iw::iw_cost60<T>, dim3(nb), dim3(kBlock), 0, stream_, a, red_.slot(nb, sc_out));
         } else {
@@ -2886,6 +2896,7 @@ private:
     // 270 us per pass, GN step 3.35 -> 3.30 ms) two rows with the records swapping roles,
     // 2 the same with two raw rows in flight
     int pcg_u2_ = 1;
+    int cost_rows_ = 0;
     bool jtf_nt_ = false;               // OPT_AMD_IW_JTF_NT=1: iw_jtf_apply with streaming stores
     bool offsets32_ = true;             // iw_apply_res's 32-bit byte offsets cover every plan vector
     int rows_ = 0, nstrips_ = 0, nrowblocks_ = 0;
