@@ -65,6 +65,20 @@ def test_generated_source_compiles(name):
     api.generic_compile_check(E(name))
 
 
+def test_strip_wave_index_form_per_kernel():
+    """The strip kernels take the wave index through readfirstlane only when they read no
+    two-channel pair windows (codegen.cpp, OPT_AMD_GEN_WIDU=2, the default): image_warping's
+    strips (Offset / UrShape pairs) ran 204-206 us with it against 165-166 without,
+    shape_from_shading's 139-142 against 146-148."""
+    if os.environ.get("OPT_AMD_GEN_WIDU") not in (None, "2"):
+        pytest.skip("OPT_AMD_GEN_WIDU overrides the default")
+    uni = "readfirstlane((int)opt_xcd_block()"
+    iw = api.generic_source(E("image_warping"))
+    assert "gen_apply_strip" in iw and "opt_ldm2" in iw and uni not in iw
+    sfs = api.generic_source(E("shape_from_shading"))
+    assert "gen_apply_strip" in sfs and uni in sfs
+
+
 @pytest.mark.parametrize("name", ["image_warping", "poisson_image_editing", "arap_mesh_deformation",
                                   "volume_denoise", "curve_smoothing", "intrinsic_image_decomposition",
                                   "shape_from_shading", "optical_flow", "cotangent_mesh_smoothing",
