@@ -260,6 +260,7 @@ class OptSolver:
         pk = ParamPack(problem_params)
         out = ctypes.c_double()
         if self.lib.OptAMD_EvalJTF(self.state, self.plan, pk.ptr, _ptr(r), _ptr(pre), ctypes.byref(out)):
+            self._raise_plan_error()
             raise OptError("OptAMD_EvalJTF failed")
         return out.value
 
@@ -267,12 +268,17 @@ class OptSolver:
         pk = ParamPack(problem_params)
         out = ctypes.c_double()
         if self.lib.OptAMD_ApplyJTJ(self.state, self.plan, pk.ptr, _ptr(p), _ptr(Ap), ctypes.byref(out)):
+            self._raise_plan_error()
             raise OptError("OptAMD_ApplyJTJ failed")
         return out.value
 
     def eval_cost(self, problem_params) -> float:
         pk = ParamPack(problem_params)
-        return self.lib.OptAMD_EvalCost(self.state, self.plan, pk.ptr)
+        c = self.lib.OptAMD_EvalCost(self.state, self.plan, pk.ptr)
+        if c == -1.0:   # a cost is >= 0: the call failed (OptAMD_PlanError holds why)
+            self._raise_plan_error()
+            raise OptError("OptAMD_EvalCost failed")
+        return c
 
     def time_apply(self, problem_params, p, Ap, reps: int) -> float:
         pk = ParamPack(problem_params)

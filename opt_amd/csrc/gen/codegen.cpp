@@ -1100,6 +1100,23 @@ GenSource generate(GModel& m, bool dbl, bool off32) {
                         fsum += " + " + dname[ei] + " * " + b.vec(ents[ei].u, "p");
                     }
                     b.line("const T jp" + std::to_string(ci) + " = m" + std::to_string(ci) + " ? " + fsum + " : (T)0;");
+                    // A partial that reads a known array (or a ComputedArray) may be non-finite
+                    // where the mask is off — NaN / Inf is a common "no data" value there — and
+                    // d * jp would then be NaN * 0. The reference's Select discards that branch,
+                    // so those partials keep the mask on their transpose contribution;
+                    // partials over unknowns, parameters and constants alone need none.
+                    for (size_t ei = 0; ei < ents.size(); ++ei) {
+                        if (ents[ei].r != (int)ci || ents[ei].slot < 0) continue;
+                        bool data = false;
+                        P.visit(de[ei], [&](int, const Node& n) {
+                            data = data || (n.op == Op::Read && !(n.i >= 0 && n.i < (int)m.images.size() &&
+                                                                   m.images[n.i].unknown));
+                        });
+                        if (!data) continue;
+                        const std::string dm = "dm" + std::to_string(ei);
+                        b.line("const T " + dm + " = m" + std::to_string(ci) + " ? " + dname[ei] + " : (T)0;");
+                        dname[ei] = dm;
+                    }
                     continue;
                 }
                 std::string sum = "(T)0";

@@ -2163,16 +2163,13 @@ public:
         // every p_i kept (OPT_AMD_IW_ALLP, lIterations <= kAllPMax): no pass carries a delta
         // term, iw_update_all forms delta once at the end
         const bool allp = allp_ && fused_init_ && offsets32_ && res && apfree_ && !recl_ && L >= 2 &&
-                          L <= iw::kAllPMax;
+                          L <= iw::kAllPMax && ensure_pall(L);
         const bool defer = res && defer_ && !allp;
         T* pb[3] = {p0_, p1_, p2_};
         // allp with P0: r_0 stays in r_ for the update (the passes ping-pong r over r1_ and the
         // unused Ap_), which forms p_0 = pre r_0 itself, so PCGInit1 does not store it
         const bool keep0 = allp && res && L >= 3;
-        if (allp) {
-            ensure_pall(L);
-            pcur = pall_;
-        }
+        if (allp) pcur = pall_;
         // lIterations >= 3 with the fused loop: nothing but passes 1 and 2 reads p_0, and both
         // form it from r_0 (iw_apply_res P0), so PCGInit1 does not store it
         const bool p0 = res && L >= 3;
@@ -2441,6 +2438,7 @@ private:
         // with the neighbouring strips: plain stores (merged in the L2) measured 217-220 us
         // against 233-245 with streaming ones (round 5, same box, interleaved)
         jtf_nt_ = env_int("OPT_AMD_IW_JTF_NT", 0) != 0;
+        pall_limit_mb_ = env_int("OPT_AMD_IW_ALLP_LIMIT_MB", -1);
     }
     // A zeroed plan vector with kSlack spare bytes: place() may move each vector's base
     // within them between Steps (every vector is rewritten before it is read in a Step).
@@ -2521,15 +2519,33 @@ private:
         if (!keep0) return (i & 1) ? r1_ : r_;
         return i == 0 ? r_ : (i & 1) ? r1_ : Ap_;
     }
-    // allp's p vectors, grown to L (lIterations may rise between Steps)
-    void ensure_pall(int L) {
-        if (L <= pall_cap_) return;
+    // allp's p vectors, grown to L (lIterations may rise between Steps). False when the L
+    // vectors (3 N L values: 2 GB at 4096^2 fp32, L = 10) do not fit in the free HBM: the
+    // Step then runs the deferred-delta loop, which needs no extra vectors
+    bool ensure_pall(int L) {
+        if (L <= pall_cap_) return true;
         OPT_HIP_CHECK(hipStreamSynchronize(stream_));
         dfree(pall_);
-        pall_ = (T*)dmalloc(sizeof(T) * 3 * (size_t)dom_.npix_mem() * L);
+        pall_ = nullptr;
+        pall_cap_ = 0;
+        const size_t bytes = sizeof(T) * 3 * (size_t)dom_.npix_mem() * L;
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess || bytes + (64u << 20) > free_b ||
+            (pall_limit_mb_ >= 0 && bytes > ((size_t)pall_limit_mb_ << 20)) ||
+            hipMalloc((void**)&pall_, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            pall_ = nullptr;
+            if (!pall_warned_) {
+                fprintf(stderr, "[opt_amd] image_warping: %zu MiB for the kept p vectors do not fit (%zu MiB free): "
+                        "deferred-delta loop\n", bytes >> 20, free_b >> 20);
+                pall_warned_ = true;
+            }
+            return false;
+        }
         // (ordered on the plan's stream: a null-stream memset is not ordered against it)
-        OPT_HIP_CHECK(hipMemsetAsync(pall_, 0, sizeof(T) * 3 * (size_t)dom_.npix_mem() * L, stream_));
+        OPT_HIP_CHECK(hipMemsetAsync(pall_, 0, bytes, stream_));
         pall_cap_ = L;
+        return true;
     }
     void release() {
         for (char* p : raw_) dfree(p);
@@ -2888,6 +2904,8 @@ private:
     int upd_blocks_ = 2048;             // OPT_AMD_IW_UPD_BLOCKS: iw_update_all's grid cap (grid-stride beyond)
     T* pall_ = nullptr;                 // allp: lIterations p vectors of 3 N, p_i = pall_ + 3 N i
     int pall_cap_ = 0;
+    bool pall_warned_ = false;
+    long long pall_limit_mb_ = -1;      // OPT_AMD_IW_ALLP_LIMIT_MB: cap on the kept p vectors (tests the fallback)
     bool recl_ = false;                 // the plan holds the REC layout (rec_on_ and the fused loop's knobs)
     T* rec_[3] = {nullptr, nullptr, nullptr};   // REC: iteration i's record in rec_[i % 3] (i % 2 undeferred)
     T* srec_ = nullptr;                 // REC: the S record [u.x u.y angle pre_t], written by iw_jtf_apply

@@ -42,6 +42,23 @@ bool valid_plan(Opt_Plan* p, const char* fn) {
 }
 }  // namespace
 
+// Every entry point that binds the caller's arrays (and so may raise a PlanError, e.g. the
+// ARAP adjacency limit found by build_csr inside bind) runs its body through guarded(): no
+// C++ exception crosses the extern "C" frame into the caller (ctypes, cgo, C), the plan's
+// stream is drained of whatever the call had queued before the throw (its begin_call /
+// end_call pair did not complete), and the call returns its error value.
+template <typename F, typename R>
+static R guarded(Opt_Plan* plan, const char* fn, R err, F&& body) {
+    try {
+        return body();
+    } catch (const std::exception& e) {
+        plan->error = e.what();
+        fprintf(stderr, "[opt_amd] %s: %s\n", fn, e.what());
+        plan->impl->drain();
+        return err;
+    }
+}
+
 extern "C" {
 
 Opt_State* Opt_NewState(Opt_InitializationParameters params) {
@@ -169,24 +186,16 @@ void Opt_SetSolverParameter(Opt_State* state, Opt_Plan* plan, const char* name, 
 void Opt_ProblemInit(Opt_State* state, Opt_Plan* plan, void** problemparams) {
     if (!valid_state(state, "Opt_ProblemInit") || !valid_plan(plan, "Opt_ProblemInit")) exit(1);
     plan->error.clear();
-    try {
+    guarded(plan, "Opt_ProblemInit", 0, [&] {
         plan->impl->init(problemparams);
-    } catch (const optamd::PlanError& e) {
-        plan->error = e.what();
-        fprintf(stderr, "[opt_amd] Opt_ProblemInit: %s\n", e.what());
-    }
+        return 0;
+    });
 }
 
 int Opt_ProblemStep(Opt_State* state, Opt_Plan* plan, void** problemparams) {
     if (!valid_state(state, "Opt_ProblemStep") || !valid_plan(plan, "Opt_ProblemStep")) exit(1);
     if (!plan->error.empty()) return 0;
-    try {
-        return plan->impl->step(problemparams);
-    } catch (const optamd::PlanError& e) {
-        plan->error = e.what();
-        fprintf(stderr, "[opt_amd] Opt_ProblemStep: %s\n", e.what());
-        return 0;
-    }
+    return guarded(plan, "Opt_ProblemStep", 0, [&] { return plan->impl->step(problemparams); });
 }
 
 void Opt_ProblemSolve(Opt_State* state, Opt_Plan* plan, void** problemparams) {
@@ -223,8 +232,8 @@ int OptAMD_ProblemFamily(Opt_Problem* problem, char* buf, int n) {
 int OptAMD_EvalJTF(Opt_State* state, Opt_Plan* plan, void** params, void* r, void* pre, double* rz) {
     if (!valid_state(state, "OptAMD_EvalJTF") || !valid_plan(plan, "OptAMD_EvalJTF") || !r || !pre)
         return 1;
-    double t;
-    int e = plan->impl->eval_jtf(params, r, pre, &t);
+    double t = 0;
+    int e = guarded(plan, "OptAMD_EvalJTF", 1, [&] { return plan->impl->eval_jtf(params, r, pre, &t); });
     if (rz) *rz = t;
     return e;
 }
@@ -232,20 +241,20 @@ int OptAMD_ApplyJTJ(Opt_State* state, Opt_Plan* plan, void** params, const void*
                     double* pAp) {
     if (!valid_state(state, "OptAMD_ApplyJTJ") || !valid_plan(plan, "OptAMD_ApplyJTJ") || !p || !Ap)
         return 1;
-    double t;
-    int e = plan->impl->apply_jtj(params, p, Ap, &t);
+    double t = 0;
+    int e = guarded(plan, "OptAMD_ApplyJTJ", 1, [&] { return plan->impl->apply_jtj(params, p, Ap, &t); });
     if (pAp) *pAp = t;
     return e;
 }
 double OptAMD_EvalCost(Opt_State* state, Opt_Plan* plan, void** params) {
     if (!valid_state(state, "OptAMD_EvalCost") || !valid_plan(plan, "OptAMD_EvalCost")) return -1.0;
-    return plan->impl->eval_cost(params);
+    return guarded(plan, "OptAMD_EvalCost", -1.0, [&] { return plan->impl->eval_cost(params); });
 }
 double OptAMD_TimeApplyJTJ(Opt_State* state, Opt_Plan* plan, void** params, const void* p, void* Ap,
                            int reps) {
     if (!valid_state(state, "OptAMD_TimeApplyJTJ") || !valid_plan(plan, "OptAMD_TimeApplyJTJ"))
         return -1.0;
-    return plan->impl->time_apply(params, p, Ap, reps);
+    return guarded(plan, "OptAMD_TimeApplyJTJ", -1.0, [&] { return plan->impl->time_apply(params, p, Ap, reps); });
 }
 void OptAMD_SetKernelTiming(Opt_Plan* plan, int mode) {
     if (!valid_plan(plan, "OptAMD_SetKernelTiming")) return;
@@ -356,7 +365,7 @@ int OptAMD_EvalJacobian(Opt_State* state, Opt_Plan* plan, void** params, int* ro
     if (!valid_state(state, "OptAMD_EvalJacobian") || !valid_plan(plan, "OptAMD_EvalJacobian") || !rowPtr ||
         !colInd || !val)
         return 1;
-    return plan->impl->eval_jacobian(params, rowPtr, colInd, val);
+    return guarded(plan, "OptAMD_EvalJacobian", 1, [&] { return plan->impl->eval_jacobian(params, rowPtr, colInd, val); });
 }
 
 // ---- sparse building blocks (synchronous, on the null stream) -------------------

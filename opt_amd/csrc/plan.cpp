@@ -201,6 +201,9 @@ void Plan::end_call() {
     OPT_HIP_CHECK(hipStreamSynchronize(stream_));
     OPT_HIP_CHECK(hipGetLastError());
 }
+void Plan::drain() noexcept {
+    (void)hipStreamSynchronize(stream_);
+}
 
 std::unique_ptr<Plan> make_plan(const ProblemSpec& spec, const StateOptions& opts,
                                 const unsigned* dims, std::string* err) {

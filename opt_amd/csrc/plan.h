@@ -144,6 +144,7 @@ public:
     int iterations() const { return n_iter_; }
     hipStream_t stream() const { return stream_; }
     KernelTimer& timer() { return timer_; }
+    void drain() noexcept;          // end_call after a throw (opt_api.cpp: guarded): waits, reports nothing
 
 protected:
     Plan(const ProblemSpec& spec, const StateOptions& opts);

@@ -353,8 +353,8 @@ public:
             }
             allreduce(pap(i), 1);
             const bool reset = lm_ && ((i + 1) % std::max(1, sp_.residual_reset_period)) == 0;
-            if (reset) {   // the classic halves, with step23's guards (a zero step / beta = 0)
-                hipLaunchKernelGGL((half1_kernel<T, true>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)p_,
+            if (reset) {   // the classic halves, the reference's unguarded division (:742)
+                hipLaunchKernelGGL((half1_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)p_,
                                    delta_, red_.scalars, rz(i), pap(i), stop);
                 exchange_vec(delta_);
                 op_->apply(delta_, Adelta_, CtC_, stop, red_.slot(nb(), kScTmp), stream_);
@@ -432,8 +432,8 @@ public:
                 pending = false;
             }
             const bool reset = lm_ && ((i + 1) % std::max(1, sp_.residual_reset_period)) == 0;
-            if (reset) {
-                hipLaunchKernelGGL((half1_kernel<T>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)p_, delta_,
+            if (reset) {   // the classic halves with step23's guards (a zero step / beta = 0)
+                hipLaunchKernelGGL((half1_kernel<T, true>), dim3(fg()), dim3(kBlock), 0, stream_, n_, (const T*)p_, delta_,
                                    red_.scalars, rz(i), pap(i), stop);
                 exchange_vec(delta_);
                 op_->apply(delta_, Adelta_, CtC_, stop, red_.slot(nb(), kScTmp), stream_);

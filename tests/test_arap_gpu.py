@@ -358,6 +358,24 @@ def test_adjacency_over_the_index_range_is_an_error_not_an_exit():
     with pytest.raises(OptError, match="adjacency too large"):   # Step returns 0; the wrapper raises
         s.step()
     s.close()
+    # the extension entry points bind too (StencilPlan::prepare -> build_csr);
+    # the PlanError is caught at the C boundary there as well (no std::terminate through the
+    # extern "C" frame), on a fresh plan whose first call is the extension
+    import torch
+
+    for call in ("eval_cost", "eval_jtf", "apply_jtj"):
+        s = solver(w)
+        prm = params(w)
+        x = torch.zeros(6 * N, dtype=torch.float32, device="cuda")
+        y = torch.zeros_like(x)
+        with pytest.raises(OptError, match="adjacency too large"):
+            if call == "eval_cost":
+                s.eval_cost(prm)
+            elif call == "eval_jtf":
+                s.eval_jtf(prm, x, y)
+            else:
+                s.apply_jtj(prm, x, y)
+        s.close()
     del w, v0, v1, P, C
     w2 = perturbed(7, 5, seed=3)
     s2 = solver(w2)

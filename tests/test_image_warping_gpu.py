@@ -239,7 +239,7 @@ def test_fp64_bench_workload_matches_double_oracle(monkeypatch, N, fused):
     np.testing.assert_allclose(c, truth, rtol=1e-8)
 
 
-@pytest.mark.parametrize("N", [1024, 2048])
+@pytest.mark.parametrize("N", [1024, 2048, 4096])
 def test_fp64_trajectory_at_size_within_the_fp64_floor(N):
     """The fp64 headline trajectory at 1024^2 and 2048^2 (2 GN x 10 PCG) against the
     double oracle. Round 4 measured 2-5e-7 here and suspected a precision leak; round 5
@@ -256,7 +256,8 @@ def test_fp64_trajectory_at_size_within_the_fp64_floor(N):
     slab counts (16 vs 7 threads) is the fp64 floor of the trajectory. Assert: the fp64 GPU
     path within max(1e-8, 2 x that spread) (measured round 5: 1.4e-8 / 1.0e-8 at 1024^2
     against a spread of 1.2e-8 / 1.0e-8; 2.1e-8 / 7.9e-8 at 2048^2 against 8.6e-8 /
-    2.2e-7), the initial energy within 1e-13."""
+    2.2e-7), the initial energy within 1e-13. 4096^2 is the headline size (fp64
+    parity pinned there too, with the same spread-derived bar)."""
     from opt_amd import workloads
 
     w = workloads.image_warping(N, N, seed=1234)
@@ -273,40 +274,53 @@ def test_fp64_trajectory_at_size_within_the_fp64_floor(N):
     assert np.all(e64[1:] <= np.maximum(1e-8, 2 * spread[1:])), (e64, spread)
 
 
+# fp32 GPU error against the fp64 truth after GN steps 1 / 2, measured with the round-5/6 loop
+# (iw_pcg, every p_i kept: bitwise the same trajectory in both rounds; round 4's separate
+# passes measured 3.3e-4 / 1.9e-4, 8.2e-4 / 3.4e-4, 1.2e-3 / 1.2e-4)
+FP32_RECORDED = {1024: (6.8e-4, 5.4e-4), 2048: (1.13e-3, 4.0e-4), 4096: (9.7e-4, 7.8e-5)}
+
+
 @pytest.mark.parametrize("N", [1024, 2048, 4096])
 def test_bench_workload_trajectory_against_fp64_truth(N):
     """The bench generator's workload (seeded) at 1024^2, config 2's 2048^2
     and the headline's 4096^2, 2 GN steps x 10 PCG (solverGPUGaussNewton.t:1913-2349),
     measured against the TRUE trajectory: the double oracle (doublePrecision, Opt.h:11-14,
     80-bit sums), whose own fp64 floor is ~1e-8 .. 1e-6 at these sizes
-    (test_fp64_trajectory_at_size_within_the_fp64_floor):
-      * the fp32 GPU path is no further from it than fp32 arithmetic itself reaches: its
-        error at every step is at most twice the worst error of the fp32 oracle run on the
-        same inputs and on two 1-ulp perturbations of Offset (or 1e-5), and within 1e-6 at
-        the initial energy (measured round 4: the fp32 GPU path lands 10-100x closer to the
-        truth than the fp32 oracle, thanks to its fp64 sums and fmas);
-      * one short-PCG step (1 GN x 1 PCG) agrees with the fp32 oracle within 1e-5.
-    The errors are printed (the fp32 oracle and the fp32 GPU path land at 1e-4 .. 1e-2
-    of the true energy after one 10-iteration PCG solve: the energy is evaluated in
-    absolute pixel coordinates)."""
+    (test_fp64_trajectory_at_size_within_the_fp64_floor). VERDICT r5 #4: the bar is the fp32
+    GPU path's OWN floor, not the fp32 oracle's (which sits 10-100x further from the truth):
+      * the error at every step is at most twice the worst error of the same GPU path on two
+        1-ulp perturbations of Offset (what fp32 rounding of the inputs alone moves), or 1e-5;
+      * and at most twice the error recorded for this path (FP32_RECORDED: 9.7e-4 / 7.8e-5 at
+        4096^2), so a systematic regression that moves all three runs together fails too;
+      * the initial energy within 1e-6, and one short-PCG step (1 GN x 1 PCG) within 1e-5
+        of the fp32 oracle.
+    The errors are printed (1e-4 .. 1e-3 after one 10-iteration PCG solve: the energy is
+    evaluated in absolute pixel coordinates)."""
     from opt_amd import workloads
 
     W = H = N
     w = workloads.image_warping(W, H, seed=1234)
     _, _, truth, _ = oracle.iw_solve(w, 2, 10, nthreads=16, double=True)
-    s = solver(W, H)
-    prm = device_params(w)
-    s.set_solver_params({"nIterations": 2, "lIterations": 10})
-    c = np.array(s.profiled_solve(prm))
+
+    def gpu(wi):
+        s = solver(W, H)
+        prm = device_params(wi)
+        s.set_solver_params({"nIterations": 2, "lIterations": 10})
+        c = np.array(s.profiled_solve(prm))
+        s.close()
+        return c
+
+    c = gpu(w)
     e_gpu = np.abs(c - truth) / truth
-    e_or = np.zeros_like(truth)
-    for seed in (0, 1, 2):
-        _, _, r32, _ = oracle.iw_solve(w if seed == 0 else _perturb_offset(w, seed), 2, 10, nthreads=16)
-        e_or = np.maximum(e_or, np.abs(r32 - truth) / truth)
-    print(f"N={N} vs fp64 truth: fp32 GPU {e_gpu}, fp32 oracle (3 samples, max) {e_or}")
+    floor = np.zeros_like(truth)
+    for seed in (1, 2):
+        floor = np.maximum(floor, np.abs(gpu(_perturb_offset(w, seed)) - truth) / truth)
+    rec = np.array((0.0,) + FP32_RECORDED[N])
+    print(f"N={N} vs fp64 truth: fp32 GPU {e_gpu}, on 1-ulp perturbed inputs (max of 2) {floor}, recorded {rec}")
     assert len(c) == len(truth)
     assert e_gpu[0] < 1e-6
-    assert np.all(e_gpu[1:] <= np.maximum(2 * e_or[1:], 1e-5)), (e_gpu, e_or)
+    assert np.all(e_gpu[1:] <= np.maximum(2 * floor[1:], 1e-5)), (e_gpu, floor)
+    assert np.all(e_gpu[1:] <= 2 * rec[1:]), (e_gpu, rec)
     s1 = solver(W, H)
     p1 = device_params(w)
     s1.set_solver_params({"nIterations": 1, "lIterations": 1})
@@ -682,18 +696,22 @@ def test_kept_p_update_is_bitwise_the_deferred_delta(monkeypatch, W, H, lit, dou
     """OPT_AMD_IW_ALLP (default 1, lIterations 2..16): every p_i kept and delta formed once
     by iw_update_all (alpha_0 p_0, then one fma per iteration) against the deferred delta
     (pairs folded by the even passes): the trajectory is bitwise the same, fp32 and fp64
-    (lIterations 1 and 17 take the deferred path either way)."""
+    (lIterations 1 and 17 take the deferred path either way). ADVICE r5: when the kept
+    vectors do not fit in HBM the Step falls back to the deferred delta — forced here with
+    OPT_AMD_IW_ALLP_LIMIT_MB=0 — and is again bitwise the same."""
     out = []
-    for v in ("0", "1"):
-        monkeypatch.setenv("OPT_AMD_IW_ALLP", v)
+    for v in ("0", "1", "fallback"):
+        monkeypatch.setenv("OPT_AMD_IW_ALLP", "0" if v == "0" else "1")
+        monkeypatch.setenv("OPT_AMD_IW_ALLP_LIMIT_MB", "0" if v == "fallback" else "-1")
         w = perturbed(W, H, seed=5 * W + H)
         s = solver(W, H, double=double)
         prm = device_params(w, double=double)
         s.set_solver_params({"nIterations": 3, "lIterations": lit})
         c = np.array(s.profiled_solve(prm))
         out.append((c, to_np(prm[0]), to_np(prm[1]), np.array(s.scalars(2 + 5 * (lit + 2)))))
-    for a, b in zip(out[0], out[1]):
-        np.testing.assert_array_equal(a, b)
+    for k in (1, 2):
+        for a, b in zip(out[0], out[k]):
+            np.testing.assert_array_equal(a, b)
 
 
 @pytest.mark.parametrize("W,H,lit", [(150, 110, 10), (5, 3, 4), (200, 1, 3), (700, 300, 10), (64, 64, 2),

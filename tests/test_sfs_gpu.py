@@ -361,3 +361,29 @@ def test_lm_far_past_convergence_with_residual_resets_stays_finite(monkeypatch, 
     if fuse == "1":
         assert np.all(np.isfinite(costs)) and np.all(np.isfinite(X[w["D_i"] > 0]))
         assert np.all(np.diff(costs) <= 0) and costs[-1] <= costs[0]
+
+
+@pytest.mark.parametrize("double", [False, True])
+def test_fused_lm_reset_iteration_with_zero_pap_keeps_delta_finite(monkeypatch, double):
+    """the fused LM loop's residual-reset iterations launch the guarded
+    half1_kernel (alpha = 0 unless p.Ap > 0, as step23_kernel). With no depth anywhere every
+    unknown is excluded (Exclude(Not(has_depth)), shape_from_shading.t), so r_0 = p_0 = 0 and
+    p.Ap = 0 exactly; residual_reset_period = 1 makes every PCG iteration a reset. The
+    unguarded division (0 / 0) would put NaN into delta, and half2's q = 1/2 delta.(r + b)
+    would carry it: every rz / q slot stays finite (zero) and the unknowns are unchanged."""
+    monkeypatch.setenv("OPT_AMD_FUSE23", "1")
+    W, H, lit = 16, 12, 4
+    w = synthetic(W, H, seed=11)
+    w["D_i"] = np.zeros_like(w["D_i"])
+    s = OptSolver([W, H], ENERGY, "LMGPU", double_precision=double)
+    s.set_solver_params({"nIterations": 2, "lIterations": lit, "residual_reset_period": 1, "q_tolerance": 0.0})
+    prm = params64(w) if double else params(w)
+    X0 = to_np(prm[16]).copy()
+    costs = np.array(s.profiled_solve(prm))
+    sc = np.array(s.scalars(8 + 7 * (lit + 2)))
+    s.close()
+    assert np.all(np.isfinite(costs)), costs
+    for i in range(lit + 1):
+        rz, q = sc[8 + 7 * i], sc[8 + 7 * i + 1]
+        assert np.isfinite(rz) and np.isfinite(q), (i, rz, q)
+    np.testing.assert_array_equal(to_np(prm[16]), X0)
