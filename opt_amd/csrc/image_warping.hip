@@ -52,13 +52,16 @@ constexpr int kStrip = 64;   // columns per wavefront strip (aligned: x = 64*str
 // Rows per wave of the stencil kernels: 32 while that still gives >= 2048 tiles of
 // 4 waves (4096^2: 64 strips x 32 row blocks, two resident rounds at 4 waves per SIMD);
 // a row slab of the multi-GPU split (4096 x 512 at 8 ranks) would otherwise fill a
-// quarter of the chip, so shorter waves down to 8 rows keep the tile count up.
-// Measured on one GPU at each rank's slab shape (GN step, rows 32 / 16 / 8 / 4):
-// 4096 x 512 0.89 / 0.73 / 0.70 / 0.76 ms, 4096 x 1024 1.33 / 1.17 / 1.21 / 1.40,
-// 4096 x 2048 2.33 / 2.21 / 2.31 / 2.78 (this rule: 8, 8, 16).
+// quarter of the chip, so shorter waves down to 16 rows keep the tile count up.
+// Measured on one GPU at each rank's slab shape (GN step, rows 32 / 16 / 8 / 4; round 4's
+// loop): 4096 x 512 0.89 / 0.73 / 0.70 / 0.76 ms, 4096 x 1024 1.33 / 1.17 / 1.21 / 1.40,
+// 4096 x 2048 2.33 / 2.21 / 2.31 / 2.78. Round 6 (iw_pcg, one rank's interior 4096 x 512
+// slab alone, tools/slab_rank.py): rows 8 / 16 / 24 0.580 / 0.566 / 0.561 ms — the radius-2
+// pass loads rows y0 - 2 .. y1 + 1, 50 % more rows than it outputs at 8 rows — so the floor
+// is 16 (this rule: 16, 16, 16).
 inline int rows_for(int nstrips, int nrows) {
     int rows = 32;
-    while (rows > 8 && (long long)nstrips * ((nrows + 4 * rows - 1) / (4 * rows)) < 2048) rows /= 2;
+    while (rows > 16 && (long long)nstrips * ((nrows + 4 * rows - 1) / (4 * rows)) < 2048) rows /= 2;
     return rows;
 }
 
@@ -559,16 +562,24 @@ __device__ __forceinline__ WaveGeom geom_fused(const Args<T>& a) {
     const int lt = xcd_remap(blockIdx.x, gridDim.x);
     const int t = lt < a.tn0 ? a.tb0 + lt : a.tb1 + (lt - a.tn0);   // the launch's tile ranges (geom)
     g.tile = t;
-    const int strip = t % a.nstrips, rb = t / a.nstrips;
     g.lane = threadIdx.x & (kWave - 1);
     // the wave index as a wave-uniform (SGPR) value: every row index, bound and row base
     // derived from it is then scalar arithmetic, not per-lane VALU work
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    int strip, y0;
+    if (a.side) {   // the block's waves: four adjacent strips over the same rows (Args::side)
+        const int ng = (a.nstrips + kBlock / kWave - 1) / (kBlock / kWave);
+        strip = (t % ng) * (kBlock / kWave) + w;
+        y0 = a.dom.y_lo + (t / ng) * a.rows;
+    } else {
+        strip = t % a.nstrips;
+        y0 = a.dom.y_lo + ((t / a.nstrips) * (kBlock / kWave) + w) * a.rows;
+    }
     g.x = strip * kFStrip - 2 + g.lane;
     g.edge_lane = false;
     g.ex = g.x;
-    g.y0 = a.dom.y_lo + (rb * (kBlock / kWave) + w) * a.rows;
-    g.y1 = min(g.y0 + a.rows, a.dom.y_hi);
+    g.y0 = y0;
+    g.y1 = strip < a.nstrips ? min(g.y0 + a.rows, a.dom.y_hi) : g.y0;
     g.out_lane = g.lane >= 2 && g.lane < 2 + kFStrip && g.x < a.dom.W;
     return g;
 }
@@ -1977,6 +1988,70 @@ __global__ __launch_bounds__(kBlock) void iw_update_all(Args<T> a, T* __restrict
     }
 }
 
+// iw_update_all over pixel PAIRS (round 6): each thread loads two pixels'
+// Offset pairs of every p_i as one 16-B vector (8-B for the angle channel), so the pass
+// issues half the load instructions, each twice as wide. Every value is formed by the same
+// expressions in the same order as iw_update_all: bitwise the same update. The plan takes it
+// when the pairs are aligned (N % 4 == 0, even row starts, 16-B aligned arrays).
+template <typename T>
+using vec4_t = T __attribute__((ext_vector_type(4)));
+template <typename T, int L, bool P0R, bool NT = false>
+__global__ __launch_bounds__(kBlock) void iw_update_all2(Args<T> a, T* __restrict__ O, T* __restrict__ A,
+                                                         const T* __restrict__ pall, long long pstride,
+                                                         const double* __restrict__ sc, int sc0,
+                                                         const T* __restrict__ r0, const T* __restrict__ pre) {
+    IW_PRE_TABLE(a);
+    const long long N = a.dom.npix_mem();
+    T al[L];
+#pragma unroll
+    for (int i = 0; i < L; ++i) al[i] = pcg_alpha<T>(sc[sc0 + kSlots * i], sc[sc0 + kSlots * i + 1]);
+    const long long b = a.dom.off(0, a.dom.y_lo), np = (a.dom.off(0, a.dom.y_hi) - b) >> 1;
+    for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < np; j += (long long)gridDim.x * blockDim.x) {
+        const long long k = b + 2 * j;
+        const unsigned short ff = *reinterpret_cast<const unsigned short*>(a.flags + k);
+        const int f0 = ff & 255, f1 = ff >> 8;
+        vec4_t<T> q[L];
+        vec2_t<T> qt[L];
+#pragma unroll
+        for (int i = P0R ? 1 : 0; i < L; ++i) {
+            const T* pi = pall + i * pstride;
+            q[i] = ld_v<NT>(reinterpret_cast<const vec4_t<T>*>(pi + 2 * k));
+            qt[i] = ld_v<NT>(reinterpret_cast<const vec2_t<T>*>(pi + 2 * N + k));
+        }
+        if constexpr (P0R) {   // iw_update_all's p_0 per pixel: the same rounded products
+            const vec4_t<T> r = *reinterpret_cast<const vec4_t<T>*>(r0 + 2 * k);
+            const vec2_t<T> rt = *reinterpret_cast<const vec2_t<T>*>(r0 + 2 * N + k);
+            const vec2_t<T> w2 = *reinterpret_cast<const vec2_t<T>*>(pre + k);
+            vec2_t<T> ra, rb;
+            ra.x = r.x; ra.y = r.y; rb.x = r.z; rb.y = r.w;
+            const vec2_t<T> pa = opaque(pre_offset(a, f0) * ra), pb = opaque(pre_offset(a, f1) * rb);
+            q[0].x = pa.x; q[0].y = pa.y; q[0].z = pb.x; q[0].w = pb.y;
+            qt[0].x = opaque(w2.x * rt.x);
+            qt[0].y = opaque(w2.y * rt.y);
+        }
+        vec4_t<T> d = al[0] * q[0];
+        vec2_t<T> dt = al[0] * qt[0];
+#pragma unroll
+        for (int i = 1; i < L; ++i) {
+            d = __builtin_elementwise_fma((vec4_t<T>)al[i], q[i], d);
+            dt = __builtin_elementwise_fma((vec2_t<T>)al[i], qt[i], dt);
+        }
+        const bool a0 = f0 & 1, a1 = f1 & 1;
+        if (a0 && a1) {
+            vec4_t<T>* op = reinterpret_cast<vec4_t<T>*>(O + 2 * k);
+            vec2_t<T>* ap = reinterpret_cast<vec2_t<T>*>(A + k);
+            *op = *op + d;
+            *ap = *ap + dt;
+        } else if (a0 || a1) {
+            const long long kk = a0 ? k : k + 1;
+            Vec2<T>* op = reinterpret_cast<Vec2<T>*>(O) + kk;
+            const Vec2<T> o = *op;
+            *op = a0 ? Vec2<T>{o.x + d.x, o.y + d.y} : Vec2<T>{o.x + d.z, o.y + d.w};
+            A[kk] = A[kk] + (a0 ? dt.x : dt.y);
+        }
+    }
+}
+
 // ---------------------------------------------------- materialized Jacobian
 // saveJToCRS (solverGPUGaussNewton.t:1004-1022) with generateDumpJ (:385-442): every
 // pixel (excluded ones included, as the reference) writes its 10 residual rows — for s
@@ -2137,7 +2212,8 @@ public:
         bind(params, false);
         exchange_unknowns();
         const int L = std::max(0, sp_.lIterations);
-        red_.ensure(std::max({stencil_blocks(), fused_blocks(), side_blocks(), 2048}), 4, kScBase + iw::kSlots * (L + 2));
+        red_.ensure(std::max({stencil_blocks(), fused_blocks(), side_blocks(), fused_side_blocks(), cost_side_blocks(), 2048}), 4,
+                    kScBase + iw::kSlots * (L + 2));
         if (print_addr_) {   // OPT_AMD_PRINT_ADDR=1: placement of every stream (HBM channel study)
             print_addr_ = false;
             fprintf(stderr, "[opt_amd] addr r=%p r1=%p p0=%p p1=%p Ap=%p Ap1=%p delta=%p pre=%p flags=%p "
@@ -2211,8 +2287,10 @@ public:
         // launch overhead, so the loop stays as plain stream launches)
         // row slabs with >= 3 row blocks: the halo refresh of r and p_{i-1} runs beside the
         // interior row blocks of the next apply (halo_mark / halo_begin / halo_join)
-        const bool split = distributed() && overlap_ && comm_->concurrent_halo() && nrowblocks_ >= 3 &&
-                           (dom_.y_hi - dom_.y_lo) - (nrowblocks_ - 1) * 4 * rows_ >= 2;
+        // (the last row block / chunk must hold >= 2 rows: only the first and last read halo rows)
+        const bool split = distributed() && overlap_ && comm_->concurrent_halo() &&
+                           (pcg_side_ && apfree ? side_chunks() >= 3 && (dom_.y_hi - dom_.y_lo) - (side_chunks() - 1) * rows_ >= 2
+                                                : nrowblocks_ >= 3 && (dom_.y_hi - dom_.y_lo) - (nrowblocks_ - 1) * 4 * rows_ >= 2);
         if (res) {
             // p_i in pb[i % 3] (deferred delta) or pb[i % 2]
             auto pbuf = [&](int i) { return allp ? pall_ + (size_t)i * 3 * dom_.npix_mem() : pb[defer ? i % 3 : i % 2]; };
@@ -2439,6 +2517,10 @@ private:
         // against 233-245 with streaming ones (round 5, same box, interleaved)
         jtf_nt_ = env_int("OPT_AMD_IW_JTF_NT", 0) != 0;
         pall_limit_mb_ = env_int("OPT_AMD_IW_ALLP_LIMIT_MB", -1);
+        pcg_side_ = env_int("OPT_AMD_IW_PCG_SIDE", 1) != 0;
+        jtf_side_ = env_int("OPT_AMD_IW_JTF_SIDE", 0) != 0;
+        cost_side_ = env_int("OPT_AMD_IW_COST_SIDE", 0) != 0;
+        upd_pairs_ = env_int("OPT_AMD_IW_UPD_PAIRS", 1) != 0;
     }
     // A zeroed plan vector with kSlack spare bytes: place() may move each vector's base
     // within them between Steps (every vector is rewritten before it is read in a Step).
@@ -2485,7 +2567,8 @@ private:
         nstrips_ = (dom_.W + iw::kStrip - 1) / iw::kStrip;
         if (rows_ <= 0 || rows_auto_) { rows_auto_ = true; rows_ = iw::rows_for(nstrips_, dom_.y_hi - dom_.y_lo); }
         nrowblocks_ = (dom_.y_hi - dom_.y_lo + rows_ * 4 - 1) / (rows_ * 4);
-        red_.ensure(std::max({stencil_blocks(), fused_blocks(), cost_blocks(), 2048}), 1, 64);
+        red_.ensure(std::max({stencil_blocks(), fused_blocks(), cost_blocks(), cost_side_blocks(), fused_side_blocks(), 2048}),
+                    1, 64);
         if (opts_.host_buffers) {
             dO_ = (T*)dmalloc(sizeof(T) * 2 * N);
             dA_ = (T*)dmalloc(sizeof(T) * N);
@@ -2500,6 +2583,22 @@ private:
             if (L != K) { launch_update_all_k<K + 1>(L, p0r); return; }
             auto k = upd_nt_ ? (p0r ? iw::iw_update_all<T, K, true, true> : iw::iw_update_all<T, K, false, true>)
                              : (p0r ? iw::iw_update_all<T, K, true> : iw::iw_update_all<T, K, false>);
+            // pixel pairs when every pair is aligned (iw_update_all2)
+            const long long Np = dom_.npix_mem(), b = dom_.off(0, dom_.y_lo), e = dom_.off(0, dom_.y_hi);
+            auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+            const bool pairs = upd_pairs_ && Np % 4 == 0 && b % 2 == 0 && (e - b) % 2 == 0 && al16(pall_) &&
+                               al16(cur_O_) && ((uintptr_t)cur_A_ & (2 * sizeof(T) - 1)) == 0 && al16(r_) && al16(pre_);
+            if (pairs) {
+                auto k2 = upd_nt_ ? (p0r ? iw::iw_update_all2<T, K, true, true> : iw::iw_update_all2<T, K, false, true>)
+                                  : (p0r ? iw::iw_update_all2<T, K, true> : iw::iw_update_all2<T, K, false>);
+                const long long need = ((e - b) / 2 + kBlock - 1) / kBlock;
+                const int grid = (int)std::max(1LL, std::min<long long>(need, upd_blocks_));
+                hipLaunchKernelGGL(k2, dim3(grid), dim3(kBlock), 0, stream_, args(), cur_O_, cur_A_,
+                                   (const T*)pall_, 3 * Np, (const double*)red_.scalars, rz(0), (const T*)r_,
+                                   (const T*)pre_);
+                OPT_HIP_CHECK(hipGetLastError());
+                return;
+            }
             const long long need = (dom_.npix_mem() + kBlock - 1) / kBlock;
             const int grid = (int)std::max(1LL, std::min<long long>(need, upd_blocks_));
             hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, stream_, args(), cur_O_, cur_A_,
@@ -2596,11 +2695,20 @@ private:
     }
     // tiles of iw_jtf_apply: 60-column strips
     int fused_strips() const { return (dom_.W + iw::kFStrip - 1) / iw::kFStrip; }
+    // the same with side-by-side waves (Args::side): groups of 4 strips x row chunks of rows_
+    int side_chunks() const { return (dom_.y_hi - dom_.y_lo + rows_ - 1) / rows_; }
+    int fused_side_blocks() const {
+        return (fused_strips() + kBlock / kWave - 1) / (kBlock / kWave) * side_chunks();
+    }
     int fused_blocks() const { return fused_strips() * nrowblocks_; }
     // iw_cost60's rows per wave (OPT_AMD_IW_COST_ROWS; 0: the plan's rows, 32 at 4096^2 —
     // 16 / 24 / 48 / 64 ran 138-146 us against 132-135, tools/r05_cost_rows_ab.sh; held to
     // 64 VGPRs for 8 waves per SIMD instead of 6 it spilled and ran 141-142)
     int cost_rows() const { return cost_rows_ > 0 ? cost_rows_ : rows_; }
+    int cost_side_blocks() const {
+        return (fused_strips() + kBlock / kWave - 1) / (kBlock / kWave) *
+               ((dom_.y_hi - dom_.y_lo + cost_rows() - 1) / cost_rows());
+    }
     int cost_blocks() const {
         return fused_strips() * ((dom_.y_hi - dom_.y_lo + cost_rows() * 4 - 1) / (cost_rows() * 4));
     }
@@ -2694,7 +2802,8 @@ private:
     void launch_jtf_apply(T* pout, bool no_ap, bool rec = false) {
         iw::Args<T> a = args();
         a.nstrips = fused_strips();
-        const int nb = fused_blocks();
+        a.side = jtf_side_ ? 1 : 0;
+        const int nb = jtf_side_ ? fused_side_blocks() : fused_blocks();
         a.tb0 = 0; a.tn0 = nb; a.tb1 = 0;   // every tile (geom_fused)
         if (rec) {
             if (!no_ap || (pout && pout != rec_[0])) throw std::logic_error("iw_jtf_apply<REC>: record 0 only, no Ap");
@@ -2722,14 +2831,26 @@ private:
         const int nb = fused_blocks();   // the reduction slot spans every tile
         a.tb0 = 0; a.tn0 = nb; a.tb1 = 0;
         int grid = nb;
-        if (part == 1) {
+        int nbr = nb;
+        if (pcg_side_) {   // side-by-side waves (Args::side): tile = row chunk x group of 4 strips
+            const int ng = (fs + kBlock / kWave - 1) / (kBlock / kWave), nch = side_chunks();
+            a.side = 1;
+            nbr = grid = a.tn0 = ng * nch;
+            if (part == 1) {
+                a.tb0 = ng; a.tn0 = ng * (nch - 2);
+                grid = a.tn0;
+            } else if (part == 2) {
+                a.tb0 = 0; a.tn0 = ng; a.tb1 = ng * (nch - 1);
+                grid = 2 * ng;
+            }
+        } else if (part == 1) {
             a.tb0 = fs; a.tn0 = fs * (nrowblocks_ - 2);
             grid = a.tn0;
         } else if (part == 2) {
             a.tb0 = 0; a.tn0 = fs; a.tb1 = fs * (nrowblocks_ - 1);
             grid = 2 * fs;
         }
-        const ReduceSlot rs = red_.slot(nb, rz(i));
+        const ReduceSlot rs = red_.slot(nbr, rz(i));
         auto go = [&](auto kern) {
             launch_timed("iw_pcg", kern, grid, a, pin, rin, (const T*)pre_, pout, rout, delta_, red_.scalars,
                          rz(i - 1), base_scale, rs, pin2);
@@ -2854,7 +2975,11 @@ private:
             a.nstrips = fused_strips();
             a.rows = cost_rows();
             a.nrowblocks = (dom_.y_hi - dom_.y_lo + a.rows * 4 - 1) / (a.rows * 4);
-            const int nb = a.nstrips * a.nrowblocks;
+            int nb = a.nstrips * a.nrowblocks;
+            if (cost_side_) {   // side-by-side waves (Args::side)
+                a.side = 1;
+                nb = cost_side_blocks();
+            }
             a.tb0 = 0; a.tn0 = nb; a.tb1 = 0;
             hipLaunchKernelGGL(iw::iw_cost60<T>, dim3(nb), dim3(kBlock), 0, stream_, a, red_.slot(nb, sc_out));
         } else {
@@ -2905,6 +3030,13 @@ private:
     T* pall_ = nullptr;                 // allp: lIterations p vectors of 3 N, p_i = pall_ + 3 N i
     int pall_cap_ = 0;
     bool pall_warned_ = false;
+    bool upd_pairs_ = true;             // OPT_AMD_IW_UPD_PAIRS=0: iw_update_all one pixel per thread
+    // OPT_AMD_IW_PCG_SIDE (default 1): iw_pcg with side-by-side waves (Args::side) — the block's
+    // four waves walk the same rows of four adjacent 60-column strips (round 6: 270 -> 257 us
+    // per pass at 4096^2, same box interleaved); 0 the four waves stacked over one strip
+    bool pcg_side_ = true;
+    bool jtf_side_ = false;             // OPT_AMD_IW_JTF_SIDE=1: iw_jtf_apply side by side
+    bool cost_side_ = false;            // OPT_AMD_IW_COST_SIDE=1: iw_cost60 side by side
     long long pall_limit_mb_ = -1;      // OPT_AMD_IW_ALLP_LIMIT_MB: cap on the kept p vectors (tests the fallback)
     bool recl_ = false;                 // the plan holds the REC layout (rec_on_ and the fused loop's knobs)
     T* rec_[3] = {nullptr, nullptr, nullptr};   // REC: iteration i's record in rec_[i % 3] (i % 2 undeferred)

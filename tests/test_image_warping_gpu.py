@@ -698,18 +698,20 @@ def test_kept_p_update_is_bitwise_the_deferred_delta(monkeypatch, W, H, lit, dou
     (pairs folded by the even passes): the trajectory is bitwise the same, fp32 and fp64
     (lIterations 1 and 17 take the deferred path either way). ADVICE r5: when the kept
     vectors do not fit in HBM the Step falls back to the deferred delta — forced here with
-    OPT_AMD_IW_ALLP_LIMIT_MB=0 — and is again bitwise the same."""
+    OPT_AMD_IW_ALLP_LIMIT_MB=0 — and is again bitwise the same; so is iw_update_all one pixel
+    per thread against pixel pairs (OPT_AMD_IW_UPD_PAIRS, taken where N % 4 == 0)."""
     out = []
-    for v in ("0", "1", "fallback"):
+    for v in ("0", "1", "fallback", "nopairs"):
         monkeypatch.setenv("OPT_AMD_IW_ALLP", "0" if v == "0" else "1")
         monkeypatch.setenv("OPT_AMD_IW_ALLP_LIMIT_MB", "0" if v == "fallback" else "-1")
+        monkeypatch.setenv("OPT_AMD_IW_UPD_PAIRS", "0" if v == "nopairs" else "1")
         w = perturbed(W, H, seed=5 * W + H)
         s = solver(W, H, double=double)
         prm = device_params(w, double=double)
         s.set_solver_params({"nIterations": 3, "lIterations": lit})
         c = np.array(s.profiled_solve(prm))
         out.append((c, to_np(prm[0]), to_np(prm[1]), np.array(s.scalars(2 + 5 * (lit + 2)))))
-    for k in (1, 2):
+    for k in (1, 2, 3):
         for a, b in zip(out[0], out[k]):
             np.testing.assert_array_equal(a, b)
 

@@ -21,6 +21,10 @@
 //   pair124   two pixels per lane: 124-column strips, x = 124 s - 2 + 2 lane (+0 / +1)
 //   shiftK    strip64 with every window shifted by K columns (x = 64 s + K + lane): the cost of
 //             a window's byte alignment alone (K = 2: 8 B, 8: 32 B, 16: 64 B, 32: 128 B)
+//   side60    (round 6) strip60 with the block's four waves side by side over four adjacent
+//             60-column strips walking the same rows: iw_pcg's geometry since round 6
+// `pcgbench r06` runs the round-6 set, each walk also with its occupancy capped by dynamic LDS
+// at iw_pcg's 3 waves per SIMD (48 KB per block: 3 blocks per CU).
 // Not part of the library.  hipcc --offload-arch=gfx950 -O3 -o tools/pcgbench tools/pcgbench.hip
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -51,7 +55,7 @@ template <int MODE, int PF>   // MODE 0 strip60, 1 strip64, 2 side64, 3 pad60, 4
 __global__ __launch_bounds__(256) void walk(Arr A, int W, int H, int rows, int nstrips) {
     const int t = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int strip, y0;
-    if (MODE == 2) {
+    if (MODE == 2 || MODE == 7) {
         const int ng = (nstrips + 3) / 4;
         strip = (t % ng) * 4 + w;
         y0 = (t / ng) * rows;
@@ -60,17 +64,18 @@ __global__ __launch_bounds__(256) void walk(Arr A, int W, int H, int rows, int n
         y0 = ((t / nstrips) * 4 + w) * rows;
     }
     constexpr bool S60 = MODE == 0 || MODE >= 3;
+    constexpr bool PADL = MODE >= 3 && MODE <= 6;   // the strip-padded layouts
     const int x = S60 ? strip * 60 - 2 + lane : strip * 64 + lane;
     const bool out = S60 ? (lane >= 2 && lane < 62 && x < W) : x < W;
     const int xc = x < 0 ? 0 : (x >= W ? W - 1 : x);
     const int y1 = min(y0 + rows, H);
-    if (y0 >= y1) return;
+    if (y0 >= y1 || strip >= nstrips) return;
     const int lo = S60 ? 2 : 1;   // halo rows above / below
     const int pw = nstrips * 64;  // padded row (MODE 3 / 4)
     const int xs = (xc / 60) * 64 + xc % 60;
     auto idx = [&](int y) {
         const int yc = y < 0 ? 0 : (y >= H ? H - 1 : y);
-        return MODE >= 3 ? (long long)yc * pw + xs : (long long)yc * W + xc;
+        return PADL ? (long long)yc * pw + xs : (long long)yc * W + xc;
     };
     auto idu = [&](int y) {
         const int yc = y < 0 ? 0 : (y >= H ? H - 1 : y);
@@ -88,7 +93,7 @@ __global__ __launch_bounds__(256) void walk(Arr A, int W, int H, int rows, int n
         const float v = mix(c);
         acc += v;
         const int ys = y - (lo - 1) - 1;   // the row stored this trip (one behind the loads)
-        if (MODE >= 5) {   // full-line stores: every lane, a bijection lane -> slot
+        if (MODE == 5 || MODE == 6) {   // full-line stores: every lane, a bijection lane -> slot
             if (ys >= y0 && ys < y1) {
                 const int sl = (lane >= 2 && lane < 62) ? lane - 2 : (lane < 2 ? 60 + lane : lane);
                 const long long i = (long long)ys * pw + 64 * strip + sl;
@@ -244,21 +249,24 @@ __global__ __launch_bounds__(256) void flat(Arr A, long long n) {
 }
 
 template <typename K, typename... Args>
-static float timeit(K k, int grid, Args... a) {
+static float timeit_lds(K k, int grid, unsigned lds, Args... a) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
-    hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, a...);
+    hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, 0, a...);
     (void)hipEventRecord(e0);
     const int reps = 20;
-    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k, dim3(grid), dim3(256), 0, 0, a...);
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL(k, dim3(grid), dim3(256), lds, 0, a...);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e0, e1);
     return 1000.f * ms / reps;
 }
+template <typename K, typename... Args>
+static float timeit(K k, int grid, Args... a) { return timeit_lds(k, grid, 0u, a...); }
 
-int main() {
+int main(int argc, char** argv) {
+    const bool r06 = argc > 1 && argv[1][0] == 'r';
     const int W = 4096, H = 4096;
     const long long N = (long long)W * H;
     Arr A;
@@ -275,6 +283,30 @@ int main() {
     A.qt = (float*)bufs[10];
     const double bytes = 65.0 * N;
     auto rep = [&](const char* name, float us) { printf("%-28s %8.1f us  %6.0f GB/s (65 B/px)\n", name, us, bytes / us / 1e3); };
+    if (r06) {   // iw_pcg's geometries at its occupancy (3 waves per SIMD: 48 KB of LDS per block)
+        const unsigned cap = 48 * 1024;
+        for (int rows : {32}) {
+            const int n60 = (W + 59) / 60, n64 = W / 64, rb = (H + 4 * rows - 1) / (4 * rows);
+            const int g60 = (n60 + 3) / 4 * (H / rows), g64 = (n64 / 4) * (H / rows);
+            for (int k = 0; k < 2; ++k) {
+                const unsigned l = k ? cap : 0u;
+                const char* o = k ? " occ3" : " free";
+                char nm[64];
+                snprintf(nm, 64, "strip60 pf1%s", o); rep(nm, timeit_lds(walk<0, 1>, n60 * rb, l, A, W, H, rows, n60));
+                snprintf(nm, 64, "strip60 pf2%s", o); rep(nm, timeit_lds(walk<0, 2>, n60 * rb, l, A, W, H, rows, n60));
+                snprintf(nm, 64, "side60 pf1%s", o); rep(nm, timeit_lds(walk<7, 1>, g60, l, A, W, H, rows, n60));
+                snprintf(nm, 64, "side60 pf2%s", o); rep(nm, timeit_lds(walk<7, 2>, g60, l, A, W, H, rows, n60));
+                snprintf(nm, 64, "strip64 pf1%s", o); rep(nm, timeit_lds(walk<1, 1>, n64 * rb, l, A, W, H, rows, n64));
+                snprintf(nm, 64, "side64 pf1%s", o); rep(nm, timeit_lds(walk<2, 1>, g64, l, A, W, H, rows, n64));
+                snprintf(nm, 64, "side64 pf2%s", o); rep(nm, timeit_lds(walk<2, 2>, g64, l, A, W, H, rows, n64));
+            }
+        }
+        for (int g : {2048, 8192}) {
+            char nm[64];
+            snprintf(nm, 64, "flat grid=%d", g); rep(nm, timeit(flat, g, A, N));
+        }
+        return 0;
+    }
     for (int rows : {16, 32}) {
         const int n60 = (W + 59) / 60, n64 = W / 64, rb = (H + 4 * rows - 1) / (4 * rows);
         char nm[64];
