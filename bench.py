@@ -64,7 +64,7 @@ def apply_bytes_per_px(i: int, liter: int = 10) -> int:
 # bench). FETCH_SIZE reads exactly 1/2 of the bytes on gfx950 for 1/4/8/16-B-per-lane
 # streaming reads and WRITE_SIZE is exact (profiles/r01_fetchcal.json, 1 GiB arrays), so
 # traffic = 2 FETCH_SIZE + WRITE_SIZE, averaged over the lIterations in-loop launches.
-PMC_FILE = os.path.join(ROOT, "profiles", "r05_final_pmc.json")
+PMC_FILE = os.path.join(ROOT, "profiles", "r06_pmc.json")
 APPLY_VARIANT = {0: "iw_apply<float, 1, 0,", 1: "iw_apply<float, 2, 1,", 2: "iw_apply<float, 2, 2,"}
 
 
@@ -213,7 +213,7 @@ def pmc_limiter(liter: int, first: int = 0):
             "source": os.path.relpath(PMC_FILE, ROOT) + " (fractions of SQ_WAVE_CYCLES)"}
 
 
-PMC_FILE_SFS = os.path.join(ROOT, "profiles", "r05_final_pmc_sfs.json")
+PMC_FILE_SFS = os.path.join(ROOT, "profiles", "r06_pmc_sfs.json")
 
 
 def pmc_traffic_sfs():
