@@ -183,6 +183,20 @@ int Pool::sample(int image, int ch, int x, int y, int dx_image, int dy_image) {
     return intern(n);
 }
 
+int Pool::substitute(int id, const std::map<int, int>& repl) {
+    if (id < 0) return id;
+    auto it = repl.find(id);
+    if (it != repl.end()) return it->second;
+    Node n = nodes_[id];
+    if (n.a < 0 && n.b < 0 && n.d < 0) return id;
+    Node m = n;
+    m.a = substitute(n.a, repl);
+    m.b = substitute(n.b, repl);
+    m.d = substitute(n.d, repl);
+    if (m.a == n.a && m.b == n.b && m.d == n.d) return id;
+    return intern(m);
+}
+
 int Pool::diff(int id, int var) {
     auto it = dmemo_.find({id, var});
     if (it != dmemo_.end()) return it->second;

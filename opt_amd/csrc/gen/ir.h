@@ -64,6 +64,8 @@ public:
     int diff(int id, int var);
     // id with every centred access / bounds test / coordinate moved by `s`
     int shift(int id, const int* s);
+    // id with every node in `repl` replaced by its image (children rebuilt, hash-consed)
+    int substitute(int id, const std::map<int, int>& repl);
     // Visit every node reachable from id once.
     template <class F>
     void visit(int id, F&& f) const {

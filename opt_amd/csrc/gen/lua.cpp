@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -582,6 +583,8 @@ private:
     GModel* m_;
     std::shared_ptr<Scope> globals_;
     std::vector<int> energy_terms_;   // scalar residual expressions, in Energy order
+    std::vector<std::pair<int, int>> sample_cache_;   // cached Sample node (offset 0) -> its image
+    int cache_samples(int e);
     int line_ = 0;
 
     Pool& P() { return m_->pool; }
@@ -1416,6 +1419,94 @@ void Interp::install() {
     }
 }
 
+// Per-step sample cache (round 6): a SampledImage read whose coordinates use the unknowns
+// and coordinates of ONE pixel (offset o) — optical_flow's I_hat(x + u(0,0), y + v(0,0)) — is
+// fixed while the PCG loop runs (the unknowns change only at the update). It becomes a
+// T-valued ComputedArray of its own (value + one gradient image per unknown access: the
+// sampled derivative images times the coordinates' derivatives, the same expressions
+// diff() forms for the Sample node, ad.sampledimage / o.t:3266-3280), evaluated once per
+// Step by the precompute kernels, and the residual reads it at offset o. The applies then
+// read two cached partials per pixel instead of re-sampling eight taps in every PCG
+// iteration (the reference re-samples, as the generic path did before). The values are
+// the same expressions on the same inputs. OPT_AMD_GEN_SAMPLE_CACHE=0 keeps the samples
+// in the residuals.
+int Interp::cache_samples(int e) {
+    const char* sv = getenv("OPT_AMD_GEN_SAMPLE_CACHE");
+    if (sv && atoi(sv) == 0) return e;
+    std::map<int, int> repl;
+    P().visit(e, [&](int id, const Node& n) {
+        // (a sample without derivative images stays: the residual check below names it when
+        // its coordinates use the unknowns)
+        if (n.op != Op::Sample || n.off2[0] < 0 || n.off2[1] < 0 || repl.count(id)) return;
+        int off[3] = {0, 0, 0};
+        bool set[3] = {false, false, false}, ok = true, reads = false;
+        auto want = [&](int d, int v) {
+            if (set[d] && off[d] != v) ok = false;
+            set[d] = true;
+            off[d] = v;
+        };
+        for (int c : {n.a, n.b})
+            P().visit(c, [&](int, const Node& q) {
+                if (q.op == Op::Read) {
+                    if (q.slot >= 0 || computed_of(q.i)) { ok = false; return; }
+                    reads = true;
+                    for (int d = 0; d < 3; ++d) want(d, q.off[d]);
+                } else if (q.op == Op::Coord) {
+                    want(q.i, q.off[q.i]);
+                } else if (q.op == Op::Sample || q.op == Op::InBox) {
+                    ok = false;
+                }
+            });
+        if (!ok || !reads || m_->images.size() + 3 > 16) return;   // GenArgs::img holds 16 images
+        const int neg[3] = {-off[0], -off[1], -off[2]};
+        const int s0 = P().shift(id, neg);
+        int img = -1;
+        for (auto& c : sample_cache_)
+            if (c.first == s0) img = c.second;
+        if (img < 0) {
+            GImage im;
+            im.name = "sample_cache_" + std::to_string(sample_cache_.size());
+            const std::vector<int> unk = m_->unknown_images();
+            if (unk.empty()) return;
+            im.dims = m_->images[unk[0]].dims;
+            im.channels = 1;
+            im.internal = im.tvalued = true;
+            m_->images.push_back(im);
+            img = (int)m_->images.size() - 1;
+            GComputed c;
+            c.image = img;
+            c.expr = {s0};
+            std::set<int> unkr;
+            P().visit(s0, [&](int nid, const Node& q) {
+                if (q.op == Op::Read && q.slot < 0 && m_->images[q.i].unknown) unkr.insert(nid);
+            });
+            for (int u : unkr) {
+                GGrad g;
+                g.ch = 0;
+                g.u = u;
+                g.expr = P().diff(s0, u);
+                int gnode = g.expr;
+                if (!P().is_const(g.expr)) {
+                    GImage gi;
+                    gi.name = im.name + "_d_" + std::to_string(u);
+                    gi.dims = im.dims;
+                    gi.internal = gi.tvalued = true;
+                    m_->images.push_back(gi);
+                    g.gimg = (int)m_->images.size() - 1;
+                    const int z[3] = {0, 0, 0};
+                    gnode = P().read(g.gimg, 0, z);
+                }
+                P().add_computed_grad(img, 0, u, gnode);
+                c.grads.push_back(g);
+            }
+            m_->computed.push_back(c);
+            sample_cache_.push_back({s0, img});
+        }
+        repl[id] = P().read(img, 0, off);
+    });
+    return repl.empty() ? e : P().substitute(e, repl);
+}
+
 // Classify and finish the residual templates (classifyexpression + bbox, o.t:2669-2715).
 void Interp::finish() {
     // an Array declared on an Unknown's parameter slot is a view of that unknown
@@ -1424,6 +1515,7 @@ void Interp::finish() {
         if (!im.unknown && !im.internal)
             for (auto& u : m_->images)
                 if (u.unknown && u.index == im.index) im.tvalued = true;
+    for (int& e : energy_terms_) e = cache_samples(e);
     for (int e : energy_terms_) {
         GResidual r;
         bool any = false;

@@ -301,9 +301,16 @@ public:
     std::string slab_refusal() const {
         if (m_.unknown_dims() != 2) return "generic: row-slab decomposition needs a 2-D energy";
         if (!m_.graphs.empty()) return "generic: no row-slab decomposition for graph energies";
-        for (auto& r : m_.residuals) {
+        // (sampled reads may sit in a residual or, cached per Step, in a ComputedArray)
+        std::vector<int> roots;
+        for (auto& r : m_.residuals) roots.push_back(r.expr);
+        for (auto& c : m_.computed) {
+            roots.insert(roots.end(), c.expr.begin(), c.expr.end());
+            for (auto& g : c.grads) roots.push_back(g.expr);
+        }
+        for (int e : roots) {
             bool sample = false;
-            m_.pool.visit(r.expr, [&](int, const gen::Node& n) { sample |= n.op == gen::Op::Sample; });
+            m_.pool.visit(e, [&](int, const gen::Node& n) { sample |= n.op == gen::Op::Sample; });
             if (sample) return "generic: no row-slab decomposition with sampled images (data-dependent reads)";
         }
         return "";

@@ -1246,7 +1246,10 @@ __device__ __forceinline__ void iw_pcg_body(const Args<T>& a, const T* __restric
 }
 template <typename T, int DM, int E = 0, bool P0 = false, bool SNT = false, bool U2 = false, bool PF2 = false,
           bool REC = false>
-__global__ __launch_bounds__(kBlock) void iw_pcg(Args<T> a, const T* __restrict__ pin, const T* __restrict__ rin,
+#ifndef IW_PCG_WAVES
+#define IW_PCG_WAVES 1   // A/B builds (tools/ab_build.sh): the minimum waves per SIMD iw_pcg is held to
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IW_PCG_WAVES))) void iw_pcg(Args<T> a, const T* __restrict__ pin, const T* __restrict__ rin,
                                                  const T* __restrict__ pre, T* __restrict__ pout, T* rout,
                                                  T* __restrict__ delta, double* __restrict__ sc, int prev,
                                                  double base_scale, ReduceSlot rs, const T* pin2 = nullptr) {

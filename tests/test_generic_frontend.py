@@ -247,10 +247,15 @@ def test_our_energy_files_lower_exactly_as_the_reference_files(name):
 @pytest.mark.parametrize("name,kernel", [("image_warping", "gen_apply_strip"), ("poisson_image_editing", "gen_apply_strip"),
                                          ("shape_from_shading", "gen_apply_strip"),
                                          ("intrinsic_image_decomposition", "gen_apply_strip"),
-                                         ("optical_flow", "gen_apply ")])
-def test_apply_variant_rule(name, kernel):
+                                         ("optical_flow", "gen_apply_strip"), ("optical_flow:nocache", "gen_apply ")])
+def test_apply_variant_rule(monkeypatch, name, kernel):
     """Static choice of the centred apply (codegen.cpp): the register strips for 2-D
-    energies without sampled reads (data-dependent addresses: optical_flow keeps the
-    gather), else tiles when the energy has many residual instances per centred residual."""
+    energies without sampled reads in their residuals, else tiles when the energy has many
+    residual instances per centred residual. optical_flow's sample is cached per Step as a
+    ComputedArray (lua.cpp cache_samples), so it takes the strip too; without the cache
+    (OPT_AMD_GEN_SAMPLE_CACHE=0) the data-dependent sample keeps the gather."""
+    if name.endswith(":nocache"):
+        monkeypatch.setenv("OPT_AMD_GEN_SAMPLE_CACHE", "0")
+        name = name.split(":")[0]
     head = api.generic_source(E(name)).splitlines()[0]
     assert head.startswith("// apply: " + kernel)
