@@ -176,6 +176,83 @@ __global__ __launch_bounds__(kBlock) void of_apply(Args<T> a, const T* __restric
     block_reduce_publish<1>(v, rs, blockIdx.x);
 }
 
+// The same apply as a register strip (round 6): a wave owns 62 output columns
+// (x = 62 strip - 1 + lane, outputs at lanes 1..62) and walks `rows` rows keeping p of rows
+// y-1, y, y+1 in registers (row y+2, G and dadd of row y+1 in flight), the horizontal
+// neighbours are DPP lane shifts; a block's four waves are side by side over four adjacent
+// strips (as iw_pcg). Each p element is loaded once per wave instead of five times per
+// pixel by the flat kernel's gathers. Same terms in the same order per pixel (fit, then per
+// direction the own instance and the neighbour's, then dadd); p.Ap sums in lane / row order.
+constexpr int kOfOut = 62;
+template <typename T>
+__device__ __forceinline__ V2<T> of_lane_left(V2<T> v) { return V2<T>{from_left0(v.x), from_left0(v.y)}; }
+template <typename T>
+__device__ __forceinline__ V2<T> of_lane_right(V2<T> v) { return V2<T>{from_right0(v.x), from_right0(v.y)}; }
+template <typename T>
+__global__ __launch_bounds__(kBlock) void of_apply_strip(Args<T> a, const T* __restrict__ p, T* __restrict__ Ap,
+                                                         const T* __restrict__ dadd, const int* stop, ReduceSlot rs,
+                                                         int nstrips, int rows) {
+    if (stop && *stop) return;
+    const Domain& d = a.dom;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+    const int lb = xcd_remap(blockIdx.x, gridDim.x);
+    const int ng = (nstrips + kBlock / kWave - 1) / (kBlock / kWave);
+    const int strip = (lb % ng) * (kBlock / kWave) + w;
+    const int y0 = d.y_lo + (lb / ng) * rows, y1 = strip < nstrips ? min(y0 + rows, d.y_hi) : y0;
+    const int x = strip * kOfOut - 1 + lane;
+    const bool xin = x >= 0 && x < d.W;
+    const bool out = xin && lane >= 1 && lane <= kOfOut;
+    T dot = 0;
+    if (y0 < y1) {
+        // masked loads without a branch: element 0 when outside, the value selected after
+        auto ld = [&](const T* b, int y) -> V2<T> {
+            const bool ok = xin && y >= 0 && y < d.H;
+            const V2<T> v = ld2(b, ok ? d.off(x, y) : 0);
+            return ok ? v : V2<T>{0, 0};
+        };
+        V2<T> pm = ld(p, y0 - 1), pc = ld(p, y0), pn = ld(p, y0 + 1);
+        V2<T> gc = ld((const T*)a.G, y0), cc = dadd ? ld(dadd, y0) : V2<T>{0, 0};
+        const T wr = a.wr;
+        for (int y = y0; y < y1; ++y) {
+            const V2<T> pnn = ld(p, y + 2), gn = ld((const T*)a.G, y + 1);
+            const V2<T> cn = dadd ? ld(dadd, y + 1) : V2<T>{0, 0};
+            const V2<T> pk = pc;
+            const V2<T> pr = of_lane_right(pc), pl = of_lane_left(pc);
+            const T jx = -a.wf * gc.x, jy = -a.wf * gc.y;
+            const T jp = jx * pk.x + jy * pk.y;
+            T ax = jx * jp, ay = jy * jp;
+            const bool in_r = x + 1 < d.W, in_l = x - 1 >= 0, in_d = y + 1 < d.H, in_u = y - 1 >= 0;
+            // DX / DY order: (+1, 0), (-1, 0), (0, +1), (0, -1); per direction the instance
+            // centred here (t = k + s), then the neighbour's (q = k - s)
+            const V2<T> nt[4] = {pr, pl, pn, pm}, nq[4] = {pl, pr, pm, pn};
+            const bool it[4] = {in_r, in_l, in_d, in_u}, iq[4] = {in_l, in_r, in_u, in_d};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (it[k]) {
+                    ax += wr * (wr * (pk.x - nt[k].x));
+                    ay += wr * (wr * (pk.y - nt[k].y));
+                }
+                if (iq[k]) {
+                    ax += -wr * (wr * (nq[k].x - pk.x));
+                    ay += -wr * (wr * (nq[k].y - pk.y));
+                }
+            }
+            if (dadd) {
+                ax += cc.x * pk.x;
+                ay += cc.y * pk.y;
+            }
+            if (out) {
+                st2(Ap, d.off(x, y), ax, ay);
+                dot += pk.x * ax + pk.y * ay;
+            }
+            pm = pc; pc = pn; pn = pnn; gc = gn; cc = cn;
+        }
+    }
+    double v[1] = {(double)dot};
+    block_reduce_publish<1>(v, rs, blockIdx.x);
+}
+
 // cost 1/2 sum r^2 (delta == nullptr) or the LM model cost 1/2 sum (r + J delta)^2
 // (o.t:3119-3129, 2915-2943)
 template <typename T>
@@ -304,7 +381,7 @@ public:
         return L;
     }
     int halo() const { return 1; }
-    int stencil_blocks() const { return std::max<int>(grid().x * grid().y, tgrid()); }
+    int stencil_blocks() const { return std::max<int>(std::max<int>(grid().x * grid().y, tgrid()), strip_blocks()); }
     void bind(void** params, hipStream_t s) {
         a_.wf = (T)*(const float*)params[idx_wf_];
         a_.wr = (T)*(const float*)params[idx_wr_];
@@ -341,8 +418,15 @@ public:
         OPT_HIP_CHECK(hipGetLastError());
     }
     void apply(const T* p, T* Ap, const T* dadd, const int* stop, ReduceSlot rs, hipStream_t s) {
-        rs.nblocks = tgrid();
-        hipLaunchKernelGGL((of::of_apply<T>), dim3(tgrid()), dim3(kBlock), 0, s, a_, p, Ap, dadd, stop, rs);
+        if (strip_) {   // OPT_AMD_OF_STRIP (default 1): of_apply_strip
+            const int ns = (dom_.W + of::kOfOut - 1) / of::kOfOut;
+            rs.nblocks = strip_blocks();
+            hipLaunchKernelGGL((of::of_apply_strip<T>), dim3(rs.nblocks), dim3(kBlock), 0, s, a_, p, Ap, dadd, stop, rs,
+                               ns, strip_rows_);
+        } else {
+            rs.nblocks = tgrid();
+            hipLaunchKernelGGL((of::of_apply<T>), dim3(tgrid()), dim3(kBlock), 0, s, a_, p, Ap, dadd, stop, rs);
+        }
         OPT_HIP_CHECK(hipGetLastError());
     }
     void cost(ReduceSlot rs, hipStream_t s) {
@@ -368,6 +452,13 @@ public:
 private:
     dim3 grid() const { return dim3((dom_.W + 63) / 64, (dom_.y_hi - dom_.y_lo + 3) / 4); }
     int tgrid() const { return tile_blocks(pix_tiles(dom_)); }
+    // the strip apply's grid: groups of four 62-column strips x row chunks of strip_rows_
+    int strip_blocks() const {
+        const int ns = (dom_.W + of::kOfOut - 1) / of::kOfOut;
+        return (ns + kBlock / kWave - 1) / (kBlock / kWave) * ((dom_.y_hi - dom_.y_lo + strip_rows_ - 1) / strip_rows_);
+    }
+    const bool strip_ = env_int("OPT_AMD_OF_STRIP", 1) != 0;
+    const int strip_rows_ = std::max(1, env_int("OPT_AMD_OF_ROWS", 8));   // 8 / 16 / 32: 81.5 / 88.2 / 89.1 us at 3840x2160 fp64
     Domain dom_;
     StateOptions opts_;
     int idx_X_, idx_I_, idx_Ih_, idx_Ihx_, idx_Ihy_, idx_wf_, idx_wr_;

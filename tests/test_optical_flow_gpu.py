@@ -36,6 +36,37 @@ def perturbed(W, H, seed, sigma=3.0, max_flow=1.0):
 
 
 @pytest.mark.parametrize("double", [False, True])
+@pytest.mark.parametrize("W,H,rows", [(64, 48, "16"), (97, 61, "16"), (130, 7, "16"), (1, 30, "16"), (124, 33, "5"),
+                                      (125, 2, "16"), (63, 70, "1")])
+def test_strip_apply_equals_flat_apply(monkeypatch, W, H, rows, double):
+    """of_apply_strip (round 6: 62-column register strips, side-by-side waves, OPT_AMD_OF_ROWS
+    rows per wave) against the flat per-pixel of_apply (OPT_AMD_OF_STRIP=0): the same terms
+    per pixel in the same order — Ap within 1e-15 (fp64) / 1e-6 (fp32) relative (fp
+    contraction may fuse differently in the two kernels), p.Ap likewise; strip edges at
+    widths 62 k +- 1 and row chunks that do not divide the height."""
+    import torch
+
+    w = perturbed(W, H, seed=W + 7 * H)
+    dt = torch.float64 if double else torch.float32
+    n = 2 * W * H
+    p = torch.from_numpy(np.random.default_rng(3).normal(size=n)).to("cuda", dt)
+    out = {}
+    for strip in ("1", "0"):
+        monkeypatch.setenv("OPT_AMD_OF_STRIP", strip)
+        monkeypatch.setenv("OPT_AMD_OF_ROWS", rows)
+        s = OptSolver([W, H], ENERGY, "LMGPU", double_precision=double)
+        prm = params(w, double)
+        r = torch.zeros(n, device="cuda", dtype=dt)
+        s.eval_jtf(prm, r, torch.zeros_like(r))   # caches the sampled gradient
+        Ap = torch.zeros(n, device="cuda", dtype=dt)
+        out[strip] = (s.apply_jtj(prm, p, Ap), to_np(Ap))
+        s.close()
+    tol = 1e-14 if double else 1e-6
+    assert rel_err(out["1"][1], out["0"][1]) < tol
+    assert out["1"][0] == pytest.approx(out["0"][0], rel=tol)
+
+
+@pytest.mark.parametrize("double", [False, True])
 @pytest.mark.parametrize("W,H", [(64, 48), (97, 61), (130, 7), (1, 30)])
 def test_kernels_match_oracle(W, H, double):
     import torch
