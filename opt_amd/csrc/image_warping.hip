@@ -85,6 +85,10 @@ struct Args {
     // side != 0 (geom): the block's four waves walk the SAME rows over four adjacent strips
     // (tile = row chunk x group of 4 strips) instead of four stacked row ranges of one strip
     int side;
+    // alt != 0 (iw_pcg): waves of odd row chunks ((y0 - y_lo) / rows odd) walk their rows
+    // bottom to top, so the two waves on either side of every chunk boundary read the shared
+    // halo rows at the same time (both at their start or both at their end)
+    int alt;
     // REC layout (round 5; the fused loop's iw_jtf_apply / iw_pcg / iw_update with REC): the
     // PCG vectors of iteration i as ONE record per pixel, [r.x r.y | p.x p.y | r.t p.t]
     // (6 T: three aligned pairs), and the per-Step static data as the record
@@ -1167,16 +1171,23 @@ __device__ __forceinline__ void iw_pcg_body(const Args<T>& a, const T* __restric
             if (!h.act) { h.p = (vec2_t<T>)0; h.pt = 0; }
             return h;
         };
-        const GRow<T> g0 = fin(raw(g.y0 - 2));
-        GRow<T> qc = fin(raw(g.y0 - 1));
-        GRow<T> qd = fin(raw(g.y0));
+        // the walk: row Y(k), k = 0 .. n - 1 (halo rows Y(-2), Y(-1), Y(n), Y(n + 1)); top to
+        // bottom, or with Args::alt on odd row chunks bottom to top — the same chain with
+        // "the next row" the one above (apply_ap2's carries then come from below: the same
+        // residual values, summed in the mirrored order)
+        const int n = g.y1 - g.y0;
+        const bool up = a.alt && (((g.y0 - a.dom.y_lo) / a.rows) & 1);
+        auto Y = [&](int k) { return up ? g.y1 - 1 - k : g.y0 + k; };
+        const GRow<T> g0 = fin(raw(Y(-2)));
+        GRow<T> qc = fin(raw(Y(-1)));
+        GRow<T> qd = fin(raw(Y(0)));
         ka = acarry_init(g0.p, g0.pt, g0.c, g0.s, g0.u, g0.act(), qc.p, qc.pt, qc.c, qc.s, qc.u, qc.act(), wr);
-        HRow<T> hup = stage_a(qc, qd, g.y0 - 1);
+        HRow<T> hup = stage_a(qc, qd, Y(-1));
         qc = qd;
-        qd = fin(raw(g.y0 + 1));
-        HRow<T> hc = stage_a(qc, qd, g.y0);
+        qd = fin(raw(Y(1)));
+        HRow<T> hc = stage_a(qc, qd, Y(0));
         qc = qd;
-        qd = fin(raw(g.y0 + 2));
+        qd = fin(raw(Y(2)));
         ACarry<T> kb = acarry_init(hup.p, hup.pt, hup.c, hup.s, hup.u, hup.act, hc.p, hc.pt, hc.c, hc.s, hc.u, hc.act, wr);
         // stage B at row y: Ap_i from (cur = row y, dn = row y+1), stores p_i, the three sums
         auto stage_b = [&](const HRow<T>& cur, const HRow<T>& dn, int y) {
@@ -1201,10 +1212,10 @@ __device__ __forceinline__ void iw_pcg_body(const Args<T>& a, const T* __restric
         // two rows per trip, the row records swapping roles (no register copies): entering a
         // trip at row y, q0 / q1 hold rows y+1 / y+2 and h0 row y
         if constexpr (!U2) {
-            for (int y = g.y0; y < g.y1; ++y) {
-                const GRaw<T> nx = raw(min(y + 3, g.y1 + 1));
-                const HRow<T> hd = stage_a(qc, qd, y + 1);
-                stage_b(hc, hd, y);
+            for (int k = 0; k < n; ++k) {
+                const GRaw<T> nx = raw(Y(min(k + 3, n + 1)));
+                const HRow<T> hd = stage_a(qc, qd, Y(k + 1));
+                stage_b(hc, hd, Y(k));
                 hc = hd;
                 qc = qd;
                 qd = fin(nx);
@@ -1212,31 +1223,31 @@ __device__ __forceinline__ void iw_pcg_body(const Args<T>& a, const T* __restric
         } else if constexpr (PF2) {
             GRow<T> q0 = qc, q1 = qd;
             HRow<T> h0 = hc, h1;
-            GRaw<T> na = raw(min(g.y0 + 3, g.y1 + 1)), nb = raw(min(g.y0 + 4, g.y1 + 1));
-            for (int y = g.y0; y < g.y1; y += 2) {
-                h1 = stage_a(q0, q1, y + 1);
-                stage_b(h0, h1, y);
+            GRaw<T> na = raw(Y(min(3, n + 1))), nb = raw(Y(min(4, n + 1)));
+            for (int k = 0; k < n; k += 2) {
+                h1 = stage_a(q0, q1, Y(k + 1));
+                stage_b(h0, h1, Y(k));
                 q0 = fin(na);
-                if (y + 1 >= g.y1) break;
-                na = raw(min(y + 5, g.y1 + 1));
-                h0 = stage_a(q1, q0, y + 2);
-                stage_b(h1, h0, y + 1);
+                if (k + 1 >= n) break;
+                na = raw(Y(min(k + 5, n + 1)));
+                h0 = stage_a(q1, q0, Y(k + 2));
+                stage_b(h1, h0, Y(k + 1));
                 q1 = fin(nb);
-                nb = raw(min(y + 6, g.y1 + 1));
+                nb = raw(Y(min(k + 6, n + 1)));
             }
         } else {
         GRow<T> q0 = qc, q1 = qd;
         HRow<T> h0 = hc, h1;
-        for (int y = g.y0; y < g.y1; y += 2) {
-            // stage A needs rows up to y1 + 1; the last trip re-reads that row (an L2 hit)
-            const GRaw<T> n1 = raw(min(y + 3, g.y1 + 1));
-            h1 = stage_a(q0, q1, y + 1);
-            stage_b(h0, h1, y);
+        for (int k = 0; k < n; k += 2) {
+            // stage A needs rows up to Y(n + 1); the last trip re-reads that row (an L2 hit)
+            const GRaw<T> n1 = raw(Y(min(k + 3, n + 1)));
+            h1 = stage_a(q0, q1, Y(k + 1));
+            stage_b(h0, h1, Y(k));
             q0 = fin(n1);
-            if (y + 1 >= g.y1) break;
-            const GRaw<T> n2 = raw(min(y + 4, g.y1 + 1));
-            h0 = stage_a(q1, q0, y + 2);
-            stage_b(h1, h0, y + 1);
+            if (k + 1 >= n) break;
+            const GRaw<T> n2 = raw(Y(min(k + 4, n + 1)));
+            h0 = stage_a(q1, q0, Y(k + 2));
+            stage_b(h1, h0, Y(k + 1));
             q1 = fin(n2);
         }
         }
@@ -2524,6 +2535,7 @@ private:
         jtf_side_ = env_int("OPT_AMD_IW_JTF_SIDE", 0) != 0;
         cost_side_ = env_int("OPT_AMD_IW_COST_SIDE", 0) != 0;
         upd_pairs_ = env_int("OPT_AMD_IW_UPD_PAIRS", 1) != 0;
+        pcg_alt_ = env_int("OPT_AMD_IW_PCG_ALT", 0) != 0;
     }
     // A zeroed plan vector with kSlack spare bytes: place() may move each vector's base
     // within them between Steps (every vector is rewritten before it is read in a Step).
@@ -2726,6 +2738,7 @@ private:
         a.nstrips = nstrips_; a.nrowblocks = nrowblocks_; a.rows = rows_;
         a.tb0 = 0; a.tn0 = nstrips_ * nrowblocks_; a.tb1 = 0;
         a.side = 0;
+        a.alt = 0;
         a.S = srec_;
         // same float expression the reference's evalJTF + guardedInvert evaluate
         const T wr2 = (T)wr_ * (T)wr_, wf2 = (T)wf_ * (T)wf_;
@@ -2835,6 +2848,7 @@ private:
         a.tb0 = 0; a.tn0 = nb; a.tb1 = 0;
         int grid = nb;
         int nbr = nb;
+        a.alt = pcg_alt_ ? 1 : 0;
         if (pcg_side_) {   // side-by-side waves (Args::side): tile = row chunk x group of 4 strips
             const int ng = (fs + kBlock / kWave - 1) / (kBlock / kWave), nch = side_chunks();
             a.side = 1;
@@ -3033,6 +3047,7 @@ private:
     T* pall_ = nullptr;                 // allp: lIterations p vectors of 3 N, p_i = pall_ + 3 N i
     int pall_cap_ = 0;
     bool pall_warned_ = false;
+    bool pcg_alt_ = false;              // OPT_AMD_IW_PCG_ALT=1: iw_pcg's odd row chunks walk upward (Args::alt)
     bool upd_pairs_ = true;             // OPT_AMD_IW_UPD_PAIRS=0: iw_update_all one pixel per thread
     // OPT_AMD_IW_PCG_SIDE (default 1): iw_pcg with side-by-side waves (Args::side) — the block's
     // four waves walk the same rows of four adjacent 60-column strips (round 6: 270 -> 257 us
