@@ -228,6 +228,27 @@ __device__ __forceinline__ void eedge(T ojx, T ojy, T cj, T sj, float ujx, float
     ey = v ? wr * (ojy - oty - ry) : (T)0;
 }
 
+// wr^2 |a|^2 for the edge j -> t, a = dR(t_j)/dt (U_j - U_t): the edge's term of the angle
+// channel's diag(J^T J) at pixel j (evalJTF's preconditioner, o.t:2870-2913). Every rounding
+// is explicit (fmas, opaque products), so iw_jtf / iw_jtf_apply, which store the angle
+// preconditioner from it, and iw_pcg, which recomputes it (PRC), form bitwise the same
+// value whatever the surrounding code lets the compiler contract.
+template <typename T>
+__device__ __forceinline__ T diag_a2(T cj, T sj, float ujx, float ujy, float utx, float uty, T wr2) {
+    const T dx = (T)(ujx - utx), dy = (T)(ujy - uty);
+    const T ax = fmad(-sj, dx, -opaque(cj * dy));
+    const T ay = fmad(cj, dx, -opaque(sj * dy));
+    return opaque(wr2 * fmad(ax, ax, opaque(ay * ay)));
+}
+
+// the angle channel's preconditioner from its diag(J^T J) (CERES guardedInvert form,
+// PCGInit1 :543-550), one expression for every kernel that forms it
+template <typename T>
+__device__ __forceinline__ T pre_angle(T dt) {
+    const T st = (T)1 + sqrt(dt);
+    return (T)1 / (st * st);
+}
+
 // Accumulation of the fused passes' sums: fp64 products summed in fp64 (the identity's
 // terms cancel, so their rounding is amplified by rz_{i-1} / rz_i; round 2 measured fp32
 // products ~1e-7 of rz off, enough to matter there)
@@ -1013,7 +1034,7 @@ struct GRaw {
 };
 // REC: flags, S and the record of iteration i-1 (pin == rin); p_{i-2} (E) from its record,
 // r_0's part when P0 (pass 2 forms p_0 from it). oob: an offset past every buffer.
-template <typename T, int DM, int E, bool P0, bool REC>
+template <typename T, int DM, int E, bool P0, bool REC, bool PRC = false>
 __device__ __forceinline__ GRaw<T> raw_grow(const Args<T>& a, const WaveGeom& g, int y, unsigned tb, const T* pin,
                                             const T* rin, const T* pre, __amdgpu_buffer_rsrc_t rdl,
                                             __amdgpu_buffer_rsrc_t rq2, unsigned oob, bool own) {
@@ -1042,7 +1063,8 @@ __device__ __forceinline__ GRaw<T> raw_grow(const Args<T>& a, const WaveGeom& g,
     q.u = ldb<false, vec2_t<float>>(a.U, 8u * i);
     q.ang = ldb<false, T>(a.A, o.s);
     q.r = ldb<false, vec2_t<T>>(rin, o.xy); q.rt = ldb<false, T>(rin, o.t);
-    q.w2 = ldb<false, T>(pre, o.s);
+    if constexpr (!PRC) q.w2 = ldb<false, T>(pre, o.s);
+    else q.w2 = 0;
     if (!(P0 && !E)) { q.p = ldb<false, vec2_t<T>>(pin, o.xy); q.pt = ldb<false, T>(pin, o.t); }
     if (DM == 2) { q.d = bld<vec2_t<T>>(rdl, oxy); q.dt = bld<T>(rdl, ot); }
     if (E) { q.q2 = bld<vec2_t<T>>(rq2, oxy); q.q2t = bld<T>(rq2, ot); }
@@ -1084,7 +1106,10 @@ struct HRow {
 // PF2 (with U2): two raw rows in flight per wave instead of one.
 // REC: the REC layout (Args::S): pin == rin is the record of iteration i-1, pout == rout
 // that of iteration i, both halves stored by stage A; pin2 the record of iteration i-2.
-template <typename T, int DM, int E, bool P0, bool SNT, bool U2, bool PF2, bool REC>
+// PRC (passes without P0): the angle preconditioner recomputed from the stencil's geometry
+// (diag_a2 over the four edges, in iw_jtf's order, pre_angle) instead of read: bitwise the
+// stored value, 4 B/px less per pass.
+template <typename T, int DM, int E, bool P0, bool SNT, bool U2, bool PF2, bool REC, bool PRC = false>
 __device__ __forceinline__ void iw_pcg_body(const Args<T>& a, const T* __restrict__ pin, const T* __restrict__ rin,
                                             const T* __restrict__ pre, T* __restrict__ pout, T* rout,
                                             T* __restrict__ delta, double* __restrict__ sc, int prev,
@@ -1111,12 +1136,14 @@ __device__ __forceinline__ void iw_pcg_body(const Args<T>& a, const T* __restric
     acc_t rzd = 0, papd = 0, rapd = 0, apapd = 0;
     if (g.y0 < g.y1) {
         auto raw = [&](int y) {
-            return raw_grow<T, DM, E, P0, REC>(a, g, y, tb, pin, rin, pre, r_d, r_q2, oob, y >= g.y0 && y < g.y1);
+            return raw_grow<T, DM, E, P0, REC, PRC>(a, g, y, tb, pin, rin, pre, r_d, r_q2, oob, y >= g.y0 && y < g.y1);
         };
         auto fin = [&](const GRaw<T>& q) { return finish_grow<T, E, P0>(a, q); };
         // stage A at row y (cur = row y, dn = row y+1, carry from row y-1): Ap_{i-1}, then
         // r_i and p_i (stores r_i and delta on an owned row)
         ACarry<T> ka;
+        const T wr2 = a.wr * a.wr;
+        T dthm_a = 0;   // PRC: the angle diag term of the edge to the previous row (iw_jtf's k.dthm)
         auto stage_a = [&](const GRow<T>& cur, const GRow<T>& dn, int y) {
             vec2_t<T> ap;
             T at;
@@ -1130,7 +1157,18 @@ __device__ __forceinline__ void iw_pcg_body(const Args<T>& a, const T* __restric
             h.rt = cur.rt - alpha * at;
             // (z = 1 r = r exactly without a preconditioner: one select per weight, not per channel)
             h.w0 = a.use_pre ? w0 : (T)1;
-            h.w2 = a.use_pre ? cur.w2 : (T)1;
+            if constexpr (PRC) {   // iw_jtf's dt: previous row's edge, +x, -x, next row's edge
+                const vec2_t<float> lu = shl2(cur.u), ru = shr2(cur.u);
+                const bool ca = cur.act(), da = dn.act();
+                const bool lact = from_left0_i((int)ca) != 0, ract = from_right0_i((int)ca) != 0;
+                const T dt = dthm_a + (ca && ract ? diag_a2(cur.c, cur.s, cur.u.x, cur.u.y, ru.x, ru.y, wr2) : (T)0) +
+                             (ca && lact ? diag_a2(cur.c, cur.s, cur.u.x, cur.u.y, lu.x, lu.y, wr2) : (T)0) +
+                             (ca && da ? diag_a2(cur.c, cur.s, cur.u.x, cur.u.y, dn.u.x, dn.u.y, wr2) : (T)0);
+                dthm_a = ca && da ? diag_a2(dn.c, dn.s, dn.u.x, dn.u.y, cur.u.x, cur.u.y, wr2) : (T)0;
+                h.w2 = a.use_pre ? (ca ? pre_angle(dt) : (T)0) : (T)1;
+            } else {
+                h.w2 = a.use_pre ? cur.w2 : (T)1;
+            }
             const vec2_t<T> z = h.w0 * h.r;
             const T zt = h.w2 * h.rt;
             h.p = z + beta * cur.p;
@@ -1182,6 +1220,8 @@ __device__ __forceinline__ void iw_pcg_body(const Args<T>& a, const T* __restric
         GRow<T> qc = fin(raw(Y(-1)));
         GRow<T> qd = fin(raw(Y(0)));
         ka = acarry_init(g0.p, g0.pt, g0.c, g0.s, g0.u, g0.act(), qc.p, qc.pt, qc.c, qc.s, qc.u, qc.act(), wr);
+        if constexpr (PRC)
+            dthm_a = g0.act() && qc.act() ? diag_a2(qc.c, qc.s, qc.u.x, qc.u.y, g0.u.x, g0.u.y, wr2) : (T)0;
         HRow<T> hup = stage_a(qc, qd, Y(-1));
         qc = qd;
         qd = fin(raw(Y(1)));
@@ -1256,7 +1296,7 @@ __device__ __forceinline__ void iw_pcg_body(const Args<T>& a, const T* __restric
     block_reduce_publish<4>(v, rs, g.tile);
 }
 template <typename T, int DM, int E = 0, bool P0 = false, bool SNT = false, bool U2 = false, bool PF2 = false,
-          bool REC = false>
+          bool REC = false, bool PRC = false>
 #ifndef IW_PCG_WAVES
 #define IW_PCG_WAVES 1   // A/B builds (tools/ab_build.sh): the minimum waves per SIMD iw_pcg is held to
 #endif
@@ -1264,7 +1304,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IW_PCG_W
                                                  const T* __restrict__ pre, T* __restrict__ pout, T* rout,
                                                  T* __restrict__ delta, double* __restrict__ sc, int prev,
                                                  double base_scale, ReduceSlot rs, const T* pin2 = nullptr) {
-    iw_pcg_body<T, DM, E, P0, SNT, U2, PF2, REC>(a, pin, rin, pre, pout, rout, delta, sc, prev, base_scale, rs, pin2);
+    iw_pcg_body<T, DM, E, P0, SNT, U2, PF2, REC, PRC>(a, pin, rin, pre, pout, rout, delta, sc, prev, base_scale, rs,
+                                                      pin2);
 }
 
 // ------------------------------------------------------------- value rows
@@ -1367,7 +1408,7 @@ __device__ __forceinline__ JCarry<T> jcarry_init(const VRow<T>& up, const VRow<T
     eedge(cur.ox, cur.oy, cur.c, cur.s, cur.ux, cur.uy, up.ox, up.oy, up.ux, up.uy, vup, wr,
           k.my_x, k.my_y, ax, ay);
     k.thm = -wr * (ax * k.my_x + ay * k.my_y);
-    k.dthm = vup ? wr * wr * (ax * ax + ay * ay) : (T)0;
+    k.dthm = vup ? diag_a2(cur.c, cur.s, cur.ux, cur.uy, up.ux, up.uy, wr * wr) : (T)0;
     k.vmy = vup;
     return k;
 }
@@ -1425,9 +1466,9 @@ __device__ __forceinline__ JRow<T> jtf_row(const Args<T>& a, const VRow<T>& cur,
     o.ft = k.thm - wr * ((apx_x * epx_x + apx_y * epx_y) + (amx_x * emx_x + amx_y * emx_y) +
                          (apy_x * epy_x + apy_y * epy_y));
     o.nv = (int)vpx + (int)vmx + (int)vpy + k.vmy;
-    o.dt = k.dthm + (vpx ? wr2 * (apx_x * apx_x + apx_y * apx_y) : (T)0) +
-           (vmx ? wr2 * (amx_x * amx_x + amx_y * amx_y) : (T)0) +
-           (vpy ? wr2 * (apy_x * apy_x + apy_y * apy_y) : (T)0);
+    o.dt = k.dthm + (vpx ? diag_a2(cur.c, cur.s, cur.ux, cur.uy, rux, ruy, wr2) : (T)0) +
+           (vmx ? diag_a2(cur.c, cur.s, cur.ux, cur.uy, lux, luy, wr2) : (T)0) +
+           (vpy ? diag_a2(cur.c, cur.s, cur.ux, cur.uy, dn.ux, dn.uy, wr2) : (T)0);
     if (cur.fit) {
         o.fx += wf * wf * (cur.ox - (T)cur.cx);
         o.fy += wf * wf * (cur.oy - (T)cur.cy);
@@ -1435,7 +1476,7 @@ __device__ __forceinline__ JRow<T> jtf_row(const Args<T>& a, const VRow<T>& cur,
     k.inup_x = epy_x; k.inup_y = epy_y;
     k.my_x = edn_x; k.my_y = edn_y;
     k.thm = -wr * (adn_x * edn_x + adn_y * edn_y);
-    k.dthm = vpy ? wr2 * (adn_x * adn_x + adn_y * adn_y) : (T)0;
+    k.dthm = vpy ? diag_a2(dn.c, dn.s, dn.ux, dn.uy, cur.ux, cur.uy, wr2) : (T)0;
     k.vmy = vpy;
     return o;
 }
@@ -1456,8 +1497,7 @@ __device__ __forceinline__ JOut<T> jtf_out(const Args<T>& a, const VRow<T>& cur,
         o.rx = -j.fx; o.ry = -j.fy; o.rt = -j.ft;
         o.wo = pre_offset(a, o.f);   // 1/(1+sqrt(2 wr^2 nv + wf^2 [fit]))^2
         if (a.use_pre) {
-            const T st = (T)1 + sqrt(j.dt);
-            o.wt = (T)1 / (st * st);
+            o.wt = pre_angle(j.dt);
         } else {
             o.wt = (T)0.25;
         }
@@ -2536,6 +2576,7 @@ private:
         cost_side_ = env_int("OPT_AMD_IW_COST_SIDE", 0) != 0;
         upd_pairs_ = env_int("OPT_AMD_IW_UPD_PAIRS", 1) != 0;
         pcg_alt_ = env_int("OPT_AMD_IW_PCG_ALT", 0) != 0;
+        pcg_prc_ = env_int("OPT_AMD_IW_PCG_PRC", 1) != 0;
     }
     // A zeroed plan vector with kSlack spare bytes: place() may move each vector's base
     // within them between Steps (every vector is rewritten before it is read in a Step).
@@ -2849,6 +2890,9 @@ private:
         int grid = nb;
         int nbr = nb;
         a.alt = pcg_alt_ ? 1 : 0;
+        // the angle preconditioner recomputed (iw_pcg PRC): the mirrored walk sums its four
+        // edge terms in another order, so not with alt
+        const bool prc = pcg_prc_ && !pcg_alt_ && !rec;
         if (pcg_side_) {   // side-by-side waves (Args::side): tile = row chunk x group of 4 strips
             const int ng = (fs + kBlock / kWave - 1) / (kBlock / kWave), nch = side_chunks();
             a.side = 1;
@@ -2876,6 +2920,12 @@ private:
             constexpr bool SNT = decltype(nt)::value, U2 = decltype(u2)::value, PF2 = decltype(pf2)::value,
                            DP = decltype(dp)::value;
             if (nodelta) {
+                if constexpr (!DP && !PF2 && !SNT) {
+                    if (prc && !(i == 1 && p0)) {
+                        go(iw::iw_pcg<T, 0, 0, false, SNT, U2, PF2, DP, true>);
+                        return;
+                    }
+                }
                 if (i == 1 && p0) go(iw::iw_pcg<T, 0, 0, true, SNT, U2, PF2, DP>);
                 else go(iw::iw_pcg<T, 0, 0, false, SNT, U2, PF2, DP>);
             } else if (pin2 || (defer_ && i == 1)) {
@@ -3047,6 +3097,7 @@ private:
     T* pall_ = nullptr;                 // allp: lIterations p vectors of 3 N, p_i = pall_ + 3 N i
     int pall_cap_ = 0;
     bool pall_warned_ = false;
+    bool pcg_prc_ = true;               // OPT_AMD_IW_PCG_PRC=0: iw_pcg reads the stored angle preconditioner
     bool pcg_alt_ = false;              // OPT_AMD_IW_PCG_ALT=1: iw_pcg's odd row chunks walk upward (Args::alt)
     bool upd_pairs_ = true;             // OPT_AMD_IW_UPD_PAIRS=0: iw_update_all one pixel per thread
     // OPT_AMD_IW_PCG_SIDE (default 1): iw_pcg with side-by-side waves (Args::side) — the block's

@@ -716,6 +716,29 @@ def test_kept_p_update_is_bitwise_the_deferred_delta(monkeypatch, W, H, lit, dou
             np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("W,H,lit", [(150, 110, 10), (5, 3, 4), (200, 1, 3), (700, 300, 10), (61, 2, 5), (1, 9, 4),
+                                     (240, 97, 7), (130, 257, 12)])
+@pytest.mark.parametrize("double", [False, True])
+def test_recomputed_angle_pre_is_bitwise_the_stored(monkeypatch, W, H, lit, double):
+    """Round 6 (iw_pcg PRC, default on): the passes after the first recompute the angle
+    channel's Jacobi preconditioner from the stencil geometry (diag_a2 over the four edges
+    in iw_jtf's order, pre_angle) instead of reading the value iw_jtf_apply stored; every
+    rounding of that formula is explicit, so the trajectory (energies, Offset, Angle, PCG
+    scalars) is bitwise the stored-pre one (OPT_AMD_IW_PCG_PRC=0), fp32 and fp64."""
+    out = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("OPT_AMD_IW_PCG_PRC", v)
+        w = perturbed(W, H, seed=11 * W + H)
+        s = solver(W, H, double=double)
+        prm = device_params(w, double=double)
+        s.set_solver_params({"nIterations": 3, "lIterations": lit})
+        c = np.array(s.profiled_solve(prm))
+        out.append((c, to_np(prm[0]), to_np(prm[1]), np.array(s.scalars(2 + 5 * (lit + 2)))))
+        s.close()
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("W,H,lit", [(150, 110, 10), (5, 3, 4), (200, 1, 3), (700, 300, 10), (64, 64, 2),
                                      (61, 2, 5), (1, 9, 4), (121, 66, 1), (240, 97, 7)])
 @pytest.mark.parametrize("double", [False, True])
