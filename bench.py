@@ -109,9 +109,11 @@ def res_variant(i: int, defer: bool = IW_DEFER, liter: int = 10) -> str:
 # UrShape 8 + flag 1 + angle pre 4 + r_{i-1} 12 + p_{i-1} 12 read, p_i 12 written, r_i 12
 # written except in the last iteration; P0 and the deferred delta as iw_apply_res. With every
 # p_i kept (OPT_AMD_IW_ALLP, the default for lIterations 2..16) no pass carries a delta term:
-# iw_update_all reads the L p vectors once at the end.
+# iw_update_all reads the L p vectors once at the end. Since round 6 the passes without P0
+# recompute the angle pre from the stencil geometry (PRC) instead of reading it: 4 B/px less.
 PCG_KERNEL = "iw_pcg"
 IW_ALLP = os.environ.get("OPT_AMD_IW_ALLP", "1") != "0"
+IW_PRC = os.environ.get("OPT_AMD_IW_PCG_PRC", "1") != "0"
 
 
 def allp_on(liter: int) -> bool:
@@ -125,6 +127,8 @@ def pcg_bytes_per_px(i: int, liter: int = 10, defer: bool = IW_DEFER) -> int:
     if i < liter - 1:
         b += 12
     if allp_on(liter):
+        if IW_PRC and not (i == 1 and liter >= 3):
+            b -= 4   # PRC: no angle pre read
         return b
     if defer:
         b += 0 if i % 2 == 1 else (24 if i == 2 else 36)
@@ -143,8 +147,9 @@ def pcg_variant(i: int, defer: bool = IW_DEFER, liter: int = 10) -> str:
         dm, e = (1 if i == 1 else 2), 0
     p0 = "true" if liter >= 3 and (i == 1 or (defer and i == 2)) else "false"
     u2 = int(os.environ.get("OPT_AMD_IW_PCG_U2", "1"))   # the plan's default: two rows per trip
+    prc = allp_on(liter) and IW_PRC and p0 == "false" and u2 != 2
     return (f"iw_pcg<float, {dm}, {e}, {p0}, false, {'true' if u2 >= 1 else 'false'}, "
-            f"{'true' if u2 == 2 else 'false'}, false>")
+            f"{'true' if u2 == 2 else 'false'}, false{', true' if prc else ''}>")
 
 
 # PCGInit1 fused with the first apply (iw_jtf_apply, one strip pass): Offset 8 + Angle 4 +
