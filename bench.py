@@ -138,7 +138,7 @@ def pcg_bytes_per_px(i: int, liter: int = 10, defer: bool = IW_DEFER) -> int:
 
 
 def pcg_variant(i: int, defer: bool = IW_DEFER, liter: int = 10) -> str:
-    """The iw_pcg instantiation PCG iteration i >= 1 runs (<T, DM, E, P0, SNT, U2, PF2, REC>)."""
+    """The iw_pcg instantiation PCG iteration i >= 1 runs (<T, DM, E, P0, SNT, U2, PF2, REC, PRC>)."""
     if allp_on(liter):
         dm, e, defer = 0, 0, False
     elif defer:
@@ -149,7 +149,7 @@ def pcg_variant(i: int, defer: bool = IW_DEFER, liter: int = 10) -> str:
     u2 = int(os.environ.get("OPT_AMD_IW_PCG_U2", "1"))   # the plan's default: two rows per trip
     prc = allp_on(liter) and IW_PRC and p0 == "false" and u2 != 2
     return (f"iw_pcg<float, {dm}, {e}, {p0}, false, {'true' if u2 >= 1 else 'false'}, "
-            f"{'true' if u2 == 2 else 'false'}, false{', true' if prc else ''}>")
+            f"{'true' if u2 == 2 else 'false'}, false, {'true' if prc else 'false'}>")
 
 
 # PCGInit1 fused with the first apply (iw_jtf_apply, one strip pass): Offset 8 + Angle 4 +
