@@ -167,7 +167,8 @@ def init_bytes_per_px(liter: int = 10, ap: bool = True) -> int:
 # The step's two other kernels (HIP-event timed like the passes): iw_update reads the flag 1,
 # Offset 8, Angle 4, delta 12, p_{L-1} 12 (+ p_{L-2} 12 when the deferred pair is pending,
 # lIterations even) and writes Offset + Angle 12; iw_cost reads Offset 8, Angle 4, UrShape 8,
-# Constraints 8, Mask 4.
+# Constraints 8, Mask 4 — or, with the Step's flags (OPT_AMD_IW_COST_FLAGS, default on), Offset 8,
+# Angle 4, UrShape 8, the flag 1 (Constraints only at the workload's few fit pixels, not counted).
 STEP_KERNELS = ("iw_jtf_apply", "iw_pcg", "iw_update", "iw_cost")   # iw_update: iw_update_all with allp
 
 
@@ -177,7 +178,7 @@ def update_bytes_per_px(liter: int = 10) -> int:
     return 1 + 8 + 4 + (12 if liter >= 2 else 0) + 12 + (12 if liter % 2 == 0 else 0) + 12
 
 
-COST_BYTES_PER_PX = 32
+COST_BYTES_PER_PX = 21 if os.environ.get("OPT_AMD_IW_COST_FLAGS", "1") != "0" else 32
 
 
 def pmc_traffic(liter: int, first: int = 0, res=False):

@@ -1749,20 +1749,66 @@ __global__ __launch_bounds__(kBlock) void iw_cost(Args<T> a, ReduceSlot rs) {
 // edge record — round 4's 64-column form above fetched the strip's two outside columns per
 // row with separate 2-lane loads (141 us at 4096^2, 0.48 of 8 TB/s). Per pixel the same
 // eedge calls in the same order; the sums group by 60-column strips instead.
+// FL (round 6, the cost at the end of a Step): the flag byte this Step's iw_jtf_apply wrote
+// (bit 0 inside and Mask == 0, bit 1 Constraints >= 0 — the same tests on the same arrays
+// bound at this Step) stands in for Mask, and Constraints are read only where bit 1 says the
+// fit term exists (a raw buffer load at an out-of-range offset elsewhere touches no memory):
+// 32 -> 21 B/px plus the few constraint pixels, bitwise the same cost.
 template <typename T>
+struct CRaw {
+    vec2_t<T> o;
+    T t;
+    vec2_t<float> u;
+    int f, in;
+    unsigned i;
+};
+template <typename T, bool FL = false>
 __global__ __launch_bounds__(kBlock) void iw_cost60(Args<T> a, ReduceSlot rs) {
     const WaveGeom g = geom_fused(a);
     const T wr = a.wr, wf = a.wf;
     T acc = 0;
+    const unsigned cb = (unsigned)(8 * a.dom.npix_mem());   // Constraints' bytes: the drop offset
+    const __amdgpu_buffer_rsrc_t r_c = bres(a.C, cb);
     if (g.y0 < g.y1) {
-        auto row = [&](const VRaw<T>& q) { return finish_vrow<T, false, false>(q); };
-        VRow<T> up = row(raw_vrow<T, false, false>(a, g, g.y0 - 1)), cur = row(raw_vrow<T, false, false>(a, g, g.y0)),
-                dn = row(raw_vrow<T, false, false>(a, g, g.y0 + 1));
+        auto raw = [&](int y) {
+            if constexpr (FL) {
+                CRaw<T> q;
+                q.in = present(a.dom, g.x, y);
+                q.i = q.in ? (unsigned)a.dom.off(g.x, y) : 0u;
+                q.o = ldb<false, vec2_t<T>>(a.O, q.i * 2u * (unsigned)sizeof(T));
+                q.t = ldb<false, T>(a.A, q.i * (unsigned)sizeof(T));
+                q.u = ldb<false, vec2_t<float>>(a.U, 8u * q.i);
+                q.f = ldb<false, uint8_t>(a.flags, q.i);
+                return q;
+            } else {
+                return raw_vrow<T, false, false>(a, g, y);
+            }
+        };
+        auto row = [&](const auto& q) {
+            if constexpr (FL) {
+                VRow<T> v;
+                v.ox = q.in ? q.o.x : (T)0;
+                v.oy = q.in ? q.o.y : (T)0;
+                v.t = q.in ? q.t : (T)0;
+                v.ux = q.in ? q.u.x : 0.f; v.uy = q.in ? q.u.y : 0.f;
+                v.act = q.in && (q.f & 1);
+                v.fit = q.in && ((q.f >> 1) & 1);
+                // the row's Constraints, only where the fit term exists (used two rows later)
+                const vec2_t<float> c = bld<vec2_t<float>>(r_c, v.fit ? 8u * q.i : cb);
+                v.cx = c.x; v.cy = c.y;
+                sc_of(v.t, &v.c, &v.s);
+                v.eox = 0; v.eoy = 0; v.eux = 0.f; v.euy = 0.f; v.eact = 0; v.ec = 0; v.es = 0;
+                return v;
+            } else {
+                return finish_vrow<T, false, false>(q);
+            }
+        };
+        VRow<T> up = row(raw(g.y0 - 1)), cur = row(raw(g.y0)), dn = row(raw(g.y0 + 1));
         // two raw rows in flight (the walk waits on memory, not on issue: SQ_WAIT_ANY 0.49)
-        VRaw<T> n1 = raw_vrow<T, false, false>(a, g, min(g.y0 + 2, g.y1));
+        auto n1 = raw(min(g.y0 + 2, g.y1));
         for (int y = g.y0; y < g.y1; ++y) {
-            const VRaw<T> nx = n1;
-            n1 = raw_vrow<T, false, false>(a, g, min(y + 3, g.y1));
+            const auto nx = n1;
+            n1 = raw(min(y + 3, g.y1));
             const T lox = from_left0(cur.ox), loy = from_left0(cur.oy);
             const T rox = from_right0(cur.ox), roy = from_right0(cur.oy);
             const float lux = from_left0(cur.ux), luy = from_left0(cur.uy);
@@ -2475,8 +2521,8 @@ public:
             tend();
             exchange_unknowns();
         }
-        // computeCost at the updated unknowns (:2245)
-        tbegin("iw_cost"); launch_cost(kScCost); tend();
+        // computeCost at the updated unknowns (:2245); the flags of this Step's J^T F pass
+        tbegin("iw_cost"); launch_cost(kScCost, true); tend();
         allreduce(kScCost);
         const double c = read_scalar(kScCost);
         unbind_after_step();
@@ -2577,6 +2623,7 @@ private:
         upd_pairs_ = env_int("OPT_AMD_IW_UPD_PAIRS", 1) != 0;
         pcg_alt_ = env_int("OPT_AMD_IW_PCG_ALT", 0) != 0;
         pcg_prc_ = env_int("OPT_AMD_IW_PCG_PRC", 1) != 0;
+        cost_flags_ = env_int("OPT_AMD_IW_COST_FLAGS", 1) != 0;
     }
     // A zeroed plan vector with kSlack spare bytes: place() may move each vector's base
     // within them between Steps (every vector is rewritten before it is read in a Step).
@@ -3036,7 +3083,9 @@ private:
         OPT_HIP_CHECK(hipGetLastError());
     }
     // iw_cost60 on the fused strips when its 32-bit offsets fit (offsets32_), else iw_cost
-    void launch_cost(int sc_out) {
+    // fl: the flag byte of this Step's iw_jtf_apply / iw_jtf is valid for the bound arrays
+    // (the cost at the end of a Step; not Init's or OptAMD_EvalCost's)
+    void launch_cost(int sc_out, bool fl = false) {
         if (offsets32_ && cost60_) {
             iw::Args<T> a = args();
             a.nstrips = fused_strips();
@@ -3048,7 +3097,10 @@ private:
                 nb = cost_side_blocks();
             }
             a.tb0 = 0; a.tn0 = nb; a.tb1 = 0;
-            hipLaunchKernelGGL(iw::iw_cost60<T>, dim3(nb), dim3(kBlock), 0, stream_, a, red_.slot(nb, sc_out));
+            if (fl && cost_flags_)
+                hipLaunchKernelGGL((iw::iw_cost60<T, true>), dim3(nb), dim3(kBlock), 0, stream_, a, red_.slot(nb, sc_out));
+            else
+                hipLaunchKernelGGL(iw::iw_cost60<T>, dim3(nb), dim3(kBlock), 0, stream_, a, red_.slot(nb, sc_out));
         } else {
             const int nb = stencil_blocks();
             hipLaunchKernelGGL(iw::iw_cost<T>, dim3(nb), dim3(kBlock), 0, stream_, args(), red_.slot(nb, sc_out));
@@ -3097,6 +3149,7 @@ private:
     T* pall_ = nullptr;                 // allp: lIterations p vectors of 3 N, p_i = pall_ + 3 N i
     int pall_cap_ = 0;
     bool pall_warned_ = false;
+    bool cost_flags_ = true;            // OPT_AMD_IW_COST_FLAGS=0: the Step's cost reads Mask and every Constraint
     bool pcg_prc_ = true;               // OPT_AMD_IW_PCG_PRC=0: iw_pcg reads the stored angle preconditioner
     bool pcg_alt_ = false;              // OPT_AMD_IW_PCG_ALT=1: iw_pcg's odd row chunks walk upward (Args::alt)
     bool upd_pairs_ = true;             // OPT_AMD_IW_UPD_PAIRS=0: iw_update_all one pixel per thread

@@ -739,6 +739,29 @@ def test_recomputed_angle_pre_is_bitwise_the_stored(monkeypatch, W, H, lit, doub
         np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("W,H,lit", [(150, 110, 10), (5, 3, 4), (200, 1, 3), (700, 300, 10), (61, 2, 5), (1, 9, 4),
+                                     (240, 97, 7)])
+@pytest.mark.parametrize("double", [False, True])
+def test_step_cost_from_flags_is_bitwise_the_mask_cost(monkeypatch, W, H, lit, double):
+    """Round 6 (iw_cost60 FL, default on): the cost at the end of a Step takes the active and
+    fit tests from the flag byte this Step's J^T F pass wrote and reads Constraints only at
+    fit pixels, instead of Mask and every Constraint (OPT_AMD_IW_COST_FLAGS=0): the energies
+    and the trajectory are bitwise the same, fp32 and fp64 (the masked pixels and the
+    constraint pixels of perturbed() included)."""
+    out = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("OPT_AMD_IW_COST_FLAGS", v)
+        w = perturbed(W, H, seed=13 * W + H)
+        s = solver(W, H, double=double)
+        prm = device_params(w, double=double)
+        s.set_solver_params({"nIterations": 3, "lIterations": lit})
+        c = np.array(s.profiled_solve(prm))
+        out.append((c, to_np(prm[0]), to_np(prm[1]), np.array(s.scalars(2 + 5 * (lit + 2)))))
+        s.close()
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("W,H,lit", [(150, 110, 10), (5, 3, 4), (200, 1, 3), (700, 300, 10), (64, 64, 2),
                                      (61, 2, 5), (1, 9, 4), (121, 66, 1), (240, 97, 7)])
 @pytest.mark.parametrize("double", [False, True])
