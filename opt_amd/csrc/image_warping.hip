@@ -89,6 +89,11 @@ struct Args {
     // bottom to top, so the two waves on either side of every chunk boundary read the shared
     // halo rows at the same time (both at their start or both at their end)
     int alt;
+    // rev != 0 (round 6, OPT_AMD_IW_MALL_REV): the launch takes its tiles in reverse order
+    // (logical tile gridDim - 1 - remapped block), so it starts where the previous kernel of
+    // the Step ended, on the vectors that kernel wrote last and that still sit in the 256 MB
+    // Infinity Cache. Each tile keeps its reduction slot (g.tile): the sums are bitwise the same.
+    int rev;
     // REC layout (round 5; the fused loop's iw_jtf_apply / iw_pcg / iw_update with REC): the
     // PCG vectors of iteration i as ONE record per pixel, [r.x r.y | p.x p.y | r.t p.t]
     // (6 T: three aligned pairs), and the per-Step static data as the record
@@ -169,7 +174,8 @@ struct WaveGeom {
 template <typename T>
 __device__ __forceinline__ WaveGeom geom(const Args<T>& a) {
     WaveGeom g;
-    const int lt = xcd_remap(blockIdx.x, gridDim.x);
+    int lt = xcd_remap(blockIdx.x, gridDim.x);
+    if (a.rev) lt = (int)gridDim.x - 1 - lt;
     const int t = lt < a.tn0 ? a.tb0 + lt : a.tb1 + (lt - a.tn0);
     g.tile = t;
     g.lane = threadIdx.x & (kWave - 1);
@@ -584,7 +590,8 @@ constexpr int kFStrip = 60;
 template <typename T>
 __device__ __forceinline__ WaveGeom geom_fused(const Args<T>& a) {
     WaveGeom g;
-    const int lt = xcd_remap(blockIdx.x, gridDim.x);
+    int lt = xcd_remap(blockIdx.x, gridDim.x);
+    if (a.rev) lt = (int)gridDim.x - 1 - lt;   // Args::rev
     const int t = lt < a.tn0 ? a.tb0 + lt : a.tb1 + (lt - a.tn0);   // the launch's tile ranges (geom)
     g.tile = t;
     g.lane = threadIdx.x & (kWave - 1);
@@ -2048,8 +2055,9 @@ __global__ __launch_bounds__(kBlock) void iw_update_all(Args<T> a, T* __restrict
 #pragma unroll
     for (int i = 0; i < L; ++i) al[i] = pcg_alpha<T>(sc[sc0 + kSlots * i], sc[sc0 + kSlots * i + 1]);
     const long long b = a.dom.off(0, a.dom.y_lo), e = a.dom.off(0, a.dom.y_hi);
-    for (long long k = b + (long long)blockIdx.x * blockDim.x + threadIdx.x; k < e;
-         k += (long long)gridDim.x * blockDim.x) {
+    for (long long kf = b + (long long)blockIdx.x * blockDim.x + threadIdx.x; kf < e;
+         kf += (long long)gridDim.x * blockDim.x) {
+        const long long k = a.rev ? e - 1 - (kf - b) : kf;   // Args::rev: last pixel first
         const int f = a.flags[k];
         Vec2<T> q[L];
         T qt[L];
@@ -2106,7 +2114,8 @@ __global__ __launch_bounds__(kBlock) void iw_update_all2(Args<T> a, T* __restric
 #pragma unroll
     for (int i = 0; i < L; ++i) al[i] = pcg_alpha<T>(sc[sc0 + kSlots * i], sc[sc0 + kSlots * i + 1]);
     const long long b = a.dom.off(0, a.dom.y_lo), np = (a.dom.off(0, a.dom.y_hi) - b) >> 1;
-    for (long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x; j < np; j += (long long)gridDim.x * blockDim.x) {
+    for (long long jf = (long long)blockIdx.x * blockDim.x + threadIdx.x; jf < np; jf += (long long)gridDim.x * blockDim.x) {
+        const long long j = a.rev ? np - 1 - jf : jf;   // Args::rev: last pair first
         const long long k = b + 2 * j;
         const unsigned short ff = *reinterpret_cast<const unsigned short*>(a.flags + k);
         const int f0 = ff & 255, f1 = ff >> 8;
@@ -2522,7 +2531,9 @@ public:
             exchange_unknowns();
         }
         // computeCost at the updated unknowns (:2245); the flags of this Step's J^T F pass
-        tbegin("iw_cost"); launch_cost(kScCost, true); tend();
+        // (Args::rev: backward after a forward update, so the next Step's forward J^T F pass
+        // starts where it ends)
+        tbegin("iw_cost"); launch_cost(kScCost, true, mall_rev_ && (allp ? ((L - 1) & 1) != 0 : true)); tend();
         allreduce(kScCost);
         const double c = read_scalar(kScCost);
         unbind_after_step();
@@ -2624,6 +2635,7 @@ private:
         pcg_alt_ = env_int("OPT_AMD_IW_PCG_ALT", 0) != 0;
         pcg_prc_ = env_int("OPT_AMD_IW_PCG_PRC", 1) != 0;
         cost_flags_ = env_int("OPT_AMD_IW_COST_FLAGS", 1) != 0;
+        mall_rev_ = env_int("OPT_AMD_IW_MALL_REV", 1) != 0;
     }
     // A zeroed plan vector with kSlack spare bytes: place() may move each vector's base
     // within them between Steps (every vector is rewritten before it is read in a Step).
@@ -2691,12 +2703,16 @@ private:
             auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
             const bool pairs = upd_pairs_ && Np % 4 == 0 && b % 2 == 0 && (e - b) % 2 == 0 && al16(pall_) &&
                                al16(cur_O_) && ((uintptr_t)cur_A_ & (2 * sizeof(T) - 1)) == 0 && al16(r_) && al16(pre_);
+            // Args::rev: the update starts where the last pass ended (pass L-1 runs backward when
+            // L-1 is odd, launch_pcg)
+            iw::Args<T> ua = args();
+            ua.rev = mall_rev_ && !((L - 1) & 1) ? 1 : 0;
             if (pairs) {
                 auto k2 = upd_nt_ ? (p0r ? iw::iw_update_all2<T, K, true, true> : iw::iw_update_all2<T, K, false, true>)
                                   : (p0r ? iw::iw_update_all2<T, K, true> : iw::iw_update_all2<T, K, false>);
                 const long long need = ((e - b) / 2 + kBlock - 1) / kBlock;
                 const int grid = (int)std::max(1LL, std::min<long long>(need, upd_blocks_));
-                hipLaunchKernelGGL(k2, dim3(grid), dim3(kBlock), 0, stream_, args(), cur_O_, cur_A_,
+                hipLaunchKernelGGL(k2, dim3(grid), dim3(kBlock), 0, stream_, ua, cur_O_, cur_A_,
                                    (const T*)pall_, 3 * Np, (const double*)red_.scalars, rz(0), (const T*)r_,
                                    (const T*)pre_);
                 OPT_HIP_CHECK(hipGetLastError());
@@ -2704,7 +2720,7 @@ private:
             }
             const long long need = (dom_.npix_mem() + kBlock - 1) / kBlock;
             const int grid = (int)std::max(1LL, std::min<long long>(need, upd_blocks_));
-            hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, stream_, args(), cur_O_, cur_A_,
+            hipLaunchKernelGGL(k, dim3(grid), dim3(kBlock), 0, stream_, ua, cur_O_, cur_A_,
                                (const T*)pall_, 3 * dom_.npix_mem(), (const double*)red_.scalars, rz(0),
                                (const T*)r_, (const T*)pre_);
             OPT_HIP_CHECK(hipGetLastError());
@@ -2827,6 +2843,7 @@ private:
         a.tb0 = 0; a.tn0 = nstrips_ * nrowblocks_; a.tb1 = 0;
         a.side = 0;
         a.alt = 0;
+        a.rev = 0;
         a.S = srec_;
         // same float expression the reference's evalJTF + guardedInvert evaluate
         const T wr2 = (T)wr_ * (T)wr_, wf2 = (T)wf_ * (T)wf_;
@@ -2937,6 +2954,7 @@ private:
         int grid = nb;
         int nbr = nb;
         a.alt = pcg_alt_ ? 1 : 0;
+        a.rev = mall_rev_ && (i & 1) ? 1 : 0;   // pass i after a forward iw_jtf_apply: odd passes backward
         // the angle preconditioner recomputed (iw_pcg PRC): the mirrored walk sums its four
         // edge terms in another order, so not with alt
         const bool prc = pcg_prc_ && !pcg_alt_ && !rec;
@@ -3085,7 +3103,7 @@ private:
     // iw_cost60 on the fused strips when its 32-bit offsets fit (offsets32_), else iw_cost
     // fl: the flag byte of this Step's iw_jtf_apply / iw_jtf is valid for the bound arrays
     // (the cost at the end of a Step; not Init's or OptAMD_EvalCost's)
-    void launch_cost(int sc_out, bool fl = false) {
+    void launch_cost(int sc_out, bool fl = false, bool rev = false) {
         if (offsets32_ && cost60_) {
             iw::Args<T> a = args();
             a.nstrips = fused_strips();
@@ -3097,6 +3115,7 @@ private:
                 nb = cost_side_blocks();
             }
             a.tb0 = 0; a.tn0 = nb; a.tb1 = 0;
+            a.rev = rev ? 1 : 0;
             if (fl && cost_flags_)
                 hipLaunchKernelGGL((iw::iw_cost60<T, true>), dim3(nb), dim3(kBlock), 0, stream_, a, red_.slot(nb, sc_out));
             else
@@ -3149,6 +3168,7 @@ private:
     T* pall_ = nullptr;                 // allp: lIterations p vectors of 3 N, p_i = pall_ + 3 N i
     int pall_cap_ = 0;
     bool pall_warned_ = false;
+    bool mall_rev_ = true;              // OPT_AMD_IW_MALL_REV=0: every kernel of the Step walks forward (Args::rev)
     bool cost_flags_ = true;            // OPT_AMD_IW_COST_FLAGS=0: the Step's cost reads Mask and every Constraint
     bool pcg_prc_ = true;               // OPT_AMD_IW_PCG_PRC=0: iw_pcg reads the stored angle preconditioner
     bool pcg_alt_ = false;              // OPT_AMD_IW_PCG_ALT=1: iw_pcg's odd row chunks walk upward (Args::alt)
@@ -3262,6 +3282,7 @@ public:
         a_.nstrips = nstrips_; a_.nrowblocks = nrowblocks_; a_.rows = rows_;
         a_.tb0 = 0; a_.tn0 = nstrips_ * nrowblocks_; a_.tb1 = 0;
         a_.side = 0;
+        a_.rev = 0;
         for (int f = 0; f < 2; ++f)
             for (int v = 0; v < 5; ++v) a_.preO[f][v] = 0;   // MODE 0 never reads them
     }

@@ -762,6 +762,28 @@ def test_step_cost_from_flags_is_bitwise_the_mask_cost(monkeypatch, W, H, lit, d
         np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("W,H,lit", [(150, 110, 10), (5, 3, 4), (200, 1, 3), (700, 300, 10), (61, 2, 5), (1, 9, 4),
+                                     (240, 97, 7), (121, 66, 1), (300, 200, 9)])
+@pytest.mark.parametrize("double", [False, True])
+def test_reversed_tile_order_is_bitwise_the_forward(monkeypatch, W, H, lit, double):
+    """Round 6 (Args::rev, OPT_AMD_IW_MALL_REV): the odd PCG passes, and the update or the
+    cost after them, take their tiles (pixels) in reverse order so that each kernel starts
+    on what the previous one wrote last. Every tile keeps its reduction slot, so the
+    trajectory is bitwise the forward one, fp32 and fp64."""
+    out = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("OPT_AMD_IW_MALL_REV", v)
+        w = perturbed(W, H, seed=17 * W + H)
+        s = solver(W, H, double=double)
+        prm = device_params(w, double=double)
+        s.set_solver_params({"nIterations": 3, "lIterations": lit})
+        c = np.array(s.profiled_solve(prm))
+        out.append((c, to_np(prm[0]), to_np(prm[1]), np.array(s.scalars(2 + 5 * (lit + 2)))))
+        s.close()
+    for a, b in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("W,H,lit", [(150, 110, 10), (5, 3, 4), (200, 1, 3), (700, 300, 10), (64, 64, 2),
                                      (61, 2, 5), (1, 9, 4), (121, 66, 1), (240, 97, 7)])
 @pytest.mark.parametrize("double", [False, True])
