@@ -2887,10 +2887,7 @@ private:
     }
 
     double read_scalar(int idx) {
-        double v;
-        OPT_HIP_CHECK(hipMemcpyAsync(&v, red_.scalars + idx, sizeof(double), hipMemcpyDeviceToHost, stream_));
-        OPT_HIP_CHECK(hipStreamSynchronize(stream_));
-        return v;
+        return read_device_scalar(red_.scalars + idx);
     }
 
     void launch_jtf(T* r, T* pre, int sc_out, bool full_pre = false, bool acc = false) {

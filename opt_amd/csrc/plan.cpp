@@ -1,4 +1,5 @@
 // plan.cpp — Plan base class, solver parameters, kernel timer, reduction scratch.
+#include <cstdlib>
 #include <cstdarg>
 #include "plan.h"
 #include <cstring>
@@ -143,6 +144,7 @@ ReduceScratch::~ReduceScratch() {
 Plan::Plan(const ProblemSpec& spec, const StateOptions& opts) : spec_(spec), opts_(opts) {
     OPT_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     timer_.mode = opts.kernel_timing ? 1 : 0;
+    if (const char* v = getenv("OPT_AMD_HOST_SYNC")) host_sync_ = atoi(v);
 }
 
 Plan::~Plan() {
@@ -152,6 +154,7 @@ Plan::~Plan() {
     }
     for (hipEvent_t e : halo_ev_)
         if (e) OPT_HIP_CHECK(hipEventDestroy(e));
+    if (pinned_) (void)hipHostFree(pinned_);
 }
 
 void Plan::halo_mark() {
@@ -175,7 +178,9 @@ void Plan::set_solver_param(const char* name, const void* value) {
 
 void Plan::begin_call() {
     // Order this plan's stream after everything the caller queued on the default
-    // stream (the reference runs all device work on the default stream).
+    // stream (the reference runs all device work on the default stream). Nothing to order
+    // after when that stream has finished its work (OPT_AMD_HOST_SYNC bit 0).
+    if ((host_sync_ & 1) && hipStreamQuery(nullptr) == hipSuccess) return;
     hipEvent_t e;
     OPT_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     OPT_HIP_CHECK(hipEventRecord(e, 0));
@@ -197,6 +202,24 @@ void Plan::cleanup_log() {
     fflush(stdout);
 }
 
+double Plan::read_device_scalar(const double* dev) {
+    double v = 0.0;
+    double* dst = &v;
+    if (host_sync_ & 2) {
+        if (!pinned_) OPT_HIP_CHECK(hipHostMalloc((void**)&pinned_, sizeof(double), hipHostMallocDefault));
+        dst = pinned_;
+    }
+    OPT_HIP_CHECK(hipMemcpyAsync(dst, dev, sizeof(double), hipMemcpyDeviceToHost, stream_));
+    if (host_sync_ & 4) {
+        hipError_t q;
+        while ((q = hipStreamQuery(stream_)) == hipErrorNotReady) {
+        }
+        OPT_HIP_CHECK(q);
+    } else {
+        OPT_HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+    return *dst;
+}
 void Plan::end_call() {
     OPT_HIP_CHECK(hipStreamSynchronize(stream_));
     OPT_HIP_CHECK(hipGetLastError());

@@ -150,6 +150,10 @@ protected:
     Plan(const ProblemSpec& spec, const StateOptions& opts);
     void begin_call();              // order after the caller's default-stream work
     void end_call();                // wait for this plan's device work
+    // One device double to the host, waiting for stream_'s work (the Step's cost): with
+    // OPT_AMD_HOST_SYNC bit 1 through a pinned host word (no staging copy), bit 2 waiting by
+    // polling the stream instead of hipStreamSynchronize
+    double read_device_scalar(const double* dev);
     // Launch bookkeeping: wraps a kernel launch with the timer when enabled.
     // The reference's cleanup (solverGPUGaussNewton.t:1902-1910), run when Step returns 0:
     // with verbosityLevel > 0 it logs "final cost=%.16f" (the line the examples' test
@@ -179,6 +183,10 @@ protected:
     KernelTimer timer_;
     ReduceScratch red_;
     double prev_cost_ = 0.0;
+    // OPT_AMD_HOST_SYNC: bit 0 begin_call skips the default-stream event when that stream is
+    // idle (hipStreamQuery), bit 1 pinned read-back, bit 2 polled wait (read_device_scalar)
+    int host_sync_ = 3;   // same box: GN step 3.008 / 3.030 -> 2.986 / 2.993 ms with 3 (7: 2.993 / 2.987)
+    double* pinned_ = nullptr;
     int n_iter_ = 0;
     bool initialised_ = false;
 };

@@ -828,12 +828,7 @@ private:
             if (b) tbegin(n); else tend();
         }, stream_);
     }
-    double read(int idx) {
-        double v;
-        OPT_HIP_CHECK(hipMemcpyAsync(&v, red_.scalars + idx, sizeof(double), hipMemcpyDeviceToHost, stream_));
-        OPT_HIP_CHECK(hipStreamSynchronize(stream_));
-        return v;
-    }
+    double read(int idx) { return read_device_scalar(red_.scalars + idx); }
 
     Domain dom_;
     std::unique_ptr<Op> op_;
