@@ -1,21 +1,28 @@
 #!/bin/bash
 # Round 6: one rank's slab (tools/slab_rank.py) for image_warping GN and shape_from_shading LM,
 # with the rows-per-wave / side / FUSE23 A/B: tools/r06_slab.sh <outdir> [iw|sfs|both]
+# (VARIANTS=closing: the round-6 closing set)
 set -o pipefail
 O=gpurun_out/$1; mkdir -p $O; WHICH=${2:-both}
 run() { local tag=$1; shift; env "$@" timeout -k 10 300 python -u tools/slab_rank.py $ARGS > $O/$tag.json 2> $O/$tag.err || { tail -5 $O/$tag.err; exit 1; };
   python3 -c "import json; d=json.load(open('$O/$tag.json')); print('$tag', d['ms_per_step_slab'], d['ms_per_step_full_image'], d['slab_over_full_div_world'])"; }
 if [ $WHICH != sfs ]; then
 ARGS="image_warping 8 3 4096 4096 10"
+if [ "$VARIANTS" = closing ]; then   # round 6 closing set: the defaults, rows 12, forward-only kernels
+run iw_rows_auto OPT_AMD_X=0
+run iw_rows12 OPT_AMD_ROWS=12
+run iw_rows_auto_norev OPT_AMD_IW_MALL_REV=0
+else
 run iw_rows_auto OPT_AMD_X=0
 run iw_rows16 OPT_AMD_ROWS=16
 run iw_rows24 OPT_AMD_ROWS=24
 run iw_rows_auto_noside OPT_AMD_IW_PCG_SIDE=0
 run iw_rows16_jtfside OPT_AMD_ROWS=16 OPT_AMD_IW_JTF_SIDE=1 OPT_AMD_IW_COST_SIDE=1
 fi
+fi
 if [ $WHICH != iw ]; then
 ARGS="shape_from_shading 8 3 4096 4096 10"
 run sfs_classic OPT_AMD_FUSE23=0
-run sfs_fused OPT_AMD_FUSE23=1
+[ "$VARIANTS" = closing ] || run sfs_fused OPT_AMD_FUSE23=1
 fi
 exit 0
