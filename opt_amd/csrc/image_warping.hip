@@ -64,6 +64,18 @@ inline int rows_for(int nstrips, int nrows) {
     while (rows > 16 && (long long)nstrips * ((nrows + 4 * rows - 1) / (4 * rows)) < 2048) rows /= 2;
     return rows;
 }
+// Row slabs (round 6): a slab whose 16-row tiles are less than one resident round of iw_pcg
+// costs one wave's walk per pass (latency, not bandwidth: DESIGN.md §4), so the waves take
+// the fewest rows (>= 8) whose side-by-side tiles (ngroups x row chunks, 4 waves each) still
+// fit ONE round at the one-row form's 4 waves per SIMD (rows < 16 run without row pairs).
+// 16 when none does. Rank 3 of the 8-way 4096^2 split: rows 10, 0.582 -> 0.555 ms per GN
+// step (tools/r06_slab.sh u2).
+inline int rows_one_round(int ngroups, int nrows, int ncu) {
+    const long long slots = 4LL * 4 * ncu;   // waves: 4 SIMDs x 4 waves per CU
+    for (int r = 8; r < 16; ++r)
+        if ((long long)ngroups * ((nrows + r - 1) / r) * 4 <= slots) return r;
+    return 16;
+}
 
 template <typename T>
 struct Args {
@@ -2623,6 +2635,7 @@ private:
         upd_blocks_ = std::max(1, env_int("OPT_AMD_IW_UPD_BLOCKS", 2048));
         pcg_nt_ = env_int("OPT_AMD_IW_PCG_NT", 0) != 0;
         pcg_u2_ = env_int("OPT_AMD_IW_PCG_U2", 1);
+        slab_rows_ = env_int("OPT_AMD_IW_SLAB_ROWS", 1) != 0;
         // iw_jtf_apply's 60-column strips store 240-B row segments that share cache lines
         // with the neighbouring strips: plain stores (merged in the L2) measured 217-220 us
         // against 233-245 with streaming ones (round 5, same box, interleaved)
@@ -2680,7 +2693,19 @@ private:
         }
         place();
         nstrips_ = (dom_.W + iw::kStrip - 1) / iw::kStrip;
-        if (rows_ <= 0 || rows_auto_) { rows_auto_ = true; rows_ = iw::rows_for(nstrips_, dom_.y_hi - dom_.y_lo); }
+        if (rows_ <= 0 || rows_auto_) {
+            rows_auto_ = true;
+            rows_ = iw::rows_for(nstrips_, dom_.y_hi - dom_.y_lo);
+            // a proper row slab (set_decomposition over part of the image; a one-rank
+            // "split" of the whole image keeps the single-domain tiling, bitwise that path)
+            if (rows_ <= 16 && comm_ && slab_rows_ && (dom_.y_lo > 0 || dom_.y_hi < dom_.H)) {
+                int dev = 0, cu = 0;
+                OPT_HIP_CHECK(hipGetDevice(&dev));
+                OPT_HIP_CHECK(hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev));
+                const int ng = (fused_strips() + kBlock / kWave - 1) / (kBlock / kWave);
+                rows_ = iw::rows_one_round(ng, dom_.y_hi - dom_.y_lo, std::max(1, cu));
+            }
+        }
         nrowblocks_ = (dom_.y_hi - dom_.y_lo + rows_ * 4 - 1) / (rows_ * 4);
         red_.ensure(std::max({stencil_blocks(), fused_blocks(), cost_blocks(), cost_side_blocks(), fused_side_blocks(), 2048}),
                     1, 64);
@@ -3185,6 +3210,7 @@ private:
     // 270 us per pass, GN step 3.35 -> 3.30 ms) two rows with the records swapping roles,
     // 2 the same with two raw rows in flight
     int pcg_u2_ = 1;
+    bool slab_rows_ = true;   // OPT_AMD_IW_SLAB_ROWS=0: row slabs keep rows_for's 16-row floor (iw::rows_one_round)
     int cost_rows_ = 0;
     bool jtf_nt_ = false;               // OPT_AMD_IW_JTF_NT=1: iw_jtf_apply with streaming stores
     bool offsets32_ = true;             // iw_apply_res's 32-bit byte offsets cover every plan vector

@@ -8,7 +8,13 @@ run() { local tag=$1; shift; env "$@" timeout -k 10 300 python -u tools/slab_ran
   python3 -c "import json; d=json.load(open('$O/$tag.json')); print('$tag', d['ms_per_step_slab'], d['ms_per_step_full_image'], d['slab_over_full_div_world'])"; }
 if [ $WHICH != sfs ]; then
 ARGS="image_warping 8 3 4096 4096 10"
-if [ "$VARIANTS" = closing ]; then   # round 6 closing set: the defaults, rows 12, forward-only kernels
+if [ "$VARIANTS" = u2 ]; then   # one row per trip (fewer VGPRs) with fewer rows per wave
+run iw_rows_auto OPT_AMD_X=0
+run iw_u2off OPT_AMD_IW_PCG_U2=0
+run iw_u2off_rows10 OPT_AMD_IW_PCG_U2=0 OPT_AMD_ROWS=10
+run iw_u2off_rows8 OPT_AMD_IW_PCG_U2=0 OPT_AMD_ROWS=8
+run iw_rows10 OPT_AMD_ROWS=10
+elif [ "$VARIANTS" = closing ]; then   # round 6 closing set: the defaults, rows 12, forward-only kernels
 run iw_rows_auto OPT_AMD_X=0
 run iw_rows12 OPT_AMD_ROWS=12
 run iw_rows_auto_norev OPT_AMD_IW_MALL_REV=0
