@@ -28,7 +28,13 @@ fi
 fi
 if [ $WHICH != iw ]; then
 ARGS="shape_from_shading 8 3 4096 4096 10"
+if [ "$VARIANTS" = flat ]; then   # the flat PCG kernels' grid cap
+run sfs_classic OPT_AMD_FUSE23=0
+run sfs_flat8192 OPT_AMD_FUSE23=0 OPT_AMD_FLAT_BLOCKS=8192
+run sfs_flat65536 OPT_AMD_FUSE23=0 OPT_AMD_FLAT_BLOCKS=65536
+else
 run sfs_classic OPT_AMD_FUSE23=0
 [ "$VARIANTS" = closing ] || run sfs_fused OPT_AMD_FUSE23=1
+fi
 fi
 exit 0
