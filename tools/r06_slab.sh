@@ -28,7 +28,12 @@ fi
 fi
 if [ $WHICH != iw ]; then
 ARGS="shape_from_shading 8 3 4096 4096 10"
-if [ "$VARIANTS" = flat ]; then   # the flat PCG kernels' grid cap
+if [ "$VARIANTS" = sfsrows ]; then   # rows per wave of the once-per-step strips (cost, model cost, precompute)
+run sfs_classic OPT_AMD_FUSE23=0
+run sfs_cp16 OPT_AMD_FUSE23=0 OPT_AMD_SFS_COST_ROWS=16 OPT_AMD_SFS_PRE_ROWS=16
+run sfs_cp12 OPT_AMD_FUSE23=0 OPT_AMD_SFS_COST_ROWS=12 OPT_AMD_SFS_PRE_ROWS=12
+run sfs_cp8 OPT_AMD_FUSE23=0 OPT_AMD_SFS_COST_ROWS=8 OPT_AMD_SFS_PRE_ROWS=8
+elif [ "$VARIANTS" = flat ]; then   # the flat PCG kernels' grid cap
 run sfs_classic OPT_AMD_FUSE23=0
 run sfs_flat8192 OPT_AMD_FUSE23=0 OPT_AMD_FLAT_BLOCKS=8192
 run sfs_flat65536 OPT_AMD_FUSE23=0 OPT_AMD_FLAT_BLOCKS=65536
