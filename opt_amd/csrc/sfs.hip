@@ -1079,13 +1079,19 @@ private:
     // rows, 12-row waves (LM step at 4096 x 512: 20 rows 0.748 ms, 16 0.736, 12 0.704,
     // 8 0.712; 4096 x 1024: 1.033 / 1.028 / 1.016 / 1.091; 4096 x 2048: 20 rows best,
     // 1.711 ms; tools/sweep_sfs_rows.py)
-    int strip_rows_ = env_int("OPT_AMD_SFS_ROWS", 0) > 0 ? env_int("OPT_AMD_SFS_ROWS", 0)
-        : ((long long)((dom_.W + sfs::kStripOut - 1) / sfs::kStripOut) * ((dom_.y_hi - dom_.y_lo + 19) / 20) < 4096 ? 12 : 20);
-    int cost_rows_ = env_int("OPT_AMD_SFS_COST_ROWS", 32);
+    const bool small_dom_ =
+        (long long)((dom_.W + sfs::kStripOut - 1) / sfs::kStripOut) * ((dom_.y_hi - dom_.y_lo + 19) / 20) < 4096;
+    int strip_rows_ = env_int("OPT_AMD_SFS_ROWS", 0) > 0 ? env_int("OPT_AMD_SFS_ROWS", 0) : (small_dom_ ? 12 : 20);
+    // the once-per-Step strips (cost, model cost, precompute): 12 rows per wave (round 6:
+    // 4096 x 512 slab, 32 / 16 / 12 / 8 rows: LM step 0.705 / 0.674 / 0.657 / 0.666 ms —
+    // cost 32.8 -> 19.5, model cost 33.3 -> 22.1, precompute 48.8 -> 29.1 us at 12,
+    // tools/r06_slab.sh with VARIANTS=sfsrows; whole 4096^2 image, same box: 3.177 / 3.202
+    // -> 3.146 / 3.161 ms, tools/r06_sfs_ab.sh)
+    int cost_rows_ = env_int("OPT_AMD_SFS_COST_ROWS", 0) > 0 ? env_int("OPT_AMD_SFS_COST_ROWS", 0) : 12;
     bool cost_strip_ = env_int("OPT_AMD_SFS_COST_STRIP", 1) != 0;   // 0: the per-pixel sfs_cost
     bool jtf_strip_ = env_int("OPT_AMD_SFS_JTF_STRIP", 1) != 0;     // 0: the LDS-tile J^T F
     bool pre_strip_ = env_int("OPT_AMD_SFS_PRE_STRIP", 1) != 0;     // 0: the per-pixel precompute
-    int pre_rows_ = std::max(1, env_int("OPT_AMD_SFS_PRE_ROWS", 32));
+    int pre_rows_ = env_int("OPT_AMD_SFS_PRE_ROWS", 0) > 0 ? env_int("OPT_AMD_SFS_PRE_ROWS", 0) : 12;
     T *BI_ = nullptr, *G00_ = nullptr, *Gm0_ = nullptr, *G0m_ = nullptr;
     uint8_t* valid_ = nullptr;
     T* userX_ = nullptr;
