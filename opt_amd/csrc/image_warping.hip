@@ -2115,8 +2115,11 @@ __global__ __launch_bounds__(kBlock) void iw_update_all(Args<T> a, T* __restrict
 // when the pairs are aligned (N % 4 == 0, even row starts, 16-B aligned arrays).
 template <typename T>
 using vec4_t = T __attribute__((ext_vector_type(4)));
+#ifndef IW_UPD_WAVES
+#define IW_UPD_WAVES 1   // A/B builds (tools/ab_build.sh): the minimum waves per SIMD iw_update_all2 is held to
+#endif
 template <typename T, int L, bool P0R, bool NT = false>
-__global__ __launch_bounds__(kBlock) void iw_update_all2(Args<T> a, T* __restrict__ O, T* __restrict__ A,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IW_UPD_WAVES))) void iw_update_all2(Args<T> a, T* __restrict__ O, T* __restrict__ A,
                                                          const T* __restrict__ pall, long long pstride,
                                                          const double* __restrict__ sc, int sc0,
                                                          const T* __restrict__ r0, const T* __restrict__ pre) {
